@@ -1,0 +1,197 @@
+/*
+ * orbgpu.h — C-ABI of the MI355X-native ORB front-end (gfx950 HIP kernels).
+ *
+ * Drop-in boundary for the ORB front-end of donglinb/ORB-SLAM-BIRDVIEW.  Each entry point names the
+ * reference interface it replaces; the C++ mirror classes ORB_SLAM2::ORBextractor / ORBmatcher
+ * (orb-slam-birdview_amd/csrc/host/) and the Python binding (orbgpu/) are thin layers over it.
+ *
+ *  - Plain pointers and sizes only: no HIP, torch or OpenCV types in any signature.
+ *  - Nothing throws across the ABI; every function returns an orb_status (0 = OK).
+ *  - A context owns one HIP stream on one device; entry points call hipSetDevice on entry, so a
+ *    context may be driven from any host thread (Frame.cc:124-127 spawns fresh threads per frame),
+ *    but one context must not be used by two threads at once (same contract as the reference's
+ *    one-extractor-per-thread, ORBextractor.h:85 mvImagePyramid is instance state).
+ *  - There is no CPU fallback: if the HIP runtime or device is unavailable, orb_create fails.
+ */
+#ifndef ORBGPU_H
+#define ORBGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBGPU_ABI_VERSION 1
+#define ORBGPU_MAX_LEVELS 16
+
+typedef enum {
+    ORB_OK = 0,
+    ORB_ERR_ARG = -1,        /* bad argument / NULL pointer                                     */
+    ORB_ERR_HIP = -2,        /* HIP runtime error (message via orb_last_error)                   */
+    ORB_ERR_CAPACITY = -3,   /* caller buffer too small; *n receives the required count          */
+    ORB_ERR_GEOMETRY = -4,   /* image too small for the pyramid (reference: division by zero UB) */
+    ORB_ERR_NOMEM = -5,      /* device allocation failed                                         */
+    ORB_ERR_INTERNAL = -6    /* a kernel reported an overflow of an internal bound               */
+} orb_status;
+
+/* Bit-compatible with cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id;}
+ * (28 bytes), so the OpenCV-side adapter can memcpy. */
+typedef struct {
+    float x, y, size, angle, response;
+    int octave, class_id;
+} orb_keypoint;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * replaces ORBextractor::ORBextractor, reference src/ORBextractor.cc:410-470 / include/ORBextractor.h:52-53 */
+typedef struct {
+    int nfeatures;
+    float scaleFactor;
+    int nlevels;
+    int iniThFAST;
+    int minThFAST;
+    int device;       /* HIP device ordinal                                     */
+    int max_width;    /* capacity hints (contexts grow on demand for host input) */
+    int max_height;
+    int max_batch;    /* frames per batched launch (device-resident path)       */
+} orb_params;
+
+typedef struct orb_ctx orb_ctx;
+
+int  orb_abi_version(void);
+const char* orb_last_error(void);      /* thread-local message for the last failure */
+int  orb_device_count(void);
+
+orb_ctx* orb_create(const orb_params* p, int* status);
+void     orb_destroy(orb_ctx* ctx);
+
+/* GetLevels/GetScaleFactor(s)/GetInverseScaleFactors/GetScaleSigmaSquares/GetInverseScaleSigmaSquares
+ * (include/ORBextractor.h:63-83) + mnFeaturesPerLevel (ORBextractor.cc:435-446) + umax (:454-469).
+ * Any pointer may be NULL. Arrays hold nlevels entries (umax: 16). */
+int orb_scale_tables(const orb_ctx* ctx, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                     int* n_per_level, int* umax16);
+
+/* ORBextractor::operator()(InputArray image, InputArray mask, vector<KeyPoint>&, OutputArray)
+ * — reference src/ORBextractor.cc:1043-1105.  Host gray image in (mask ignored, as in the reference,
+ * include/ORBextractor.h:58); keypoints (level-0 coordinates, level-major order) and n x 32
+ * descriptors out.  Empty image (w==0 || h==0 || img==NULL) returns ORB_OK leaving *n and the
+ * outputs untouched (:1046-1047).  If *n would exceed cap, returns ORB_ERR_CAPACITY with *n set. */
+int orb_extract(orb_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
+                orb_keypoint* kps, int cap, int* n, uint8_t* desc);
+
+/* public std::vector<cv::Mat> mvImagePyramid (include/ORBextractor.h:85), read by
+ * Frame::ComputeStereoMatches (Frame.cc:669,759): host view of level `level` of the last
+ * orb_extract, copied lazily device->host into context-owned memory (valid until the next call). */
+int orb_get_level(orb_ctx* ctx, int level, const uint8_t** data, int* w, int* h, size_t* stride);
+
+/* ---- device-resident batched path (bench, multi-camera streams). Asynchronous on the context
+ * stream; call orb_sync before reading outputs. d_frames: nframes gray frames, frame f at
+ * d_frames + f*frame_pitch, rows `row_stride` apart.  Outputs: frame f's keypoints at
+ * d_kps + f*kp_cap, descriptors at d_desc + f*kp_cap*32, count in d_counts[f].
+ * kp_cap must be >= orb_batch_kp_cap(ctx, w, h). ---- */
+int orb_batch_kp_cap(orb_ctx* ctx, int w, int h);
+int orb_extract_batch_device(orb_ctx* ctx, const uint8_t* d_frames, int nframes, int w, int h,
+                             size_t frame_pitch, size_t row_stride,
+                             orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int kp_cap);
+int orb_sync(orb_ctx* ctx);
+
+/* device memory helpers (so callers need no HIP headers) */
+void* orb_device_alloc(orb_ctx* ctx, size_t bytes);
+int   orb_device_free(orb_ctx* ctx, void* p);
+int   orb_memcpy_h2d(orb_ctx* ctx, void* dst, const void* src, size_t bytes);
+int   orb_memcpy_d2h(orb_ctx* ctx, void* dst, const void* src, size_t bytes);
+int   orb_memset_device(orb_ctx* ctx, void* dst, int value, size_t bytes);
+
+/* ---- per-kernel timing with HIP events on the context stream (bench roofline) ---- */
+enum { ORB_K_RESIZE = 0, ORB_K_FAST = 1, ORB_K_OCTREE = 2, ORB_K_DESCRIBE = 3, ORB_K_HAMMING = 4,
+       ORB_K_COUNT = 5 };
+int orb_profile_enable(orb_ctx* ctx, int on);   /* clears accumulated times */
+int orb_profile_read(orb_ctx* ctx, double* ms_total /*ORB_K_COUNT*/, int* launches /*ORB_K_COUNT*/);
+
+/* ---- debug views of intermediate device buffers (parity tests pinpoint the failing stage) ---- */
+/* FAST candidates of `level` for frame `frame` of the last batch, in vToDistributeKeys order
+ * (ORBextractor.cc:820-825): 3 ints (x, y, score) each, coords relative to minBorder. */
+int orb_debug_candidates(orb_ctx* ctx, int frame, int level, int* out, int cap);
+/* Octree output of `level` (DistributeOctTree list order): 3 ints (x, y, score), level coords. */
+int orb_debug_level_keypoints(orb_ctx* ctx, int frame, int level, int* out, int cap);
+int orb_debug_level_image(orb_ctx* ctx, int frame, int level, uint8_t* out, int* w, int* h);
+
+/* =========================== ORBmatcher =========================== */
+
+/* static int ORBmatcher::DescriptorDistance(const cv::Mat&, const cv::Mat&)  ORBmatcher.cc:1647-1663
+ * (host helper: a single pair is never worth a kernel launch). */
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Top-k smallest Hamming distances per query on the GPU (the inner loop of every ORBmatcher search).
+ * Candidates of query i: cand_idx[cand_off[i] .. cand_off[i+1]) (CSR, in the reference's iteration
+ * order), or all trains 0..nt-1 if cand_off == NULL.  A candidate t is skipped when
+ * train_thr != NULL and train_thr[t] <= dist (covers vbMatched2 / vMatchedDistance / invalid
+ * MapPoints).  Results sorted by (dist, candidate position): out_dist/out_idx[i*k + j], -1 padded;
+ * out_nvalid[i] = number of candidates that passed the filter (tells whether the list is complete).
+ * Host pointers, synchronous. */
+int orb_hamming_topk(orb_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                     const int* cand_off, const int* cand_idx, const int* train_thr, int k,
+                     int* out_dist, int* out_idx, int* out_nvalid);
+
+/* Device-pointer variant of the all-pairs (cand_off == NULL, no filter) top-2: best distance,
+ * its train index (first on ties) and second-best distance per query. Asynchronous. */
+int orb_hamming_top2_device(orb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
+                            int* d_best, int* d_best_idx, int* d_second);
+
+/* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21) as CSR. */
+typedef struct {
+    int nnodes;
+    const uint32_t* node_ids;   /* ascending */
+    const int* offsets;         /* nnodes + 1 */
+    const int* indices;
+} orb_featvec;
+
+/* int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+ * ORBmatcher.cc:159-288.  mp_kf[i]!=0 <=> KF feature i has a non-bad MapPoint; angles are
+ * mvKeysUn (KF) / mvKeys (F) angles.  match_f[iF] = KF feature index whose MapPoint was assigned
+ * to F feature iF, or -1.  *nmatches receives the return value of the reference function. */
+int orb_search_by_bow_kf_f(orb_ctx* ctx, float nnratio, int check_ori,
+                           int n_kf, const uint8_t* desc_kf, const float* angle_kf, const uint8_t* mp_kf,
+                           orb_featvec fv_kf, int n_f, const uint8_t* desc_f, const float* angle_f,
+                           orb_featvec fv_f, int* match_f, int* nmatches);
+
+/* int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+ * ORBmatcher.cc:522-655.  match12[i1] = KF2 feature index whose MapPoint was assigned, or -1. */
+int orb_search_by_bow_kf_kf(orb_ctx* ctx, float nnratio, int check_ori,
+                            int n1, const uint8_t* desc1, const float* angle1, const uint8_t* mp1,
+                            orb_featvec fv1, int n2, const uint8_t* desc2, const float* angle2,
+                            const uint8_t* mp2, orb_featvec fv2, int* match12, int* nmatches);
+
+/* int ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12,
+ *     vector<pair<size_t,size_t>>&, const bool bOnlyStereo)   ORBmatcher.cc:657-823
+ * Keypoints are mvKeysUn; has_mp[i] <=> GetMapPoint(i) != NULL; uright = mvuRight; F12 row-major
+ * 3x3; (ex, ey) the epipole of KF1's centre in KF2 (:662-668, computed by the caller from poses);
+ * scale2/sigma2_2 = pKF2->mvScaleFactors / mvLevelSigma2.  pairs_out: 2 ints per pair (ascending
+ * idx1), *npairs = count (ORB_ERR_CAPACITY if > cap). */
+int orb_search_for_triangulation(orb_ctx* ctx, int check_ori, int only_stereo,
+                                 int n1, const uint8_t* desc1, const orb_keypoint* kps1, const uint8_t* has_mp1,
+                                 const float* uright1, orb_featvec fv1,
+                                 int n2, const uint8_t* desc2, const orb_keypoint* kps2, const uint8_t* has_mp2,
+                                 const float* uright2, orb_featvec fv2,
+                                 const float* F12, float ex, float ey, const float* scale2, const float* sigma2_2,
+                                 int nlevels2, int* pairs_out, int cap, int* npairs);
+
+/* int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<Point2f>& vbPrevMatched,
+ *     vector<int>& vnMatches12, int windowSize)  ORBmatcher.cc:405-520 (level0_only = 1), and
+ * int ORBmatcher::BirdviewMatch(const Frame&, const Frame&, vector<int>&, int)  :1790-1899
+ * (level0_only = 0).  Candidates per query = Frame::GetFeaturesInArea (CSR), computed by the caller
+ * (orb_features_in_area restates it).  match12 out. */
+int orb_window_match(orb_ctx* ctx, float nnratio, int check_ori, int level0_only,
+                     int n1, const uint8_t* desc1, const orb_keypoint* kps1,
+                     int n2, const uint8_t* desc2, const orb_keypoint* kps2,
+                     const int* cand_off, const int* cand_idx, int* match12, int* nmatches);
+
+/* Frame::GetFeaturesInArea over the 64x48 Frame grid (Frame.cc:378-412, 494-560): host helper the
+ * C++ mirror uses to build window candidate lists. Returns count or -(needed)-1. */
+int orb_features_in_area(int n, const orb_keypoint* kps_un, float min_x, float max_x, float min_y, float max_y,
+                         float x, float y, float r, int min_level, int max_level, int* out, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1074 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  See orb_oracle.h for scope and parity status.
+ *
+ * Built with -O3 -march=native -ffp-contract=off (oracle/Makefile): the restatement never
+ * contracts a*b+c into an FMA, matching the pinned float semantics the HIP path uses.
+ * Every function cites the reference file:line it restates.
+ */
+#include "orb_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <thread>
+#include <utility>
+#include <vector>
+#include <climits>
+#include <cfloat>
+
+namespace {
+
+const int PATCH_SIZE = 31;        // ORBextractor.cc:72
+const int HALF_PATCH_SIZE = 15;   // ORBextractor.cc:73
+const int EDGE_THRESHOLD = 19;    // ORBextractor.cc:74
+
+#include "pattern31_data.inc"
+const int kPattern[1024] = { ORACLE_PATTERN31_VALUES };
+
+/* ---------------- OpenCV 3.2 rounding helpers ---------------- */
+inline int cvRound(float v) { return (int)std::nearbyint(v); }     // _mm_cvtss_si32, half-even
+inline int cvRound(double v) { return (int)std::nearbyint(v); }    // _mm_cvtsd_si32, half-even
+inline int cvFloor(float v) { return (int)std::floor(v); }
+inline int cvCeil(float v) { return (int)std::ceil(v); }
+inline short sat_short(int v) { return (short)std::min(std::max(v, (int)SHRT_MIN), (int)SHRT_MAX); }
+inline uint8_t sat_u8(int v) { return (uint8_t)std::min(std::max(v, 0), 255); }
+
+struct Img {
+    int w = 0, h = 0;
+    std::vector<uint8_t> d;
+    void create(int W, int H) { w = W; h = H; d.assign((size_t)W * H, 0); }
+    uint8_t* row(int y) { return d.data() + (size_t)y * w; }
+    const uint8_t* row(int y) const { return d.data() + (size_t)y * w; }
+};
+
+struct KP {
+    float x, y, size, angle, response;
+    int octave, class_id;
+};
+static_assert(sizeof(KP) == 28, "cv::KeyPoint layout");
+
+/* ---------------- cv::resize INTER_LINEAR, 8UC1 (OpenCV 3.2 imgwarp.cpp; Appendix A.1) ------ */
+void resize_linear_8u(const Img& src, Img& dst, int dw, int dh, int flags) {
+    const int sw = src.w, sh = src.h;
+    dst.create(dw, dh);
+    double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    std::vector<int> xofs(dw), yofs(dh);
+    std::vector<short> ialpha(2 * dw), ibeta(2 * dh);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cvFloor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        float c0 = 1.f - fx, c1 = fx;
+        ialpha[2 * dx] = sat_short(cvRound(c0 * 2048));
+        ialpha[2 * dx + 1] = sat_short(cvRound(c1 * 2048));
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cvFloor(fy);
+        fy -= sy;
+        yofs[dy] = sy;
+        float c0 = 1.f - fy, c1 = fy;
+        ibeta[2 * dy] = sat_short(cvRound(c0 * 2048));
+        ibeta[2 * dy + 1] = sat_short(cvRound(c1 * 2048));
+    }
+    std::vector<int> H0(dw), H1(dw);
+    auto hresize = [&](const uint8_t* S, int* D) {
+        for (int dx = 0; dx < dw; dx++) {
+            int sx = xofs[dx];
+            if (dx < xmax) D[dx] = S[sx] * ialpha[2 * dx] + S[sx + 1] * ialpha[2 * dx + 1];
+            else D[dx] = S[sx] * 2048;
+        }
+    };
+    for (int dy = 0; dy < dh; dy++) {
+        int sy0 = std::min(std::max(yofs[dy], 0), sh - 1);
+        int sy1 = std::min(std::max(yofs[dy] + 1, 0), sh - 1);
+        hresize(src.row(sy0), H0.data());
+        hresize(src.row(sy1), H1.data());
+        int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
+        uint8_t* D = dst.row(dy);
+        for (int x = 0; x < dw; x++) {
+            if (flags & ORACLE_RESIZE_GENERIC)
+                D[x] = sat_u8((b0 * H0[x] + b1 * H1[x] + (1 << 21)) >> 22);
+            else
+                D[x] = (uint8_t)((((b0 * (H0[x] >> 4)) >> 16) + ((b1 * (H1[x] >> 4)) >> 16) + 2) >> 2);
+        }
+    }
+}
+
+/* ---------------- GaussianBlur(7x7, sigma 2, REFLECT_101), 8U (Appendix A.2) ---------------- */
+void gaussian_kernel_q8(int k[7]) {
+    // getGaussianKernel(7, 2, CV_32F) then convertTo(CV_32S, 256) (cvRound half-even)
+    float cf[7];
+    double sum = 0;
+    const double sigmaX = 2.0, scale2X = -0.5 / (sigmaX * sigmaX);
+    for (int i = 0; i < 7; i++) {
+        double x = i - 3.0;
+        double t = std::exp(scale2X * x * x);
+        cf[i] = (float)t;
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 7; i++) cf[i] = (float)(cf[i] * sum);
+    for (int i = 0; i < 7; i++) k[i] = cvRound(cf[i] * 256.f);
+}
+
+inline int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+void gauss7_blur(const Img& src, Img& dst, int flags) {
+    int k[7];
+    gaussian_kernel_q8(k);
+    const int W = src.w, H = src.h;
+    std::vector<int> R((size_t)W * H);
+    for (int y = 0; y < H; y++) {             // RowFilter<uchar,int>: exact integer
+        const uint8_t* s = src.row(y);
+        int* r = &R[(size_t)y * W];
+        for (int x = 0; x < W; x++) {
+            int acc = 0;
+            for (int j = 0; j < 7; j++) acc += k[j] * s[reflect101(x + j - 3, W)];
+            r[x] = acc;
+        }
+    }
+    dst.create(W, H);
+    const int xsimd = W & ~3;                 // SymmColumnVec_32s8u covers multiples of 4
+    for (int y = 0; y < H; y++) {
+        uint8_t* o = dst.row(y);
+        for (int x = 0; x < W; x++) {
+            int S = 0;
+            for (int i = 0; i < 7; i++) S += k[i] * R[(size_t)reflect101(y + i - 3, H) * W + x];
+            int q = S >> 16, rem = S & 0xFFFF, v;
+            if (x < xsimd && !(flags & ORACLE_BLUR_ALL_HALFUP))
+                v = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));   // _mm_cvtps_epi32
+            else
+                v = (S + 32768) >> 16;                                       // FixedPtCastEx
+            o[x] = sat_u8(v);
+        }
+    }
+}
+
+/* ---------------- cv::FAST 9/16 with NMS (OpenCV 3.2 fast.cpp FAST_t; Appendix A.3) --------- */
+int corner_score16(const uint8_t* ptr, const int pixel[25], int threshold) {
+    const int K = 8, N = K * 3 + 1;
+    int v = ptr[0];
+    short d[N];
+    for (int k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = std::min((int)d[k + 1], (int)d[k + 2]);
+        a = std::min(a, (int)d[k + 3]);
+        if (a <= a0) continue;
+        a = std::min(a, (int)d[k + 4]);
+        a = std::min(a, (int)d[k + 5]);
+        a = std::min(a, (int)d[k + 6]);
+        a = std::min(a, (int)d[k + 7]);
+        a = std::min(a, (int)d[k + 8]);
+        a0 = std::max(a0, std::min(a, (int)d[k]));
+        a0 = std::max(a0, std::min(a, (int)d[k + 9]));
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = std::max((int)d[k + 1], (int)d[k + 2]);
+        b = std::max(b, (int)d[k + 3]);
+        b = std::max(b, (int)d[k + 4]);
+        b = std::max(b, (int)d[k + 5]);
+        if (b >= b0) continue;
+        b = std::max(b, (int)d[k + 6]);
+        b = std::max(b, (int)d[k + 7]);
+        b = std::max(b, (int)d[k + 8]);
+        b0 = std::min(b0, std::max(b, (int)d[k]));
+        b0 = std::min(b0, std::max(b, (int)d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+struct Corner { int x, y, score; };
+
+// FAST on an image ROI (base points at ROI(0,0)); emits (x, y, score) in detection order.
+void fast9_roi(const uint8_t* base, int step, int rows, int cols, int threshold, std::vector<Corner>& out) {
+    out.clear();
+    const int K = 8, N = 25;
+    static const int offs[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                                    {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+    int pixel[25];
+    for (int k = 0; k < 16; k++) pixel[k] = offs[k][0] + offs[k][1] * step;
+    for (int k = 16; k < 25; k++) pixel[k] = pixel[k - 16];
+    threshold = std::min(std::max(threshold, 0), 255);
+    uint8_t tab[512];
+    for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+    if (cols <= 0 || rows <= 0) return;
+    std::vector<uint8_t> bufv((size_t)cols * 3, 0);
+    std::vector<int> cpv((size_t)(cols + 1) * 3, 0);
+    uint8_t* buf[3] = {bufv.data(), bufv.data() + cols, bufv.data() + 2 * cols};
+    int* cpbuf[3] = {cpv.data() + 1, cpv.data() + (cols + 1) + 1, cpv.data() + 2 * (cols + 1) + 1};
+    for (int i = 3; i < rows - 2; i++) {
+        const uint8_t* ptr = base + (size_t)i * step + 3;
+        uint8_t* curr = buf[(i - 3) % 3];
+        int* cornerpos = cpbuf[(i - 3) % 3];
+        std::memset(curr, 0, cols);
+        int ncorners = 0;
+        if (i < rows - 3) {
+            for (int j = 3; j < cols - 3; j++, ptr++) {
+                int v = ptr[0];
+                const uint8_t* t = tab - v + 255;
+                int d = t[ptr[pixel[0]]] | t[ptr[pixel[8]]];
+                if (d == 0) continue;
+                d &= t[ptr[pixel[2]]] | t[ptr[pixel[10]]];
+                d &= t[ptr[pixel[4]]] | t[ptr[pixel[12]]];
+                d &= t[ptr[pixel[6]]] | t[ptr[pixel[14]]];
+                if (d == 0) continue;
+                d &= t[ptr[pixel[1]]] | t[ptr[pixel[9]]];
+                d &= t[ptr[pixel[3]]] | t[ptr[pixel[11]]];
+                d &= t[ptr[pixel[5]]] | t[ptr[pixel[13]]];
+                d &= t[ptr[pixel[7]]] | t[ptr[pixel[15]]];
+                if (d & 1) {
+                    int vt = v - threshold, count = 0;
+                    for (int k = 0; k < N; k++) {
+                        int x = ptr[pixel[k]];
+                        if (x < vt) {
+                            if (++count > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else count = 0;
+                    }
+                }
+                if (d & 2) {
+                    int vt = v + threshold, count = 0;
+                    for (int k = 0; k < N; k++) {
+                        int x = ptr[pixel[k]];
+                        if (x > vt) {
+                            if (++count > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else count = 0;
+                    }
+                }
+            }
+        }
+        cornerpos[-1] = ncorners;
+        if (i == 3) continue;
+        const uint8_t* prev = buf[(i - 4 + 3) % 3];
+        const uint8_t* pprev = buf[(i - 5 + 3) % 3];
+        cornerpos = cpbuf[(i - 4 + 3) % 3];
+        ncorners = cornerpos[-1];
+        for (int k = 0; k < ncorners; k++) {
+            int j = cornerpos[k];
+            int score = prev[j];
+            if (score > prev[j + 1] && score > prev[j - 1] && score > pprev[j - 1] && score > pprev[j] &&
+                score > pprev[j + 1] && score > curr[j - 1] && score > curr[j] && score > curr[j + 1])
+                out.push_back({j, i - 1, score});
+        }
+    }
+}
+
+/* ---------------- fastAtan2 (OpenCV 3.2 mathfuncs; Appendix A.4) ---------------- */
+const float atan2_p1 = 0.9997878412794807f * (float)(180 / M_PI);
+const float atan2_p3 = -0.3258083974640975f * (float)(180 / M_PI);
+const float atan2_p5 = 0.1555786518463281f * (float)(180 / M_PI);
+const float atan2_p7 = -0.04432655554792128f * (float)(180 / M_PI);
+
+float fastAtan2(float y, float x) {
+    float ax = std::abs(x), ay = std::abs(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((atan2_p7 * c2 + atan2_p5) * c2 + atan2_p3) * c2 + atan2_p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((atan2_p7 * c2 + atan2_p5) * c2 + atan2_p3) * c2 + atan2_p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+/* IC_Angle  ORBextractor.cc:77-104 */
+float IC_Angle(const Img& image, float px, float py, const std::vector<int>& u_max) {
+    int m_01 = 0, m_10 = 0;
+    const uint8_t* center = image.row(cvRound(py)) + cvRound(px);
+    for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * center[u];
+    int step = image.w;
+    for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+        int v_sum = 0;
+        int d = u_max[v];
+        for (int u = -d; u <= d; ++u) {
+            int val_plus = center[u + v * step], val_minus = center[u - v * step];
+            v_sum += (val_plus - val_minus);
+            m_10 += u * (val_plus + val_minus);
+        }
+        m_01 += v * v_sum;
+    }
+    return fastAtan2((float)m_01, (float)m_10);
+}
+
+/* Pinned trig: the reference calls glibc cosf/sinf (:113), whose
+ * last-bit behaviour differs across glibc ifunc variants; the restatement and the HIP path both
+ * use the correctly-rounded value, computed in double and rounded once. */
+inline float cos_cr(float a) { return (float)std::cos((double)a); }
+inline float sin_cr(float a) { return (float)std::sin((double)a); }
+
+const float factorPI = (float)(M_PI / 180.f);   // ORBextractor.cc:107
+
+/* computeOrbDescriptor  ORBextractor.cc:108-147 */
+void computeOrbDescriptor(const KP& kpt, const Img& img, const int* pattern, uint8_t* desc) {
+    float angle = (float)kpt.angle * factorPI;
+    float a = cos_cr(angle), b = sin_cr(angle);
+    const uint8_t* center = img.row(cvRound(kpt.y)) + cvRound(kpt.x);
+    const int step = img.w;
+    auto GET = [&](const int* p, int idx) -> int {
+        float px = (float)p[2 * idx], py = (float)p[2 * idx + 1];
+        float t1 = px * b, t2 = py * a, t3 = px * a, t4 = py * b;
+        return center[cvRound(t1 + t2) * step + cvRound(t3 - t4)];
+    };
+    for (int i = 0; i < 32; ++i, pattern += 32) {
+        int val = 0;
+        for (int k = 0; k < 8; k++) {
+            int t0 = GET(pattern, 2 * k), t1 = GET(pattern, 2 * k + 1);
+            val |= (t0 < t1) << k;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+/* ---------------- ExtractorNode / DistributeOctTree  ORBextractor.cc:481-763 ---------------- */
+struct Node {
+    std::vector<KP> vKeys;
+    int ULx = 0, ULy = 0, URx = 0, URy = 0, BLx = 0, BLy = 0, BRx = 0, BRy = 0;
+    std::list<Node>::iterator lit;
+    bool bNoMore = false;
+    long seq = -1;   // creation sequence: the pinned stand-in for the node's heap address (:684)
+
+    void DivideNode(Node& n1, Node& n2, Node& n3, Node& n4) const {   // :481-537
+        const int halfX = (int)std::ceil(static_cast<float>(URx - ULx) / 2);
+        const int halfY = (int)std::ceil(static_cast<float>(BRy - ULy) / 2);
+        n1.ULx = ULx; n1.ULy = ULy;
+        n1.URx = ULx + halfX; n1.URy = ULy;
+        n1.BLx = ULx; n1.BLy = ULy + halfY;
+        n1.BRx = ULx + halfX; n1.BRy = ULy + halfY;
+        n1.vKeys.reserve(vKeys.size());
+        n2.ULx = n1.URx; n2.ULy = n1.URy;
+        n2.URx = URx; n2.URy = URy;
+        n2.BLx = n1.BRx; n2.BLy = n1.BRy;
+        n2.BRx = URx; n2.BRy = ULy + halfY;
+        n2.vKeys.reserve(vKeys.size());
+        n3.ULx = n1.BLx; n3.ULy = n1.BLy;
+        n3.URx = n1.BRx; n3.URy = n1.BRy;
+        n3.BLx = BLx; n3.BLy = BLy;
+        n3.BRx = n1.BRx; n3.BRy = BLy;
+        n3.vKeys.reserve(vKeys.size());
+        n4.ULx = n3.URx; n4.ULy = n3.URy;
+        n4.URx = n2.BRx; n4.URy = n2.BRy;
+        n4.BLx = n3.BRx; n4.BLy = n3.BRy;
+        n4.BRx = BRx; n4.BRy = BRy;
+        n4.vKeys.reserve(vKeys.size());
+        for (size_t i = 0; i < vKeys.size(); i++) {
+            const KP& kp = vKeys[i];
+            if (kp.x < n1.URx) {
+                if (kp.y < n1.BRy) n1.vKeys.push_back(kp);
+                else n3.vKeys.push_back(kp);
+            } else if (kp.y < n1.BRy) n2.vKeys.push_back(kp);
+            else n4.vKeys.push_back(kp);
+        }
+        if (n1.vKeys.size() == 1) n1.bNoMore = true;
+        if (n2.vKeys.size() == 1) n2.bNoMore = true;
+        if (n3.vKeys.size() == 1) n3.bNoMore = true;
+        if (n4.vKeys.size() == 1) n4.bNoMore = true;
+    }
+};
+
+std::vector<KP> DistributeOctTree(const std::vector<KP>& vToDistributeKeys, int minX, int maxX, int minY,
+                                  int maxY, int N, bool reverseTie) {
+    const int nIni = (int)std::round(static_cast<float>(maxX - minX) / (maxY - minY));   // :543
+    const float hX = static_cast<float>(maxX - minX) / nIni;
+    std::list<Node> lNodes;
+    long seqCounter = 0;
+    std::vector<Node*> vpIniNodes(nIni);
+    for (int i = 0; i < nIni; i++) {
+        Node ni;
+        ni.ULx = (int)(hX * static_cast<float>(i)); ni.ULy = 0;
+        ni.URx = (int)(hX * static_cast<float>(i + 1)); ni.URy = 0;
+        ni.BLx = ni.ULx; ni.BLy = maxY - minY;
+        ni.BRx = ni.URx; ni.BRy = maxY - minY;
+        ni.vKeys.reserve(vToDistributeKeys.size());
+        ni.seq = seqCounter++;
+        lNodes.push_back(ni);
+        vpIniNodes[i] = &lNodes.back();
+    }
+    for (size_t i = 0; i < vToDistributeKeys.size(); i++) {
+        const KP& kp = vToDistributeKeys[i];
+        vpIniNodes[(size_t)(kp.x / hX)]->vKeys.push_back(kp);
+    }
+    auto lit = lNodes.begin();
+    while (lit != lNodes.end()) {
+        if (lit->vKeys.size() == 1) { lit->bNoMore = true; lit++; }
+        else if (lit->vKeys.empty()) lit = lNodes.erase(lit);
+        else lit++;
+    }
+    bool bFinish = false;
+    std::vector<std::pair<int, Node*>> vSizeAndPointerToNode;
+    vSizeAndPointerToNode.reserve(lNodes.size() * 4);
+    auto push_child = [&](Node& c, std::vector<std::pair<int, Node*>>& vec, int* nToExpand) {
+        if (c.vKeys.size() > 0) {
+            c.seq = seqCounter++;
+            lNodes.push_front(c);
+            if (c.vKeys.size() > 1) {
+                if (nToExpand) (*nToExpand)++;
+                vec.push_back(std::make_pair((int)c.vKeys.size(), &lNodes.front()));
+                lNodes.front().lit = lNodes.begin();
+            }
+        }
+    };
+    while (!bFinish) {                                                            // :594-739
+        int prevSize = (int)lNodes.size();
+        lit = lNodes.begin();
+        int nToExpand = 0;
+        vSizeAndPointerToNode.clear();
+        while (lit != lNodes.end()) {
+            if (lit->bNoMore) { lit++; continue; }
+            Node n1, n2, n3, n4;
+            lit->DivideNode(n1, n2, n3, n4);
+            push_child(n1, vSizeAndPointerToNode, &nToExpand);
+            push_child(n2, vSizeAndPointerToNode, &nToExpand);
+            push_child(n3, vSizeAndPointerToNode, &nToExpand);
+            push_child(n4, vSizeAndPointerToNode, &nToExpand);
+            lit = lNodes.erase(lit);
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+            bFinish = true;
+        } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+            while (!bFinish) {
+                prevSize = (int)lNodes.size();
+                std::vector<std::pair<int, Node*>> vPrev = vSizeAndPointerToNode;
+                vSizeAndPointerToNode.clear();
+                // :684 sort(pair<int,ExtractorNode*>) — pointer tie pinned to creation sequence
+                std::sort(vPrev.begin(), vPrev.end(),
+                          [reverseTie](const std::pair<int, Node*>& a, const std::pair<int, Node*>& b) {
+                              if (a.first != b.first) return a.first < b.first;
+                              return reverseTie ? a.second->seq > b.second->seq : a.second->seq < b.second->seq;
+                          });
+                for (int j = (int)vPrev.size() - 1; j >= 0; j--) {
+                    Node n1, n2, n3, n4;
+                    vPrev[j].second->DivideNode(n1, n2, n3, n4);
+                    push_child(n1, vSizeAndPointerToNode, nullptr);
+                    push_child(n2, vSizeAndPointerToNode, nullptr);
+                    push_child(n3, vSizeAndPointerToNode, nullptr);
+                    push_child(n4, vSizeAndPointerToNode, nullptr);
+                    lNodes.erase(vPrev[j].second->lit);
+                    if ((int)lNodes.size() >= N) break;
+                }
+                if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
+            }
+        }
+    }
+    std::vector<KP> vResultKeys;                                                   // :741-762
+    for (auto it = lNodes.begin(); it != lNodes.end(); it++) {
+        std::vector<KP>& vNodeKeys = it->vKeys;
+        KP* pKP = &vNodeKeys[0];
+        float maxResponse = pKP->response;
+        for (size_t k = 1; k < vNodeKeys.size(); k++)
+            if (vNodeKeys[k].response > maxResponse) { pKP = &vNodeKeys[k]; maxResponse = vNodeKeys[k].response; }
+        vResultKeys.push_back(*pKP);
+    }
+    return vResultKeys;
+}
+
+/* ---------------- the extractor object (ORBextractor.cc:410-470, 765-853, 1043-1132) ------- */
+struct Extractor {
+    int nfeatures, nlevels, iniThFAST, minThFAST, flags;
+    double scaleFactor;   // ORBextractor.h:98 stores it as double
+    std::vector<float> mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2;
+    std::vector<int> mnFeaturesPerLevel, umax;
+    std::vector<Img> pyr, blurred;
+    std::vector<std::vector<KP>> cand, lvlKps;
+    std::vector<KP> outKps;
+    std::vector<uint8_t> outDesc;
+
+    Extractor(int nf, float sf, int nl, int ini, int mn, int fl)
+        : nfeatures(nf), nlevels(nl), iniThFAST(ini), minThFAST(mn), flags(fl), scaleFactor(sf) {
+        mvScaleFactor.resize(nlevels);
+        mvLevelSigma2.resize(nlevels);
+        mvScaleFactor[0] = 1.0f;
+        mvLevelSigma2[0] = 1.0f;
+        for (int i = 1; i < nlevels; i++) {
+            mvScaleFactor[i] = (float)(mvScaleFactor[i - 1] * scaleFactor);
+            mvLevelSigma2[i] = mvScaleFactor[i] * mvScaleFactor[i];
+        }
+        mvInvScaleFactor.resize(nlevels);
+        mvInvLevelSigma2.resize(nlevels);
+        for (int i = 0; i < nlevels; i++) {
+            mvInvScaleFactor[i] = 1.0f / mvScaleFactor[i];
+            mvInvLevelSigma2[i] = 1.0f / mvLevelSigma2[i];
+        }
+        mnFeaturesPerLevel.resize(nlevels);
+        float factor = (float)(1.0f / scaleFactor);
+        float nDesiredFeaturesPerScale =
+            nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+        int sumFeatures = 0;
+        for (int level = 0; level < nlevels - 1; level++) {
+            mnFeaturesPerLevel[level] = cvRound(nDesiredFeaturesPerScale);
+            sumFeatures += mnFeaturesPerLevel[level];
+            nDesiredFeaturesPerScale *= factor;
+        }
+        mnFeaturesPerLevel[nlevels - 1] = std::max(nfeatures - sumFeatures, 0);
+        umax.resize(HALF_PATCH_SIZE + 1);
+        int v, v0, vmax = cvFloor(HALF_PATCH_SIZE * std::sqrt(2.f) / 2 + 1);
+        int vmin = cvCeil(HALF_PATCH_SIZE * std::sqrt(2.f) / 2);
+        const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+        for (v = 0; v <= vmax; ++v) umax[v] = cvRound(std::sqrt(hp2 - v * v));
+        for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+    }
+
+    bool ComputePyramid(const Img& image) {                                        // :1107-1132
+        pyr.assign(nlevels, Img());
+        for (int level = 0; level < nlevels; ++level) {
+            float scale = mvInvScaleFactor[level];
+            int w = cvRound((float)image.w * scale), h = cvRound((float)image.h * scale);
+            if (w < 2 || h < 2) return false;
+            if (level != 0) resize_linear_8u(pyr[level - 1], pyr[level], w, h, flags);
+            else pyr[0] = image;
+        }
+        return true;
+    }
+
+    bool ComputeKeyPointsOctTree() {                                                // :765-853
+        cand.assign(nlevels, {});
+        lvlKps.assign(nlevels, {});
+        const float W = 30;
+        std::vector<Corner> vKeysCell;
+        for (int level = 0; level < nlevels; ++level) {
+            const Img& im = pyr[level];
+            const int minBorderX = EDGE_THRESHOLD - 3;
+            const int minBorderY = minBorderX;
+            const int maxBorderX = im.w - EDGE_THRESHOLD + 3;
+            const int maxBorderY = im.h - EDGE_THRESHOLD + 3;
+            std::vector<KP>& vToDistributeKeys = cand[level];
+            const float width = (float)(maxBorderX - minBorderX);
+            const float height = (float)(maxBorderY - minBorderY);
+            const int nCols = (int)(width / W);
+            const int nRows = (int)(height / W);
+            if (nCols <= 0 || nRows <= 0) return false;   // reference: division by zero (UB)
+            const int wCell = (int)std::ceil(width / nCols);
+            const int hCell = (int)std::ceil(height / nRows);
+            for (int i = 0; i < nRows; i++) {
+                const float iniY = (float)(minBorderY + i * hCell);
+                float maxY = iniY + hCell + 6;
+                if (iniY >= maxBorderY - 3) continue;
+                if (maxY > maxBorderY) maxY = (float)maxBorderY;
+                for (int j = 0; j < nCols; j++) {
+                    const float iniX = (float)(minBorderX + j * wCell);
+                    float maxX = iniX + wCell + 6;
+                    if (iniX >= maxBorderX - 6) continue;
+                    if (maxX > maxBorderX) maxX = (float)maxBorderX;
+                    const int y0 = (int)iniY, y1 = (int)maxY, x0 = (int)iniX, x1 = (int)maxX;
+                    const uint8_t* roi = im.row(y0) + x0;
+                    fast9_roi(roi, im.w, y1 - y0, x1 - x0, iniThFAST, vKeysCell);
+                    if (vKeysCell.empty()) fast9_roi(roi, im.w, y1 - y0, x1 - x0, minThFAST, vKeysCell);
+                    for (const Corner& c : vKeysCell) {
+                        KP kp{(float)c.x, (float)c.y, 7.f, -1.f, (float)c.score, 0, -1};
+                        kp.x += j * wCell;
+                        kp.y += i * hCell;
+                        vToDistributeKeys.push_back(kp);
+                    }
+                }
+            }
+            if ((float)(maxBorderX - minBorderX) / (maxBorderY - minBorderY) < 0.5f) return false;  // nIni==0
+            std::vector<KP>& keypoints = lvlKps[level];
+            keypoints = DistributeOctTree(vToDistributeKeys, minBorderX, maxBorderX, minBorderY, maxBorderY,
+                                          mnFeaturesPerLevel[level], (flags & ORACLE_TIE_REVERSE_SEQ) != 0);
+            const int scaledPatchSize = (int)(PATCH_SIZE * mvScaleFactor[level]);
+            for (KP& kp : keypoints) {
+                kp.x += minBorderX;
+                kp.y += minBorderY;
+                kp.octave = level;
+                kp.size = (float)scaledPatchSize;
+            }
+        }
+        for (int level = 0; level < nlevels; ++level)                             // :851-852
+            for (KP& kp : lvlKps[level]) kp.angle = IC_Angle(pyr[level], kp.x, kp.y, umax);
+        return true;
+    }
+
+    int run(const Img& image) {                                                     // :1043-1105
+        if (image.w == 0 || image.h == 0) return -1;
+        if (!ComputePyramid(image)) return -2;
+        if (!ComputeKeyPointsOctTree()) return -2;
+        int nkeypoints = 0;
+        for (int level = 0; level < nlevels; ++level) nkeypoints += (int)lvlKps[level].size();
+        outKps.clear();
+        outDesc.assign((size_t)nkeypoints * 32, 0);
+        blurred.assign(nlevels, Img());
+        int offset = 0;
+        for (int level = 0; level < nlevels; ++level) {
+            std::vector<KP> keypoints = lvlKps[level];
+            const int nkl = (int)keypoints.size();
+            if (nkl == 0) continue;
+            gauss7_blur(pyr[level], blurred[level], flags);
+            for (int i = 0; i < nkl; i++)
+                computeOrbDescriptor(keypoints[i], blurred[level], kPattern, &outDesc[(size_t)(offset + i) * 32]);
+            offset += nkl;
+            if (level != 0) {
+                float scale = mvScaleFactor[level];
+                for (KP& kp : keypoints) { kp.x *= scale; kp.y *= scale; }
+            }
+            outKps.insert(outKps.end(), keypoints.begin(), keypoints.end());
+        }
+        return nkeypoints;
+    }
+};
+
+/* ---------------- matcher helpers (ORBmatcher.cc) ---------------- */
+const int TH_LOW = 50, HISTO_LENGTH = 30;   // ORBmatcher.cc:37-39 (TH_HIGH=100 unused on this path)
+
+int DescriptorDistance(const uint8_t* a, const uint8_t* b) {   // ORBmatcher.cc:1647-1663
+    int32_t pa[8], pb[8];
+    std::memcpy(pa, a, 32);
+    std::memcpy(pb, b, 32);
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        unsigned int v = (unsigned)pa[i] ^ (unsigned)pb[i];
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+    }
+    return dist;
+}
+
+void ComputeThreeMaxima(const std::vector<int>* histo, const int L, int& ind1, int& ind2, int& ind3) {  // :1601-1642
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = (int)histo[i].size();
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+int rot_bin(float a1, float a2) {   // e.g. ORBmatcher.cc:236-243
+    const float factor = 1.0f / HISTO_LENGTH;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)std::round(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+// Iterate nodes present in both FeatureVectors in ascending id order (the std::map merge with
+// lower_bound jumps of ORBmatcher.cc:175-264 visits exactly these pairs in this order).
+template <class F>
+void for_common_nodes(const OracleFeatVec& a, const OracleFeatVec& b, F f) {
+    int i = 0, j = 0;
+    while (i < a.nnodes && j < b.nnodes) {
+        if (a.node_ids[i] == b.node_ids[j]) { f(i, j); i++; j++; }
+        else if (a.node_ids[i] < b.node_ids[j]) i++;
+        else j++;
+    }
+}
+
+void cull_rotation(std::vector<int>* rotHist, std::vector<int>& matches, int& nmatches) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    ComputeThreeMaxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        if (i == ind1 || i == ind2 || i == ind3) continue;
+        for (size_t j = 0; j < rotHist[i].size(); j++) {
+            if (matches[rotHist[i][j]] >= 0) { matches[rotHist[i][j]] = -1; nmatches--; }
+        }
+    }
+}
+
+const float* CheckF(const float* F, int r, int c) { return &F[r * 3 + c]; }
+
+bool CheckDistEpipolarLine(const KP& kp1, const KP& kp2, const float* F12, const float* sigma2) {  // :140-157
+    const float a = kp1.x * *CheckF(F12, 0, 0) + kp1.y * *CheckF(F12, 1, 0) + *CheckF(F12, 2, 0);
+    const float b = kp1.x * *CheckF(F12, 0, 1) + kp1.y * *CheckF(F12, 1, 1) + *CheckF(F12, 2, 1);
+    const float c = kp1.x * *CheckF(F12, 0, 2) + kp1.y * *CheckF(F12, 1, 2) + *CheckF(F12, 2, 2);
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * sigma2[kp2.octave];
+}
+
+}  // namespace
+
+/* ============================== extern "C" API ============================== */
+extern "C" {
+
+void* oracle_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int flags) {
+    if (nlevels < 1 || nfeatures < 0) return nullptr;
+    return new Extractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, flags);
+}
+void oracle_destroy(void* h) { delete (Extractor*)h; }
+
+int oracle_run(void* h, const uint8_t* img, int w, int hgt, int stride) {
+    Extractor* e = (Extractor*)h;
+    if (!img || w <= 0 || hgt <= 0) return -1;
+    Img im;
+    im.create(w, hgt);
+    for (int y = 0; y < hgt; y++) std::memcpy(im.row(y), img + (size_t)y * stride, w);
+    return e->run(im);
+}
+
+int oracle_level_size(void* h, int level, int* w, int* hgt) {
+    Extractor* e = (Extractor*)h;
+    if (level < 0 || level >= (int)e->pyr.size()) return -1;
+    *w = e->pyr[level].w;
+    *hgt = e->pyr[level].h;
+    return 0;
+}
+int oracle_get_level(void* h, int level, uint8_t* out) {
+    Extractor* e = (Extractor*)h;
+    if (level < 0 || level >= (int)e->pyr.size()) return -1;
+    std::memcpy(out, e->pyr[level].d.data(), e->pyr[level].d.size());
+    return 0;
+}
+int oracle_get_blurred(void* h, int level, uint8_t* out) {
+    Extractor* e = (Extractor*)h;
+    if (level < 0 || level >= (int)e->pyr.size()) return -1;
+    Img b;
+    gauss7_blur(e->pyr[level], b, e->flags);
+    std::memcpy(out, b.d.data(), b.d.size());
+    return 0;
+}
+int oracle_get_candidates(void* h, int level, int* out, int cap) {
+    Extractor* e = (Extractor*)h;
+    if (level < 0 || level >= (int)e->cand.size()) return -1;
+    const auto& c = e->cand[level];
+    if ((int)c.size() > cap) return -(int)c.size() - 1;
+    for (size_t i = 0; i < c.size(); i++) {
+        out[3 * i] = (int)c[i].x;
+        out[3 * i + 1] = (int)c[i].y;
+        out[3 * i + 2] = (int)c[i].response;
+    }
+    return (int)c.size();
+}
+int oracle_get_level_keypoints(void* h, int level, OracleKeyPoint* out, int cap) {
+    Extractor* e = (Extractor*)h;
+    if (level < 0 || level >= (int)e->lvlKps.size()) return -1;
+    const auto& k = e->lvlKps[level];
+    if ((int)k.size() > cap) return -(int)k.size() - 1;
+    std::memcpy(out, k.data(), k.size() * sizeof(KP));
+    return (int)k.size();
+}
+int oracle_get_output(void* h, OracleKeyPoint* kps, uint8_t* desc, int cap) {
+    Extractor* e = (Extractor*)h;
+    int n = (int)e->outKps.size();
+    if (n > cap) return -n - 1;
+    std::memcpy(kps, e->outKps.data(), n * sizeof(KP));
+    std::memcpy(desc, e->outDesc.data(), (size_t)n * 32);
+    return n;
+}
+void oracle_tables(void* h, float* scale, float* invScale, float* sigma2, float* invSigma2, int* nPerLevel,
+                   int* umax16) {
+    Extractor* e = (Extractor*)h;
+    for (int i = 0; i < e->nlevels; i++) {
+        scale[i] = e->mvScaleFactor[i];
+        invScale[i] = e->mvInvScaleFactor[i];
+        sigma2[i] = e->mvLevelSigma2[i];
+        invSigma2[i] = e->mvInvLevelSigma2[i];
+        nPerLevel[i] = e->mnFeaturesPerLevel[i];
+    }
+    for (int i = 0; i < 16; i++) umax16[i] = e->umax[i];
+}
+
+float oracle_fast_atan2(float y, float x) { return fastAtan2(y, x); }
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return DescriptorDistance(a, b); }
+void oracle_three_maxima(const int* sizes, int L, int* i1, int* i2, int* i3) {
+    std::vector<std::vector<int>> h(L);
+    for (int i = 0; i < L; i++) h[i].resize(sizes[i]);
+    *i1 = *i2 = *i3 = -1;
+    ComputeThreeMaxima(h.data(), L, *i1, *i2, *i3);
+}
+int oracle_rot_bin(float a1, float a2) { return rot_bin(a1, a2); }
+int oracle_fast_roi(const uint8_t* roi, int w, int h, int stride, int th, int* out, int cap) {
+    std::vector<Corner> v;
+    fast9_roi(roi, stride, h, w, th, v);
+    if ((int)v.size() > cap) return -(int)v.size() - 1;
+    for (size_t i = 0; i < v.size(); i++) {
+        out[3 * i] = v[i].x;
+        out[3 * i + 1] = v[i].y;
+        out[3 * i + 2] = v[i].score;
+    }
+    return (int)v.size();
+}
+void oracle_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh, int flags) {
+    Img s, d;
+    s.create(sw, sh);
+    std::memcpy(s.d.data(), src, (size_t)sw * sh);
+    resize_linear_8u(s, d, dw, dh, flags);
+    std::memcpy(dst, d.d.data(), (size_t)dw * dh);
+}
+void oracle_blur(const uint8_t* src, int w, int h, uint8_t* dst, int flags) {
+    Img s, d;
+    s.create(w, h);
+    std::memcpy(s.d.data(), src, (size_t)w * h);
+    gauss7_blur(s, d, flags);
+    std::memcpy(dst, d.d.data(), (size_t)w * h);
+}
+void oracle_pattern(int* out) { std::memcpy(out, kPattern, sizeof(kPattern)); }
+
+double oracle_time_extract(const uint8_t* frames, int nframes, int w, int h, int nfeatures, float scaleFactor,
+                           int nlevels, int iniTh, int minTh, int nthreads, int iters, long long* total_kps) {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<Img> imgs(nframes);
+    for (int f = 0; f < nframes; f++) {
+        imgs[f].create(w, h);
+        std::memcpy(imgs[f].d.data(), frames + (size_t)f * w * h, (size_t)w * h);
+    }
+    std::atomic<long long> kps{0};
+    std::atomic<int> next{0};
+    const int total = nframes * iters;
+    auto t0 = std::chrono::steady_clock::now();
+    auto worker = [&]() {
+        Extractor e(nfeatures, scaleFactor, nlevels, iniTh, minTh, 0);   // one instance per thread
+        for (;;) {
+            int k = next.fetch_add(1);
+            if (k >= total) break;
+            int n = e.run(imgs[k % nframes]);
+            if (k < nframes) kps += n;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++) th.emplace_back(worker);
+    for (auto& t : th) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    if (total_kps) *total_kps = kps.load();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+/* SearchByBoW(KF, F)  ORBmatcher.cc:159-288 */
+int oracle_search_by_bow_kf_f(float nnratio, int checkOri, int n_kf, const uint8_t* desc_kf, const float* angle_kf,
+                              const uint8_t* mp_kf, OracleFeatVec fv_kf, int n_f, const uint8_t* desc_f,
+                              const float* angle_f, OracleFeatVec fv_f, int* match_f) {
+    (void)n_kf;
+    std::vector<int> matches(n_f, -1);
+    int nmatches = 0;
+    std::vector<int> rotHist[HISTO_LENGTH];
+    for_common_nodes(fv_kf, fv_f, [&](int a, int b) {
+        for (int iKF = fv_kf.offsets[a]; iKF < fv_kf.offsets[a + 1]; iKF++) {
+            const int realIdxKF = fv_kf.indices[iKF];
+            if (!mp_kf[realIdxKF]) continue;
+            const uint8_t* dKF = desc_kf + (size_t)realIdxKF * 32;
+            int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+            for (int iF = fv_f.offsets[b]; iF < fv_f.offsets[b + 1]; iF++) {
+                const int realIdxF = fv_f.indices[iF];
+                if (matches[realIdxF] >= 0) continue;
+                const int dist = DescriptorDistance(dKF, desc_f + (size_t)realIdxF * 32);
+                if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = realIdxF; }
+                else if (dist < bestDist2) bestDist2 = dist;
+            }
+            if (bestDist1 <= TH_LOW) {
+                if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+                    matches[bestIdxF] = realIdxKF;
+                    if (checkOri) rotHist[rot_bin(angle_kf[realIdxKF], angle_f[bestIdxF])].push_back(bestIdxF);
+                    nmatches++;
+                }
+            }
+        }
+    });
+    if (checkOri) cull_rotation(rotHist, matches, nmatches);
+    std::memcpy(match_f, matches.data(), n_f * sizeof(int));
+    return nmatches;
+}
+
+/* SearchByBoW(KF1, KF2)  ORBmatcher.cc:522-655 */
+int oracle_search_by_bow_kf_kf(float nnratio, int checkOri, int n1, const uint8_t* desc1, const float* angle1,
+                               const uint8_t* mp1, OracleFeatVec fv1, int n2, const uint8_t* desc2,
+                               const float* angle2, const uint8_t* mp2, OracleFeatVec fv2, int* match12) {
+    std::vector<int> matches(n1, -1);
+    std::vector<char> vbMatched2(n2, 0);
+    int nmatches = 0;
+    std::vector<int> rotHist[HISTO_LENGTH];
+    for_common_nodes(fv1, fv2, [&](int a, int b) {
+        for (int i1 = fv1.offsets[a]; i1 < fv1.offsets[a + 1]; i1++) {
+            const int idx1 = fv1.indices[i1];
+            if (!mp1[idx1]) continue;
+            const uint8_t* d1 = desc1 + (size_t)idx1 * 32;
+            int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+            for (int i2 = fv2.offsets[b]; i2 < fv2.offsets[b + 1]; i2++) {
+                const int idx2 = fv2.indices[i2];
+                if (vbMatched2[idx2] || !mp2[idx2]) continue;
+                int dist = DescriptorDistance(d1, desc2 + (size_t)idx2 * 32);
+                if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdx2 = idx2; }
+                else if (dist < bestDist2) bestDist2 = dist;
+            }
+            if (bestDist1 < TH_LOW) {
+                if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+                    matches[idx1] = bestIdx2;
+                    vbMatched2[bestIdx2] = 1;
+                    if (checkOri) rotHist[rot_bin(angle1[idx1], angle2[bestIdx2])].push_back(idx1);
+                    nmatches++;
+                }
+            }
+        }
+    });
+    if (checkOri) cull_rotation(rotHist, matches, nmatches);
+    std::memcpy(match12, matches.data(), n1 * sizeof(int));
+    return nmatches;
+}
+
+/* SearchForTriangulation  ORBmatcher.cc:657-823 */
+int oracle_search_for_triangulation(int checkOri, int onlyStereo, int n1, const uint8_t* desc1,
+                                    const OracleKeyPoint* kps1_, const uint8_t* has_mp1, const float* uright1,
+                                    OracleFeatVec fv1, int n2, const uint8_t* desc2, const OracleKeyPoint* kps2_,
+                                    const uint8_t* has_mp2, const float* uright2, OracleFeatVec fv2, const float* F12,
+                                    float ex, float ey, const float* scaleFactors2, const float* levelSigma2_2,
+                                    int* pairs_out, int cap) {
+    const KP* kps1 = (const KP*)kps1_;
+    const KP* kps2 = (const KP*)kps2_;
+    std::vector<char> vbMatched2(n2, 0);   // never set in the reference (:738): kept for fidelity
+    std::vector<int> vMatches12(n1, -1);
+    int nmatches = 0;
+    std::vector<int> rotHist[HISTO_LENGTH];
+    for_common_nodes(fv1, fv2, [&](int a, int b) {
+        for (int i1 = fv1.offsets[a]; i1 < fv1.offsets[a + 1]; i1++) {
+            const int idx1 = fv1.indices[i1];
+            if (has_mp1[idx1]) continue;
+            const bool bStereo1 = uright1[idx1] >= 0;
+            if (onlyStereo && !bStereo1) continue;
+            const KP& kp1 = kps1[idx1];
+            const uint8_t* d1 = desc1 + (size_t)idx1 * 32;
+            int bestDist = TH_LOW, bestIdx2 = -1;
+            for (int i2 = fv2.offsets[b]; i2 < fv2.offsets[b + 1]; i2++) {
+                const int idx2 = fv2.indices[i2];
+                if (vbMatched2[idx2] || has_mp2[idx2]) continue;
+                const bool bStereo2 = uright2[idx2] >= 0;
+                if (onlyStereo && !bStereo2) continue;
+                const int dist = DescriptorDistance(d1, desc2 + (size_t)idx2 * 32);
+                if (dist > TH_LOW || dist > bestDist) continue;
+                const KP& kp2 = kps2[idx2];
+                if (!bStereo1 && !bStereo2) {
+                    const float distex = ex - kp2.x;
+                    const float distey = ey - kp2.y;
+                    if (distex * distex + distey * distey < 100 * scaleFactors2[kp2.octave]) continue;
+                }
+                if (CheckDistEpipolarLine(kp1, kp2, F12, levelSigma2_2)) { bestIdx2 = idx2; bestDist = dist; }
+            }
+            if (bestIdx2 >= 0) {
+                const KP& kp2 = kps2[bestIdx2];
+                vMatches12[idx1] = bestIdx2;
+                nmatches++;
+                if (checkOri) rotHist[rot_bin(kp1.angle, kp2.angle)].push_back(idx1);
+            }
+        }
+    });
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ComputeThreeMaxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (size_t j = 0; j < rotHist[i].size(); j++) { vMatches12[rotHist[i][j]] = -1; nmatches--; }
+        }
+    }
+    int np = 0;
+    for (int i = 0; i < n1; i++) {
+        if (vMatches12[i] < 0) continue;
+        if (np < cap) { pairs_out[2 * np] = i; pairs_out[2 * np + 1] = vMatches12[i]; }
+        np++;
+    }
+    return np;
+}
+
+/* SearchForInitialization (:405-520) / BirdviewMatch(const Frame&,...) (:1790-1899) */
+int oracle_window_match(float nnratio, int checkOri, int level0_only, int n1, const uint8_t* desc1,
+                        const OracleKeyPoint* kps1_, int n2, const uint8_t* desc2, const OracleKeyPoint* kps2_,
+                        const int* cand_off, const int* cand_idx, int* match12) {
+    const KP* kps1 = (const KP*)kps1_;
+    const KP* kps2 = (const KP*)kps2_;
+    int nmatches = 0;
+    std::vector<int> vnMatches12(n1, -1);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    std::vector<int> vMatchedDistance(n2, INT_MAX);
+    std::vector<int> vnMatches21(n2, -1);
+    for (int i1 = 0; i1 < n1; i1++) {
+        const KP kp1 = kps1[i1];
+        if (level0_only && kp1.octave > 0) continue;
+        if (cand_off[i1 + 1] == cand_off[i1]) continue;
+        const uint8_t* d1 = desc1 + (size_t)i1 * 32;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int c = cand_off[i1]; c < cand_off[i1 + 1]; c++) {
+            const int i2 = cand_idx[c];
+            int dist = DescriptorDistance(d1, desc2 + (size_t)i2 * 32);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        }
+        if (bestDist <= TH_LOW) {
+            if (bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) { vnMatches12[vnMatches21[bestIdx2]] = -1; nmatches--; }
+                vnMatches12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (checkOri) rotHist[rot_bin(kps1[i1].angle, kps2[bestIdx2].angle)].push_back(i1);
+            }
+        }
+    }
+    if (checkOri) cull_rotation(rotHist, vnMatches12, nmatches);
+    std::memcpy(match12, vnMatches12.data(), n1 * sizeof(int));
+    return nmatches;
+}
+
+/* Frame::GetFeaturesInArea  Frame.cc:494-547 over the grid of Frame.cc:378-392, 549-560 */
+int oracle_features_in_area(int n, const OracleKeyPoint* kpsUn_, float mnMinX, float mnMaxX, float mnMinY,
+                            float mnMaxY, float x, float y, float r, int minLevel, int maxLevel, int* out, int cap) {
+    const KP* kpsUn = (const KP*)kpsUn_;
+    const int COLS = 64, ROWS = 48;   // Frame.h:39-40
+    const float gw = static_cast<float>(COLS) / static_cast<float>(mnMaxX - mnMinX);
+    const float gh = static_cast<float>(ROWS) / static_cast<float>(mnMaxY - mnMinY);
+    std::vector<std::vector<int>> grid((size_t)COLS * ROWS);
+    for (int i = 0; i < n; i++) {
+        int px = (int)std::round((kpsUn[i].x - mnMinX) * gw);
+        int py = (int)std::round((kpsUn[i].y - mnMinY) * gh);
+        if (px < 0 || px >= COLS || py < 0 || py >= ROWS) continue;
+        grid[(size_t)px * ROWS + py].push_back(i);
+    }
+    std::vector<int> v;
+    const int nMinCellX = std::max(0, (int)std::floor((x - mnMinX - r) * gw));
+    const int nMaxCellX = std::min(COLS - 1, (int)std::ceil((x - mnMinX + r) * gw));
+    const int nMinCellY = std::max(0, (int)std::floor((y - mnMinY - r) * gh));
+    const int nMaxCellY = std::min(ROWS - 1, (int)std::ceil((y - mnMinY + r) * gh));
+    if (nMinCellX < COLS && nMaxCellX >= 0 && nMinCellY < ROWS && nMaxCellY >= 0) {
+        const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+                for (int idx : grid[(size_t)ix * ROWS + iy]) {
+                    const KP& kpUn = kpsUn[idx];
+                    if (bCheckLevels) {
+                        if (kpUn.octave < minLevel) continue;
+                        if (maxLevel >= 0 && kpUn.octave > maxLevel) continue;
+                    }
+                    const float distx = kpUn.x - x, disty = kpUn.y - y;
+                    if (std::fabs(distx) < r && std::fabs(disty) < r) v.push_back(idx);
+                }
+    }
+    if ((int)v.size() > cap) return -(int)v.size() - 1;
+    std::memcpy(out, v.data(), v.size() * sizeof(int));
+    return (int)v.size();
+}
+
+}  // extern "C"

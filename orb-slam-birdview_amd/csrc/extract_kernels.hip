@@ -1,0 +1,773 @@
+// gfx950 kernels of the ORB extractor: pyramid, per-cell FAST+NMS, DistributeOctTree, and the fused
+// IC-angle + 7x7 Gaussian + rBRIEF descriptor.  Integer/byte work: no MFMA anywhere; the bounds
+// are HBM bytes and VALU issue.
+//
+// Compiled with -ffp-contract=off and correctly-rounded fp32 divide: every float expression on the
+// path (root split hX, fastAtan2, BRIEF rotation, keypoint scaling) is evaluated exactly as the
+// reference's scalar C++ evaluates it.
+#include "orbgpu_internal.h"
+#include "pattern31_data.inc"
+
+namespace orbgpu {
+
+__constant__ int8_t c_pattern[1024] = {ORBGPU_PATTERN31_VALUES};
+
+namespace {
+
+struct LevelPtr {
+    const uint8_t* p;
+    int stride;
+};
+
+__device__ __forceinline__ LevelPtr level_ptr(const Geom* __restrict__ g, int l, const uint8_t* frames,
+                                              long long framePitch, int rowStride, const uint8_t* pyr, int f) {
+    if (l == 0) return {frames + (long long)f * framePitch, rowStride};
+    return {pyr + (long long)f * g->pyr_bytes + g->L[l].pyr_off, g->L[l].pitch};
+}
+
+__device__ __forceinline__ int reflect101(int p, int len) {   // BORDER_REFLECT_101
+    if (len == 1) return 0;
+    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+}
+
+// Exclusive block scan of one int per thread; sc needs (waves+1) ints. Ends with a barrier.
+__device__ int block_excl_scan(int v, int* sc, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sc[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int i = 0; i < nw; i++) {
+            int t = sc[i];
+            sc[i] = acc;
+            acc += t;
+        }
+        sc[nw] = acc;
+    }
+    __syncthreads();
+    const int r = x - v + sc[wave];
+    total = sc[nw];
+    __syncthreads();
+    return r;
+}
+
+// In-place exclusive scan of arr[0..n) by the whole block (contiguous chunk per thread).
+__device__ int block_scan_array(int* arr, int n, int* sc) {
+    const int nt = blockDim.x;
+    const int chunk = (n + nt - 1) / nt;
+    const int s0 = threadIdx.x * chunk, s1 = min(s0 + chunk, n);
+    int local = 0;
+    for (int i = s0; i < s1; i++) local += arr[i];
+    int total;
+    int run = block_excl_scan(local, sc, total);
+    for (int i = s0; i < s1; i++) {
+        int t = arr[i];
+        arr[i] = run;
+        run += t;
+    }
+    __syncthreads();
+    return total;
+}
+
+}  // namespace
+
+/* ------------------------------------------------------------------------------------------------
+ * Pyramid: cv::resize(level l-1 -> level l, INTER_LINEAR) for every frame of the batch
+ * (ComputePyramid, ORBextractor.cc:1118-1120).  OpenCV-3.x 8U fixed point: 11-bit horizontal
+ * weights, vertical pass ((b0*(H0>>4))>>16 + (b1*(H1>>4))>>16 + 2)>>2.
+ * Only the ROI values matter: the reference's REFLECT_101 padding is never read on the path.
+ * --------------------------------------------------------------------------------------------- */
+__global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef,
+                                                int level, const uint8_t* __restrict__ frames, long long framePitch,
+                                                int rowStride, uint8_t* __restrict__ pyr) {
+    const int f = blockIdx.z;
+    const int dw = g->L[level].w, dh = g->L[level].h;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= dw || y >= dh) return;
+    const LevelPtr src = level_ptr(g, level - 1, frames, framePitch, rowStride, pyr, f);
+    const ResizeCoef cx = coef[x], cy = coef[dw + y];
+    const uint8_t* r0 = src.p + (long long)cy.s0 * src.stride;
+    const uint8_t* r1 = src.p + (long long)cy.s1 * src.stride;
+    const int h0 = r0[cx.s0] * cx.c0 + r0[cx.s1] * cx.c1;
+    const int h1 = r1[cx.s0] * cx.c0 + r1[cx.s1] * cx.c1;
+    const int v = (((cy.c0 * (h0 >> 4)) >> 16) + ((cy.c1 * (h1 >> 4)) >> 16) + 2) >> 2;
+    uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off;
+    dst[(long long)y * g->L[level].pitch + x] = (uint8_t)v;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * FAST-9/16 + NMS per cell, with the iniThFAST -> minThFAST fallback
+ * (ComputeKeyPointsOctTree, ORBextractor.cc:789-828; cv::FAST semantics SURVEY Appendix A.3).
+ * One workgroup per (cell, frame).  The cell ROI is staged in LDS; M = max over the 16 9-arcs of
+ * the min |difference| (bright or dark) is threshold-independent, so:
+ *   corner(th)  <=>  M > th,     score = M - 1,
+ * and NMS compares against neighbours inside the cell's detection domain only (cells' domains
+ * tile the level without overlap; outside / non-corner neighbours count 0, as OpenCV's row
+ * buffers do for a ROI).  Survivors are emitted in raster order (FAST emission order), packed
+ * x_rel | y_rel<<12 | score<<24 with coordinates relative to minBorder (:822-823).
+ * --------------------------------------------------------------------------------------------- */
+__device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
+    constexpr int P = kFastTilePitch;
+    const int v = c[0];
+    int d[16];
+    d[0] = v - c[3 * P];
+    d[1] = v - c[1 + 3 * P];
+    d[2] = v - c[2 + 2 * P];
+    d[3] = v - c[3 + 1 * P];
+    d[4] = v - c[3];
+    d[5] = v - c[3 - 1 * P];
+    d[6] = v - c[2 - 2 * P];
+    d[7] = v - c[1 - 3 * P];
+    d[8] = v - c[-3 * P];
+    d[9] = v - c[-1 - 3 * P];
+    d[10] = v - c[-2 - 2 * P];
+    d[11] = v - c[-3 - 1 * P];
+    d[12] = v - c[-3];
+    d[13] = v - c[-3 + 1 * P];
+    d[14] = v - c[-2 + 2 * P];
+    d[15] = v - c[-1 + 3 * P];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int A = -1024, Bn = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        A = max(A, mn9);      // dark arc: all v - p > th
+        Bn = min(Bn, mx9);    // bright arc: all p - v > th  <=>  max(v - p) < -th
+    }
+    return max(max(A, -Bn), 0);
+}
+
+__global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
+                                              long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
+                                              uint32_t* __restrict__ cands, int* __restrict__ cellCount) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kFastMaxRoi * kFastTilePitch];
+    __shared__ uint8_t sM[64 * 64];
+    __shared__ int s_cnt;
+    __shared__ int s_wave[4];
+    const int tid = threadIdx.x;
+    const int f = blockIdx.y;
+    const int cell = blockIdx.x;
+    int l = 0;
+    while (l + 1 < g->nlevels && cell >= g->L[l + 1].cell_base) ++l;
+    const LevelGeom& L = g->L[l];
+    const int c = cell - L.cell_base;
+    const int ci = c / L.nCols, cj = c - ci * L.nCols;
+    int* cntOut = cellCount + (long long)f * g->ncells + cell;
+    const int iniY = kMinBorder + ci * L.hCell;
+    const int iniX = kMinBorder + cj * L.wCell;
+    // :794-806 (integer-valued floats in the reference)
+    if (iniY >= L.maxBY - 3 || iniX >= L.maxBX - 6) {
+        if (tid == 0) *cntOut = 0;
+        return;
+    }
+    const int maxY = min(iniY + L.hCell + 6, L.maxBY);
+    const int maxX = min(iniX + L.wCell + 6, L.maxBX);
+    const int rw = maxX - iniX, rh = maxY - iniY;
+    const int dw = rw - 6, dh = rh - 6;   // FAST detection domain: ROI rows/cols 3 .. n-4
+    if (dw <= 0 || dh <= 0) {
+        if (tid == 0) *cntOut = 0;
+        return;
+    }
+    const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
+    const uint8_t* base = src.p + (long long)iniY * src.stride;
+    int xoff = 0;
+    if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
+        const int x0w = iniX >> 2;
+        const int nw = ((iniX + rw + 3) >> 2) - x0w;
+        for (int idx = tid; idx < rh * nw; idx += 256) {
+            const int yy = idx / nw, ww = idx - yy * nw;
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (long long)yy * src.stride + (x0w + ww) * 4);
+            *reinterpret_cast<uint32_t*>(&tile[yy * kFastTilePitch + ww * 4]) = v;
+        }
+        xoff = iniX & 3;
+    } else {
+        for (int idx = tid; idx < rh * rw; idx += 256) {
+            const int yy = idx / rw, xx = idx - yy * rw;
+            tile[yy * kFastTilePitch + xx] = base[(long long)yy * src.stride + iniX + xx];
+        }
+    }
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    const int npx = dw * dh;
+    for (int p = tid; p < npx; p += 256) {
+        const int dy = p / dw, dx = p - dy * dw;
+        sM[p] = (uint8_t)fast_arc_strength(&tile[(dy + 3) * kFastTilePitch + dx + 3 + xoff]);
+    }
+    __syncthreads();
+
+    auto keep = [&](int p, int th) -> bool {
+        const int dy = p / dw, dx = p - dy * dw;
+        const int m = sM[p];
+        if (m <= th) return false;
+        const int s = m - 1;
+#pragma unroll
+        for (int oy = -1; oy <= 1; oy++) {
+#pragma unroll
+            for (int ox = -1; ox <= 1; ox++) {
+                if (ox == 0 && oy == 0) continue;
+                const int ny = dy + oy, nx = dx + ox;
+                if (ny < 0 || ny >= dh || nx < 0 || nx >= dw) continue;
+                const int mn = sM[ny * dw + nx];
+                const int sn = mn > th ? mn - 1 : 0;
+                if (!(s > sn)) return false;
+            }
+        }
+        return true;
+    };
+
+    int th = g->iniTh;
+    int mine = 0;
+    for (int p = tid; p < npx; p += 256) mine += keep(p, th) ? 1 : 0;
+    if (mine) atomicAdd(&s_cnt, mine);
+    __syncthreads();
+    if (s_cnt == 0) th = g->minTh;   // :812-816 fallback, evaluated after NMS
+    __syncthreads();
+
+    uint32_t* out = cands + (long long)f * g->ncand + L.cand_base + (long long)c * L.cell_cap;
+    const int lane = tid & 63, wave = tid >> 6;
+    int running = 0;
+    for (int b0 = 0; b0 < npx; b0 += 256) {
+        const int p = b0 + tid;
+        const bool k = p < npx && keep(p, th);
+        const unsigned long long mask = __ballot(k);
+        if (lane == 0) s_wave[wave] = __popcll(mask);
+        __syncthreads();
+        int before = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int cw = s_wave[w];
+            before += w < wave ? cw : 0;
+            tot += cw;
+        }
+        if (k) {
+            const int pos = running + before + lanes_below(mask);
+            const int dy = p / dw, dx = p - dy * dw;
+            const uint32_t xr = (uint32_t)(dx + 3 + cj * L.wCell);
+            const uint32_t yr = (uint32_t)(dy + 3 + ci * L.hCell);
+            out[pos] = xr | (yr << 12) | ((uint32_t)(sM[p] - 1) << 24);
+        }
+        running += tot;
+        __syncthreads();
+    }
+    if (tid == 0) *cntOut = running;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * DistributeOctTree (ORBextractor.cc:539-763) — one workgroup per (level, frame).
+ *
+ * The reference's std::list of ExtractorNodes is kept as a node TABLE IN LIST ORDER in LDS; keys
+ * (the FAST candidates, in vToDistributeKeys order) stay in a per-level global scratch with a node
+ * index each.  A round divides a set of nodes; children are pushed to the list front in
+ * processing order (n1..n4), so the new table is
+ *     [children of the last-processed node (n4..n1)] ... [children of the first] [unprocessed nodes].
+ * Phase 1 (:594-665) processes every node with > 1 key in list order; phase 2 (:676-737) sorts the
+ * > 1-key nodes by (size, creation sequence) — the pinned stand-in for the pair's heap pointer
+ * (:684) — and divides from the largest down, stopping as soon as the list reaches N nodes (:730).
+ * Finally each node keeps its max-response key, first in key order on ties (:741-762).
+ * --------------------------------------------------------------------------------------------- */
+__device__ __forceinline__ int quadrant_of(uint32_t key, uint32_t rx, uint32_t ry) {
+    const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
+    const int x0 = rx & 0xFFFF, x1 = rx >> 16, y0 = ry & 0xFFFF, y1 = ry >> 16;
+    const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;   // ceil((float)w/2) (:483-484)
+    return (x >= x0 + hx ? 1 : 0) | (y >= y0 + hy ? 2 : 0);     // n1 TL, n2 TR, n3 BL, n4 BR (:512-526)
+}
+
+__device__ __forceinline__ void child_rect(uint32_t rx, uint32_t ry, int q, uint32_t& crx, uint32_t& cry) {
+    const int x0 = rx & 0xFFFF, x1 = rx >> 16, y0 = ry & 0xFFFF, y1 = ry >> 16;
+    const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
+    const int xm = x0 + hx, ym = y0 + hy;
+    const int cx0 = (q & 1) ? xm : x0, cx1 = (q & 1) ? x1 : xm;
+    const int cy0 = (q & 2) ? ym : y0, cy1 = (q & 2) ? y1 : ym;
+    crx = (uint32_t)cx0 | ((uint32_t)cx1 << 16);
+    cry = (uint32_t)cy0 | ((uint32_t)cy1 << 16);
+}
+
+__global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restrict__ g,
+                                                           const uint32_t* __restrict__ cands,
+                                                           const int* __restrict__ cellCount,
+                                                           uint32_t* __restrict__ keysAll,
+                                                           uint16_t* __restrict__ knodeAll,
+                                                           uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
+                                                           int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int NC = g->node_cap;
+    const int tid = threadIdx.x;
+    constexpr int NT = kOctreeThreads;
+    const int l = blockIdx.x, f = blockIdx.y;
+    const LevelGeom& L = g->L[l];
+    // LDS carve: A table, B table (also the sort buffer), quad, rank, info, ord, nchr, scalars.
+    uint32_t* rxA = (uint32_t*)smem;
+    uint32_t* ryA = rxA + NC;
+    int* cntA = (int*)(ryA + NC);
+    int* seqA = cntA + NC;
+    uint32_t* rxB = (uint32_t*)(seqA + NC);
+    uint32_t* ryB = rxB + NC;
+    int* cntB = (int*)(ryB + NC);
+    int* seqB = cntB + NC;
+    int* quad = seqB + NC;        // 4*NC
+    int* rank = quad + 4 * NC;
+    int* info = rank + NC;        // new position (| child mask << 16 for processed nodes)
+    int* ord = info + NC;         // rank -> node
+    int* nchr = ord + NC;         // per rank: #children, then its exclusive prefix
+    int* sc = nchr + NC;          // 32 ints of scan scratch
+    int* sv = sc + 32;            // scalars
+    unsigned long long* skey = (unsigned long long*)rxB;   // phase-2 sort keys alias table B
+    int NC2 = 1;
+    while (NC2 < NC) NC2 <<= 1;
+
+    uint32_t* keys = keysAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
+    uint16_t* knode = knodeAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
+    uint32_t* outK = lvlKps + (long long)f * g->nkpcap + L.kp_base;
+
+    // 1. gather candidates in cell order (vToDistributeKeys, :818-825)
+    const int ncl = L.nCols * L.nRows;
+    const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
+    const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
+    int C = 0;
+    for (int c0 = 0; c0 < ncl; c0 += NT) {
+        const int c = c0 + tid;
+        const int n = c < ncl ? cc[c] : 0;
+        int tot;
+        const int off = block_excl_scan(n, sc, tot);
+        for (int k = 0; k < n; k++) keys[C + off + k] = cs[(long long)c * L.cell_cap + k];
+        C += tot;
+    }
+    __syncthreads();
+
+    // 2. root nodes (:543-585)
+    const int N = L.nfeat;
+    const int nIni = L.nIni;
+    const float hX = L.hX;
+    const int Hn = L.maxBY - kMinBorder;
+    if (nIni > NC) {
+        if (tid == 0) { atomicOr(err, 1); lvlCount[f * g->nlevels + l] = 0; }
+        return;
+    }
+    for (int t = tid; t < nIni; t += NT) {
+        const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
+        rxB[t] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+        ryB[t] = (uint32_t)Hn << 16;
+        cntB[t] = 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < C; i += NT) {
+        const int x = keys[i] & 0xFFF;
+        int r = (int)((float)x / hX);
+        r = min(r, nIni - 1);
+        knode[i] = (uint16_t)r;
+        atomicAdd(&cntB[r], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {   // erase empty roots, keep list order
+        int s = 0;
+        for (int t = 0; t < nIni; t++) {
+            if (cntB[t] > 0) {
+                rxA[s] = rxB[t];
+                ryA[s] = ryB[t];
+                cntA[s] = cntB[t];
+                seqA[s] = -1 - t;
+                info[t] = s++;
+            }
+        }
+        sv[0] = s;
+    }
+    __syncthreads();
+    for (int i = tid; i < C; i += NT) knode[i] = (uint16_t)info[knode[i]];
+    int S = sv[0];
+    int nextSeq = 0;
+    int phase = 1;
+    __syncthreads();
+
+    for (int round = 0; round < 4 * NC + 64; round++) {
+        const int prevSize = S;
+        for (int t = tid; t < 4 * S; t += NT) quad[t] = 0;
+        for (int t = tid; t < S; t += NT) rank[t] = -1;
+        __syncthreads();
+        for (int i = tid; i < C; i += NT) {
+            const int t = knode[i];
+            if (cntA[t] > 1) atomicAdd(&quad[4 * t + quadrant_of(keys[i], rxA[t], ryA[t])], 1);
+        }
+        __syncthreads();
+        int nproc;
+        if (phase == 1) {
+            // every node with > 1 key, in list order
+            for (int t = tid; t < S; t += NT) nchr[t] = cntA[t] > 1 ? 1 : 0;
+            __syncthreads();
+            block_scan_array(nchr, S, sc);
+            if (tid == 0) sv[1] = 0;
+            __syncthreads();
+            for (int t = tid; t < S; t += NT) {
+                if (cntA[t] > 1) {
+                    const int r = nchr[t];
+                    rank[t] = r;
+                    ord[r] = t;
+                    atomicAdd(&sv[1], 1);
+                }
+            }
+            __syncthreads();
+            nproc = sv[1];
+        } else {
+            // sort > 1-key nodes by (size, seq) descending (:684-685), then cut at N (:730)
+            for (int j = tid; j < NC2; j += NT) {
+                unsigned long long key = 0;
+                if (j < S && cntA[j] > 1)
+                    key = ((unsigned long long)cntA[j] << 40) | ((unsigned long long)seqA[j] << 16) |
+                          (unsigned long long)j;
+                skey[j] = key;
+            }
+            __syncthreads();
+            for (int k = 2; k <= NC2; k <<= 1) {
+                for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                    for (int i = tid; i < NC2; i += NT) {
+                        const int ixj = i ^ jj;
+                        if (ixj > i) {
+                            const unsigned long long a = skey[i], b = skey[ixj];
+                            const bool desc = (i & k) == 0;
+                            if (desc ? (a < b) : (a > b)) {
+                                skey[i] = b;
+                                skey[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            if (tid == 0) sv[1] = 0;
+            __syncthreads();
+            for (int j = tid; j < NC2; j += NT) {
+                const unsigned long long key = skey[j];
+                if (key) {
+                    const int t = (int)(key & 0xFFFF);
+                    ord[j] = t;
+                    const int* qd = &quad[4 * t];
+                    nchr[j] = (qd[0] > 0) + (qd[1] > 0) + (qd[2] > 0) + (qd[3] > 0) - 1;
+                    atomicAdd(&sv[1], 1);
+                }
+            }
+            __syncthreads();
+            const int nsort = sv[1];
+            block_scan_array(nchr, nsort, sc);
+            if (tid == 0) sv[2] = 0;
+            __syncthreads();
+            for (int j = tid; j < nsort; j += NT) {
+                const int t = ord[j];
+                const int* qd = &quad[4 * t];
+                const int d = (qd[0] > 0) + (qd[1] > 0) + (qd[2] > 0) + (qd[3] > 0) - 1;
+                if (S + nchr[j] + d < N) atomicAdd(&sv[2], 1);   // still below N after dividing j
+            }
+            __syncthreads();
+            const int below = sv[2];
+            nproc = below < nsort ? below + 1 : nsort;
+            for (int j = tid; j < nproc; j += NT) rank[ord[j]] = j;
+            __syncthreads();
+        }
+        // children counts by rank, positions, sequence numbers
+        for (int r = tid; r < nproc; r += NT) {
+            const int* qd = &quad[4 * ord[r]];
+            nchr[r] = (qd[0] > 0) + (qd[1] > 0) + (qd[2] > 0) + (qd[3] > 0);
+        }
+        __syncthreads();
+        const int CH = block_scan_array(nchr, nproc, sc);
+        // non-processed nodes keep their relative order after the children block
+        for (int t = tid; t < S; t += NT) info[t] = rank[t] < 0 ? 1 : 0;
+        __syncthreads();
+        const int nrest = block_scan_array(info, S, sc);
+        const int Snew = CH + nrest;
+        if (Snew > NC) {
+            if (tid == 0) { atomicOr(err, 2); lvlCount[f * g->nlevels + l] = 0; }
+            return;
+        }
+        if (tid == 0) sv[3] = 0;
+        for (int t = tid; t < S; t += NT) {
+            const int r = rank[t];
+            if (r < 0) {
+                const int pos = CH + info[t];
+                rxB[pos] = rxA[t];
+                ryB[pos] = ryA[t];
+                cntB[pos] = cntA[t];
+                seqB[pos] = seqA[t];
+                info[t] = pos;
+            }
+        }
+        __syncthreads();
+        for (int r = tid; r < nproc; r += NT) {
+            const int t = ord[r];
+            const int* qd = &quad[4 * t];
+            const int mask = (qd[0] > 0) | ((qd[1] > 0) << 1) | ((qd[2] > 0) << 2) | ((qd[3] > 0) << 3);
+            const int nch = __popc(mask);
+            const int P = nchr[r];
+            const int start = CH - P - nch;          // later-processed nodes end up nearer the front
+            int big = 0;
+            for (int q = 0; q < 4; q++) {
+                if (!(mask & (1 << q))) continue;
+                const int pos = start + __popc(mask >> (q + 1));              // n4 first .. n1 last
+                uint32_t crx, cry;
+                child_rect(rxA[t], ryA[t], q, crx, cry);
+                rxB[pos] = crx;
+                ryB[pos] = cry;
+                cntB[pos] = qd[q];
+                seqB[pos] = nextSeq + P + __popc(mask & ((1 << q) - 1));      // creation order n1..n4
+                big += qd[q] > 1;
+            }
+            info[t] = start | (mask << 16);
+            if (big) atomicAdd(&sv[3], big);
+        }
+        __syncthreads();
+        for (int i = tid; i < C; i += NT) {
+            const int t = knode[i];
+            int nt;
+            if (rank[t] >= 0) {
+                const int inf = info[t];
+                const int q = quadrant_of(keys[i], rxA[t], ryA[t]);
+                nt = (inf & 0xFFFF) + __popc((inf >> 16) >> (q + 1));
+            } else {
+                nt = info[t];
+            }
+            knode[i] = (uint16_t)nt;
+        }
+        const int nToExpand = sv[3];
+        __syncthreads();
+        // swap tables
+        for (int t = tid; t < Snew; t += NT) {
+            rxA[t] = rxB[t];
+            ryA[t] = ryB[t];
+            cntA[t] = cntB[t];
+            seqA[t] = seqB[t];
+        }
+        nextSeq += CH;
+        S = Snew;
+        __syncthreads();
+        if (S >= N || S == prevSize) break;                       // :669-672 / :734-735
+        if (phase == 1 && S + nToExpand * 3 > N) phase = 2;       // :673
+    }
+
+    // 3. retain the best key per node (:741-762): max response, first in key order on ties
+    uint32_t* best = (uint32_t*)quad;
+    for (int t = tid; t < S; t += NT) best[t] = 0;
+    __syncthreads();
+    for (int i = tid; i < C; i += NT) {
+        const uint32_t v = ((keys[i] >> 24) << 24) | (uint32_t)(0xFFFFFF - i);
+        atomicMax(&best[knode[i]], v);
+    }
+    __syncthreads();
+    for (int t = tid; t < S; t += NT) {
+        const int i = 0xFFFFFF - (int)(best[t] & 0xFFFFFF);
+        const uint32_t k = keys[i];
+        const uint32_t x = (k & 0xFFF) + kMinBorder, y = ((k >> 12) & 0xFFF) + kMinBorder;   // :841-847
+        outK[t] = x | (y << 12) | (k & 0xFF000000u);
+    }
+    if (tid == 0) lvlCount[f * g->nlevels + l] = S;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Fused IC_Angle (ORBextractor.cc:77-104) + GaussianBlur 7x7 sigma 2 (:1085-1086) +
+ * computeOrbDescriptor (:108-147) + output assembly (:1093-1103).  One wavefront per keypoint:
+ * a 43x43 window of the unblurred level (REFLECT_101 at the level border) is staged in LDS, the
+ * 37x37 blurred patch is computed from it (exact integer row pass, column pass rounded as the
+ * pinned OpenCV 3.2 8U path does), and the 256 tests are four 64-lane ballots.
+ * --------------------------------------------------------------------------------------------- */
+constexpr float kAtanScale = (float)(180 / 3.14159265358979323846);
+constexpr float kP1 = 0.9997878412794807f * kAtanScale;
+constexpr float kP3 = -0.3258083974640975f * kAtanScale;
+constexpr float kP5 = 0.1555786518463281f * kAtanScale;
+constexpr float kP7 = -0.04432655554792128f * kAtanScale;
+constexpr float kFactorPI = (float)(3.14159265358979323846 / 180.f);
+
+__device__ __forceinline__ float fast_atan2(float y, float x) {   // cv::fastAtan2 (Appendix A.4)
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.220446049250313e-16);
+        c2 = c * c;
+        a = (((kP7 * c2 + kP5) * c2 + kP3) * c2 + kP1) * c;
+    } else {
+        c = ax / (ay + (float)2.220446049250313e-16);
+        c2 = c * c;
+        a = 90.f - (((kP7 * c2 + kP5) * c2 + kP3) * c2 + kP1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
+                                                  long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
+                                                  const uint32_t* __restrict__ lvlKps,
+                                                  const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
+                                                  uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kDescWin * kDescWinPitch];
+    __shared__ __attribute__((aligned(16))) uint16_t s_row[4][kDescWin * kDescBlur];
+    __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][kDescBlur * kDescBlurPitch];
+    const int f = blockIdx.y;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nl = g->nlevels;
+    const int* cnts = lvlCount + f * nl;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int tot = 0;
+        for (int i = 0; i < nl; i++) tot += cnts[i];
+        outN[f] = tot;
+    }
+    const int s = blockIdx.x * 4 + wv;
+    if (s >= g->nkpcap) return;
+    int l = 0;
+    while (l + 1 < nl && s >= g->L[l + 1].kp_base) ++l;
+    const LevelGeom& L = g->L[l];
+    const int k = s - L.kp_base;
+    if (k >= cnts[l]) return;
+    int outIdx = k;
+    for (int i = 0; i < l; i++) outIdx += cnts[i];
+    const uint32_t kp = lvlKps[(long long)f * g->nkpcap + s];
+    const int x = kp & 0xFFF, y = (kp >> 12) & 0xFFF, score = kp >> 24;
+    const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
+    uint8_t* win = s_win[wv];
+    uint16_t* rowp = s_row[wv];
+    uint8_t* blur = s_blur[wv];
+    for (int idx = lane; idx < kDescWin * kDescWin; idx += 64) {
+        const int wy = idx / kDescWin, wx = idx - wy * kDescWin;
+        const int sy = reflect101(y - 21 + wy, L.h), sx = reflect101(x - 21 + wx, L.w);
+        win[wy * kDescWinPitch + wx] = src.p[(long long)sy * src.stride + sx];
+    }
+    wave_lds_sync();
+    // IC angle on the unblurred level (:77-104): exact integer moments
+    int m10 = 0, m01 = 0;
+    for (int idx = lane; idx < 31 * 31; idx += 64) {
+        const int v = idx / 31 - 15, u = idx - (idx / 31) * 31 - 15;
+        if (abs(u) <= g->umax[abs(v)]) {
+            const int I = win[(21 + v) * kDescWinPitch + 21 + u];
+            m10 += u * I;
+            m01 += v * I;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m10 += __shfl_xor(m10, o);
+        m01 += __shfl_xor(m01, o);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // Gaussian 7x7: exact integer row pass over 43 rows x 37 cols
+    int gk[7];
+#pragma unroll
+    for (int j = 0; j < 7; j++) gk[j] = g->gk[j];
+    for (int idx = lane; idx < kDescWin * kDescBlur; idx += 64) {
+        const int wy = idx / kDescBlur, rx = idx - wy * kDescBlur;
+        const uint8_t* p = &win[wy * kDescWinPitch + rx];
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < 7; j++) acc += gk[j] * p[j];
+        rowp[idx] = (uint16_t)acc;
+    }
+    wave_lds_sync();
+    const int xsimd = L.w & ~3;   // SymmColumnVec_32s8u covers column blocks of 4; scalar tail rounds half-up
+    for (int idx = lane; idx < kDescBlur * kDescBlur; idx += 64) {
+        const int by = idx / kDescBlur, bx = idx - by * kDescBlur;
+        int S = 0;
+#pragma unroll
+        for (int i = 0; i < 7; i++) S += gk[i] * rowp[(by + i) * kDescBlur + bx];
+        const int X = x - 18 + bx;
+        int v;
+        if (X < xsimd) {
+            const int q = S >> 16, rem = S & 0xFFFF;
+            v = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));
+        } else {
+            v = (S + 32768) >> 16;
+        }
+        blur[by * kDescBlurPitch + bx] = (uint8_t)min(v, 255);
+    }
+    wave_lds_sync();
+    // rBRIEF (:108-147): pinned correctly-rounded cos/sin
+    const float ang = angle * kFactorPI;
+    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    const uint8_t* ctr = &blur[18 * kDescBlurPitch + 18];
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(outD + ((long long)f * kpCap + outIdx) * 32);
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+        const int p = lane + 64 * gq;
+        const float px0 = (float)c_pattern[4 * p], py0 = (float)c_pattern[4 * p + 1];
+        const float px1 = (float)c_pattern[4 * p + 2], py1 = (float)c_pattern[4 * p + 3];
+        const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
+        const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
+        const int t0 = ctr[__float2int_rn(u0 + u1) * kDescBlurPitch + __float2int_rn(u2 - u3)];
+        const int t1 = ctr[__float2int_rn(w0 + w1) * kDescBlurPitch + __float2int_rn(w2 - w3)];
+        const unsigned long long m = __ballot(t0 < t1);
+        if (lane == 0) dst[gq] = m;
+    }
+    if (lane == 0) {
+        orb_keypoint o;
+        o.x = (float)x;
+        o.y = (float)y;
+        if (l != 0) {   // :1095-1101
+            o.x *= L.scale;
+            o.y *= L.scale;
+        }
+        o.size = L.patch_size;
+        o.angle = angle;
+        o.response = (float)score;
+        o.octave = l;
+        o.class_id = -1;
+        outK[(long long)f * kpCap + outIdx] = o;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+static inline unsigned cdiv(unsigned a, unsigned b) { return (a + b - 1) / b; }
+
+size_t octree_lds_bytes(int node_cap) { return (size_t)node_cap * (16 * 4) + (32 + 8) * 4; }
+
+hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
+                          int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
+                          int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
+    if (nframes <= 0) return hipSuccess;
+    if (marker) marker(user, ORB_K_RESIZE, 1);
+    for (int l = 1; l < g.nlevels; l++) {
+        dim3 grid(cdiv(g.L[l].w, 64), cdiv(g.L[l].h, 4), nframes);
+        hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l, d_frames,
+                           frame_pitch, row_stride, b.d_pyr);
+    }
+    if (marker) marker(user, ORB_K_RESIZE, 0);
+    if (marker) marker(user, ORB_K_FAST, 1);
+    hipLaunchKernelGGL(k_fast, dim3(g.ncells, nframes), dim3(256), 0, stream, b.d_geom, d_frames, frame_pitch,
+                       row_stride, b.d_pyr, b.d_cands, b.d_cellCount);
+    if (marker) marker(user, ORB_K_FAST, 0);
+    if (marker) marker(user, ORB_K_OCTREE, 1);
+    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, nframes), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap),
+                       stream, b.d_geom, b.d_cands, b.d_cellCount, b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount,
+                       b.d_err);
+    if (marker) marker(user, ORB_K_OCTREE, 0);
+    if (marker) marker(user, ORB_K_DESCRIBE, 1);
+    hipLaunchKernelGGL(k_describe, dim3(cdiv(g.nkpcap, 4), nframes), dim3(256), 0, stream, b.d_geom, d_frames,
+                       frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap);
+    if (marker) marker(user, ORB_K_DESCRIBE, 0);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

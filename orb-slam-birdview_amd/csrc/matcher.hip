@@ -1,0 +1,570 @@
+// ORBmatcher entry points of the C-ABI.  Distances and top-k lists come from the gfx950 kernels
+// (hamming_kernels.hip); the parts of the reference that depend on the ORDER of earlier accepted
+// matches — SearchByBoW's "already assigned" skip (ORBmatcher.cc:209-210, :576/:603) and
+// SearchForInitialization's vMatchedDistance stealing (:444-445, :463-470) — are replayed on the
+// host in the reference's iteration order.  A top-k list is exact for a query as long as two of its
+// entries are still admissible at replay time or it holds every admissible candidate; otherwise the
+// remaining queries are re-ranked on the GPU against the current exclusion state.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "orbgpu_ctx.h"
+
+namespace orbgpu {
+namespace {
+
+constexpr int TH_LOW = 50;          // ORBmatcher.cc:38
+constexpr int HISTO_LENGTH = 30;    // :39
+constexpr int K = 8;
+
+struct Arena {
+    Ctx* c;
+    size_t off = 0;
+    static size_t align(size_t x) { return (x + 255) & ~(size_t)255; }
+    // reserve the total first, then take() pieces
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= c->scratch_cap && c->d_scratch) return hipSuccess;
+        if (c->d_scratch) (void)hipFree(c->d_scratch);
+        c->d_scratch = nullptr;
+        c->scratch_cap = 0;
+        hipError_t e = hipMalloc((void**)&c->d_scratch, bytes);
+        if (e == hipSuccess) c->scratch_cap = bytes;
+        return e;
+    }
+    template <class T>
+    T* take(size_t n) {
+        off = align(off);
+        T* p = (T*)(c->d_scratch + off);
+        off += std::max<size_t>(n, 1) * sizeof(T);
+        return p;
+    }
+};
+
+int rot_bin(float a1, float a2) {   // ORBmatcher.cc:236-243 (round(rot*(1/30)): bins 0..12, upstream quirk)
+    const float factor = 1.0f / HISTO_LENGTH;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)std::round(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+void three_maxima(const std::vector<int>* histo, int& ind1, int& ind2, int& ind3) {   // :1601-1642
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = (int)histo[i].size();
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s; ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+// Drop matches outside the three dominant rotation bins (e.g. :265-285).
+void cull_rotation(const std::vector<int>* rotHist, std::vector<int>& matches, int& nmatches) {
+    int i1 = -1, i2 = -1, i3 = -1;
+    three_maxima(rotHist, i1, i2, i3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        if (i == i1 || i == i2 || i == i3) continue;
+        for (int q : rotHist[i])
+            if (matches[q] >= 0) { matches[q] = -1; nmatches--; }
+    }
+}
+
+template <class F>
+void for_common_nodes(const orb_featvec& a, const orb_featvec& b, F f) {   // std::map merge (:175-264)
+    int i = 0, j = 0;
+    while (i < a.nnodes && j < b.nnodes) {
+        if (a.node_ids[i] == b.node_ids[j]) { f(i, j); i++; j++; }
+        else if (a.node_ids[i] < b.node_ids[j]) i++;
+        else j++;
+    }
+}
+
+// One matcher call: static data on the device, re-rankable from any item with fresh thresholds.
+struct TopkSession {
+    Ctx* c;
+    int nitems = 0, nt = 0;
+    std::vector<int> item_q;         // query feature per item
+    std::vector<int2> item_rng;      // [begin, end) into cand
+    const int* cand = nullptr;       // host candidate list
+    int ncand = 0;
+    // device
+    uint8_t* d_q = nullptr;
+    uint8_t* d_t = nullptr;
+    int2* d_rng = nullptr;
+    int* d_cand = nullptr;
+    int* d_thr = nullptr;
+    int* d_dist = nullptr;
+    int* d_idx = nullptr;
+    int* d_nvalid = nullptr;
+    // host results (indexed by item)
+    std::vector<int> dist, idx, nvalid;
+
+    int setup(const uint8_t* qdesc, const uint8_t* tdesc, int ntrain) {
+        nitems = (int)item_q.size();
+        nt = ntrain;
+        Arena a{c};
+        const size_t need = Arena::align((size_t)nitems * 32) + Arena::align((size_t)nt * 32) +
+                            Arena::align((size_t)nitems * 8) + Arena::align((size_t)ncand * 4) +
+                            Arena::align((size_t)nt * 4) + 3 * Arena::align((size_t)nitems * K * 4) + 4096;
+        hipError_t e = a.reserve(need);
+        if (e != hipSuccess) return set_error("matcher scratch", e), ORB_ERR_NOMEM;
+        d_q = a.take<uint8_t>((size_t)nitems * 32);
+        d_t = a.take<uint8_t>((size_t)nt * 32);
+        d_rng = a.take<int2>(nitems);
+        d_cand = a.take<int>(ncand);
+        d_thr = a.take<int>(nt);
+        d_dist = a.take<int>((size_t)nitems * K);
+        d_idx = a.take<int>((size_t)nitems * K);
+        d_nvalid = a.take<int>(nitems);
+        std::vector<uint8_t> qg((size_t)nitems * 32);
+        for (int i = 0; i < nitems; i++) std::memcpy(&qg[(size_t)i * 32], qdesc + (size_t)item_q[i] * 32, 32);
+        if (nitems && (e = hipMemcpyAsync(d_q, qg.data(), qg.size(), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return set_error("upload queries", e), ORB_ERR_HIP;
+        if (nt && (e = hipMemcpyAsync(d_t, tdesc, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return set_error("upload trains", e), ORB_ERR_HIP;
+        if (nitems && (e = hipMemcpyAsync(d_rng, item_rng.data(), (size_t)nitems * sizeof(int2), hipMemcpyHostToDevice,
+                                          c->stream)) != hipSuccess)
+            return set_error("upload ranges", e), ORB_ERR_HIP;
+        if (ncand && (e = hipMemcpyAsync(d_cand, cand, (size_t)ncand * 4, hipMemcpyHostToDevice, c->stream)) !=
+                         hipSuccess)
+            return set_error("upload candidates", e), ORB_ERR_HIP;
+        dist.assign((size_t)nitems * K, -1);
+        idx.assign((size_t)nitems * K, -1);
+        nvalid.assign(nitems, 0);
+        return ORB_OK;
+    }
+
+    // Re-rank items [from, nitems) with train thresholds thr (NULL = admit all).
+    int run(int from, const int* thr) {
+        const int n = nitems - from;
+        if (n <= 0) return ORB_OK;
+        hipError_t e;
+        if (thr && (e = hipMemcpyAsync(d_thr, thr, (size_t)nt * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return set_error("upload thresholds", e), ORB_ERR_HIP;
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+        e = launch_hamming_topk(d_q + (size_t)from * 32, n, d_t, nt, d_rng + from, d_cand, thr ? d_thr : nullptr, K,
+                                d_dist + (size_t)from * K, d_idx + (size_t)from * K, d_nvalid + from, c->stream);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+        if (e != hipSuccess) return set_error("hamming kernel", e), ORB_ERR_HIP;
+        if ((e = hipMemcpyAsync(dist.data() + (size_t)from * K, d_dist + (size_t)from * K, (size_t)n * K * 4,
+                                hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(idx.data() + (size_t)from * K, d_idx + (size_t)from * K, (size_t)n * K * 4,
+                                hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(nvalid.data() + from, d_nvalid + from, (size_t)n * 4, hipMemcpyDeviceToHost,
+                                c->stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+            return set_error("download top-k", e), ORB_ERR_HIP;
+        return ORB_OK;
+    }
+
+    // First two admissible entries of item i's list. Returns false if the list cannot decide them.
+    template <class Admit>
+    bool best_two(int i, Admit admit, int& d1, int& i1, int& d2, int init) const {
+        d1 = init;
+        i1 = -1;
+        d2 = init;
+        int found = 0;
+        for (int j = 0; j < K; j++) {
+            const int d = dist[(size_t)i * K + j];
+            if (d < 0) break;
+            const int t = idx[(size_t)i * K + j];
+            if (!admit(t, d)) continue;
+            if (found == 0) { d1 = d; i1 = t; found = 1; }
+            else { d2 = d; found = 2; break; }
+        }
+        return found == 2 || nvalid[i] <= K;
+    }
+};
+
+}  // namespace
+}  // namespace orbgpu
+
+using namespace orbgpu;
+
+#define CTX_GUARD(ctx)                                                              \
+    if (!(ctx)) {                                                                   \
+        set_error("NULL context", hipSuccess);                                      \
+        return ORB_ERR_ARG;                                                         \
+    }                                                                               \
+    {                                                                               \
+        hipError_t _e = hipSetDevice((ctx)->device);                                \
+        if (_e != hipSuccess) return set_error("hipSetDevice", _e), ORB_ERR_HIP;    \
+    }
+
+extern "C" {
+
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {   // ORBmatcher.cc:1647-1663
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        std::memcpy(&x, a + 4 * i, 4);
+        std::memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+int orb_hamming_topk(orb_ctx* h, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_off,
+                     const int* cand_idx, const int* train_thr, int k, int* out_dist, int* out_idx, int* out_nvalid) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (nq < 0 || nt < 0 || k < 1 || k > K || (nq && (!q || !out_dist || !out_idx)) || (nt && !t))
+        return set_error("orb_hamming_topk: bad arguments", hipSuccess), ORB_ERR_ARG;
+    if (nq == 0) return ORB_OK;
+    const int ncand = cand_off ? cand_off[nq] : 0;
+    Arena a{c};
+    hipError_t e = a.reserve(Arena::align((size_t)nq * 32) + Arena::align((size_t)nt * 32) + Arena::align(nq * 8) +
+                             Arena::align((size_t)ncand * 4) + Arena::align((size_t)nt * 4) +
+                             2 * Arena::align((size_t)nq * k * 4) + Arena::align(nq * 4) + 4096);
+    if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
+    uint8_t* d_q = a.take<uint8_t>((size_t)nq * 32);
+    uint8_t* d_t = a.take<uint8_t>((size_t)nt * 32);
+    int2* d_rng = a.take<int2>(nq);
+    int* d_cand = a.take<int>(ncand);
+    int* d_thr = a.take<int>(nt);
+    int* d_dist = a.take<int>((size_t)nq * k);
+    int* d_idx = a.take<int>((size_t)nq * k);
+    int* d_nv = a.take<int>(nq);
+    std::vector<int2> rng;
+    if (cand_off) {
+        rng.resize(nq);
+        for (int i = 0; i < nq; i++) rng[i] = make_int2(cand_off[i], cand_off[i + 1]);
+    }
+    if ((e = hipMemcpyAsync(d_q, q, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (nt && (e = hipMemcpyAsync(d_t, t, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream)) != hipSuccess) ||
+        (cand_off && (e = hipMemcpyAsync(d_rng, rng.data(), nq * sizeof(int2), hipMemcpyHostToDevice, c->stream)) !=
+                         hipSuccess) ||
+        (ncand && (e = hipMemcpyAsync(d_cand, cand_idx, (size_t)ncand * 4, hipMemcpyHostToDevice, c->stream)) !=
+                      hipSuccess) ||
+        (train_thr && (e = hipMemcpyAsync(d_thr, train_thr, (size_t)nt * 4, hipMemcpyHostToDevice, c->stream)) !=
+                          hipSuccess))
+        return set_error("upload", e), ORB_ERR_HIP;
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+    e = launch_hamming_topk(d_q, nq, d_t, nt, cand_off ? d_rng : nullptr, d_cand, train_thr ? d_thr : nullptr, k,
+                            d_dist, d_idx, d_nv, c->stream);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+    if (e != hipSuccess) return set_error("hamming kernel", e), ORB_ERR_HIP;
+    if ((e = hipMemcpyAsync(out_dist, d_dist, (size_t)nq * k * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out_idx, d_idx, (size_t)nq * k * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (out_nvalid && (e = hipMemcpyAsync(out_nvalid, d_nv, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream)) !=
+                           hipSuccess) ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return set_error("download", e), ORB_ERR_HIP;
+    return ORB_OK;
+}
+
+int orb_hamming_top2_device(orb_ctx* h, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int* d_best,
+                            int* d_best_idx, int* d_second) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (nq <= 0) return ORB_OK;
+    Arena a{c};
+    const int ns = top2_slices(nq, nt);
+    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(int4)) + 256);
+    if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
+    int4* part = a.take<int4>((size_t)ns * nq);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+    e = launch_hamming_top2(d_q, nq, d_t, nt, d_best, d_best_idx, d_second, part, c->stream);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+    return e == hipSuccess ? ORB_OK : (set_error("top2 kernel", e), ORB_ERR_HIP);
+}
+
+/* SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)  ORBmatcher.cc:159-288 */
+int orb_search_by_bow_kf_f(orb_ctx* h, float nnratio, int check_ori, int n_kf, const uint8_t* desc_kf,
+                           const float* angle_kf, const uint8_t* mp_kf, orb_featvec fv_kf, int n_f,
+                           const uint8_t* desc_f, const float* angle_f, orb_featvec fv_f, int* match_f,
+                           int* nmatches_out) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n_kf < 0 || n_f < 0 || !match_f) return ORB_ERR_ARG;
+    TopkSession s{c};
+    s.cand = fv_f.indices;
+    s.ncand = fv_f.nnodes ? fv_f.offsets[fv_f.nnodes] : 0;
+    for_common_nodes(fv_kf, fv_f, [&](int a, int b) {
+        for (int iKF = fv_kf.offsets[a]; iKF < fv_kf.offsets[a + 1]; iKF++) {
+            const int realIdxKF = fv_kf.indices[iKF];
+            if (!mp_kf[realIdxKF]) continue;   // !pMP || pMP->isBad()  (:204-208)
+            s.item_q.push_back(realIdxKF);
+            s.item_rng.push_back(make_int2(fv_f.offsets[b], fv_f.offsets[b + 1]));
+        }
+    });
+    int st = s.setup(desc_kf, desc_f, n_f);
+    if (st == ORB_OK) st = s.run(0, nullptr);
+    if (st != ORB_OK) return st;
+    std::vector<int> matches(n_f, -1);
+    std::vector<int> thr(n_f);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    auto admit = [&](int t, int) { return matches[t] < 0; };   // if(vpMapPointMatches[realIdxF]) continue;
+    for (int i = 0; i < s.nitems; i++) {
+        int d1, i1, d2;
+        if (!s.best_two(i, admit, d1, i1, d2, 256)) {
+            for (int t = 0; t < n_f; t++) thr[t] = matches[t] >= 0 ? -1 : INT_MAX;
+            if ((st = s.run(i, thr.data())) != ORB_OK) return st;
+            s.best_two(i, admit, d1, i1, d2, 256);
+        }
+        if (d1 <= TH_LOW && static_cast<float>(d1) < nnratio * static_cast<float>(d2)) {   // :228-230
+            const int realIdxKF = s.item_q[i];
+            matches[i1] = realIdxKF;
+            if (check_ori) rotHist[rot_bin(angle_kf[realIdxKF], angle_f[i1])].push_back(i1);
+            nmatches++;
+        }
+    }
+    if (check_ori) cull_rotation(rotHist, matches, nmatches);
+    std::memcpy(match_f, matches.data(), (size_t)n_f * sizeof(int));
+    if (nmatches_out) *nmatches_out = nmatches;
+    return ORB_OK;
+}
+
+/* SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)  ORBmatcher.cc:522-655 */
+int orb_search_by_bow_kf_kf(orb_ctx* h, float nnratio, int check_ori, int n1, const uint8_t* desc1,
+                            const float* angle1, const uint8_t* mp1, orb_featvec fv1, int n2, const uint8_t* desc2,
+                            const float* angle2, const uint8_t* mp2, orb_featvec fv2, int* match12,
+                            int* nmatches_out) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || n2 < 0 || !match12) return ORB_ERR_ARG;
+    TopkSession s{c};
+    s.cand = fv2.indices;
+    s.ncand = fv2.nnodes ? fv2.offsets[fv2.nnodes] : 0;
+    for_common_nodes(fv1, fv2, [&](int a, int b) {
+        for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
+            const int idx1 = fv1.indices[i];
+            if (!mp1[idx1]) continue;   // :567-571
+            s.item_q.push_back(idx1);
+            s.item_rng.push_back(make_int2(fv2.offsets[b], fv2.offsets[b + 1]));
+        }
+    });
+    std::vector<int> thr(n2);
+    std::vector<char> matched2(n2, 0);
+    for (int t = 0; t < n2; t++) thr[t] = mp2[t] ? INT_MAX : -1;   // !pMP2 || isBad (:584-588)
+    int st = s.setup(desc1, desc2, n2);
+    if (st == ORB_OK) st = s.run(0, thr.data());
+    if (st != ORB_OK) return st;
+    std::vector<int> matches(n1, -1);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    auto admit = [&](int t, int) { return !matched2[t]; };
+    for (int i = 0; i < s.nitems; i++) {
+        int d1, i1, d2;
+        if (!s.best_two(i, admit, d1, i1, d2, 256)) {
+            for (int t = 0; t < n2; t++) thr[t] = (matched2[t] || !mp2[t]) ? -1 : INT_MAX;
+            if ((st = s.run(i, thr.data())) != ORB_OK) return st;
+            s.best_two(i, admit, d1, i1, d2, 256);
+        }
+        if (d1 < TH_LOW && static_cast<float>(d1) < nnratio * static_cast<float>(d2)) {   // :598-600
+            const int idx1 = s.item_q[i];
+            matches[idx1] = i1;
+            matched2[i1] = 1;
+            if (check_ori) rotHist[rot_bin(angle1[idx1], angle2[i1])].push_back(idx1);
+            nmatches++;
+        }
+    }
+    if (check_ori) cull_rotation(rotHist, matches, nmatches);
+    std::memcpy(match12, matches.data(), (size_t)n1 * sizeof(int));
+    if (nmatches_out) *nmatches_out = nmatches;
+    return ORB_OK;
+}
+
+/* SearchForTriangulation  ORBmatcher.cc:657-823: no cross-query dependence (vbMatched2 is never
+ * set, :738), so every (idx1, node) item is decided on the GPU. */
+int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int n1, const uint8_t* desc1,
+                                 const orb_keypoint* kps1, const uint8_t* has_mp1, const float* uright1,
+                                 orb_featvec fv1, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
+                                 const uint8_t* has_mp2, const float* uright2, orb_featvec fv2, const float* F12,
+                                 float ex, float ey, const float* scale2, const float* sigma2_2, int nlevels2,
+                                 int* pairs_out, int cap, int* npairs) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
+    std::vector<int> item_q;
+    std::vector<int2> rng;
+    for_common_nodes(fv1, fv2, [&](int a, int b) {
+        for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
+            const int idx1 = fv1.indices[i];
+            if (has_mp1[idx1]) continue;                              // :694-696
+            if (only_stereo && !(uright1[idx1] >= 0)) continue;       // :698-702
+            item_q.push_back(idx1);
+            rng.push_back(make_int2(fv2.offsets[b], fv2.offsets[b + 1]));
+        }
+    });
+    const int nitems = (int)item_q.size();
+    const int ncand = fv2.nnodes ? fv2.offsets[fv2.nnodes] : 0;
+    std::vector<int> best(nitems, -1);
+    if (nitems) {
+        Arena a{c};
+        hipError_t e = a.reserve(Arena::align((size_t)n1 * 32) + Arena::align((size_t)n1 * sizeof(orb_keypoint)) +
+                                 Arena::align((size_t)n1 * 4) + Arena::align((size_t)n2 * 32) +
+                                 Arena::align((size_t)n2 * sizeof(orb_keypoint)) + Arena::align(n2) +
+                                 Arena::align((size_t)n2 * 4) + Arena::align((size_t)nitems * 4) +
+                                 Arena::align((size_t)nitems * 8) + Arena::align((size_t)ncand * 4) +
+                                 Arena::align((size_t)nitems * 4) + 4096);
+        if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
+        uint8_t* d_d1 = a.take<uint8_t>((size_t)n1 * 32);
+        orb_keypoint* d_k1 = a.take<orb_keypoint>(n1);
+        float* d_u1 = a.take<float>(n1);
+        uint8_t* d_d2 = a.take<uint8_t>((size_t)n2 * 32);
+        orb_keypoint* d_k2 = a.take<orb_keypoint>(n2);
+        uint8_t* d_m2 = a.take<uint8_t>(n2);
+        float* d_u2 = a.take<float>(n2);
+        int* d_q = a.take<int>(nitems);
+        int2* d_r = a.take<int2>(nitems);
+        int* d_c = a.take<int>(ncand);
+        int* d_b = a.take<int>(nitems);
+        auto up = [&](void* d, const void* hsrc, size_t bytes) {
+            return bytes ? hipMemcpyAsync(d, hsrc, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+        };
+        if ((e = up(d_d1, desc1, (size_t)n1 * 32)) != hipSuccess || (e = up(d_k1, kps1, n1 * sizeof(orb_keypoint))) ||
+            (e = up(d_u1, uright1, (size_t)n1 * 4)) || (e = up(d_d2, desc2, (size_t)n2 * 32)) ||
+            (e = up(d_k2, kps2, n2 * sizeof(orb_keypoint))) || (e = up(d_m2, has_mp2, n2)) ||
+            (e = up(d_u2, uright2, (size_t)n2 * 4)) || (e = up(d_q, item_q.data(), (size_t)nitems * 4)) ||
+            (e = up(d_r, rng.data(), (size_t)nitems * 8)) || (e = up(d_c, fv2.indices, (size_t)ncand * 4)))
+            return set_error("upload", e), ORB_ERR_HIP;
+        TriParams tp;
+        std::memset(&tp, 0, sizeof tp);
+        std::memcpy(tp.F, F12, sizeof tp.F);
+        tp.ex = ex;
+        tp.ey = ey;
+        for (int l = 0; l < nlevels2; l++) {
+            tp.scale2[l] = scale2[l];
+            tp.sigma2[l] = sigma2_2[l];
+        }
+        tp.only_stereo = only_stereo;
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+        e = launch_triangulation(d_d1, d_k1, d_u1, d_d2, d_k2, d_m2, d_u2, d_q, d_r, d_c, nitems, tp, d_b, c->stream);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+        if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
+        if ((e = hipMemcpyAsync(best.data(), d_b, (size_t)nitems * 4, hipMemcpyDeviceToHost, c->stream)) !=
+                hipSuccess ||
+            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+            return set_error("download", e), ORB_ERR_HIP;
+    }
+    std::vector<int> vMatches12(n1, -1);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    for (int i = 0; i < nitems; i++) {
+        if (best[i] < 0) continue;
+        const int idx1 = item_q[i];
+        vMatches12[idx1] = best[i];
+        nmatches++;
+        if (check_ori) rotHist[rot_bin(kps1[idx1].angle, kps2[best[i]].angle)].push_back(idx1);
+    }
+    if (check_ori) {   // :792-813 (no ">= 0" guard in this function: every culled entry decrements)
+        int i1 = -1, i2 = -1, i3 = -1;
+        three_maxima(rotHist, i1, i2, i3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int q : rotHist[i]) { vMatches12[q] = -1; nmatches--; }
+        }
+    }
+    int np = 0;
+    for (int i = 0; i < n1; i++) {
+        if (vMatches12[i] < 0) continue;
+        if (np < cap && pairs_out) {
+            pairs_out[2 * np] = i;
+            pairs_out[2 * np + 1] = vMatches12[i];
+        }
+        np++;
+    }
+    *npairs = np;
+    if (np > cap) return set_error("pairs_out too small", hipSuccess), ORB_ERR_CAPACITY;
+    return ORB_OK;
+}
+
+/* SearchForInitialization (:405-520) / BirdviewMatch(const Frame&, const Frame&, ...) (:1790-1899) */
+int orb_window_match(orb_ctx* h, float nnratio, int check_ori, int level0_only, int n1, const uint8_t* desc1,
+                     const orb_keypoint* kps1, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
+                     const int* cand_off, const int* cand_idx, int* match12, int* nmatches_out) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || n2 < 0 || !match12 || !cand_off) return ORB_ERR_ARG;
+    TopkSession s{c};
+    s.cand = cand_idx;
+    s.ncand = cand_off[n1];
+    for (int i1 = 0; i1 < n1; i1++) {
+        if (level0_only && kps1[i1].octave > 0) continue;   // :420-423
+        if (cand_off[i1 + 1] == cand_off[i1]) continue;     // :427-428
+        s.item_q.push_back(i1);
+        s.item_rng.push_back(make_int2(cand_off[i1], cand_off[i1 + 1]));
+    }
+    int st = s.setup(desc1, desc2, n2);
+    if (st == ORB_OK) st = s.run(0, nullptr);
+    if (st != ORB_OK) return st;
+    std::vector<int> vnMatches12(n1, -1), vnMatches21(n2, -1), vMatchedDistance(n2, INT_MAX);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    auto admit = [&](int t, int d) { return vMatchedDistance[t] > d; };   // if(vMatchedDistance[i2]<=dist) continue;
+    for (int i = 0; i < s.nitems; i++) {
+        int d1, b2, d2;
+        if (!s.best_two(i, admit, d1, b2, d2, INT_MAX)) {
+            if ((st = s.run(i, vMatchedDistance.data())) != ORB_OK) return st;
+            s.best_two(i, admit, d1, b2, d2, INT_MAX);
+        }
+        const int i1 = s.item_q[i];
+        if (d1 <= TH_LOW && d1 < (float)d2 * nnratio) {   // :457-459
+            if (vnMatches21[b2] >= 0) {
+                vnMatches12[vnMatches21[b2]] = -1;
+                nmatches--;
+            }
+            vnMatches12[i1] = b2;
+            vnMatches21[b2] = i1;
+            vMatchedDistance[b2] = d1;
+            nmatches++;
+            if (check_ori) rotHist[rot_bin(kps1[i1].angle, kps2[b2].angle)].push_back(i1);
+        }
+    }
+    if (check_ori) cull_rotation(rotHist, vnMatches12, nmatches);
+    std::memcpy(match12, vnMatches12.data(), (size_t)n1 * sizeof(int));
+    if (nmatches_out) *nmatches_out = nmatches;
+    return ORB_OK;
+}
+
+/* Frame::GetFeaturesInArea over the Frame grid (Frame.cc:378-392, 494-560) */
+int orb_features_in_area(int n, const orb_keypoint* kps_un, float mnMinX, float mnMaxX, float mnMinY, float mnMaxY,
+                         float x, float y, float r, int minLevel, int maxLevel, int* out, int cap) {
+    const int COLS = 64, ROWS = 48;   // Frame.h:39-40
+    const float gw = static_cast<float>(COLS) / static_cast<float>(mnMaxX - mnMinX);
+    const float gh = static_cast<float>(ROWS) / static_cast<float>(mnMaxY - mnMinY);
+    std::vector<std::vector<int>> grid((size_t)COLS * ROWS);
+    for (int i = 0; i < n; i++) {
+        const int px = (int)std::round((kps_un[i].x - mnMinX) * gw);
+        const int py = (int)std::round((kps_un[i].y - mnMinY) * gh);
+        if (px < 0 || px >= COLS || py < 0 || py >= ROWS) continue;
+        grid[(size_t)px * ROWS + py].push_back(i);
+    }
+    int cnt = 0;
+    const int x0 = std::max(0, (int)std::floor((x - mnMinX - r) * gw));
+    const int x1 = std::min(COLS - 1, (int)std::ceil((x - mnMinX + r) * gw));
+    const int y0 = std::max(0, (int)std::floor((y - mnMinY - r) * gh));
+    const int y1 = std::min(ROWS - 1, (int)std::ceil((y - mnMinY + r) * gh));
+    if (x0 >= COLS || x1 < 0 || y0 >= ROWS || y1 < 0) return 0;
+    const bool checkLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = x0; ix <= x1; ix++)
+        for (int iy = y0; iy <= y1; iy++)
+            for (int idx : grid[(size_t)ix * ROWS + iy]) {
+                const orb_keypoint& k = kps_un[idx];
+                if (checkLevels) {
+                    if (k.octave < minLevel) continue;
+                    if (maxLevel >= 0 && k.octave > maxLevel) continue;
+                }
+                if (std::fabs(k.x - x) < r && std::fabs(k.y - y) < r) {
+                    if (cnt < cap && out) out[cnt] = idx;
+                    cnt++;
+                }
+            }
+    return cnt > cap ? -cnt - 1 : cnt;
+}
+
+}  // extern "C"

@@ -1,0 +1,610 @@
+// liborbgpu host side: context, geometry, device buffers, and the extractor entry points of the C-ABI
+// (include/orbgpu.h).  Matcher entry points live in matcher.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orbgpu_ctx.h"
+
+namespace orbgpu {
+
+thread_local std::string g_last_error;
+
+void set_error(const char* what, hipError_t e) {
+    char buf[512];
+    if (e != hipSuccess) std::snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    else std::snprintf(buf, sizeof buf, "%s", what);
+    g_last_error = buf;
+}
+
+/* ---------------- ORBextractor tables (ORBextractor.cc:410-470) ---------------- */
+static inline int round_half_even(float v) { return (int)std::nearbyint(v); }   // cvRound(float)
+static inline int round_half_even(double v) { return (int)std::nearbyint(v); }  // cvRound(double)
+
+void compute_tables(Ctx* c) {
+    const int nl = c->p.nlevels;
+    const double sf = (double)c->p.scaleFactor;   // ORBextractor.h:98 keeps scaleFactor as double
+    c->scale[0] = 1.0f;
+    c->sigma2[0] = 1.0f;
+    for (int i = 1; i < nl; i++) {
+        c->scale[i] = (float)(c->scale[i - 1] * sf);
+        c->sigma2[i] = c->scale[i] * c->scale[i];
+    }
+    for (int i = 0; i < nl; i++) {
+        c->inv_scale[i] = 1.0f / c->scale[i];
+        c->inv_sigma2[i] = 1.0f / c->sigma2[i];
+    }
+    const float factor = (float)(1.0f / sf);
+    float ndesired = c->p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+    int sum = 0;
+    for (int l = 0; l < nl - 1; l++) {
+        c->n_per_level[l] = round_half_even(ndesired);
+        sum += c->n_per_level[l];
+        ndesired *= factor;
+    }
+    c->n_per_level[nl - 1] = std::max(c->p.nfeatures - sum, 0);
+    // umax: pre-computed ends of the rows of the circular patch (:454-469)
+    const int hp = kHalfPatch;
+    int v, v0, vmax = (int)std::floor(hp * std::sqrt(2.f) / 2 + 1);
+    int vmin = (int)std::ceil(hp * std::sqrt(2.f) / 2);
+    const double hp2 = hp * hp;
+    for (v = 0; v <= vmax; ++v) c->umax[v] = round_half_even(std::sqrt(hp2 - v * v));
+    for (v = hp, v0 = 0; v >= vmin; --v) {
+        while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
+        c->umax[v] = v0;
+        ++v0;
+    }
+    // Gaussian 7x7 sigma 2: getGaussianKernel(7, 2, CV_32F) -> convertTo(CV_32S, 256)
+    float cf[7];
+    double s = 0;
+    for (int i = 0; i < 7; i++) {
+        const double x = i - 3.0;
+        cf[i] = (float)std::exp(-0.5 / (2.0 * 2.0) * x * x);
+        s += cf[i];
+    }
+    s = 1. / s;
+    for (int i = 0; i < 7; i++) cf[i] = (float)(cf[i] * s);
+    for (int i = 0; i < 7; i++) c->gk[i] = round_half_even(cf[i] * 256.f);
+}
+
+/* ---------------- per-image-size geometry ---------------- */
+static void resize_coefs(int sw, int dw, std::vector<ResizeCoef>& out, bool vertical) {
+    // OpenCV 3.2 resize INTER_LINEAR coefficient setup (imgwarp.cpp)
+    const double scale = 1. / ((double)dw / sw);
+    for (int d = 0; d < dw; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s0 = (int)std::floor(f);
+        f -= s0;
+        if (!vertical) {
+            if (s0 < 0) { f = 0; s0 = 0; }
+            if (s0 + 1 >= sw && s0 >= sw - 1) { f = 0; s0 = sw - 1; }
+        }
+        ResizeCoef rc;
+        auto sat_short = [](int x) { return std::min(std::max(x, -32768), 32767); };
+        rc.c0 = sat_short(round_half_even((1.f - f) * 2048));
+        rc.c1 = sat_short(round_half_even(f * 2048));
+        rc.s0 = std::min(std::max(s0, 0), sw - 1);
+        rc.s1 = std::min(std::max(s0 + 1, 0), sw - 1);
+        out.push_back(rc);
+    }
+}
+
+int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs, int* rcoef_off) {
+    std::memset(&g, 0, sizeof g);
+    const int nl = c->p.nlevels;
+    g.nlevels = nl;
+    g.W = W;
+    g.H = H;
+    g.iniTh = std::min(std::max(c->p.iniThFAST, 0), 255);
+    g.minTh = std::min(std::max(c->p.minThFAST, 0), 255);
+    for (int i = 0; i < 16; i++) g.umax[i] = c->umax[i];
+    for (int i = 0; i < 7; i++) g.gk[i] = c->gk[i];
+    long long pyr = 0;
+    int cells = 0, cand = 0, kpc = 0, maxN = 0, maxNini = 0, maxLevelCand = 0;
+    coefs.clear();
+    for (int l = 0; l < nl; l++) {
+        LevelGeom& L = g.L[l];
+        L.w = round_half_even((float)W * c->inv_scale[l]);   // ComputePyramid :1112
+        L.h = round_half_even((float)H * c->inv_scale[l]);
+        L.pitch = (L.w + 63) & ~63;
+        if (l > 0) {
+            L.pyr_off = pyr;
+            pyr += (long long)L.pitch * L.h;
+            rcoef_off[l] = (int)coefs.size();
+            resize_coefs(g.L[l - 1].w, L.w, coefs, false);
+            resize_coefs(g.L[l - 1].h, L.h, coefs, true);
+        }
+        L.maxBX = L.w - kEdgeThreshold + 3;
+        L.maxBY = L.h - kEdgeThreshold + 3;
+        const float width = (float)(L.maxBX - kMinBorder), height = (float)(L.maxBY - kMinBorder);
+        L.nCols = (int)(width / 30.f);
+        L.nRows = (int)(height / 30.f);
+        if (L.nCols <= 0 || L.nRows <= 0 || L.w < 2 || L.h < 2) return ORB_ERR_GEOMETRY;
+        L.wCell = (int)std::ceil(width / L.nCols);
+        L.hCell = (int)std::ceil(height / L.nRows);
+        if (L.wCell + 6 > kFastMaxRoi || L.hCell + 6 > kFastMaxRoi) return ORB_ERR_GEOMETRY;
+        L.cell_base = cells;
+        cells += L.nCols * L.nRows;
+        L.cell_cap = ((L.wCell + 1) / 2) * ((L.hCell + 1) / 2);
+        L.cand_base = cand;
+        L.cand_cap = L.cell_cap * L.nCols * L.nRows;
+        cand += L.cand_cap;
+        maxLevelCand = std::max(maxLevelCand, L.cand_cap);
+        L.nfeat = c->n_per_level[l];
+        L.nIni = (int)std::round(width / (float)(L.maxBY - kMinBorder));   // DistributeOctTree :543
+        if (L.nIni <= 0) return ORB_ERR_GEOMETRY;                          // reference divides by zero
+        L.hX = width / L.nIni;
+        L.kp_cap = std::max(L.nfeat + 3, 4 * L.nIni) + 4;
+        L.kp_base = kpc;
+        kpc += L.kp_cap;
+        maxN = std::max(maxN, L.nfeat);
+        maxNini = std::max(maxNini, L.nIni);
+        L.scale = c->scale[l];
+        L.patch_size = (float)(int)(kPatchSize * c->scale[l]);
+    }
+    if (W > kMaxDim || H > kMaxDim) return ORB_ERR_GEOMETRY;
+    g.ncells = cells;
+    g.ncand = cand;
+    g.nkpcap = kpc;
+    g.pyr_bytes = (pyr + 255) & ~255LL;
+    g.max_level_cand = maxLevelCand;
+    int nc = std::max(maxN + 8, 4 * maxNini + 8);
+    nc = (nc + 63) & ~63;
+    g.node_cap = nc;
+    if (octree_lds_bytes(nc) > 160 * 1024) return ORB_ERR_GEOMETRY;
+    return ORB_OK;
+}
+
+/* ---------------- buffers ---------------- */
+template <class T>
+static hipError_t grow(T*& p, size_t& cap, size_t need) {
+    if (need <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc((void**)&p, std::max<size_t>(need, 256) * sizeof(T));
+    if (e == hipSuccess) cap = std::max<size_t>(need, 256);
+    return e;
+}
+
+int Ctx::ensure_geometry(int W, int H) {
+    if (have_geom && geom.W == W && geom.H == H) return ORB_OK;
+    Geom g;
+    std::vector<ResizeCoef> coefs;
+    int off[ORBGPU_MAX_LEVELS] = {0};
+    int st = build_geometry(this, W, H, g, coefs, off);
+    if (st != ORB_OK) {
+        set_error("image too small or too large for the configured pyramid", hipSuccess);
+        return st;
+    }
+    hipError_t e;
+    if ((e = grow(d_geom, geom_cap, 1)) != hipSuccess) return set_error("hipMalloc geom", e), ORB_ERR_NOMEM;
+    if ((e = grow(d_rcoef, rcoef_cap, coefs.size())) != hipSuccess) return set_error("hipMalloc coef", e), ORB_ERR_NOMEM;
+    if ((e = hipMemcpyAsync(d_geom, &g, sizeof g, hipMemcpyHostToDevice, stream)) != hipSuccess)
+        return set_error("upload geom", e), ORB_ERR_HIP;
+    if ((e = hipMemcpyAsync(d_rcoef, coefs.data(), coefs.size() * sizeof(ResizeCoef), hipMemcpyHostToDevice,
+                            stream)) != hipSuccess)
+        return set_error("upload coefs", e), ORB_ERR_HIP;
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
+    geom = g;
+    std::memcpy(rcoef_off, off, sizeof off);
+    have_geom = true;
+    return ORB_OK;
+}
+
+int Ctx::ensure_frames(int nframes) {
+    const Geom& g = geom;
+    hipError_t e;
+    const size_t nl = g.nlevels;
+    if ((e = grow(d_pyr, pyr_cap, (size_t)nframes * g.pyr_bytes)) != hipSuccess ||
+        (e = grow(d_cands, cands_cap, (size_t)nframes * g.ncand)) != hipSuccess ||
+        (e = grow(d_cellCount, cellc_cap, (size_t)nframes * g.ncells)) != hipSuccess ||
+        (e = grow(d_keys, keys_cap, (size_t)nframes * nl * g.max_level_cand)) != hipSuccess ||
+        (e = grow(d_knode, knode_cap, (size_t)nframes * nl * g.max_level_cand)) != hipSuccess ||
+        (e = grow(d_lvlKps, lvlkps_cap, (size_t)nframes * g.nkpcap)) != hipSuccess ||
+        (e = grow(d_lvlCount, lvlc_cap, (size_t)nframes * nl)) != hipSuccess ||
+        (e = grow(d_err, err_cap, 1)) != hipSuccess) {
+        set_error("device allocation for the extractor", e);
+        return ORB_ERR_NOMEM;
+    }
+    return ORB_OK;
+}
+
+ExtractBuffers Ctx::buffers() const {
+    ExtractBuffers b;
+    b.d_geom = d_geom;
+    b.d_rcoef = d_rcoef;
+    std::memcpy(b.rcoef_off, rcoef_off, sizeof rcoef_off);
+    b.d_pyr = d_pyr;
+    b.d_cands = d_cands;
+    b.d_cellCount = d_cellCount;
+    b.d_keys = d_keys;
+    b.d_knode = d_knode;
+    b.d_lvlKps = d_lvlKps;
+    b.d_lvlCount = d_lvlCount;
+    b.d_err = d_err;
+    return b;
+}
+
+void Ctx::marker(void* user, int id, int begin) {
+    Ctx* c = (Ctx*)user;
+    if (!c->prof_on) return;
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return;
+    hipEventRecord(ev, c->stream);
+    if (begin) c->prof_open[id] = ev;
+    else c->prof_pairs.push_back({id, c->prof_open[id], ev});
+}
+
+int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
+                     uint8_t* d_desc, int* d_counts, int kp_cap) {
+    hipError_t e = hipMemsetAsync(d_err, 0, sizeof(int), stream);
+    if (e != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
+    e = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
+                       stream, &Ctx::marker, this);
+    if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
+    last_frames = d_frames;
+    last_frame_pitch = frame_pitch;
+    last_row_stride = row_stride;
+    last_nframes = nframes;
+    level_cache_valid = 0;
+    return ORB_OK;
+}
+
+}  // namespace orbgpu
+
+using namespace orbgpu;
+
+#define CTX_GUARD(ctx)                                                              \
+    if (!(ctx)) {                                                                   \
+        set_error("NULL context", hipSuccess);                                      \
+        return ORB_ERR_ARG;                                                         \
+    }                                                                               \
+    {                                                                               \
+        hipError_t _e = hipSetDevice((ctx)->device);                                \
+        if (_e != hipSuccess) return set_error("hipSetDevice", _e), ORB_ERR_HIP;    \
+    }
+
+extern "C" {
+
+int orb_abi_version(void) { return ORBGPU_ABI_VERSION; }
+const char* orb_last_error(void) { return g_last_error.c_str(); }
+
+int orb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+orb_ctx* orb_create(const orb_params* p, int* status) {
+    auto fail = [&](int st) -> orb_ctx* {
+        if (status) *status = st;
+        return nullptr;
+    };
+    if (!p || p->nlevels < 1 || p->nlevels > ORBGPU_MAX_LEVELS || p->nfeatures < 0 || !(p->scaleFactor > 1.0f)) {
+        set_error("invalid orb_params", hipSuccess);
+        return fail(ORB_ERR_ARG);
+    }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || p->device < 0 || p->device >= ndev) {
+        set_error("no HIP device (liborbgpu has no CPU fallback)", e);
+        return fail(ORB_ERR_HIP);
+    }
+    if ((e = hipSetDevice(p->device)) != hipSuccess) return set_error("hipSetDevice", e), fail(ORB_ERR_HIP);
+    Ctx* c = new (std::nothrow) Ctx();
+    if (!c) return fail(ORB_ERR_NOMEM);
+    c->p = *p;
+    c->device = p->device;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        delete c;
+        set_error("hipStreamCreate", e);
+        return fail(ORB_ERR_HIP);
+    }
+    compute_tables(c);
+    if (p->max_width > 0 && p->max_height > 0) {
+        int st = c->ensure_geometry(p->max_width, p->max_height);
+        if (st == ORB_OK) st = c->ensure_frames(std::max(1, p->max_batch));
+        if (st != ORB_OK) {
+            orb_destroy(reinterpret_cast<orb_ctx*>(c));
+            return fail(st);
+        }
+    }
+    if (status) *status = ORB_OK;
+    return reinterpret_cast<orb_ctx*>(c);
+}
+
+void orb_destroy(orb_ctx* h) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& pr : c->prof_pairs) {
+        (void)hipEventDestroy(pr.b);
+        (void)hipEventDestroy(pr.e);
+    }
+    void* bufs[] = {c->d_geom, c->d_rcoef, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
+                    c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_kps, c->d_desc, c->d_counts,
+                    c->d_scratch};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int orb_scale_tables(const orb_ctx* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                     int* n_per_level, int* umax16) {
+    const Ctx* c = reinterpret_cast<const Ctx*>(h);
+    if (!c) return ORB_ERR_ARG;
+    const int nl = c->p.nlevels;
+    for (int i = 0; i < nl; i++) {
+        if (scale) scale[i] = c->scale[i];
+        if (inv_scale) inv_scale[i] = c->inv_scale[i];
+        if (sigma2) sigma2[i] = c->sigma2[i];
+        if (inv_sigma2) inv_sigma2[i] = c->inv_sigma2[i];
+        if (n_per_level) n_per_level[i] = c->n_per_level[i];
+    }
+    if (umax16)
+        for (int i = 0; i < 16; i++) umax16[i] = c->umax[i];
+    return ORB_OK;
+}
+
+int orb_batch_kp_cap(orb_ctx* h, int w, int hgt) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    int st = c->ensure_geometry(w, hgt);
+    if (st != ORB_OK) return st;
+    return c->geom.nkpcap;
+}
+
+int orb_extract_batch_device(orb_ctx* h, const uint8_t* d_frames, int nframes, int w, int hgt, size_t frame_pitch,
+                             size_t row_stride, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int kp_cap) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (!d_frames || nframes <= 0 || !d_kps || !d_desc || !d_counts || row_stride < (size_t)w)
+        return set_error("orb_extract_batch_device: bad arguments", hipSuccess), ORB_ERR_ARG;
+    int st = c->ensure_geometry(w, hgt);
+    if (st != ORB_OK) return st;
+    if (kp_cap < c->geom.nkpcap) {
+        set_error("kp_cap smaller than orb_batch_kp_cap()", hipSuccess);
+        return ORB_ERR_CAPACITY;
+    }
+    if ((st = c->ensure_frames(nframes)) != ORB_OK) return st;
+    return c->run_extract(d_frames, nframes, (long long)frame_pitch, (int)row_stride, d_kps, d_desc, d_counts, kp_cap);
+}
+
+int orb_sync(orb_ctx* h) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return set_error("hipStreamSynchronize", e), ORB_ERR_HIP;
+    int err = 0;
+    if (c->d_err && (e = hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess)
+        return set_error("read error flag", e), ORB_ERR_HIP;
+    if (err) {
+        set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
+        return ORB_ERR_INTERNAL;
+    }
+    return ORB_OK;
+}
+
+int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, orb_keypoint* kps, int cap, int* n,
+                uint8_t* desc) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (!img || w <= 0 || hgt <= 0) return ORB_OK;   // _image.empty(): outputs untouched (:1046-1047)
+    if (!n || stride < (size_t)w) return set_error("orb_extract: bad arguments", hipSuccess), ORB_ERR_ARG;
+    int st = c->ensure_geometry(w, hgt);
+    if (st != ORB_OK) return st;
+    if ((st = c->ensure_frames(1)) != ORB_OK) return st;
+    hipError_t e;
+    const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
+    const int kcap = c->geom.nkpcap;
+    if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess ||
+        (e = grow(c->d_kps, c->kps_cap, (size_t)kcap)) != hipSuccess ||
+        (e = grow(c->d_desc, c->desc_cap, (size_t)kcap * 32)) != hipSuccess ||
+        (e = grow(c->d_counts, c->counts_cap, 1)) != hipSuccess)
+        return set_error("device allocation", e), ORB_ERR_NOMEM;
+    if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return set_error("upload image", e), ORB_ERR_HIP;
+    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, c->d_kps, c->d_desc, c->d_counts,
+                             kcap)) != ORB_OK)
+        return st;
+    int nk = 0;
+    if ((e = hipMemcpyAsync(&nk, c->d_counts, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return set_error("download count", e), ORB_ERR_HIP;
+    if ((st = orb_sync(h)) != ORB_OK) return st;
+    if (nk > cap || !kps || !desc) {
+        *n = nk;
+        set_error("orb_extract: output capacity too small", hipSuccess);
+        return ORB_ERR_CAPACITY;
+    }
+    if (nk > 0) {
+        if ((e = hipMemcpyAsync(kps, c->d_kps, (size_t)nk * sizeof(orb_keypoint), hipMemcpyDeviceToHost, c->stream)) !=
+                hipSuccess ||
+            (e = hipMemcpyAsync(desc, c->d_desc, (size_t)nk * 32, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+            return set_error("download keypoints", e), ORB_ERR_HIP;
+    }
+    *n = nk;
+    return ORB_OK;
+}
+
+static int level_view(Ctx* c, int frame, int level, uint8_t* dst, int* w, int* hgt) {
+    if (!c->have_geom || frame < 0 || frame >= c->last_nframes || level < 0 || level >= c->geom.nlevels)
+        return set_error("no such level/frame", hipSuccess), ORB_ERR_ARG;
+    const LevelGeom& L = c->geom.L[level];
+    *w = L.w;
+    *hgt = L.h;
+    if (!dst) return ORB_OK;
+    hipError_t e;
+    if (level == 0)
+        e = hipMemcpy2DAsync(dst, L.w, c->last_frames + frame * c->last_frame_pitch, c->last_row_stride, L.w, L.h,
+                             hipMemcpyDeviceToHost, c->stream);
+    else
+        e = hipMemcpy2DAsync(dst, L.w, c->d_pyr + frame * c->geom.pyr_bytes + L.pyr_off, L.pitch, L.w, L.h,
+                             hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return set_error("download level", e), ORB_ERR_HIP;
+    return ORB_OK;
+}
+
+int orb_get_level(orb_ctx* h, int level, const uint8_t** data, int* w, int* hgt, size_t* stride) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (!data || !w || !hgt) return ORB_ERR_ARG;
+    int lw, lh;
+    int st = level_view(c, 0, level, nullptr, &lw, &lh);
+    if (st != ORB_OK) return st;
+    if (!(c->level_cache_valid & (1u << level))) {
+        c->level_host[level].resize((size_t)lw * lh);
+        if ((st = level_view(c, 0, level, c->level_host[level].data(), &lw, &lh)) != ORB_OK) return st;
+        c->level_cache_valid |= 1u << level;
+    }
+    *data = c->level_host[level].data();
+    *w = lw;
+    *hgt = lh;
+    if (stride) *stride = (size_t)lw;
+    return ORB_OK;
+}
+
+int orb_debug_level_image(orb_ctx* h, int frame, int level, uint8_t* out, int* w, int* hgt) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    return level_view(c, frame, level, out, w, hgt);
+}
+
+int orb_debug_candidates(orb_ctx* h, int frame, int level, int* out, int cap) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (!c->have_geom || frame < 0 || frame >= c->last_nframes || level < 0 || level >= c->geom.nlevels)
+        return ORB_ERR_ARG;
+    const LevelGeom& L = c->geom.L[level];
+    const int ncl = L.nCols * L.nRows;
+    std::vector<int> cnt(ncl);
+    std::vector<uint32_t> slots((size_t)L.cand_cap);
+    hipError_t e;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess ||
+        (e = hipMemcpy(cnt.data(), c->d_cellCount + (size_t)frame * c->geom.ncells + L.cell_base, ncl * sizeof(int),
+                       hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(slots.data(), c->d_cands + (size_t)frame * c->geom.ncand + L.cand_base,
+                       slots.size() * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+        return set_error("download candidates", e), ORB_ERR_HIP;
+    int n = 0;
+    for (int i = 0; i < ncl; i++)
+        for (int k = 0; k < cnt[i]; k++) {
+            const uint32_t v = slots[(size_t)i * L.cell_cap + k];
+            if (n < cap && out) {
+                out[3 * n] = v & 0xFFF;
+                out[3 * n + 1] = (v >> 12) & 0xFFF;
+                out[3 * n + 2] = v >> 24;
+            }
+            n++;
+        }
+    return n > cap ? -n - 1 : n;
+}
+
+int orb_debug_level_keypoints(orb_ctx* h, int frame, int level, int* out, int cap) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (!c->have_geom || frame < 0 || frame >= c->last_nframes || level < 0 || level >= c->geom.nlevels)
+        return ORB_ERR_ARG;
+    const LevelGeom& L = c->geom.L[level];
+    int n = 0;
+    std::vector<uint32_t> v((size_t)L.kp_cap);
+    hipError_t e;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess ||
+        (e = hipMemcpy(&n, c->d_lvlCount + (size_t)frame * c->geom.nlevels + level, sizeof(int),
+                       hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(v.data(), c->d_lvlKps + (size_t)frame * c->geom.nkpcap + L.kp_base, v.size() * 4,
+                       hipMemcpyDeviceToHost)) != hipSuccess)
+        return set_error("download level keypoints", e), ORB_ERR_HIP;
+    if (n > cap) return -n - 1;
+    for (int i = 0; i < n; i++) {
+        out[3 * i] = v[i] & 0xFFF;
+        out[3 * i + 1] = (v[i] >> 12) & 0xFFF;
+        out[3 * i + 2] = v[i] >> 24;
+    }
+    return n;
+}
+
+void* orb_device_alloc(orb_ctx* h, size_t bytes) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    if (!c || hipSetDevice(c->device) != hipSuccess) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+        set_error("hipMalloc", e);
+        return nullptr;
+    }
+    return p;
+}
+
+int orb_device_free(orb_ctx* h, void* p) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    hipError_t e = hipFree(p);
+    return e == hipSuccess ? ORB_OK : (set_error("hipFree", e), ORB_ERR_HIP);
+}
+
+int orb_memcpy_h2d(orb_ctx* h, void* dst, const void* src, size_t bytes) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? ORB_OK : (set_error("h2d", e), ORB_ERR_HIP);
+}
+
+int orb_memcpy_d2h(orb_ctx* h, void* dst, const void* src, size_t bytes) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? ORB_OK : (set_error("d2h", e), ORB_ERR_HIP);
+}
+
+int orb_memset_device(orb_ctx* h, void* dst, int value, size_t bytes) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    hipError_t e = hipMemsetAsync(dst, value, bytes, c->stream);
+    return e == hipSuccess ? ORB_OK : (set_error("memset", e), ORB_ERR_HIP);
+}
+
+int orb_profile_enable(orb_ctx* h, int on) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& pr : c->prof_pairs) {
+        (void)hipEventDestroy(pr.b);
+        (void)hipEventDestroy(pr.e);
+    }
+    c->prof_pairs.clear();
+    c->prof_on = on != 0;
+    return ORB_OK;
+}
+
+int orb_profile_read(orb_ctx* h, double* ms_total, int* launches) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
+    for (int k = 0; k < ORB_K_COUNT; k++) {
+        if (ms_total) ms_total[k] = 0;
+        if (launches) launches[k] = 0;
+    }
+    for (auto& pr : c->prof_pairs) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, pr.b, pr.e) != hipSuccess) continue;
+        if (ms_total) ms_total[pr.id] += ms;
+        if (launches) launches[pr.id] += 1;
+    }
+    return ORB_OK;
+}
+
+}  // extern "C"

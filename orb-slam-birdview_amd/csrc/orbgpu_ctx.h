@@ -1,0 +1,92 @@
+// liborbgpu context (the object behind the opaque orb_ctx*).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "orbgpu_internal.h"
+
+namespace orbgpu {
+
+void set_error(const char* what, hipError_t e);
+
+struct ProfPair {
+    int id;
+    hipEvent_t b, e;
+};
+
+struct Ctx {
+    orb_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+
+    // ORBextractor tables (ORBextractor.cc:410-470)
+    float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},
+        inv_sigma2[ORBGPU_MAX_LEVELS]{};
+    int n_per_level[ORBGPU_MAX_LEVELS]{};
+    int umax[16]{};
+    int gk[8]{};
+
+    // geometry of the current image size
+    bool have_geom = false;
+    Geom geom{};
+    int rcoef_off[ORBGPU_MAX_LEVELS]{};
+    Geom* d_geom = nullptr;
+    size_t geom_cap = 0;
+    ResizeCoef* d_rcoef = nullptr;
+    size_t rcoef_cap = 0;
+
+    // extractor work buffers (capacities in elements)
+    uint8_t* d_pyr = nullptr;
+    size_t pyr_cap = 0;
+    uint32_t* d_cands = nullptr;
+    size_t cands_cap = 0;
+    int* d_cellCount = nullptr;
+    size_t cellc_cap = 0;
+    uint32_t* d_keys = nullptr;
+    size_t keys_cap = 0;
+    uint16_t* d_knode = nullptr;
+    size_t knode_cap = 0;
+    uint32_t* d_lvlKps = nullptr;
+    size_t lvlkps_cap = 0;
+    int* d_lvlCount = nullptr;
+    size_t lvlc_cap = 0;
+    int* d_err = nullptr;
+    size_t err_cap = 0;
+
+    // host-image path (orb_extract)
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    orb_keypoint* d_kps = nullptr;
+    size_t kps_cap = 0;
+    uint8_t* d_desc = nullptr;
+    size_t desc_cap = 0;
+    int* d_counts = nullptr;
+    size_t counts_cap = 0;
+    void* h_pinned = nullptr;
+
+    // matcher scratch arena (bytes)
+    uint8_t* d_scratch = nullptr;
+    size_t scratch_cap = 0;
+
+    // last batch (for the mvImagePyramid view and debug reads)
+    const uint8_t* last_frames = nullptr;
+    long long last_frame_pitch = 0;
+    int last_row_stride = 0;
+    int last_nframes = 0;
+    unsigned level_cache_valid = 0;
+    std::vector<uint8_t> level_host[ORBGPU_MAX_LEVELS];
+
+    // profiling
+    bool prof_on = false;
+    hipEvent_t prof_open[ORB_K_COUNT]{};
+    std::vector<ProfPair> prof_pairs;
+
+    int ensure_geometry(int W, int H);
+    int ensure_frames(int nframes);
+    ExtractBuffers buffers() const;
+    int run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
+                    uint8_t* d_desc, int* d_counts, int kp_cap);
+    static void marker(void* user, int id, int begin);
+};
+
+}  // namespace orbgpu

@@ -1,0 +1,110 @@
+// Internal types shared by the host side and the gfx950 kernels of liborbgpu.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbgpu.h"
+
+namespace orbgpu {
+
+constexpr int kEdgeThreshold = 19;    // ORBextractor.cc:74
+constexpr int kMinBorder = kEdgeThreshold - 3;   // :773
+constexpr int kPatchSize = 31;        // :72
+constexpr int kHalfPatch = 15;        // :73
+constexpr int kMaxDim = 4096;         // candidate coordinates are packed in 12 bits
+constexpr int kFastTilePitch = 72;    // LDS pitch of a FAST cell ROI (ROI <= 66 px + 3 align)
+constexpr int kFastMaxRoi = 66;
+constexpr int kOctreeThreads = 512;
+constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3 (blur taps)
+constexpr int kDescWinPitch = 44;
+constexpr int kDescBlur = 37;         // blurred window: radius 18
+constexpr int kDescBlurPitch = 40;
+
+// Per-level geometry (host-computed once per image size; lives in device memory).
+struct LevelGeom {
+    int w, h;            // level size (ComputePyramid, ORBextractor.cc:1112)
+    int pitch;           // row pitch of the stored level (levels >= 1)
+    int pad0;
+    long long pyr_off;   // byte offset of the level inside a frame's pyramid slot (levels >= 1)
+    int maxBX, maxBY;    // maxBorderX/Y (:775-776)
+    int nCols, nRows, wCell, hCell;   // cell grid (:781-787)
+    int cell_base;       // first cell of the level within a frame
+    int cell_cap;        // candidate slots per cell: ceil(wCell/2)*ceil(hCell/2) (NMS independent set)
+    int cand_base;       // first candidate slot of the level within a frame
+    int cand_cap;        // candidate slots of the level
+    int nfeat;           // mnFeaturesPerLevel (:435-446)
+    int kp_cap, kp_base; // octree output slots
+    int nIni;            // DistributeOctTree root count (:543)
+    float hX;            // root width (:545)
+    float scale;         // mvScaleFactor
+    float patch_size;    // (int)(PATCH_SIZE*scale) (:837)
+    int pad1;
+};
+
+struct Geom {
+    int nlevels, W, H;
+    int ncells;          // cells per frame
+    int ncand;           // candidate slots per frame
+    int nkpcap;          // octree output slots per frame
+    long long pyr_bytes; // pyramid bytes per frame (levels >= 1)
+    int iniTh, minTh;
+    int node_cap;        // octree LDS node capacity
+    int max_level_cand;  // max cand_cap over levels (octree key scratch per level)
+    int umax[16];        // ORBextractor.cc:454-469
+    int gk[8];           // 7-tap Gaussian, sigma 2, 8-bit fixed point (getGaussianKernel x 256)
+    LevelGeom L[ORBGPU_MAX_LEVELS];
+};
+
+// cv::resize INTER_LINEAR coefficient tables (OpenCV 3.2 imgwarp.cpp), one entry per dst column/row.
+struct ResizeCoef {
+    int s0, s1;          // source column/row indices (clamped)
+    int c0, c1;          // 11-bit fixed-point weights (saturate_cast<short>(w*2048))
+};
+
+// Kernel launchers (extract_kernels.hip / hamming_kernels.hip).
+struct ExtractBuffers {
+    const Geom* d_geom;
+    const ResizeCoef* d_rcoef;     // per level: w_l x-coefs then h_l y-coefs, at rcoef_off[l]
+    int rcoef_off[ORBGPU_MAX_LEVELS];
+    uint8_t* d_pyr;                // nframes * pyr_bytes
+    uint32_t* d_cands;             // nframes * ncand
+    int* d_cellCount;              // nframes * ncells
+    uint32_t* d_keys;              // nframes * nlevels * max_level_cand
+    uint16_t* d_knode;             // same
+    uint32_t* d_lvlKps;            // nframes * nkpcap
+    int* d_lvlCount;               // nframes * nlevels
+    int* d_err;                    // 1 int: internal overflow flag
+};
+
+typedef void (*KernelMarker)(void* user, int kernel_id, int begin);
+
+hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
+                          int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
+                          int kp_cap, hipStream_t stream, KernelMarker marker, void* user);
+
+// d_ranges: per query [begin, end) into d_cand_idx, or NULL = all trains.
+hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, const int2* d_ranges,
+                               const int* d_cand_idx, const int* d_thr, int k, int* d_dist, int* d_idx,
+                               int* d_nvalid, hipStream_t stream);
+
+int top2_slices(int nq, int nt);   // train slices of the all-pairs top-2 (scratch = slices*nq int4)
+hipError_t launch_hamming_top2(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int* d_best,
+                               int* d_best_idx, int* d_second, int4* d_part, hipStream_t stream);
+
+struct TriParams {
+    float F[9];
+    float ex, ey;
+    float scale2[ORBGPU_MAX_LEVELS];
+    float sigma2[ORBGPU_MAX_LEVELS];
+    int only_stereo;
+};
+// One work item per (query idx1, candidate range): returns best idx2 (or -1) per item.
+hipError_t launch_triangulation(const uint8_t* d_desc1, const orb_keypoint* d_kps1, const float* d_ur1,
+                                const uint8_t* d_desc2, const orb_keypoint* d_kps2, const uint8_t* d_mp2,
+                                const float* d_ur2, const int* d_item_q, const int2* d_ranges,
+                                const int* d_cand_idx, int nitems, const TriParams& tp, int* d_best,
+                                hipStream_t stream);
+
+size_t octree_lds_bytes(int node_cap);
+
+}  // namespace orbgpu

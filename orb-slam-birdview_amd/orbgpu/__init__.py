@@ -1,0 +1,344 @@
+"""orbgpu — MI355X-native ORB front-end (Python mirror of the reference C++ interface).
+
+ORBextractor / ORBmatcher keep the names, argument meaning and return conventions of
+donglinb/ORB-SLAM-BIRDVIEW include/ORBextractor.h:45-111 and include/ORBmatcher.h:37-119, with
+OpenCV containers replaced by numpy: keypoints are a structured array with cv::KeyPoint's 28-byte
+layout (KP_DTYPE), descriptors an (n, 32) uint8 array, FeatureVectors a dict {node_id: [indices]}.
+Every call runs on the GPU through liborbgpu.so (include/orbgpu.h); there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import OrbError, OrbFeatVec, OrbParams, check, lib
+
+__all__ = ["ORBextractor", "ORBmatcher", "BatchExtractor", "KP_DTYPE", "OrbError", "device_count",
+           "features_in_area"]
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+TH_LOW, TH_HIGH, HISTO_LENGTH = 50, 100, 30   # ORBmatcher.cc:37-39
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def device_count():
+    return lib().orb_device_count()
+
+
+class _Ctx:
+    def __init__(self, nfeatures, scale_factor, nlevels, ini_th, min_th, device=0, max_width=0,
+                 max_height=0, max_batch=1):
+        self.params = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th, device, max_width,
+                                max_height, max_batch)
+        st = ctypes.c_int()
+        self.h = lib().orb_create(ctypes.byref(self.params), ctypes.byref(st))
+        if not self.h:
+            raise OrbError(st.value, "orb_create")
+        self.nlevels = nlevels
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().orb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class ORBextractor(_Ctx):
+    """ORB_SLAM2::ORBextractor (ORBextractor.cc:410-470, 1043-1132) on one MI355X."""
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0):
+        super().__init__(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device)
+        n = nlevels
+        self._t = [np.zeros(n, np.float32) for _ in range(4)]
+        self._npl = np.zeros(n, np.int32)
+        self._umax = np.zeros(16, np.int32)
+        check(lib().orb_scale_tables(self.h, *[_p(a) for a in self._t], _p(self._npl), _p(self._umax)),
+              "orb_scale_tables")
+        self._last_shape = None
+
+    # getters (ORBextractor.h:63-83)
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return float(self.params.scaleFactor)
+
+    def GetScaleFactors(self):
+        return self._t[0].copy()
+
+    def GetInverseScaleFactors(self):
+        return self._t[1].copy()
+
+    def GetScaleSigmaSquares(self):
+        return self._t[2].copy()
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._t[3].copy()
+
+    @property
+    def mnFeaturesPerLevel(self):
+        return self._npl.copy()
+
+    @property
+    def umax(self):
+        return self._umax.copy()
+
+    def __call__(self, image, mask=None, keypoints=None, descriptors=None):
+        """operator()(image, mask, keypoints, descriptors): returns (keypoints, descriptors).
+
+        An empty image returns the given outputs untouched (ORBextractor.cc:1046-1047); mask is
+        ignored as in the reference (ORBextractor.h:58)."""
+        img = np.asarray(image)
+        if img.size == 0:
+            return keypoints, descriptors
+        assert img.dtype == np.uint8 and img.ndim == 2, "CV_8UC1 expected (ORBextractor.cc:1050)"
+        img = np.ascontiguousarray(img)
+        h, w = img.shape
+        cap = 4 * max(self.params.nfeatures, 1) + 256
+        while True:
+            kps = np.zeros(cap, KP_DTYPE)
+            desc = np.zeros((cap, 32), np.uint8)
+            n = ctypes.c_int(0)
+            st = lib().orb_extract(self.h, _p(img), w, h, img.strides[0], _p(kps), cap, ctypes.byref(n),
+                                   _p(desc))
+            if st == -3:
+                cap = n.value
+                continue
+            check(st, "orb_extract")
+            break
+        self._last_shape = (h, w)
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    @property
+    def mvImagePyramid(self):
+        """Host views of the last frame's pyramid levels (ORBextractor.h:85)."""
+        out = []
+        for l in range(self.nlevels):
+            ptr, w, h, stride = ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
+            check(lib().orb_get_level(self.h, l, ctypes.byref(ptr), ctypes.byref(w), ctypes.byref(h),
+                                      ctypes.byref(stride)), "orb_get_level")
+            buf = (ctypes.c_uint8 * (stride.value * h.value)).from_address(ptr.value)
+            out.append(np.ctypeslib.as_array(buf).reshape(h.value, stride.value)[:, :w.value].copy())
+        return out
+
+    # debug views (parity tests pinpoint the failing stage)
+    def debug_candidates(self, level, frame=0):
+        cap = 1 << 16
+        while True:
+            out = np.zeros((cap, 3), np.int32)
+            n = lib().orb_debug_candidates(self.h, frame, level, _p(out), cap)
+            if n >= 0:
+                return out[:n]
+            if n == -1:
+                raise OrbError(n, "orb_debug_candidates")
+            cap = -n
+
+    def debug_level_keypoints(self, level, frame=0):
+        out = np.zeros((1 << 15, 3), np.int32)
+        n = lib().orb_debug_level_keypoints(self.h, frame, level, _p(out), len(out))
+        if n < 0:
+            raise OrbError(n, "orb_debug_level_keypoints")
+        return out[:n]
+
+
+class BatchExtractor(_Ctx):
+    """Device-resident batched extraction (orb_extract_batch_device): frames already in HBM."""
+
+    def __init__(self, nfeatures, width, height, batch, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
+                 device=0):
+        super().__init__(nfeatures, scale_factor, nlevels, ini_th, min_th, device, width, height, batch)
+        self.w, self.hgt, self.batch = width, height, batch
+        self.kp_cap = lib().orb_batch_kp_cap(self.h, width, height)
+        if self.kp_cap < 0:
+            raise OrbError(self.kp_cap, "orb_batch_kp_cap")
+        self.pitch = width
+        self.d_frames = self._alloc(batch * width * height)
+        self.d_kps = self._alloc(batch * self.kp_cap * 28)
+        self.d_desc = self._alloc(batch * self.kp_cap * 32)
+        self.d_counts = self._alloc(batch * 4)
+
+    def _alloc(self, nbytes):
+        p = lib().orb_device_alloc(self.h, nbytes)
+        if not p:
+            raise OrbError(-5, "orb_device_alloc")
+        return p
+
+    def upload(self, frames):
+        frames = np.ascontiguousarray(frames, np.uint8)
+        assert frames.shape == (self.batch, self.hgt, self.w)
+        check(lib().orb_memcpy_h2d(self.h, self.d_frames, _p(frames), frames.nbytes), "h2d")
+
+    def launch(self, nframes=None):
+        n = self.batch if nframes is None else nframes
+        check(lib().orb_extract_batch_device(self.h, self.d_frames, n, self.w, self.hgt, self.w * self.hgt,
+                                             self.w, self.d_kps, self.d_desc, self.d_counts, self.kp_cap),
+              "orb_extract_batch_device")
+
+    def sync(self):
+        check(lib().orb_sync(self.h), "orb_sync")
+
+    def counts(self):
+        out = np.zeros(self.batch, np.int32)
+        check(lib().orb_memcpy_d2h(self.h, _p(out), self.d_counts, out.nbytes), "d2h")
+        return out
+
+    def results(self, frame):
+        n = int(self.counts()[frame])
+        kps = np.zeros(self.kp_cap, KP_DTYPE)
+        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        check(lib().orb_memcpy_d2h(self.h, _p(kps), self.d_kps + frame * self.kp_cap * 28, kps.nbytes), "d2h")
+        check(lib().orb_memcpy_d2h(self.h, _p(desc), self.d_desc + frame * self.kp_cap * 32, desc.nbytes), "d2h")
+        return kps[:n], desc[:n]
+
+    def profile(self, on=True):
+        check(lib().orb_profile_enable(self.h, int(on)), "orb_profile_enable")
+
+    def profile_read(self):
+        ms = np.zeros(5, np.float64)
+        n = np.zeros(5, np.int32)
+        check(lib().orb_profile_read(self.h, _p(ms), _p(n)), "orb_profile_read")
+        return ms, n
+
+    def hamming_top2(self, d_q, nq, d_t, nt, d_best, d_idx, d_second):
+        check(lib().orb_hamming_top2_device(self.h, d_q, nq, d_t, nt, d_best, d_idx, d_second),
+              "orb_hamming_top2_device")
+
+    def close(self):
+        if getattr(self, "h", None):
+            for p in ("d_frames", "d_kps", "d_desc", "d_counts"):
+                if getattr(self, p, None):
+                    lib().orb_device_free(self.h, getattr(self, p))
+                    setattr(self, p, None)
+        super().close()
+
+
+def _featvec(fv):
+    """dict {node_id: [indices]} (DBoW2::FeatureVector) -> (OrbFeatVec, keepalive)."""
+    ids = np.array(sorted(fv.keys()), np.uint32)
+    groups = [np.asarray(fv[int(k)], np.int32) for k in ids]
+    off = np.zeros(len(groups) + 1, np.int32)
+    if groups:
+        off[1:] = np.cumsum([len(g) for g in groups])
+    idx = np.ascontiguousarray(np.concatenate(groups) if groups else np.zeros(1, np.int32), np.int32)
+    s = OrbFeatVec(len(ids), ids.ctypes.data if len(ids) else None, off.ctypes.data, idx.ctypes.data)
+    return s, (ids, off, idx)
+
+
+def features_in_area(kps_un, min_x, max_x, min_y, max_y, x, y, r, min_level=-1, max_level=-1):
+    """Frame::GetFeaturesInArea (Frame.cc:494-547) over the 64x48 grid."""
+    k = np.ascontiguousarray(kps_un, KP_DTYPE)
+    out = np.zeros(max(1, len(k)), np.int32)
+    n = lib().orb_features_in_area(len(k), _p(k), min_x, max_x, min_y, max_y, x, y, r, min_level, max_level,
+                                   _p(out), len(out))
+    return out[:n]
+
+
+class ORBmatcher:
+    """ORB_SLAM2::ORBmatcher's descriptor matchers (ORBmatcher.cc) on the GPU."""
+
+    _shared_ctx = {}
+
+    def __init__(self, nnratio=0.6, checkOri=True, device=0):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        key = device
+        if key not in ORBmatcher._shared_ctx:   # matchers are stack objects in the reference: share a context
+            ORBmatcher._shared_ctx[key] = _Ctx(1000, 1.2, 8, 20, 7, device)
+        self._ctx = ORBmatcher._shared_ctx[key]
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return lib().orb_descriptor_distance(_p(a), _p(b))
+
+    def hamming_topk(self, q, t, k=2, cand_off=None, cand_idx=None, train_thr=None):
+        q = np.ascontiguousarray(q, np.uint8)
+        t = np.ascontiguousarray(t, np.uint8)
+        nq = len(q)
+        dist = np.zeros((nq, k), np.int32)
+        idx = np.zeros((nq, k), np.int32)
+        nv = np.zeros(nq, np.int32)
+        co = None if cand_off is None else np.ascontiguousarray(cand_off, np.int32)
+        cx = None if cand_idx is None else np.ascontiguousarray(cand_idx, np.int32)
+        th = None if train_thr is None else np.ascontiguousarray(train_thr, np.int32)
+        check(lib().orb_hamming_topk(self._ctx.h, _p(q), nq, _p(t), len(t), _p(co), _p(cx), _p(th), k,
+                                     _p(dist), _p(idx), _p(nv)), "orb_hamming_topk")
+        return dist, idx, nv
+
+    def SearchByBoW_KF_F(self, desc_kf, angle_kf, mp_kf, featvec_kf, desc_f, angle_f, featvec_f):
+        """SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (ORBmatcher.cc:159-288).
+        Returns (nmatches, match_f) with match_f[iF] = KF feature index or -1."""
+        fa, ka = _featvec(featvec_kf)
+        fb, kb = _featvec(featvec_f)
+        a = [np.ascontiguousarray(x) for x in (desc_kf, np.asarray(angle_kf, np.float32),
+                                                np.asarray(mp_kf, np.uint8), desc_f,
+                                                np.asarray(angle_f, np.float32))]
+        out = np.full(len(a[3]), -1, np.int32)
+        nm = ctypes.c_int()
+        check(lib().orb_search_by_bow_kf_f(self._ctx.h, self.mfNNratio, int(self.mbCheckOrientation), len(a[0]),
+                                           _p(a[0]), _p(a[1]), _p(a[2]), fa, len(a[3]), _p(a[3]), _p(a[4]), fb,
+                                           _p(out), ctypes.byref(nm)), "SearchByBoW(KF,F)")
+        return nm.value, out
+
+    def SearchByBoW_KF_KF(self, desc1, angle1, mp1, featvec1, desc2, angle2, mp2, featvec2):
+        """SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&) (ORBmatcher.cc:522-655)."""
+        fa, ka = _featvec(featvec1)
+        fb, kb = _featvec(featvec2)
+        a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(angle1, np.float32), np.asarray(mp1, np.uint8),
+                                                desc2, np.asarray(angle2, np.float32), np.asarray(mp2, np.uint8))]
+        out = np.full(len(a[0]), -1, np.int32)
+        nm = ctypes.c_int()
+        check(lib().orb_search_by_bow_kf_kf(self._ctx.h, self.mfNNratio, int(self.mbCheckOrientation), len(a[0]),
+                                            _p(a[0]), _p(a[1]), _p(a[2]), fa, len(a[3]), _p(a[3]), _p(a[4]),
+                                            _p(a[5]), fb, _p(out), ctypes.byref(nm)), "SearchByBoW(KF,KF)")
+        return nm.value, out
+
+    def SearchForTriangulation(self, desc1, kps1, has_mp1, uright1, featvec1, desc2, kps2, has_mp2, uright2,
+                               featvec2, F12, ex, ey, scale_factors2, level_sigma2_2, bOnlyStereo=False):
+        """SearchForTriangulation (ORBmatcher.cc:657-823). Returns an (n, 2) array of (idx1, idx2)."""
+        fa, ka = _featvec(featvec1)
+        fb, kb = _featvec(featvec2)
+        a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(kps1, KP_DTYPE), np.asarray(has_mp1, np.uint8),
+                                                np.asarray(uright1, np.float32), desc2, np.asarray(kps2, KP_DTYPE),
+                                                np.asarray(has_mp2, np.uint8), np.asarray(uright2, np.float32),
+                                                np.asarray(F12, np.float32).reshape(9),
+                                                np.asarray(scale_factors2, np.float32),
+                                                np.asarray(level_sigma2_2, np.float32))]
+        cap = len(a[0]) + 1
+        pairs = np.zeros((cap, 2), np.int32)
+        n = ctypes.c_int()
+        check(lib().orb_search_for_triangulation(self._ctx.h, int(self.mbCheckOrientation), int(bOnlyStereo),
+                                                 len(a[0]), _p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]), fa, len(a[4]),
+                                                 _p(a[4]), _p(a[5]), _p(a[6]), _p(a[7]), fb, _p(a[8]), ex, ey,
+                                                 _p(a[9]), _p(a[10]), len(a[9]), _p(pairs), cap, ctypes.byref(n)),
+              "SearchForTriangulation")
+        return pairs[:n.value]
+
+    def _window(self, level0_only, desc1, kps1, desc2, kps2, cand_off, cand_idx):
+        a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(kps1, KP_DTYPE), desc2, np.asarray(kps2, KP_DTYPE),
+                                                np.asarray(cand_off, np.int32), np.asarray(cand_idx, np.int32))]
+        if len(a[5]) == 0:
+            a[5] = np.zeros(1, np.int32)
+        out = np.full(len(a[0]), -1, np.int32)
+        nm = ctypes.c_int()
+        check(lib().orb_window_match(self._ctx.h, self.mfNNratio, int(self.mbCheckOrientation), int(level0_only),
+                                     len(a[0]), _p(a[0]), _p(a[1]), len(a[2]), _p(a[2]), _p(a[3]), _p(a[4]),
+                                     _p(a[5]), _p(out), ctypes.byref(nm)), "window match")
+        return nm.value, out
+
+    def SearchForInitialization(self, desc1, kps1, desc2, kps2, cand_off, cand_idx):
+        """SearchForInitialization (ORBmatcher.cc:405-520); candidates = F2.GetFeaturesInArea per query.
+        Returns (nmatches, vnMatches12)."""
+        return self._window(True, desc1, kps1, desc2, kps2, cand_off, cand_idx)
+
+    def BirdviewMatch(self, desc1, kps1, desc2, kps2, cand_off, cand_idx):
+        """BirdviewMatch(const Frame&, const Frame&, vector<int>&, int) (ORBmatcher.cc:1790-1899)."""
+        return self._window(False, desc1, kps1, desc2, kps2, cand_off, cand_idx)

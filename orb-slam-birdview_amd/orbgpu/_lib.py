@@ -1,0 +1,103 @@
+"""ctypes loader for liborbgpu.so (the in-tree gfx950 build) — the only compute path.
+
+There is no CPU fallback: if the library is missing, or the HIP runtime has no device, the
+calls raise.  torch (if importable) is imported first so that the process holds exactly one HIP
+runtime (torch bundles its own libamdhip64.so.7; liborbgpu binds to whichever is loaded first).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "liborbgpu.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "orbgpu.h")
+
+_LIB = None
+
+vp, ci, cf, csz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ci), ("scaleFactor", cf), ("nlevels", ci), ("iniThFAST", ci),
+                ("minThFAST", ci), ("device", ci), ("max_width", ci), ("max_height", ci),
+                ("max_batch", ci)]
+
+
+class OrbFeatVec(ctypes.Structure):
+    _fields_ = [("nnodes", ci), ("node_ids", vp), ("offsets", vp), ("indices", vp)]
+
+
+# name -> (restype, argtypes); mirrors include/orbgpu.h
+SIGNATURES = {
+    "orb_abi_version": (ci, []),
+    "orb_last_error": (ctypes.c_char_p, []),
+    "orb_device_count": (ci, []),
+    "orb_create": (vp, [ctypes.POINTER(OrbParams), ctypes.POINTER(ci)]),
+    "orb_destroy": (None, [vp]),
+    "orb_scale_tables": (ci, [vp, vp, vp, vp, vp, vp, vp]),
+    "orb_extract": (ci, [vp, vp, ci, ci, csz, vp, ci, ctypes.POINTER(ci), vp]),
+    "orb_get_level": (ci, [vp, ci, ctypes.POINTER(vp), ctypes.POINTER(ci), ctypes.POINTER(ci),
+                           ctypes.POINTER(csz)]),
+    "orb_batch_kp_cap": (ci, [vp, ci, ci]),
+    "orb_extract_batch_device": (ci, [vp, vp, ci, ci, ci, csz, csz, vp, vp, vp, ci]),
+    "orb_sync": (ci, [vp]),
+    "orb_device_alloc": (vp, [vp, csz]),
+    "orb_device_free": (ci, [vp, vp]),
+    "orb_memcpy_h2d": (ci, [vp, vp, vp, csz]),
+    "orb_memcpy_d2h": (ci, [vp, vp, vp, csz]),
+    "orb_memset_device": (ci, [vp, vp, ci, csz]),
+    "orb_profile_enable": (ci, [vp, ci]),
+    "orb_profile_read": (ci, [vp, vp, vp]),
+    "orb_debug_candidates": (ci, [vp, ci, ci, vp, ci]),
+    "orb_debug_level_keypoints": (ci, [vp, ci, ci, vp, ci]),
+    "orb_debug_level_image": (ci, [vp, ci, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci)]),
+    "orb_descriptor_distance": (ci, [vp, vp]),
+    "orb_hamming_topk": (ci, [vp, vp, ci, vp, ci, vp, vp, vp, ci, vp, vp, vp]),
+    "orb_hamming_top2_device": (ci, [vp, vp, ci, vp, ci, vp, vp, vp]),
+    "orb_search_by_bow_kf_f": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp, vp, OrbFeatVec, vp,
+                                    ctypes.POINTER(ci)]),
+    "orb_search_by_bow_kf_kf": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, OrbFeatVec, vp,
+                                     ctypes.POINTER(ci)]),
+    "orb_search_for_triangulation": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, vp,
+                                          OrbFeatVec, vp, cf, cf, vp, vp, ci, vp, ci, ctypes.POINTER(ci)]),
+    "orb_window_match": (ci, [vp, cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, ctypes.POINTER(ci)]),
+    "orb_features_in_area": (ci, [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]),
+}
+
+STATUS = {0: "ORB_OK", -1: "ORB_ERR_ARG", -2: "ORB_ERR_HIP", -3: "ORB_ERR_CAPACITY",
+          -4: "ORB_ERR_GEOMETRY", -5: "ORB_ERR_NOMEM", -6: "ORB_ERR_INTERNAL"}
+
+
+class OrbError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        msg = lib().orb_last_error()
+        super().__init__(f"{where}: {STATUS.get(status, status)} ({msg.decode() if msg else ''})")
+
+
+def _preload_torch():
+    try:
+        import torch  # noqa: F401  (binds the process to torch's HIP runtime before liborbgpu loads)
+    except Exception:
+        pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is not built: run `make -C {PKG_ROOT}` (hipcc, gfx950)")
+        _preload_torch()
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(status, where=""):
+    if status != 0:
+        raise OrbError(status, where)
+    return status

@@ -1,0 +1,103 @@
+"""Deterministic synthetic gray frames for parity tests and the bench.
+
+Frame `idx` is seeded with splitmix64(0x5EED0000 + idx):
+  * bilinear value-noise background on a 16-px lattice, lattice values U[40, 215];
+  * 300 opaque axis-aligned rectangles then 100 filled circles (painter's order),
+    intensity U[0, 255];
+  * per-pixel integer noise U[-3, 3], clamped to [0, 255].
+This gives corners on rectangle vertices plus texture, so most FAST cells pass iniThFAST.
+Edge frames: `flat` (constant 128, zero keypoints) and `noise` (pure U[0,255], maximum
+candidate count, stresses the octree).  Stereo right frames are the left frame shifted by a
+seeded per-row-band disparity in [0, 64].
+
+Counter-based splitmix64: draw k of a stream with seed s is mix64(s + (k+1)*GOLDEN), which is
+exactly the k-th output of the sequential splitmix64 generator, vectorised with numpy.
+"""
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * _M1
+    z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+class SplitMix64:
+    def __init__(self, seed):
+        self.seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+        self.k = 0
+
+    def draw(self, n):
+        with np.errstate(over="ignore"):
+            ks = np.arange(self.k + 1, self.k + 1 + n, dtype=np.uint64)
+            out = _mix64(self.seed + ks * GOLDEN)
+        self.k += n
+        return out
+
+    def uniform_int(self, lo, hi, n):
+        """n integers uniform in [lo, hi] (inclusive)."""
+        span = np.uint64(hi - lo + 1)
+        return (self.draw(n) % span).astype(np.int64) + lo
+
+
+def synth_frame(w, h, idx=0, kind="scene"):
+    """Return a (h, w) uint8 frame."""
+    rng = SplitMix64(0x5EED0000 + idx)
+    if kind == "flat":
+        return np.full((h, w), 128, np.uint8)
+    if kind == "noise":
+        return rng.uniform_int(0, 255, w * h).astype(np.uint8).reshape(h, w)
+    if kind != "scene":
+        raise ValueError(kind)
+    cell = 16
+    gw, gh = w // cell + 2, h // cell + 2
+    lat = rng.uniform_int(40, 215, gw * gh).reshape(gh, gw).astype(np.int64)
+    ys, xs = np.mgrid[0:h, 0:w]
+    gx, gy = xs // cell, ys // cell
+    fx, fy = xs % cell, ys % cell
+    top = lat[gy, gx] * (cell - fx) + lat[gy, gx + 1] * fx
+    bot = lat[gy + 1, gx] * (cell - fx) + lat[gy + 1, gx + 1] * fx
+    img = (top * (cell - fy) + bot * fy + (cell * cell) // 2) // (cell * cell)
+    rect = rng.uniform_int(0, 1 << 30, 300 * 5).reshape(300, 5)
+    for x0, y0, rw, rh, val in rect:
+        x0 %= w
+        y0 %= h
+        rw = 4 + rw % max(1, w // 8)
+        rh = 4 + rh % max(1, h // 8)
+        img[y0:y0 + rh, x0:x0 + rw] = val % 256
+    circ = rng.uniform_int(0, 1 << 30, 100 * 4).reshape(100, 4)
+    rmax = max(4, min(w, h) // 16)
+    for cx, cy, r, val in circ:
+        cx %= w
+        cy %= h
+        r = 3 + r % rmax
+        y0, y1 = max(0, cy - r), min(h, cy + r + 1)
+        x0, x1 = max(0, cx - r), min(w, cx + r + 1)
+        yy, xx = np.mgrid[y0:y1, x0:x1]
+        m = (xx - cx) ** 2 + (yy - cy) ** 2 <= r * r
+        img[y0:y1, x0:x1][m] = val % 256
+    noise = rng.uniform_int(-3, 3, w * h).reshape(h, w)
+    return np.clip(img + noise, 0, 255).astype(np.uint8)
+
+
+def synth_stereo_right(left, idx=0, max_disp=64):
+    """Right view: left shifted by a seeded disparity per 16-row band (edge-replicated)."""
+    h, w = left.shape
+    rng = SplitMix64(0x5EED8000 + idx)
+    bands = (h + 15) // 16
+    disp = rng.uniform_int(0, max_disp, bands)
+    right = np.empty_like(left)
+    for b in range(bands):
+        d = int(disp[b])
+        rows = slice(16 * b, min(h, 16 * b + 16))
+        right[rows, :w - d] = left[rows, d:]
+        right[rows, w - d:] = left[rows, w - 1:w]
+    return right
+
+
+def synth_batch(w, h, n, first=0, kind="scene"):
+    return np.stack([synth_frame(w, h, first + i, kind) for i in range(n)])
