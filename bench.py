@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""ORB front-end throughput on MI355X — BASELINE.json metric:
+"ORB features/sec per GPU (1280x720, 2000 kp, 8 levels) + Hamming matches/sec".
+
+One step = one batched pass of the extraction hot path (pyramid -> per-cell FAST+NMS ->
+DistributeOctTree -> IC angle + Gaussian + rBRIEF) over `--batch` synthetic 1280x720 frames already
+resident in HBM, on each GPU.  Frames shard across GPUs (one process per GPU, no data-path
+collective: scaling "weak"); value = keypoints produced by all ranks / max-over-ranks time.
+
+Also reported on the same line:
+  roofline      dominant kernel's algorithmic bytes per launch / its HIP-event-timed duration
+                (events on liborbgpu's own stream, recorded inside the timed region)
+  cpu_baseline  the oracle restatement of ORBextractor (oracle/, kind "port") on the box's host
+                cores, rank 0 at N=1 only, bounded sample
+  hamming       all-pairs top-2 Hamming between consecutive frames' descriptors (SearchByBoW's
+                brute-force inner loop), matches/s = distance evaluations per second
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B --config c3|c2|c5 --no-cpu]
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "orb-slam-birdview_amd"))
+
+METRIC = "ORB features/sec per GPU (1280×720, 2000 kp, 8 levels) + Hamming matches/sec"
+CONFIGS = {   # BASELINE.json configs; C3 is the headline single-GPU workload
+    "c2": dict(w=640, h=480, nfeatures=1000, name="C2 640x480 synthetic, 1000 features, 8 levels"),
+    "c3": dict(w=1280, h=720, nfeatures=2000, name="C3 1280x720 KITTI-style synthetic, 2000 features, 8 levels"),
+    "c5": dict(w=1280, h=720, nfeatures=4000, name="C5 1280x720 synthetic, 4000 features, 8 levels"),
+}
+PEAK_HBM_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+KNAMES = ["resize", "fast", "octree", "describe", "hamming"]
+
+
+# ---------------------------------------------------------------- distributed plumbing
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def dist_init(world):
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo")   # timing reductions only: the data path has no collective
+    return dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def reduce_max_sum(dist, tmax, vsum):
+    """Max of tmax and sum of vsum over ranks."""
+    if dist is None:
+        return tmax, vsum
+    import torch
+    t = torch.tensor([tmax], dtype=torch.float64)
+    v = torch.tensor([vsum], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(v.item())
+
+
+def frame_range(rank, batch):
+    """Synthetic frame indices of a rank: each GPU extracts its own distinct frames."""
+    return rank * batch, batch
+
+
+# ---------------------------------------------------------------- algorithmic bytes
+def level_sizes(w, h, nl=8, sf=1.2):
+    import numpy as np
+    s = [np.float32(1.0)]
+    for _ in range(1, nl):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(sf))))
+    return [(int(np.rint(np.float32(w) * (np.float32(1) / x))), int(np.rint(np.float32(h) * (np.float32(1) / x))))
+            for x in s]
+
+
+def algorithmic_bytes(w, h, kps_per_frame, cands_per_frame):
+    """Per-frame compulsory bytes by kernel."""
+    lv = level_sizes(w, h)
+    P = [a * b for a, b in lv]
+    Ptot = sum(P)
+    K = kps_per_frame
+    C = cands_per_frame
+    return {
+        "resize": sum(P[:-1]) + sum(P[1:]),          # read level l-1, write level l
+        "fast": Ptot + 4 * C,                         # read every level once, write packed candidates
+        "octree": 4 * C + 4 * K,                      # read candidates, write survivors
+        "describe": K * (43 * 43 + 28 + 32),          # 43x43 window per keypoint, KeyPoint + descriptor out
+        "pipeline": 3 * Ptot + 1321 * K,              # SURVEY §8d B_extract = 3P + 1321K
+    }
+
+
+def read_pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["per_launch_bytes"].get(kernel)
+    except Exception:
+        return None
+
+
+# ---------------------------------------------------------------- CPU baseline (oracle, rank 0, N=1)
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, frames_np):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle   # test infrastructure: used ONLY as the timed CPU baseline here
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    nf = cfg["nfeatures"]
+    n1 = min(8, len(frames_np))
+    oracle.time_extract(frames_np[:2], nf, 1, 1)   # warm-up
+    t1, k1 = oracle.time_extract(frames_np[:n1], nf, nthreads=1, iters=1)
+    iters = max(1, (16 * threads) // len(frames_np))
+    tN, kN = oracle.time_extract(frames_np, nf, nthreads=threads, iters=iters)
+    single = k1 / t1
+    allcore = kN * iters / tN
+    return {"value": round(allcore, 1), "unit": "features/s", "cores": threads, "kind": "port",
+            "single_thread_value": round(single, 1), "single_thread_frames_per_s": round(n1 / t1, 2),
+            "frames_per_s": round(len(frames_np) * iters / tN, 2),
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"{len(frames_np) * iters} frames ({len(frames_np)} distinct, {cfg['w']}x{cfg['h']}, "
+                      f"{nf} features) frame-parallel on {threads} threads + {n1} frames single-thread; "
+                      f"oracle/orb_oracle.cpp -O3 -march=x86-64-v3 (restated CPU baseline, not OpenCV)"}
+
+
+# ---------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-hamming", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    dist = dist_init(world)
+    import numpy as np
+    import orbgpu
+    from orbgpu.synth import synth_batch
+
+    cfg = CONFIGS[args.config]
+    w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
+    first, count = frame_range(rank, B)
+    frames = synth_batch(w, h, count, first=first)
+    ex = orbgpu.BatchExtractor(nf, w, h, B, device=local)
+    ex.upload(frames)                         # inputs resident in HBM before timing
+
+    try:
+        import torch
+        has_torch_cuda = torch.cuda.is_available()
+    except Exception:
+        torch, has_torch_cuda = None, False
+
+    def sync():
+        ex.sync()
+        if has_torch_cuda:
+            torch.cuda.synchronize(local)
+
+    for _ in range(args.warmup):
+        ex.launch()
+    sync()
+    kps_per_step = int(ex.counts().sum())
+
+    ex.profile(True)
+    barrier(dist)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ex.launch()
+    sync()
+    t1 = time.perf_counter()
+    barrier(dist)
+    kms, klaunch = ex.profile_read()
+    ex.profile(False)
+    local_time = t1 - t0
+    local_kps = kps_per_step * args.steps
+    tmax, total_kps = reduce_max_sum(dist, local_time, local_kps)
+    _, total_frames = reduce_max_sum(dist, 0.0, float(B * args.steps))
+
+    # ---- Hamming: all-pairs top-2 between consecutive frames' descriptors (device-resident)
+    ham = None
+    if not args.no_hamming:
+        counts = ex.counts()
+        L = orbgpu._lib.lib()
+        nq = int(counts.min())
+        dbest = [ex._alloc(nq * 4) for _ in range(3)]
+        pairs = B - 1
+
+        def ham_step():
+            for f in range(pairs):
+                ex.hamming_top2(ex.d_desc + f * ex.kp_cap * 32, nq, ex.d_desc + (f + 1) * ex.kp_cap * 32, nq,
+                                *dbest)
+        ham_step()
+        sync()
+        ex.profile(True)
+        hs = max(2, args.steps // 4)
+        barrier(dist)
+        th0 = time.perf_counter()
+        for _ in range(hs):
+            ham_step()
+        sync()
+        th1 = time.perf_counter()
+        hms, hl = ex.profile_read()
+        ex.profile(False)
+        for p in dbest:
+            L.orb_device_free(ex.h, p)
+        evals = float(nq) * nq * pairs * hs
+        htmax, hevals = reduce_max_sum(dist, th1 - th0, evals)
+        kt = hms[4] / 1e3 / max(hl[4], 1)
+        ham = {"matches_per_s": round(hevals / htmax, 1), "queries_per_s": round(hevals / nq / htmax, 1),
+               "pair": f"{nq}x{nq} descriptors (frame f vs f+1), {pairs} pairs per step per GPU",
+               "kernel_avg_us": round(kt * 1e6, 2),
+               "kernel_valu_ops_per_s": round(16.0 * nq * nq / kt, 1) if kt > 0 else None,
+               "kernel_hbm_gbs": round((32.0 * 2 * nq + 12 * nq) / kt / 1e9, 2) if kt > 0 else None}
+
+    # ---- roofline of the dominant kernel (per-step algorithmic bytes / per-step kernel time)
+    per_frame_kps = kps_per_step / B
+    cands_per_frame = 0   # FAST survivors of frame 0 (all levels), from the debug view of the last batch
+    for l in range(8):
+        n = orbgpu._lib.lib().orb_debug_candidates(ex.h, 0, l, None, 0)
+        cands_per_frame += (-n - 1) if n < 0 else n
+    ab = algorithmic_bytes(w, h, per_frame_kps, cands_per_frame)
+    steps = args.steps
+    ms_per_step_k = {KNAMES[i]: kms[i] / steps for i in range(4)}
+    dom = max(ms_per_step_k, key=ms_per_step_k.get)
+    dom_bytes = ab[dom] * B
+    dom_s = ms_per_step_k[dom] / 1e3
+    achieved = dom_bytes / dom_s / 1e9
+    launches_per_step = klaunch[KNAMES.index(dom)] / steps
+    traffic = read_pmc_traffic(dom)
+    sum_k_s = sum(ms_per_step_k.values()) / 1e3
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 5),
+                "traffic": (traffic * launches_per_step / B if traffic is not None else None),
+                "algorithmic_bytes_per_frame": int(ab[dom]), "launches_per_step": launches_per_step,
+                "kernel_avg_launch_us": round(dom_s / launches_per_step * 1e6, 2),
+                "pipeline": {"bytes_per_frame": int(ab["pipeline"]),
+                             "achieved": round(ab["pipeline"] * B / sum_k_s / 1e9, 2),
+                             "frac": round(ab["pipeline"] * B / sum_k_s / 1e9 / PEAK_HBM_GBS, 5)}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(cfg, frames[:32])
+
+    if rank == 0:
+        value = total_kps / tmax
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "features/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+               "config": {"workload": cfg["name"], "width": w, "height": h, "nfeatures": nf, "nlevels": 8,
+                          "scale_factor": 1.2, "ini_th_fast": 20, "min_th_fast": 7, "batch_per_gpu": B,
+                          "global_batch": B * world, "parallelism": f"frame-sharded x{world} (no collective)"},
+               "frames_per_s": round(total_frames / tmax, 1),
+               "keypoints_per_frame": round(per_frame_kps, 1),
+               "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
+               "roofline": roofline, "cpu_baseline": cpu, "hamming": ham}
+        if cpu:
+            out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
+        print(json.dumps(out), flush=True)
+    ex.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

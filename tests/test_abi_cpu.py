@@ -1,0 +1,70 @@
+"""CPU: the C-ABI library loads, exports every symbol include/orbgpu.h declares, and its host-only
+helpers agree with the oracle.  No compute call needs a GPU here; without one orb_create must fail
+loudly (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "orbgpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(orb_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from orbgpu import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    names = _declared_symbols()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # the Python binding declares a signature for each of them
+    assert set(names) <= set(_lib.SIGNATURES), set(names) - set(_lib.SIGNATURES)
+
+
+def test_abi_version_and_keypoint_layout(orbgpu_mod):
+    from orbgpu import _lib
+    assert _lib.lib().orb_abi_version() == 1
+    assert orbgpu_mod.KP_DTYPE.itemsize == 28   # cv::KeyPoint
+
+
+def test_no_cpu_fallback_without_gpu(orbgpu_mod):
+    if orbgpu_mod.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(orbgpu_mod.OrbError):
+        orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+
+
+def test_invalid_params_rejected(orbgpu_mod):
+    with pytest.raises(orbgpu_mod.OrbError):
+        orbgpu_mod.ORBextractor(1000, 1.0, 8, 20, 7)   # scaleFactor must be > 1
+    with pytest.raises(orbgpu_mod.OrbError):
+        orbgpu_mod.ORBextractor(1000, 1.2, 40, 20, 7)  # > ORBGPU_MAX_LEVELS
+
+
+def test_descriptor_distance_host_helper(orbgpu_mod, oracle_mod):
+    rng = np.random.default_rng(0)
+    for _ in range(100):
+        a, b = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+        assert orbgpu_mod.ORBmatcher.DescriptorDistance(a, b) == oracle_mod.descriptor_distance(a, b)
+
+
+def test_features_in_area_host_helper(orbgpu_mod, oracle_mod):
+    rng = np.random.default_rng(7)
+    n = 400
+    k = np.zeros(n, orbgpu_mod.KP_DTYPE)
+    k["x"] = rng.uniform(-5, 645, n)
+    k["y"] = rng.uniform(-5, 485, n)
+    k["octave"] = rng.integers(0, 8, n)
+    for _ in range(30):
+        x, y, r = rng.uniform(0, 640), rng.uniform(0, 480), rng.uniform(5, 120)
+        lv = int(rng.integers(-1, 3))
+        a = orbgpu_mod.features_in_area(k, 0, 640, 0, 480, x, y, r, lv, lv)
+        b = oracle_mod.features_in_area(k, 0, 640, 0, 480, x, y, r, lv, lv)
+        assert a.tolist() == b.tolist()

@@ -1,0 +1,198 @@
+"""GPU parity: liborbgpu's HIP extractor vs the oracle restatement of ORBextractor.cc, bit-exact
+(keypoint structs byte-for-byte, descriptors byte-for-byte), stage by stage where it fails."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # (w, h, nfeatures, frame idx, kind) — BASELINE configs C2/C3/C5 at full size + edges
+    (320, 240, 500, 0, "scene"),
+    (640, 480, 1000, 0, "scene"),      # C2
+    (640, 480, 1000, 11, "scene"),
+    (1280, 720, 2000, 0, "scene"),     # C3
+    (1280, 720, 2000, 7, "scene"),
+    (1280, 720, 4000, 4, "scene"),     # C5 per-frame workload
+    (641, 479, 1000, 2, "scene"),      # odd sizes: blur tail columns, resize edges
+    (950, 400, 2000, 5, "scene"),      # mono_fisheye driver size (mono_fisheye.cc:111-116)
+    (640, 480, 1000, 0, "flat"),       # zero keypoints, released descriptors
+    (640, 480, 1000, 3, "noise"),      # maximum candidates: octree phase-2 stress
+    (1280, 720, 2000, 9, "noise"),
+    (640, 480, 100, 1, "scene"),       # tiny N per level
+    (640, 480, 8000, 1, "scene"),      # more features than candidates on some levels
+]
+
+
+def _stage_report(o, g):
+    msgs = []
+    pyr = g.mvImagePyramid
+    for l in range(8):
+        if not np.array_equal(o.level(l), pyr[l]):
+            msgs.append(f"pyramid level {l}")
+            break
+        if not np.array_equal(o.candidates(l), g.debug_candidates(l)):
+            msgs.append(f"FAST candidates level {l}")
+            break
+        ok = o.level_keypoints(l)
+        okx = np.stack([ok["x"], ok["y"], ok["response"]], 1).astype(np.int32)
+        if not np.array_equal(okx, g.debug_level_keypoints(l)):
+            msgs.append(f"octree level {l}")
+            break
+    return msgs
+
+
+@pytest.mark.parametrize("w,h,nf,idx,kind", CASES)
+def test_extract_bit_exact(orbgpu_mod, oracle_mod, w, h, nf, idx, kind):
+    from orbgpu.synth import synth_frame
+    img = synth_frame(w, h, idx, kind)
+    o = oracle_mod.OracleExtractor(nf)
+    ok_k, ok_d = o(img)
+    g = orbgpu_mod.ORBextractor(nf, 1.2, 8, 20, 7)
+    gk, gd = g(img)
+    if len(gk) != len(ok_k) or gk.tobytes() != ok_k.tobytes() or not np.array_equal(gd, ok_d):
+        pytest.fail(f"mismatch ({len(gk)} vs {len(ok_k)} keypoints); first failing stage: {_stage_report(o, g)}")
+
+
+def test_scale_tables_match_oracle(orbgpu_mod, oracle_mod):
+    for nf in (1000, 2000, 4000):
+        g = orbgpu_mod.ORBextractor(nf, 1.2, 8, 20, 7)
+        t = oracle_mod.OracleExtractor(nf).tables()
+        assert np.array_equal(g.GetScaleFactors(), t["scale"])
+        assert np.array_equal(g.GetInverseScaleFactors(), t["inv_scale"])
+        assert np.array_equal(g.GetScaleSigmaSquares(), t["sigma2"])
+        assert np.array_equal(g.GetInverseScaleSigmaSquares(), t["inv_sigma2"])
+        assert np.array_equal(g.mnFeaturesPerLevel, t["n_per_level"])
+        assert np.array_equal(g.umax, t["umax"])
+        assert g.GetLevels() == 8 and abs(g.GetScaleFactor() - 1.2) < 1e-6
+
+
+def test_other_parameters(orbgpu_mod, oracle_mod):
+    # fisheye.yaml (2000 / 1.2 / 8 / 15 / 5) and KITTI04-12 stereo (iniTh 12)
+    from orbgpu.synth import synth_frame
+    img = synth_frame(640, 480, 21)
+    for params in [(2000, 1.2, 8, 15, 5), (1000, 1.2, 8, 12, 7), (1500, 1.3, 6, 20, 7)]:
+        o = oracle_mod.OracleExtractor(params[0], params[1], params[2], params[3], params[4])
+        ok, od = o(img)
+        gk, gd = orbgpu_mod.ORBextractor(*params)(img)
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), params
+
+
+def test_empty_image_leaves_outputs_untouched(orbgpu_mod):
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    sentinel_k, sentinel_d = object(), object()
+    k, d = g(np.zeros((0, 0), np.uint8), None, sentinel_k, sentinel_d)
+    assert k is sentinel_k and d is sentinel_d
+    from orbgpu import _lib
+    n = ctypes.c_int(12345)
+    assert _lib.lib().orb_extract(g.h, None, 0, 0, 0, None, 0, ctypes.byref(n), None) == 0
+    assert n.value == 12345
+
+
+def test_flat_image_zero_keypoints(orbgpu_mod):
+    k, d = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)(np.full((480, 640), 77, np.uint8))
+    assert len(k) == 0 and d.shape == (0, 32)
+
+
+def test_too_small_image_is_an_error(orbgpu_mod):
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    with pytest.raises(orbgpu_mod.OrbError):
+        g(np.full((120, 160), 50, np.uint8))
+
+
+def test_strided_input(orbgpu_mod, oracle_mod):
+    from orbgpu import _lib
+    from orbgpu.synth import synth_frame
+    img = synth_frame(640, 480, 6)
+    big = np.zeros((480, 777), np.uint8)
+    big[:, 5:645] = img
+    view = big[:, 5:645]
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    kps = np.zeros(4000, orbgpu_mod.KP_DTYPE)
+    desc = np.zeros((4000, 32), np.uint8)
+    n = ctypes.c_int()
+    st = _lib.lib().orb_extract(g.h, ctypes.c_void_p(view.ctypes.data), 640, 480, 777,
+                                ctypes.c_void_p(kps.ctypes.data), 4000, ctypes.byref(n),
+                                ctypes.c_void_p(desc.ctypes.data))
+    assert st == 0
+    ok, od = oracle_mod.OracleExtractor(1000)(img)
+    assert kps[:n.value].tobytes() == ok.tobytes() and np.array_equal(desc[:n.value], od)
+
+
+def test_capacity_error_reports_count(orbgpu_mod):
+    from orbgpu import _lib
+    from orbgpu.synth import synth_frame
+    img = synth_frame(640, 480, 0)
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    kps = np.zeros(10, orbgpu_mod.KP_DTYPE)
+    desc = np.zeros((10, 32), np.uint8)
+    n = ctypes.c_int()
+    st = _lib.lib().orb_extract(g.h, ctypes.c_void_p(img.ctypes.data), 640, 480, 640,
+                                ctypes.c_void_p(kps.ctypes.data), 10, ctypes.byref(n),
+                                ctypes.c_void_p(desc.ctypes.data))
+    assert st == -3 and n.value > 10
+
+
+def test_size_changes_reuse_context(orbgpu_mod, oracle_mod):
+    from orbgpu.synth import synth_frame
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    o = oracle_mod.OracleExtractor(1000)
+    for (w, h, i) in [(640, 480, 1), (1280, 720, 2), (320, 240, 3), (640, 480, 4)]:
+        img = synth_frame(w, h, i)
+        ok, od = o(img)
+        gk, gd = g(img)
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od)
+
+
+def test_batch_device_path_matches_single(orbgpu_mod, oracle_mod):
+    from orbgpu.synth import synth_batch
+    frames = synth_batch(1280, 720, 5, first=30)
+    b = orbgpu_mod.BatchExtractor(2000, 1280, 720, 5)
+    b.upload(frames)
+    b.launch()
+    b.sync()
+    o = oracle_mod.OracleExtractor(2000)
+    for f in range(5):
+        gk, gd = b.results(f)
+        ok, od = o(frames[f])
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
+    # relaunch is idempotent
+    c0 = b.counts().copy()
+    b.launch()
+    b.sync()
+    assert np.array_equal(b.counts(), c0)
+    b.close()
+
+
+def test_mv_image_pyramid(orbgpu_mod, oracle_mod):
+    from orbgpu.synth import synth_frame
+    img = synth_frame(640, 480, 8)
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    g(img)
+    o = oracle_mod.OracleExtractor(1000)
+    o(img)
+    pyr = g.mvImagePyramid
+    assert len(pyr) == 8
+    for l in range(8):
+        assert np.array_equal(pyr[l], o.level(l))
+
+
+def test_two_contexts_interleaved(orbgpu_mod, oracle_mod):
+    # stereo: left/right extractors are independent instances (Frame.cc:124-127)
+    from orbgpu.synth import synth_frame, synth_stereo_right
+    left = synth_frame(1280, 720, 12)
+    right = synth_stereo_right(left, 12)
+    gl = orbgpu_mod.ORBextractor(2000, 1.2, 8, 20, 7)
+    gr = orbgpu_mod.ORBextractor(2000, 1.2, 8, 20, 7)
+    kl, dl = gl(left)
+    kr, dr = gr(right)
+    o = oracle_mod.OracleExtractor(2000)
+    ol, odl = o(left)
+    orr, odr = o(right)
+    assert kl.tobytes() == ol.tobytes() and np.array_equal(dl, odl)
+    assert kr.tobytes() == orr.tobytes() and np.array_equal(dr, odr)
+    # each context keeps its own mvImagePyramid (instance state, ORBextractor.h:85)
+    ol3 = oracle_mod.OracleExtractor(2000)
+    ol3(left)
+    assert np.array_equal(gl.mvImagePyramid[3], ol3.level(3))
+    assert np.array_equal(gr.mvImagePyramid[3], o.level(3))

@@ -1,0 +1,216 @@
+"""GPU parity: ORBmatcher searches through liborbgpu's Hamming kernels vs the oracle restatement of
+ORBmatcher.cc — match indices bit-exact."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def frames(orbgpu_mod):
+    """Two extracted views (second shifted by a few px) -> realistic descriptor sets with matches."""
+    from orbgpu.synth import synth_frame
+    a = synth_frame(640, 480, 40)
+    b = np.roll(a, (3, 5), axis=(0, 1))
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    ka, da = g(a)
+    kb, db = g(b)
+    return ka, da, kb, db
+
+
+def _featvec(desc, nodes=16, seed=0):
+    """Synthetic vocabulary: node = high nibble of descriptor byte 0 (similar descriptors share nodes)."""
+    fv = {}
+    for i, d in enumerate(desc):
+        fv.setdefault(int(d[0] >> 4) % nodes, []).append(i)
+    return fv
+
+
+def _oracle_fv(oracle_mod, fv):
+    ids = sorted(fv)
+    return oracle_mod.make_featvec(ids, [fv[i] for i in ids])
+
+
+def test_hamming_topk_vs_numpy(orbgpu_mod):
+    rng = np.random.default_rng(0)
+    q = rng.integers(0, 256, (300, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (700, 32), dtype=np.uint8)
+    t[::7] = t[0]   # many exact ties
+    m = orbgpu_mod.ORBmatcher()
+    D = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    for k in (1, 2, 5, 8):
+        dist, idx, nv = m.hamming_topk(q, t, k)
+        order = np.lexsort((np.broadcast_to(np.arange(700), D.shape), D), axis=1)[:, :k]
+        assert np.array_equal(idx, order)
+        assert np.array_equal(dist, np.take_along_axis(D, order, 1))
+        assert (nv == 700).all()
+
+
+def test_hamming_topk_csr_and_thresholds(orbgpu_mod):
+    rng = np.random.default_rng(1)
+    q = rng.integers(0, 256, (64, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (200, 32), dtype=np.uint8)
+    lens = rng.integers(0, 30, 64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    cand = rng.integers(0, 200, off[-1]).astype(np.int32)
+    thr = np.where(rng.random(200) < 0.3, -1, 2 ** 31 - 1).astype(np.int32)
+    thr[::11] = 120
+    m = orbgpu_mod.ORBmatcher()
+    dist, idx, nv = m.hamming_topk(q, t, 4, off, cand, thr)
+    for i in range(64):
+        c = cand[off[i]:off[i + 1]]
+        d = np.unpackbits(q[i][None] ^ t[c], axis=1).sum(1)
+        keep = thr[c] > d
+        pos = np.nonzero(keep)[0]
+        order = pos[np.lexsort((pos, d[pos]))][:4]
+        assert nv[i] == keep.sum()
+        exp_i = np.full(4, -1)
+        exp_d = np.full(4, -1)
+        exp_i[:len(order)] = c[order]
+        exp_d[:len(order)] = d[order]
+        assert idx[i].tolist() == exp_i.tolist() and dist[i].tolist() == exp_d.tolist(), i
+
+
+def test_top2_device_vs_numpy(orbgpu_mod):
+    from orbgpu import _lib
+    rng = np.random.default_rng(2)
+    nq, nt = 1000, 2300
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    t[1500] = q[3]
+    t[2200] = q[3]
+    b = orbgpu_mod.BatchExtractor(1000, 640, 480, 1)
+    L = _lib.lib()
+    dq, dt = b._alloc(q.nbytes), b._alloc(t.nbytes)
+    out = [b._alloc(nq * 4) for _ in range(3)]
+    L.orb_memcpy_h2d(b.h, dq, q.ctypes.data, q.nbytes)
+    L.orb_memcpy_h2d(b.h, dt, t.ctypes.data, t.nbytes)
+    b.hamming_top2(dq, nq, dt, nt, *out)
+    b.sync()
+    res = [np.zeros(nq, np.int32) for _ in range(3)]
+    for r, d in zip(res, out):
+        L.orb_memcpy_d2h(b.h, r.ctypes.data, d, nq * 4)
+    D = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    srt = np.sort(D, 1)
+    assert np.array_equal(res[0], srt[:, 0])
+    assert np.array_equal(res[1], D.argmin(1))   # first index on ties
+    assert np.array_equal(res[2], srt[:, 1])
+    assert res[1][3] == 1500
+    for p in [dq, dt] + out:
+        L.orb_device_free(b.h, p)
+    b.close()
+
+
+@pytest.mark.parametrize("ratio,check_ori", [(0.7, True), (0.75, True), (0.6, False), (0.99, True)])
+def test_search_by_bow_kf_f(orbgpu_mod, oracle_mod, frames, ratio, check_ori):
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(3)
+    mp = (rng.random(len(da)) < 0.8).astype(np.uint8)
+    fva, fvb = _featvec(da), _featvec(db)
+    n, m = orbgpu_mod.ORBmatcher(ratio, check_ori).SearchByBoW_KF_F(da, ka["angle"], mp, fva, db, kb["angle"], fvb)
+    oa, _ka = _oracle_fv(oracle_mod, fva)
+    ob, _kb = _oracle_fv(oracle_mod, fvb)
+    on, om = oracle_mod.search_by_bow_kf_f(ratio, check_ori, da, ka["angle"], mp, oa, db, kb["angle"], ob)
+    assert n == on and np.array_equal(m, om)
+    assert n > 50
+
+
+def test_search_by_bow_single_node_bruteforce(orbgpu_mod, oracle_mod, frames):
+    # C4 semantics: one FeatureVector node with every index, all MapPoints valid, ratio 0.7, checkOri
+    ka, da, kb, db = frames
+    fva, fvb = {0: list(range(len(da)))}, {0: list(range(len(db)))}
+    mp = np.ones(len(da), np.uint8)
+    n, m = orbgpu_mod.ORBmatcher(0.7, True).SearchByBoW_KF_F(da, ka["angle"], mp, fva, db, kb["angle"], fvb)
+    oa, _ka = _oracle_fv(oracle_mod, fva)
+    ob, _kb = _oracle_fv(oracle_mod, fvb)
+    on, om = oracle_mod.search_by_bow_kf_f(0.7, True, da, ka["angle"], mp, oa, db, kb["angle"], ob)
+    assert n == on and np.array_equal(m, om)
+
+
+@pytest.mark.parametrize("ratio,check_ori", [(0.75, True), (0.9, False)])
+def test_search_by_bow_kf_kf(orbgpu_mod, oracle_mod, frames, ratio, check_ori):
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(4)
+    mp1 = (rng.random(len(da)) < 0.85).astype(np.uint8)
+    mp2 = (rng.random(len(db)) < 0.85).astype(np.uint8)
+    fva, fvb = _featvec(da), _featvec(db)
+    n, m = orbgpu_mod.ORBmatcher(ratio, check_ori).SearchByBoW_KF_KF(da, ka["angle"], mp1, fva, db, kb["angle"],
+                                                                      mp2, fvb)
+    oa, _ka = _oracle_fv(oracle_mod, fva)
+    ob, _kb = _oracle_fv(oracle_mod, fvb)
+    on, om = oracle_mod.search_by_bow_kf_kf(ratio, check_ori, da, ka["angle"], mp1, oa, db, kb["angle"], mp2, ob)
+    assert n == on and np.array_equal(m, om)
+
+
+def test_exhaustion_rerank_path(orbgpu_mod, oracle_mod):
+    # identical queries against trains at distances 0..39: each query takes the next train, so the
+    # 8-entry GPU lists run out and the remaining queries are re-ranked on the GPU.
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 256, 32, dtype=np.uint8)
+    bits = np.unpackbits(base)
+    trains = []
+    for d in range(40):
+        b = bits.copy()
+        b[:d] ^= 1
+        trains.append(np.packbits(b))
+    t = np.array(trains, np.uint8)
+    q = np.repeat(base[None], 40, 0)
+    ang = np.zeros(40, np.float32)
+    fv = {0: list(range(40))}
+    n, m = orbgpu_mod.ORBmatcher(0.99, False).SearchByBoW_KF_F(q, ang, np.ones(40, np.uint8), fv, t, ang, fv)
+    oa, _k = _oracle_fv(oracle_mod, fv)
+    on, om = oracle_mod.search_by_bow_kf_f(0.99, False, q, ang, np.ones(40, np.uint8), oa, t, ang, oa)
+    assert n == on and np.array_equal(m, om) and n > 30
+    # the window matcher's vMatchedDistance stealing over the same data
+    k = np.zeros(40, orbgpu_mod.KP_DTYPE)
+    off = np.arange(0, 41 * 40, 40, dtype=np.int32)
+    cand = np.tile(np.arange(40, dtype=np.int32), 40)
+    n2, m2 = orbgpu_mod.ORBmatcher(0.99, True).SearchForInitialization(q, k, t, k, off, cand)
+    on2, om2 = oracle_mod.window_match(0.99, True, True, q, k, t, k, off, cand)
+    assert n2 == on2 and np.array_equal(m2, om2)
+
+
+@pytest.mark.parametrize("only_stereo,check_ori,far_epipole", [(False, False, True), (False, True, False),
+                                                               (True, False, True)])
+def test_search_for_triangulation(orbgpu_mod, oracle_mod, frames, only_stereo, check_ori, far_epipole):
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(6)
+    mp1 = (rng.random(len(da)) < 0.3).astype(np.uint8)
+    mp2 = (rng.random(len(db)) < 0.3).astype(np.uint8)
+    ur1 = np.where(rng.random(len(da)) < 0.5, 10.0, -1.0).astype(np.float32)
+    ur2 = np.where(rng.random(len(db)) < 0.5, 10.0, -1.0).astype(np.float32)
+    F = np.array([[0, 0, 0], [0, 0, -1], [0, 1, 0]], np.float32)   # horizontal epipolar lines: y2 = y1
+    F += rng.normal(0, 1e-4, (3, 3)).astype(np.float32)
+    ex, ey = (1e5, 1e5) if far_epipole else (320.0, 240.0)
+    t = oracle_mod.OracleExtractor(1000).tables()
+    fva, fvb = _featvec(da, 8), _featvec(db, 8)
+    m = orbgpu_mod.ORBmatcher(0.6, check_ori)
+    pairs = m.SearchForTriangulation(da, ka, mp1, ur1, fva, db, kb, mp2, ur2, fvb, F, ex, ey, t["scale"],
+                                     t["sigma2"], only_stereo)
+    oa, _ka = _oracle_fv(oracle_mod, fva)
+    ob, _kb = _oracle_fv(oracle_mod, fvb)
+    op = oracle_mod.search_for_triangulation(check_ori, only_stereo, da, ka, mp1, ur1, oa, db, kb, mp2, ur2, ob, F,
+                                             ex, ey, t["scale"], t["sigma2"])
+    assert np.array_equal(pairs, op)
+    assert len(op) > 0
+
+
+@pytest.mark.parametrize("level0_only,window", [(True, 100), (False, 15), (True, 40)])
+def test_window_match(orbgpu_mod, oracle_mod, frames, level0_only, window):
+    ka, da, kb, db = frames
+    offs, idxs = [0], []
+    for k in ka:
+        c = orbgpu_mod.features_in_area(kb, 0, 640, 0, 480, float(k["x"]), float(k["y"]), window,
+                                        int(k["octave"]) if level0_only else -1,
+                                        int(k["octave"]) if level0_only else -1)
+        idxs.extend(c.tolist())
+        offs.append(len(idxs))
+    off = np.array(offs, np.int32)
+    cand = np.array(idxs, np.int32)
+    for ratio in (0.9, 0.99):
+        m = orbgpu_mod.ORBmatcher(ratio, True)
+        fn = m.SearchForInitialization if level0_only else m.BirdviewMatch
+        n, mm = fn(da, ka, db, kb, off, cand)
+        on, om = oracle_mod.window_match(ratio, True, level0_only, da, ka, db, kb, off, cand)
+        assert n == on and np.array_equal(mm, om)
+        assert n > 20

@@ -1,0 +1,38 @@
+"""Generate tests/golden/*.npz with the oracle restatement (SURVEY §8c "Golden vectors").
+
+The reference ships no fixtures and cannot be built here (OpenCV absent), so these vectors are
+produced by the oracle and pin it against drift; inputs are regenerated from the seeded synthetic
+generator and checked by sha256.  Run: python tools/gen_golden.py
+"""
+import hashlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "orb-slam-birdview_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+import oracle  # noqa: E402
+from orbgpu.synth import synth_frame  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+CASES = [("extract_320x240_500.npz", 320, 240, 500, 0, "scene"),
+         ("extract_640x480_1000.npz", 640, 480, 1000, 0, "scene"),
+         ("extract_noise_640x480.npz", 640, 480, 1000, 3, "noise")]
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    for name, w, h, nf, idx, kind in CASES:
+        img = synth_frame(w, h, idx, kind)
+        k, d = oracle.OracleExtractor(nf)(img)
+        np.savez_compressed(os.path.join(OUT, name), cfg=np.array([w, h, nf, idx]), kind=np.array(kind),
+                            img_sha256=np.array(hashlib.sha256(img.tobytes()).hexdigest()), kps=k, desc=d)
+        print(name, len(k))
+
+
+if __name__ == "__main__":
+    main()
