@@ -10,7 +10,7 @@
 
 namespace orbgpu {
 
-__constant__ int8_t c_pattern[1024] = {ORBGPU_PATTERN31_VALUES};
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[1024] = {ORBGPU_PATTERN31_VALUES};
 
 namespace {
 
@@ -23,12 +23,6 @@ __device__ __forceinline__ LevelPtr level_ptr(const Geom* __restrict__ g, int l,
                                               long long framePitch, int rowStride, const uint8_t* pyr, int f) {
     if (l == 0) return {frames + (long long)f * framePitch, rowStride};
     return {pyr + (long long)f * g->pyr_bytes + g->L[l].pyr_off, g->L[l].pitch};
-}
-
-__device__ __forceinline__ int reflect101(int p, int len) {   // BORDER_REFLECT_101
-    if (len == 1) return 0;
-    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
-    return p;
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -99,18 +93,26 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
                                                 int rowStride, uint8_t* __restrict__ pyr) {
     const int f = blockIdx.z;
     const int dw = g->L[level].w, dh = g->L[level].h;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;   // 4 output pixels -> one dword store
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= dw || y >= dh) return;
+    if (x0 >= dw || y >= dh) return;
     const LevelPtr src = level_ptr(g, level - 1, frames, framePitch, rowStride, pyr, f);
-    const ResizeCoef cx = coef[x], cy = coef[dw + y];
+    const ResizeCoef cy = coef[dw + y];
     const uint8_t* r0 = src.p + (long long)cy.s0 * src.stride;
     const uint8_t* r1 = src.p + (long long)cy.s1 * src.stride;
-    const int h0 = r0[cx.s0] * cx.c0 + r0[cx.s1] * cx.c1;
-    const int h1 = r1[cx.s0] * cx.c0 + r1[cx.s1] * cx.c1;
-    const int v = (((cy.c0 * (h0 >> 4)) >> 16) + ((cy.c1 * (h1 >> 4)) >> 16) + 2) >> 2;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int x = min(x0 + i, dw - 1);
+        const ResizeCoef cx = coef[x];
+        const int h0 = r0[cx.s0] * cx.c0 + r0[cx.s1] * cx.c1;
+        const int h1 = r1[cx.s0] * cx.c0 + r1[cx.s1] * cx.c1;
+        const int v = (((cy.c0 * (h0 >> 4)) >> 16) + ((cy.c1 * (h1 >> 4)) >> 16) + 2) >> 2;
+        packed |= (uint32_t)v << (8 * i);
+    }
+    // the pitch is a multiple of 64, so the dword never leaves the row (pad bytes are never read)
     uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off;
-    dst[(long long)y * g->L[level].pitch + x] = (uint8_t)v;
+    *reinterpret_cast<uint32_t*>(dst + (long long)y * g->L[level].pitch + x0) = packed;
 }
 
 /* ------------------------------------------------------------------------------------------------
@@ -144,34 +146,62 @@ __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
     d[13] = v - c[-3 + 1 * P];
     d[14] = v - c[-2 + 2 * P];
     d[15] = v - c[-1 + 3 * P];
-    int mn2[16], mx2[16];
+    // 9-arc [k, k+8] = three 3-runs: v_min3/v_max3 over runs, then over the arcs
+    int m3[16], x3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
+        m3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
     }
-    int mn4[16], mx4[16];
+    int A = 0, Bn = 0;   // clamped at 0: only positive strengths matter (thresholds are >= 0)
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+        A = max(A, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));    // dark arc:   all v - p
+        Bn = min(Bn, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15]));  // bright arc: all p - v
     }
-    int A = -1024, Bn = 1024;
+    return max(A, -Bn);
+}
+
+// Necessary condition for a FAST corner at any threshold >= t: a 9-arc always contains two
+// cyclically adjacent compass points (circle positions 0, 4, 8, 12), so two adjacent compass points
+// must both be brighter than v + t or both darker than v - t.  0xFAC8 marks the 4-bit patterns with
+// two cyclically adjacent set bits.
+__device__ __forceinline__ bool fast_maybe(const uint8_t* c, int t) {
+    constexpr int P = kFastTilePitch;
+    const int v = c[0];
+    const int p0 = c[3 * P], p4 = c[3], p8 = c[-3 * P], p12 = c[-3];
+    const int hi = v + t, lo = v - t;
+    const int bm = (p0 > hi) | ((p4 > hi) << 1) | ((p8 > hi) << 2) | ((p12 > hi) << 3);
+    const int dm = (p0 < lo) | ((p4 < lo) << 1) | ((p8 < lo) << 2) | ((p12 < lo) << 3);
+    return ((0xFAC8 >> bm) | (0xFAC8 >> dm)) & 1;
+}
+
+// Raster-ordered append of the flagged items of one 256-wide chunk: returns the running total after
+// the chunk; flagged lanes get their position in *pos.  Two barriers.
+__device__ __forceinline__ int chunk_append(bool flag, int running, int* s_wave, int& pos) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long mask = __ballot(flag);
+    if (lane == 0) s_wave[wave] = __popcll(mask);
+    __syncthreads();
+    int before = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        A = max(A, mn9);      // dark arc: all v - p > th
-        Bn = min(Bn, mx9);    // bright arc: all p - v > th  <=>  max(v - p) < -th
+    for (int w = 0; w < 4; w++) {
+        const int cw = s_wave[w];
+        before += w < wave ? cw : 0;
+        tot += cw;
     }
-    return max(max(A, -Bn), 0);
+    pos = running + before + lanes_below(mask);
+    __syncthreads();
+    return running + tot;
 }
 
 __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                               long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                               uint32_t* __restrict__ cands, int* __restrict__ cellCount) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[kFastMaxRoi * kFastTilePitch];
-    __shared__ uint8_t sM[64 * 64];
+    __shared__ uint8_t sM[64 * 64];        // arc strength M per domain pixel (0 = cannot be a corner)
+    __shared__ uint16_t sList[64 * 64];    // prefilter survivors, raster order
+    __shared__ uint8_t sKeep[64 * 64];     // NMS verdict per list entry
     __shared__ int s_cnt;
     __shared__ int s_wave[4];
     const int tid = threadIdx.x;
@@ -219,16 +249,40 @@ __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const 
     if (tid == 0) s_cnt = 0;
     __syncthreads();
     const int npx = dw * dh;
-    for (int p = tid; p < npx; p += 256) {
-        const int dy = p / dw, dx = p - dy * dw;
-        sM[p] = (uint8_t)fast_arc_strength(&tile[(dy + 3) * kFastTilePitch + dx + 3 + xoff]);
+    const uint8_t* t0 = &tile[3 * kFastTilePitch + 3 + xoff];
+    // p / dw without an integer divide: (p + 0.5) / dw is >= 1/120 away from an integer (dw <= 60)
+    const float rdw = 1.0f / (float)dw;
+    auto div_dw = [rdw](int p) -> int { return (int)(((float)p + 0.5f) * rdw); };
+    // stage 1: compass prefilter at the smaller threshold, compaction in raster order
+    const int tmin = min(g->iniTh, g->minTh);
+    int nlist = 0;
+    for (int b0 = 0; b0 < npx; b0 += 256) {
+        const int p = b0 + tid;
+        bool pass = false;
+        if (p < npx) {
+            const int dy = div_dw(p), dx = p - dy * dw;
+            pass = fast_maybe(t0 + dy * kFastTilePitch + dx, tmin);
+            sM[p] = 0;
+        }
+        int pos;
+        nlist = chunk_append(pass, nlist, s_wave, pos);
+        if (pass) sList[pos] = (uint16_t)p;
+    }
+    __syncthreads();
+    // stage 2: exact arc strength for the survivors only
+    for (int i = tid; i < nlist; i += 256) {
+        const int p = sList[i];
+        const int dy = div_dw(p), dx = p - dy * dw;
+        sM[p] = (uint8_t)fast_arc_strength(t0 + dy * kFastTilePitch + dx);
     }
     __syncthreads();
 
+    // NMS (cell-local): keep iff corner at th and score > every in-domain neighbour's score, where a
+    // neighbour that is not a corner at th counts 0 (cv::FAST row buffers)
     auto keep = [&](int p, int th) -> bool {
-        const int dy = p / dw, dx = p - dy * dw;
         const int m = sM[p];
         if (m <= th) return false;
+        const int dy = div_dw(p), dx = p - dy * dw;
         const int s = m - 1;
 #pragma unroll
         for (int oy = -1; oy <= 1; oy++) {
@@ -244,40 +298,33 @@ __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const 
         }
         return true;
     };
-
-    int th = g->iniTh;
     int mine = 0;
-    for (int p = tid; p < npx; p += 256) mine += keep(p, th) ? 1 : 0;
+    for (int i = tid; i < nlist; i += 256) {
+        const bool k = keep(sList[i], g->iniTh);
+        sKeep[i] = k;
+        mine += k;
+    }
     if (mine) atomicAdd(&s_cnt, mine);
     __syncthreads();
-    if (s_cnt == 0) th = g->minTh;   // :812-816 fallback, evaluated after NMS
-    __syncthreads();
-
-    uint32_t* out = cands + (long long)f * g->ncand + L.cand_base + (long long)c * L.cell_cap;
-    const int lane = tid & 63, wave = tid >> 6;
-    int running = 0;
-    for (int b0 = 0; b0 < npx; b0 += 256) {
-        const int p = b0 + tid;
-        const bool k = p < npx && keep(p, th);
-        const unsigned long long mask = __ballot(k);
-        if (lane == 0) s_wave[wave] = __popcll(mask);
+    if (s_cnt == 0) {   // :812-816 fallback to minThFAST, evaluated after NMS
+        for (int i = tid; i < nlist; i += 256) sKeep[i] = keep(sList[i], g->minTh);
         __syncthreads();
-        int before = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const int cw = s_wave[w];
-            before += w < wave ? cw : 0;
-            tot += cw;
-        }
+    }
+    // emission in raster order (FAST emission order)
+    uint32_t* out = cands + (long long)f * g->ncand + L.cand_base + (long long)c * L.cell_cap;
+    int running = 0;
+    for (int b0 = 0; b0 < nlist; b0 += 256) {
+        const int i = b0 + tid;
+        const bool k = i < nlist && sKeep[i];
+        int pos;
+        running = chunk_append(k, running, s_wave, pos);
         if (k) {
-            const int pos = running + before + lanes_below(mask);
-            const int dy = p / dw, dx = p - dy * dw;
+            const int p = sList[i];
+            const int dy = div_dw(p), dx = p - dy * dw;
             const uint32_t xr = (uint32_t)(dx + 3 + cj * L.wCell);
             const uint32_t yr = (uint32_t)(dy + 3 + ci * L.hCell);
             out[pos] = xr | (yr << 12) | ((uint32_t)(sM[p] - 1) << 24);
         }
-        running += tot;
-        __syncthreads();
     }
     if (tid == 0) *cntOut = running;
 }
@@ -620,14 +667,24 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {   // cv::fastAta
     return a;
 }
 
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+// IC_Angle row sums: bytes of the aligned 32-byte row slice that lie in [lo, hi] (inclusive)
+__device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
+    const int a = min(max(lo - 4 * i, 0), 4), b = min(max(hi - 4 * i + 1, 0), 4);
+    const uint32_t la = (uint32_t)((1ull << (8 * a)) - 1), lb = (uint32_t)((1ull << (8 * b)) - 1);
+    return lb & ~la;
+}
+
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kDescWin * kDescWinPitch];
-    __shared__ __attribute__((aligned(16))) uint16_t s_row[4][kDescWin * kDescBlur];
-    __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][kDescBlur * kDescBlurPitch];
+    // per wave: 43x48 window (+16 B pad; reused for the transposed 37x40 blurred patch) and the
+    // transposed row-pass sums RT[rx][wy] (u16, 40 x 48)
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kDescWin * kDescWinPitch + 16];
+    __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][40 * 48];
     const int f = blockIdx.y;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nl = g->nlevels;
@@ -649,24 +706,76 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     const uint32_t kp = lvlKps[(long long)f * g->nkpcap + s];
     const int x = kp & 0xFFF, y = (kp >> 12) & 0xFFF, score = kp >> 24;
     const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
-    uint8_t* win = s_win[wv];
-    uint16_t* rowp = s_row[wv];
-    uint8_t* blur = s_blur[wv];
-    for (int idx = lane; idx < kDescWin * kDescWin; idx += 64) {
-        const int wy = idx / kDescWin, wx = idx - wy * kDescWin;
-        const int sy = reflect101(y - 21 + wy, L.h), sx = reflect101(x - 21 + wx, L.w);
-        win[wy * kDescWinPitch + wx] = src.p[(long long)sy * src.stride + sx];
+    uint8_t* wbase = s_win[wv];
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(wbase);
+    uint16_t* rt = s_rt[wv];
+
+    // ---- 43x43 window of the unblurred level, pixel (wy, wx) at byte wy*48 + sh + wx
+    int sh;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0;
+    if (aligned && x >= 21 && x + 27 <= L.w && y >= 21 && y + 21 < L.h) {   // 48 aligned bytes stay in the row
+        const int a0 = (x - 21) & ~3;
+        const uint8_t* row0 = src.p + (long long)(y - 21) * src.stride + a0;
+        uint32_t v[9];
+#pragma unroll
+        for (int r = 0; r < 9; r++) {   // 43 rows x 12 dwords = 516 <= 9 x 64, all loads in flight
+            const int idx = lane + 64 * r;
+            const int wy = idx / 12, ww = idx - wy * 12;
+            v[r] = idx < kDescWin * 12 ? *reinterpret_cast<const uint32_t*>(row0 + (long long)wy * src.stride + 4 * ww)
+                                      : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < 9; r++) {
+            const int idx = lane + 64 * r;
+            if (idx < kDescWin * 12) w32[idx] = v[r];
+        }
+        sh = (x - 21) & 3;
+    } else {   // near the level border: REFLECT_101 gather (as the blur's border mode), byte loads in flight
+        uint8_t v[29];
+#pragma unroll
+        for (int r = 0; r < 29; r++) {   // 43*43 = 1849 <= 29 x 64
+            const int idx = lane + 64 * r;
+            const int wy = idx / kDescWin, wx = idx - wy * kDescWin;
+            int sy = y - 21 + wy, sx = x - 21 + wx;
+            sy = sy < 0 ? -sy : (sy >= L.h ? 2 * L.h - 2 - sy : sy);
+            sx = sx < 0 ? -sx : (sx >= L.w ? 2 * L.w - 2 - sx : sx);
+            v[r] = idx < kDescWin * kDescWin ? src.p[(long long)sy * src.stride + sx] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int r = 0; r < 29; r++) {
+            const int idx = lane + 64 * r;
+            const int wy = idx / kDescWin, wx = idx - wy * kDescWin;
+            if (idx < kDescWin * kDescWin) wbase[wy * kDescWinPitch + wx] = v[r];
+        }
+        sh = 0;
     }
     wave_lds_sync();
-    // IC angle on the unblurred level (:77-104): exact integer moments
+
+    // ---- IC_Angle (:77-104) on the unblurred window: lane r < 31 sums row v = r - 15 over the
+    // circular patch |u| <= umax[|v|] with v_dot4_u32_u8 (u*I = (u+16)*I - 16*I).
+    // umax (:454-469) packed 4 bits per row: [15,15,15,15,14,14,14,13,13,12,11,10,9,8,6,3]
+    constexpr unsigned long long kUmax = 0x3689ABCDDEEEFFFFull;
     int m10 = 0, m01 = 0;
-    for (int idx = lane; idx < 31 * 31; idx += 64) {
-        const int v = idx / 31 - 15, u = idx - (idx / 31) * 31 - 15;
-        if (abs(u) <= g->umax[abs(v)]) {
-            const int I = win[(21 + v) * kDescWinPitch + 21 + u];
-            m10 += u * I;
-            m01 += v * I;
+    if (lane < 31) {
+        const int v = lane - 15;
+        const int d = (int)((kUmax >> (4 * abs(v))) & 15);
+        const int base = (21 + v) * kDescWinPitch + sh + 6;   // byte of u = -15
+        const int d0 = base >> 2, bs = base & 3;
+        uint32_t w[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) w[i] = w32[d0 + i];
+        uint32_t sI = 0, sW = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t bytes = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs) & byte_range_mask(15 - d, 15 + d, i);
+            // weights (u + 16) for u = 4i-15 .. 4i-12  ->  4i+1 .. 4i+4
+            const uint32_t wt = (uint32_t)(4 * i + 1) | ((uint32_t)(4 * i + 2) << 8) | ((uint32_t)(4 * i + 3) << 16) |
+                                ((uint32_t)(4 * i + 4) << 24);
+            sI = __builtin_amdgcn_udot4(bytes, 0x01010101u, sI, false);
+            sW = __builtin_amdgcn_udot4(bytes, wt, sW, false);
         }
+        m10 = (int)sW - 16 * (int)sI;
+        m01 = v * (int)sI;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -674,50 +783,114 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         m01 += __shfl_xor(m01, o);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
-    // Gaussian 7x7: exact integer row pass over 43 rows x 37 cols
-    int gk[7];
+
+    // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass: item = (row wy, 4 outputs
+    // rx = 4g..4g+3) over window bytes 4g..4g+9; packed u16 MACs on byte pairs (b_j, b_j+1).
+    const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4], k5 = g->gk[5],
+              k6 = g->gk[6];
+    const ushort2_t K[7] = {ushort2_t{(unsigned short)k0, (unsigned short)k0}, ushort2_t{(unsigned short)k1, (unsigned short)k1},
+                            ushort2_t{(unsigned short)k2, (unsigned short)k2}, ushort2_t{(unsigned short)k3, (unsigned short)k3},
+                            ushort2_t{(unsigned short)k4, (unsigned short)k4}, ushort2_t{(unsigned short)k5, (unsigned short)k5},
+                            ushort2_t{(unsigned short)k6, (unsigned short)k6}};
 #pragma unroll
-    for (int j = 0; j < 7; j++) gk[j] = g->gk[j];
-    for (int idx = lane; idx < kDescWin * kDescBlur; idx += 64) {
-        const int wy = idx / kDescBlur, rx = idx - wy * kDescBlur;
-        const uint8_t* p = &win[wy * kDescWinPitch + rx];
-        int acc = 0;
+    for (int r = 0; r < 7; r++) {   // 43 rows x 10 groups = 430 <= 7 x 64
+        const int it = lane + 64 * r;
+        if (it < kDescWin * 10) {
+            const int wy = it / 10, gq = it - wy * 10;
+            const int d0 = wy * 12 + gq;
+            const uint32_t w0 = w32[d0], w1 = w32[d0 + 1], w2 = w32[d0 + 2], w3 = w32[d0 + 3];
+            const uint32_t a[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                   __builtin_amdgcn_alignbyte(w3, w2, sh)};
+            ushort2_t P[9];
 #pragma unroll
-        for (int j = 0; j < 7; j++) acc += gk[j] * p[j];
-        rowp[idx] = (uint16_t)acc;
-    }
-    wave_lds_sync();
-    const int xsimd = L.w & ~3;   // SymmColumnVec_32s8u covers column blocks of 4; scalar tail rounds half-up
-    for (int idx = lane; idx < kDescBlur * kDescBlur; idx += 64) {
-        const int by = idx / kDescBlur, bx = idx - by * kDescBlur;
-        int S = 0;
+            for (int j = 0; j < 9; j++) {
+                const int q = j & 3;
+                const uint32_t sel = 0x0c000c00u | ((uint32_t)(q + 1) << 16) | (uint32_t)q;
+                P[j] = __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(a[(j >> 2) + 1 < 3 ? (j >> 2) + 1 : 2],
+                                                                              a[j >> 2], sel));
+            }
+            ushort2_t r01 = P[0] * K[0], r23 = P[2] * K[0];
 #pragma unroll
-        for (int i = 0; i < 7; i++) S += gk[i] * rowp[(by + i) * kDescBlur + bx];
-        const int X = x - 18 + bx;
-        int v;
-        if (X < xsimd) {
-            const int q = S >> 16, rem = S & 0xFFFF;
-            v = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));
-        } else {
-            v = (S + 32768) >> 16;
+            for (int j = 1; j < 7; j++) {
+                r01 = P[j] * K[j] + r01;
+                r23 = P[j + 2] * K[j] + r23;
+            }
+            const int rx = 4 * gq;
+            rt[(rx + 0) * 48 + wy] = r01.x;
+            rt[(rx + 1) * 48 + wy] = r01.y;
+            rt[(rx + 2) * 48 + wy] = r23.x;
+            rt[(rx + 3) * 48 + wy] = r23.y;
         }
-        blur[by * kDescBlurPitch + bx] = (uint8_t)min(v, 255);
     }
     wave_lds_sync();
-    // rBRIEF (:108-147): pinned correctly-rounded cos/sin
+
+    // ---- column pass: item = (column bx, 4 outputs by = 4g..4g+3) over RT[bx][4g .. 4g+9],
+    // v_dot2_u32_u16 on row pairs; rounding as the pinned OpenCV 3.2 8U path: half-to-even where the
+    // SSE2 body runs (x < W & ~3), half-up in the scalar tail.  Result stored transposed,
+    // blurT[bx][by] at bx*40 + by, over the (now dead) window buffer.
+    const int xsimd = L.w & ~3;
+    const ushort2_t K01 = {(unsigned short)k0, (unsigned short)k1}, K23 = {(unsigned short)k2, (unsigned short)k3},
+                    K45 = {(unsigned short)k4, (unsigned short)k5}, K60 = {(unsigned short)k6, 0},
+                    K0s = {0, (unsigned short)k0}, K12 = {(unsigned short)k1, (unsigned short)k2},
+                    K34 = {(unsigned short)k3, (unsigned short)k4}, K56 = {(unsigned short)k5, (unsigned short)k6};
+    uint32_t outw[6];
+    int outa[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {   // 37 columns x 10 groups = 370 <= 6 x 64
+        const int it = lane + 64 * r;
+        outa[r] = -1;
+        if (it < kDescBlur * 10) {
+            const int bx = it / 10, gq = it - bx * 10;
+            const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + bx * 48 + 4 * gq);
+            ushort2_t D[5];
+#pragma unroll
+            for (int i = 0; i < 5; i++) D[i] = __builtin_bit_cast(ushort2_t, rp[i]);
+            uint32_t S[4];
+            S[0] = __builtin_amdgcn_udot2(K60, D[3], __builtin_amdgcn_udot2(K45, D[2],
+                     __builtin_amdgcn_udot2(K23, D[1], __builtin_amdgcn_udot2(K01, D[0], 0u, false), false), false), false);
+            S[1] = __builtin_amdgcn_udot2(K56, D[3], __builtin_amdgcn_udot2(K34, D[2],
+                     __builtin_amdgcn_udot2(K12, D[1], __builtin_amdgcn_udot2(K0s, D[0], 0u, false), false), false), false);
+            S[2] = __builtin_amdgcn_udot2(K60, D[4], __builtin_amdgcn_udot2(K45, D[3],
+                     __builtin_amdgcn_udot2(K23, D[2], __builtin_amdgcn_udot2(K01, D[1], 0u, false), false), false), false);
+            S[3] = __builtin_amdgcn_udot2(K56, D[4], __builtin_amdgcn_udot2(K34, D[3],
+                     __builtin_amdgcn_udot2(K12, D[2], __builtin_amdgcn_udot2(K0s, D[1], 0u, false), false), false), false);
+            const bool even = x - 18 + bx < xsimd;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int o = 0; o < 4; o++) {
+                // round(S / 65536): half-to-even = (S + 32767 + q&1) >> 16, half-up = (S + 32768) >> 16
+                const uint32_t bias = even ? 32767u + ((S[o] >> 16) & 1u) : 32768u;
+                const uint32_t v = min((S[o] + bias) >> 16, 255u);
+                packed |= v << (8 * o);
+            }
+            outw[r] = packed;
+            outa[r] = (bx * kDescBlurPitch + 4 * gq) >> 2;
+        }
+    }
+    wave_lds_sync();   // every lane has finished reading the window before it is overwritten
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+        if (outa[r] >= 0) w32[outa[r]] = outw[r];
+    wave_lds_sync();
+
+    // ---- rBRIEF (:108-147): pinned correctly-rounded cos/sin; 256 tests as
+    // four 64-lane ballots; sample (ix, iy) of the blurred patch at blurT[(18+ix)*40 + 18+iy]
     const float ang = angle * kFactorPI;
-    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
-    const uint8_t* ctr = &blur[18 * kDescBlurPitch + 18];
+    double sd, cd;
+    sincos((double)ang, &sd, &cd);
+    const float a = (float)cd, b = (float)sd;
+    const uint8_t* ctr = wbase + 18 * kDescBlurPitch + 18;
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(outD + ((long long)f * kpCap + outIdx) * 32);
 #pragma unroll
     for (int gq = 0; gq < 4; gq++) {
         const int p = lane + 64 * gq;
-        const float px0 = (float)c_pattern[4 * p], py0 = (float)c_pattern[4 * p + 1];
-        const float px1 = (float)c_pattern[4 * p + 2], py1 = (float)c_pattern[4 * p + 3];
+        const char4 pp = reinterpret_cast<const char4*>(c_pattern)[p];   // (x0, y0, x1, y1) of test pair p
+        const float px0 = (float)pp.x, py0 = (float)pp.y;
+        const float px1 = (float)pp.z, py1 = (float)pp.w;
         const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
         const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
-        const int t0 = ctr[__float2int_rn(u0 + u1) * kDescBlurPitch + __float2int_rn(u2 - u3)];
-        const int t1 = ctr[__float2int_rn(w0 + w1) * kDescBlurPitch + __float2int_rn(w2 - w3)];
+        const int t0 = ctr[__float2int_rn(u2 - u3) * kDescBlurPitch + __float2int_rn(u0 + u1)];
+        const int t1 = ctr[__float2int_rn(w2 - w3) * kDescBlurPitch + __float2int_rn(w0 + w1)];
         const unsigned long long m = __ballot(t0 < t1);
         if (lane == 0) dst[gq] = m;
     }
@@ -749,7 +922,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     if (nframes <= 0) return hipSuccess;
     if (marker) marker(user, ORB_K_RESIZE, 1);
     for (int l = 1; l < g.nlevels; l++) {
-        dim3 grid(cdiv(g.L[l].w, 64), cdiv(g.L[l].h, 4), nframes);
+        dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
         hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l, d_frames,
                            frame_pitch, row_stride, b.d_pyr);
     }

@@ -58,6 +58,10 @@ void compute_tables(Ctx* c) {
         c->umax[v] = v0;
         ++v0;
     }
+    // k_describe carries this table as the packed constant 0x3689ABCDDEEEFFFF (4 bits per row)
+    unsigned long long packed = 0;
+    for (int i = 0; i < 16; i++) packed |= (unsigned long long)c->umax[i] << (4 * i);
+    c->umax_ok = packed == 0x3689ABCDDEEEFFFFull;
     // Gaussian 7x7 sigma 2: getGaussianKernel(7, 2, CV_32F) -> convertTo(CV_32S, 256)
     float cf[7];
     double s = 0;
@@ -306,6 +310,11 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         return fail(ORB_ERR_HIP);
     }
     compute_tables(c);
+    if (!c->umax_ok) {
+        orb_destroy(reinterpret_cast<orb_ctx*>(c));
+        set_error("internal: umax table differs from the kernel's packed constant", hipSuccess);
+        return fail(ORB_ERR_INTERNAL);
+    }
     if (p->max_width > 0 && p->max_height > 0) {
         int st = c->ensure_geometry(p->max_width, p->max_height);
         if (st == ORB_OK) st = c->ensure_frames(std::max(1, p->max_batch));

@@ -24,6 +24,7 @@ struct Ctx {
         inv_sigma2[ORBGPU_MAX_LEVELS]{};
     int n_per_level[ORBGPU_MAX_LEVELS]{};
     int umax[16]{};
+    bool umax_ok = false;
     int gk[8]{};
 
     // geometry of the current image size

@@ -16,7 +16,7 @@ constexpr int kFastTilePitch = 72;    // LDS pitch of a FAST cell ROI (ROI <= 66
 constexpr int kFastMaxRoi = 66;
 constexpr int kOctreeThreads = 512;
 constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3 (blur taps)
-constexpr int kDescWinPitch = 44;
+constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as aligned dwords
 constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
 
