@@ -8,6 +8,8 @@
 #include "orbgpu_internal.h"
 #include "pattern31_data.inc"
 
+#include <algorithm>
+
 namespace orbgpu {
 
 __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024] = {ORBGPU_PATTERN31_VALUES};
@@ -166,18 +168,39 @@ __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
 // cyclically adjacent compass points (circle positions 0, 4, 8, 12), so two adjacent compass points
 // must both be brighter than v + t or both darker than v - t.  0xFAC8 marks the 4-bit patterns with
 // two cyclically adjacent set bits.
-__device__ __forceinline__ bool fast_maybe(const uint8_t* c, int t) {
-    constexpr int P = kFastTilePitch;
-    const int v = c[0];
-    const int p0 = c[3 * P], p4 = c[3], p8 = c[-3 * P], p12 = c[-3];
+__device__ __forceinline__ bool fast_maybe(int v, int p0, int p4, int p8, int p12, int t) {
     const int hi = v + t, lo = v - t;
     const int bm = (p0 > hi) | ((p4 > hi) << 1) | ((p8 > hi) << 2) | ((p12 > hi) << 3);
     const int dm = (p0 < lo) | ((p4 < lo) << 1) | ((p8 < lo) << 2) | ((p12 < lo) << 3);
     return ((0xFAC8 >> bm) | (0xFAC8 >> dm)) & 1;
 }
 
-// Raster-ordered append of the flagged items of one 256-wide chunk: returns the running total after
-// the chunk; flagged lanes get their position in *pos.  Two barriers.
+__device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xFF; }
+
+// Exclusive scan of one int per thread over a 256-thread block (two barriers).
+__device__ __forceinline__ int block256_excl_scan(int v, int* s_wave, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int cw = s_wave[w];
+        before += w < wave ? cw : 0;
+        tot += cw;
+    }
+    __syncthreads();
+    total = tot;
+    return before + x - v;
+}
+
+// Raster-ordered append of one flag per thread (ballot form of the scan above).
 __device__ __forceinline__ int chunk_append(bool flag, int running, int* s_wave, int& pos) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long mask = __ballot(flag);
@@ -195,138 +218,188 @@ __device__ __forceinline__ int chunk_append(bool flag, int running, int* s_wave,
     return running + tot;
 }
 
+struct FastCell {
+    int f, cell, l, ci, cj, iniX, iniY, rw, rh, dw, dh, x0w, nw;
+    bool valid, aligned;
+    const uint8_t* base;   // ROI row 0, column 0
+    int stride;
+};
+
+__device__ __forceinline__ FastCell fast_cell(const Geom* __restrict__ g, int item, const uint8_t* frames,
+                                              long long framePitch, int rowStride, const uint8_t* pyr) {
+    FastCell c;
+    c.f = item / g->ncells;
+    c.cell = item - c.f * g->ncells;
+    int l = 0;
+    while (l + 1 < g->nlevels && c.cell >= g->L[l + 1].cell_base) ++l;
+    c.l = l;
+    const LevelGeom& L = g->L[l];
+    const int cc = c.cell - L.cell_base;
+    c.ci = cc / L.nCols;
+    c.cj = cc - c.ci * L.nCols;
+    c.iniY = kMinBorder + c.ci * L.hCell;
+    c.iniX = kMinBorder + c.cj * L.wCell;
+    c.valid = !(c.iniY >= L.maxBY - 3 || c.iniX >= L.maxBX - 6);   // :794-806
+    const int maxY = min(c.iniY + L.hCell + 6, L.maxBY);
+    const int maxX = min(c.iniX + L.wCell + 6, L.maxBX);
+    c.rw = maxX - c.iniX;
+    c.rh = maxY - c.iniY;
+    c.dw = c.rw - 6;   // FAST detection domain: ROI rows/cols 3 .. n-4
+    c.dh = c.rh - 6;
+    c.valid = c.valid && c.dw > 0 && c.dh > 0;
+    const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, c.f);
+    c.base = src.p + (long long)c.iniY * src.stride;
+    c.stride = src.stride;
+    c.aligned = ((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0;
+    c.x0w = c.iniX >> 2;
+    c.nw = ((c.iniX + c.rw + 3) >> 2) - c.x0w;
+    return c;
+}
+
 __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                               long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
-                                              uint32_t* __restrict__ cands, int* __restrict__ cellCount) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kFastMaxRoi * kFastTilePitch];
-    __shared__ uint8_t sM[64 * 64];        // arc strength M per domain pixel (0 = cannot be a corner)
-    __shared__ uint16_t sList[64 * 64];    // prefilter survivors, raster order
-    __shared__ uint8_t sKeep[64 * 64];     // NMS verdict per list entry
-    __shared__ int s_cnt;
+                                              uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
+                                              int remap) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kFastMaxRoi * kFastTilePitch + 16];
+    // sized so that 8 blocks (32 waves) fit a CU's 160 KiB: domain <= 60 x 60 px (wCell, hCell <= 60)
+    __shared__ __attribute__((aligned(16))) uint8_t sM[60 * 64];   // arc strength, pitch 64 (0 = cannot be a corner)
+    __shared__ uint16_t sList[60 * 60];                            // prefilter survivors (dy*64+dx), raster order
+    __shared__ uint8_t sKeep[60 * 60];                             // NMS verdict per list entry
     __shared__ int s_wave[4];
+    __shared__ int s_cnt;
     const int tid = threadIdx.x;
-    const int f = blockIdx.y;
-    const int cell = blockIdx.x;
-    int l = 0;
-    while (l + 1 < g->nlevels && cell >= g->L[l + 1].cell_base) ++l;
-    const LevelGeom& L = g->L[l];
-    const int c = cell - L.cell_base;
-    const int ci = c / L.nCols, cj = c - ci * L.nCols;
-    int* cntOut = cellCount + (long long)f * g->ncells + cell;
-    const int iniY = kMinBorder + ci * L.hCell;
-    const int iniX = kMinBorder + cj * L.wCell;
-    // :794-806 (integer-valued floats in the reference)
-    if (iniY >= L.maxBY - 3 || iniX >= L.maxBX - 6) {
+    // One (frame, cell) item per block.  Blocks are dealt round-robin over the 8 XCDs, so the
+    // bijective remap below gives each XCD a contiguous range of items: neighbouring cells (which
+    // share ROI rows) then hit the same L2 (speed only; any placement is correct).
+    int item = blockIdx.x;
+    if (remap) {
+        const int q = total >> 3, r = total & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        item = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int tmin = min(g->iniTh, g->minTh);
+    constexpr int TP = kFastTilePitch;
+    const FastCell c = fast_cell(g, item, frames, framePitch, rowStride, pyr);
+    int* cntOut = cellCount + (long long)c.f * g->ncells + c.cell;
+    if (!c.valid) {
         if (tid == 0) *cntOut = 0;
         return;
     }
-    const int maxY = min(iniY + L.hCell + 6, L.maxBY);
-    const int maxX = min(iniX + L.wCell + 6, L.maxBX);
-    const int rw = maxX - iniX, rh = maxY - iniY;
-    const int dw = rw - 6, dh = rh - 6;   // FAST detection domain: ROI rows/cols 3 .. n-4
-    if (dw <= 0 || dh <= 0) {
-        if (tid == 0) *cntOut = 0;
-        return;
-    }
-    const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
-    const uint8_t* base = src.p + (long long)iniY * src.stride;
     int xoff = 0;
-    if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
-        const int x0w = iniX >> 2;
-        const int nw = ((iniX + rw + 3) >> 2) - x0w;
-        for (int idx = tid; idx < rh * nw; idx += 256) {
-            const int yy = idx / nw, ww = idx - yy * nw;
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (long long)yy * src.stride + (x0w + ww) * 4);
-            *reinterpret_cast<uint32_t*>(&tile[yy * kFastTilePitch + ww * 4]) = v;
+    if (c.aligned) {
+        for (int idx = tid; idx < c.rh * c.nw; idx += 256) {
+            const int yy = idx / c.nw, ww = idx - yy * c.nw;
+            *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) =
+                *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4);
         }
-        xoff = iniX & 3;
+        xoff = c.iniX & 3;
     } else {
-        for (int idx = tid; idx < rh * rw; idx += 256) {
-            const int yy = idx / rw, xx = idx - yy * rw;
-            tile[yy * kFastTilePitch + xx] = base[(long long)yy * src.stride + iniX + xx];
+        for (int idx = tid; idx < c.rh * c.rw; idx += 256) {
+            const int yy = idx / c.rw, xx = idx - yy * c.rw;
+            tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
         }
     }
     if (tid == 0) s_cnt = 0;
     __syncthreads();
-    const int npx = dw * dh;
-    const uint8_t* t0 = &tile[3 * kFastTilePitch + 3 + xoff];
-    // p / dw without an integer divide: (p + 0.5) / dw is >= 1/120 away from an integer (dw <= 60)
-    const float rdw = 1.0f / (float)dw;
-    auto div_dw = [rdw](int p) -> int { return (int)(((float)p + 0.5f) * rdw); };
-    // stage 1: compass prefilter at the smaller threshold, compaction in raster order
-    const int tmin = min(g->iniTh, g->minTh);
-    int nlist = 0;
-    for (int b0 = 0; b0 < npx; b0 += 256) {
-        const int p = b0 + tid;
-        bool pass = false;
-        if (p < npx) {
-            const int dy = div_dw(p), dx = p - dy * dw;
-            pass = fast_maybe(t0 + dy * kFastTilePitch + dx, tmin);
-            sM[p] = 0;
+    {
+        const int dw = c.dw, dh = c.dh;
+        // stage 1: compass prefilter on runs of 4 pixels (dword LDS reads), compaction in raster order
+        const int nruns = (dw + 3) >> 2;
+        int nlist = 0;
+        for (int b0 = 0; b0 < dh * nruns; b0 += 256) {
+            const int it = b0 + tid;
+            int pm = 0, dy = 0, x0 = 0;
+            if (it < dh * nruns) {
+                dy = it / nruns;
+                x0 = 4 * (it - dy * nruns);
+                const int sc = (dy + 3) * TP + x0 + xoff;   // center row, from pixel x0-3
+                const int s0 = (dy + 6) * TP + x0 + 3 + xoff;
+                const int s8 = dy * TP + x0 + 3 + xoff;
+                const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
+                const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
+                const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3];
+                const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);
+                const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);
+                const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);
+                const uint32_t B = __builtin_amdgcn_alignbyte(t32[d0 + 1], t32[d0], s0 & 3);
+                const uint32_t C = __builtin_amdgcn_alignbyte(t32[d8 + 1], t32[d8], s8 & 3);
+                const unsigned long long c64 = (unsigned long long)A0 | ((unsigned long long)A1 << 32);
+                const uint32_t c8_11 = A2;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int v = (int)((c64 >> (8 * (3 + i))) & 0xFF);
+                    const int p12 = (int)((c64 >> (8 * i)) & 0xFF);
+                    const int p4 = i < 2 ? (int)((c64 >> (8 * (6 + i))) & 0xFF) : byte_of(c8_11, i - 2);
+                    const int p0 = byte_of(B, i), p8 = byte_of(C, i);
+                    if (x0 + i < dw && fast_maybe(v, p0, p4, p8, p12, tmin)) pm |= 1 << i;
+                }
+                *reinterpret_cast<uint32_t*>(&sM[dy * 64 + x0]) = 0u;
+            }
+            int tot;
+            int pos = nlist + block256_excl_scan(__popc(pm), s_wave, tot);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (pm & (1 << i)) sList[pos++] = (uint16_t)(dy * 64 + x0 + i);
+            nlist += tot;
         }
-        int pos;
-        nlist = chunk_append(pass, nlist, s_wave, pos);
-        if (pass) sList[pos] = (uint16_t)p;
-    }
-    __syncthreads();
-    // stage 2: exact arc strength for the survivors only
-    for (int i = tid; i < nlist; i += 256) {
-        const int p = sList[i];
-        const int dy = div_dw(p), dx = p - dy * dw;
-        sM[p] = (uint8_t)fast_arc_strength(t0 + dy * kFastTilePitch + dx);
-    }
-    __syncthreads();
-
-    // NMS (cell-local): keep iff corner at th and score > every in-domain neighbour's score, where a
-    // neighbour that is not a corner at th counts 0 (cv::FAST row buffers)
-    auto keep = [&](int p, int th) -> bool {
-        const int m = sM[p];
-        if (m <= th) return false;
-        const int dy = div_dw(p), dx = p - dy * dw;
-        const int s = m - 1;
+        __syncthreads();
+        // stage 2: exact arc strength for the survivors only
+        const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
+        for (int i = tid; i < nlist; i += 256) {
+            const int p = sList[i];
+            sM[p] = (uint8_t)fast_arc_strength(t0 + (p >> 6) * TP + (p & 63));
+        }
+        __syncthreads();
+        // NMS (cell-local): keep iff corner at th and score > every in-domain neighbour's score, where
+        // a neighbour that is not a corner at th counts 0 (cv::FAST row buffers)
+        auto keep = [&](int p, int th) -> bool {
+            const int m = sM[p];
+            if (m <= th) return false;
+            const int dy = p >> 6, dx = p & 63;
+            const int s = m - 1;
 #pragma unroll
-        for (int oy = -1; oy <= 1; oy++) {
+            for (int oy = -1; oy <= 1; oy++) {
 #pragma unroll
-            for (int ox = -1; ox <= 1; ox++) {
-                if (ox == 0 && oy == 0) continue;
-                const int ny = dy + oy, nx = dx + ox;
-                if (ny < 0 || ny >= dh || nx < 0 || nx >= dw) continue;
-                const int mn = sM[ny * dw + nx];
-                const int sn = mn > th ? mn - 1 : 0;
-                if (!(s > sn)) return false;
+                for (int ox = -1; ox <= 1; ox++) {
+                    if (ox == 0 && oy == 0) continue;
+                    const int ny = dy + oy, nx = dx + ox;
+                    if (ny < 0 || ny >= dh || nx < 0 || nx >= dw) continue;
+                    const int mn = sM[ny * 64 + nx];
+                    const int sn = mn > th ? mn - 1 : 0;
+                    if (!(s > sn)) return false;
+                }
+            }
+            return true;
+        };
+        int mine = 0;
+        for (int i = tid; i < nlist; i += 256) {
+            const bool k = keep(sList[i], g->iniTh);
+            sKeep[i] = k;
+            mine += k;
+        }
+        if (mine) atomicAdd(&s_cnt, mine);
+        __syncthreads();
+        if (s_cnt == 0) {   // :812-816 fallback to minThFAST, evaluated after NMS
+            for (int i = tid; i < nlist; i += 256) sKeep[i] = keep(sList[i], g->minTh);
+            __syncthreads();
+        }
+        // emission in raster order (FAST emission order)
+        const LevelGeom& L = g->L[c.l];
+        uint32_t* out = cands + (long long)c.f * g->ncand + L.cand_base + (long long)(c.cell - L.cell_base) * L.cell_cap;
+        int running = 0;
+        for (int b0 = 0; b0 < nlist; b0 += 256) {
+            const int i = b0 + tid;
+            const bool k = i < nlist && sKeep[i];
+            int pos;
+            running = chunk_append(k, running, s_wave, pos);
+            if (k) {
+                const int p = sList[i];
+                const uint32_t xr = (uint32_t)((p & 63) + 3 + c.cj * L.wCell);
+                const uint32_t yr = (uint32_t)((p >> 6) + 3 + c.ci * L.hCell);
+                out[pos] = xr | (yr << 12) | ((uint32_t)(sM[p] - 1) << 24);
             }
         }
-        return true;
-    };
-    int mine = 0;
-    for (int i = tid; i < nlist; i += 256) {
-        const bool k = keep(sList[i], g->iniTh);
-        sKeep[i] = k;
-        mine += k;
+        if (tid == 0) *cntOut = running;
     }
-    if (mine) atomicAdd(&s_cnt, mine);
-    __syncthreads();
-    if (s_cnt == 0) {   // :812-816 fallback to minThFAST, evaluated after NMS
-        for (int i = tid; i < nlist; i += 256) sKeep[i] = keep(sList[i], g->minTh);
-        __syncthreads();
-    }
-    // emission in raster order (FAST emission order)
-    uint32_t* out = cands + (long long)f * g->ncand + L.cand_base + (long long)c * L.cell_cap;
-    int running = 0;
-    for (int b0 = 0; b0 < nlist; b0 += 256) {
-        const int i = b0 + tid;
-        const bool k = i < nlist && sKeep[i];
-        int pos;
-        running = chunk_append(k, running, s_wave, pos);
-        if (k) {
-            const int p = sList[i];
-            const int dy = div_dw(p), dx = p - dy * dw;
-            const uint32_t xr = (uint32_t)(dx + 3 + cj * L.wCell);
-            const uint32_t yr = (uint32_t)(dy + 3 + ci * L.hCell);
-            out[pos] = xr | (yr << 12) | ((uint32_t)(sM[p] - 1) << 24);
-        }
-    }
-    if (tid == 0) *cntOut = running;
 }
 
 /* ------------------------------------------------------------------------------------------------
@@ -928,8 +1001,9 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     }
     if (marker) marker(user, ORB_K_RESIZE, 0);
     if (marker) marker(user, ORB_K_FAST, 1);
-    hipLaunchKernelGGL(k_fast, dim3(g.ncells, nframes), dim3(256), 0, stream, b.d_geom, d_frames, frame_pitch,
-                       row_stride, b.d_pyr, b.d_cands, b.d_cellCount);
+    const int fast_items = g.ncells * nframes;
+    hipLaunchKernelGGL(k_fast, dim3(fast_items), dim3(256), 0, stream, b.d_geom, d_frames,
+                       frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
     if (marker) marker(user, ORB_K_FAST, 0);
     if (marker) marker(user, ORB_K_OCTREE, 1);
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, nframes), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap),

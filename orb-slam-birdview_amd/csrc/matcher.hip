@@ -469,6 +469,7 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
             for (int q : rotHist[i]) { vMatches12[q] = -1; nmatches--; }
         }
     }
+    (void)nmatches;   // == the number of pairs collected below (:815-820)
     int np = 0;
     for (int i = 0; i < n1; i++) {
         if (vMatches12[i] < 0) continue;

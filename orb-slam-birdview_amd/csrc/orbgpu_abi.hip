@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -231,6 +232,7 @@ ExtractBuffers Ctx::buffers() const {
     b.d_lvlKps = d_lvlKps;
     b.d_lvlCount = d_lvlCount;
     b.d_err = d_err;
+    b.fast_remap = fast_remap ? 1 : 0;
     return b;
 }
 
@@ -239,7 +241,7 @@ void Ctx::marker(void* user, int id, int begin) {
     if (!c->prof_on) return;
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) return;
-    hipEventRecord(ev, c->stream);
+    (void)hipEventRecord(ev, c->stream);
     if (begin) c->prof_open[id] = ev;
     else c->prof_pairs.push_back({id, c->prof_open[id], ev});
 }
@@ -304,6 +306,10 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (!c) return fail(ORB_ERR_NOMEM);
     c->p = *p;
     c->device = p->device;
+    if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
+        c->num_cu < 1)
+        c->num_cu = 256;
+    if (const char* e = std::getenv("ORBGPU_FAST_REMAP")) c->fast_remap = e[0] == '1';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);

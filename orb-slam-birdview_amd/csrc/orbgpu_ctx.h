@@ -17,6 +17,8 @@ struct ProfPair {
 struct Ctx {
     orb_params p{};
     int device = 0;
+    int num_cu = 256;
+    bool fast_remap = true;   // ORBGPU_FAST_REMAP=0 disables the XCD-contiguous cell remap (A/B switch)
     hipStream_t stream = nullptr;
 
     // ORBextractor tables (ORBextractor.cc:410-470)

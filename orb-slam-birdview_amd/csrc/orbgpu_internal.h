@@ -74,6 +74,7 @@ struct ExtractBuffers {
     uint32_t* d_lvlKps;            // nframes * nkpcap
     int* d_lvlCount;               // nframes * nlevels
     int* d_err;                    // 1 int: internal overflow flag
+    int fast_remap;                // XCD-contiguous block->cell remap in k_fast (speed only)
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin);
