@@ -259,7 +259,7 @@ def main():
     sum_k_s = sum(ms_per_step_k.values()) / 1e3
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5),
-                "traffic": (traffic * launches_per_step / B if traffic is not None else None),
+                "traffic": (round(traffic) if traffic is not None else None),   # HBM bytes per launch (PMC)
                 "algorithmic_bytes_per_frame": int(ab[dom]), "launches_per_step": launches_per_step,
                 "kernel_avg_launch_us": round(dom_s / launches_per_step * 1e6, 2),
                 "pipeline": {"bytes_per_frame": int(ab["pipeline"]),

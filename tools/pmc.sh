@@ -1,12 +1,15 @@
 #!/bin/bash
-# rocprofv3 PMC passes over a short bench run (one counter group per pass, --kernel-trace only,
-# no sys/runtime traces).  Results under gpurun_out/pmc/<pass>/.
-OUT=gpurun_out/pmc; mkdir -p $OUT; export TMPDIR=/tmp; cd /tmp; cd - >/dev/null
-ARGS="--steps 5 --warmup 1 --no-cpu --no-hamming"
-[ -n "$LIST" ] && { rocprofv3 -L > $OUT/counters.txt 2>&1; grep -oE "^[[:space:]]*(SQ|TCC|TCP|TA|GRBM)[A-Za-z0-9_]*" $OUT/counters.txt | sort -u > $OUT/counter_names.txt; }
-i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_GROUPS}; do
-  i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc ${grp//,/ } --kernel-trace --output-format csv -d $OUT/p$i -o run -- python bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i ($grp) failed"; tail -20 $OUT/p$i.log; exit 1; }
-  echo "pass $i ($grp) ok"
+# rocprofv3 PMC passes (one TCC counter per pass, --kernel-trace only; no sys/runtime traces):
+#   calibration binary (known byte counts per access width) and a short bench run, FETCH_SIZE then
+#   WRITE_SIZE.  Results under gpurun_out/pmc/<pass>/; tools/pmc_report.py turns them into
+#   profiles/pmc_traffic.json.  Every GPU step has its own time limit; the script stops at the first failure.
+OUT=gpurun_out/pmc; mkdir -p $OUT; export TMPDIR=/tmp
+ARGS="--steps 3 --warmup 1 --no-cpu --no-hamming ${BENCH_ARGS}"
+timeout -k 10 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/pmc_calib tools/pmc_calib.hip || { echo "calib build failed"; exit 1; }
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/calib_$ctr -o run -- /tmp/pmc_calib > $OUT/calib_$ctr.log 2>&1 || { echo "calib $ctr failed"; tail -20 $OUT/calib_$ctr.log; exit 1; }
+  echo "calib $ctr ok"
+  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/bench_$ctr -o run -- python3 bench.py $ARGS > $OUT/bench_$ctr.log 2>&1 || { echo "bench $ctr failed"; tail -20 $OUT/bench_$ctr.log; exit 1; }
+  echo "bench $ctr ok"
 done
+python3 tools/pmc_report.py $OUT > $OUT/report.json && cat $OUT/report.json
