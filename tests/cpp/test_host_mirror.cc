@@ -1,0 +1,320 @@
+// C++ parity test of the host mirror (ORB_SLAM2::ORBextractor / ORBmatcher over liborbgpu) against
+// the oracle restatement (test infrastructure, linked only here).  Written the way the reference's
+// own code drives these classes: construct an extractor, call operator(), read the getters and
+// mvImagePyramid, run each ORBmatcher search on two extracted views.
+//
+// usage: test_host_mirror <frames.raw> <w> <h> <nframes> <nfeatures>
+//   frames.raw holds nframes gray w x h frames back to back (written by tests/test_host_mirror.py).
+// Prints one "CHECK <name> PASS|FAIL <detail>" line per check and "SUMMARY <npass> <nfail>";
+// exit status 0 iff every check passed.
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../oracle/orb_oracle.h"
+#include "../../orb-slam-birdview_amd/host/ORBextractor.h"
+#include "../../orb-slam-birdview_amd/host/ORBmatcher.h"
+
+using namespace ORB_SLAM2;
+
+static int g_pass = 0, g_fail = 0;
+
+static void report(const std::string& name, bool ok, const std::string& detail = "") {
+    printf("CHECK %s %s %s\n", name.c_str(), ok ? "PASS" : "FAIL", detail.c_str());
+    (ok ? g_pass : g_fail)++;
+}
+
+struct OracleOut {
+    std::vector<OracleKeyPoint> kps;
+    std::vector<uint8_t> desc;
+    void* h = nullptr;
+};
+
+static OracleOut oracle_extract(const uint8_t* img, int w, int h, int nf, float sf = 1.2f, int nl = 8, int ini = 20,
+                                int mn = 7) {
+    OracleOut o;
+    o.h = oracle_create(nf, sf, nl, ini, mn, 0);
+    const int n = oracle_run(o.h, img, w, h, w);
+    if (n > 0) {
+        o.kps.resize(n);
+        o.desc.resize((size_t)n * 32);
+        oracle_get_output(o.h, o.kps.data(), o.desc.data(), n);
+    }
+    return o;
+}
+
+static FeatureVector make_featvec(const DescriptorMat& d, int nodes) {
+    // synthetic vocabulary: node = high nibble of descriptor byte 0 (similar descriptors share nodes)
+    FeatureVector fv;
+    for (int i = 0; i < d.rows; i++) fv[(d.ptr(i)[0] >> 4) % nodes].push_back((unsigned)i);
+    return fv;
+}
+
+struct OracleFv {
+    std::vector<uint32_t> ids;
+    std::vector<int> off, idx;
+    OracleFeatVec fv;
+    explicit OracleFv(const FeatureVector& f) {
+        off.push_back(0);
+        for (FeatureVector::const_iterator it = f.begin(); it != f.end(); ++it) {
+            ids.push_back(it->first);
+            for (size_t j = 0; j < it->second.size(); j++) idx.push_back((int)it->second[j]);
+            off.push_back((int)idx.size());
+        }
+        if (idx.empty()) idx.push_back(0);
+        fv.nnodes = (int)ids.size();
+        fv.node_ids = ids.data();
+        fv.offsets = off.data();
+        fv.indices = idx.data();
+    }
+};
+
+static std::vector<float> angles_of(const std::vector<KeyPoint>& k) {
+    std::vector<float> a(k.size());
+    for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
+    return a;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        fprintf(stderr, "usage: %s frames.raw w h nframes nfeatures\n", argv[0]);
+        return 2;
+    }
+    const int w = atoi(argv[2]), h = atoi(argv[3]), nframes = atoi(argv[4]), nf = atoi(argv[5]);
+    std::vector<uint8_t> frames((size_t)w * h * nframes);
+    FILE* fp = fopen(argv[1], "rb");
+    if (!fp || fread(frames.data(), 1, frames.size(), fp) != frames.size()) {
+        fprintf(stderr, "cannot read %s\n", argv[1]);
+        return 2;
+    }
+    fclose(fp);
+
+    try {
+        ORBextractor extractor(nf, 1.2f, 8, 20, 7);
+
+        // ---- getters (ORBextractor.h:63-83) vs the oracle's ctor tables (ORBextractor.cc:410-470)
+        {
+            std::vector<float> s(8), is(8), s2(8), is2(8);
+            std::vector<int> npl(8), um(16);
+            void* oh = oracle_create(nf, 1.2f, 8, 20, 7, 0);
+            oracle_tables(oh, s.data(), is.data(), s2.data(), is2.data(), npl.data(), um.data());
+            oracle_destroy(oh);
+            const bool ok = extractor.GetLevels() == 8 && extractor.GetScaleFactor() == 1.2f &&
+                            extractor.GetScaleFactors() == s && extractor.GetInverseScaleFactors() == is &&
+                            extractor.GetScaleSigmaSquares() == s2 && extractor.GetInverseScaleSigmaSquares() == is2;
+            report("getters", ok);
+        }
+
+        // ---- operator() on every frame: keypoints and descriptors byte-for-byte, pyramid levels
+        std::vector<std::vector<KeyPoint> > allK(nframes);
+        std::vector<DescriptorMat> allD(nframes);
+        for (int f = 0; f < nframes; f++) {
+            const uint8_t* img = frames.data() + (size_t)f * w * h;
+            extractor(ImageView(img, w, h), ImageView(), allK[f], allD[f]);
+            OracleOut o = oracle_extract(img, w, h, nf);
+            bool ok = allK[f].size() == o.kps.size() && (size_t)allD[f].rows == o.kps.size();
+            if (ok && !o.kps.empty())
+                ok = memcmp(allK[f].data(), o.kps.data(), o.kps.size() * sizeof(KeyPoint)) == 0 &&
+                     memcmp(allD[f].buf.data(), o.desc.data(), o.desc.size()) == 0;
+            char det[96];
+            snprintf(det, sizeof det, "n=%zu oracle=%zu", allK[f].size(), o.kps.size());
+            report("extract_frame" + std::to_string(f), ok, det);
+            bool pok = extractor.mvImagePyramid.size() == 8;
+            for (int l = 0; pok && l < 8; l++) {
+                int lw = 0, lh = 0;
+                oracle_level_size(o.h, l, &lw, &lh);
+                std::vector<uint8_t> ol((size_t)lw * lh);
+                oracle_get_level(o.h, l, ol.data());
+                const ImageView& v = extractor.mvImagePyramid[l];
+                pok = v.cols == lw && v.rows == lh;
+                for (int y = 0; pok && y < lh; y++) pok = memcmp(v.data + (size_t)y * v.step, &ol[(size_t)y * lw], lw) == 0;
+            }
+            report("mvImagePyramid_frame" + std::to_string(f), pok);
+            oracle_destroy(o.h);
+        }
+
+        // ---- empty image: outputs untouched (ORBextractor.cc:1046-1047)
+        {
+            std::vector<KeyPoint> k = allK[0];
+            DescriptorMat d = allD[0];
+            extractor(ImageView(), ImageView(), k, d);
+            report("empty_image_untouched", k.size() == allK[0].size() && d.rows == allD[0].rows);
+        }
+        // ---- flat image: no keypoints, descriptors released (:1061-1070)
+        {
+            std::vector<uint8_t> flat((size_t)w * h, 128);
+            std::vector<KeyPoint> k(3);
+            DescriptorMat d;
+            d.create(3);
+            extractor(ImageView(flat.data(), w, h), ImageView(), k, d);
+            report("flat_image_released", k.empty() && d.empty());
+        }
+
+        if (nframes < 2) {
+            printf("SUMMARY %d %d\n", g_pass, g_fail);
+            return g_fail ? 1 : 0;
+        }
+
+        // ---- ORBmatcher on views 0 and 1 (the test writes frame 1 = frame 0 shifted)
+        const std::vector<KeyPoint>& k1 = allK[0];
+        const std::vector<KeyPoint>& k2 = allK[1];
+        const DescriptorMat& d1 = allD[0];
+        const DescriptorMat& d2 = allD[1];
+        const int n1 = (int)k1.size(), n2 = (int)k2.size();
+        FeatureVector fv1 = make_featvec(d1, 16), fv2 = make_featvec(d2, 16);
+        OracleFv ofv1(fv1), ofv2(fv2);
+        std::vector<uint8_t> mp1(n1), mp2(n2);
+        for (int i = 0; i < n1; i++) mp1[i] = (i % 5) != 0;
+        for (int i = 0; i < n2; i++) mp2[i] = (i % 7) != 0;
+        std::vector<float> a1 = angles_of(k1), a2 = angles_of(k2);
+
+        report("DescriptorDistance", ORBmatcher::DescriptorDistance(d1.ptr(0), d2.ptr(0)) ==
+                                         oracle_descriptor_distance(d1.ptr(0), d2.ptr(0)));
+
+        const float ratios[2] = {0.7f, 0.75f};
+        for (int ri = 0; ri < 2; ri++)
+            for (int co = 0; co < 2; co++) {
+                ORBmatcher matcher(ratios[ri], co != 0);
+                const std::string tag = std::string("_r") + std::to_string(ri) + "_ori" + std::to_string(co);
+                // SearchByBoW(KeyFrame*, Frame&, ...) (ORBmatcher.cc:159-288)
+                KeyFrameData KF;
+                KF.keys = &k1;
+                KF.descriptors = &d1;
+                KF.featVec = &fv1;
+                KF.hasMapPoint = &mp1;
+                FrameData F;
+                F.keys = &k2;
+                F.descriptors = &d2;
+                F.featVec = &fv2;
+                std::vector<int> vpMapPointMatches;
+                const int nm = matcher.SearchByBoW(KF, F, vpMapPointMatches);
+                std::vector<int> om(n2, -1);
+                const int onm = oracle_search_by_bow_kf_f(ratios[ri], co, n1, d1.buf.data(), a1.data(), mp1.data(), ofv1.fv,
+                                                          n2, d2.buf.data(), a2.data(), ofv2.fv, om.data());
+                report("SearchByBoW_KF_F" + tag, nm == onm && vpMapPointMatches == om,
+                       "n=" + std::to_string(nm) + " oracle=" + std::to_string(onm));
+                // SearchByBoW(KeyFrame*, KeyFrame*, ...) (:522-655)
+                KeyFrameData KF2;
+                KF2.keys = &k2;
+                KF2.descriptors = &d2;
+                KF2.featVec = &fv2;
+                KF2.hasMapPoint = &mp2;
+                std::vector<int> vpMatches12;
+                const int nm2 = matcher.SearchByBoW(KF, KF2, vpMatches12);
+                std::vector<int> om2(n1, -1);
+                const int onm2 = oracle_search_by_bow_kf_kf(ratios[ri], co, n1, d1.buf.data(), a1.data(), mp1.data(),
+                                                            ofv1.fv, n2, d2.buf.data(), a2.data(), mp2.data(), ofv2.fv,
+                                                            om2.data());
+                report("SearchByBoW_KF_KF" + tag, nm2 == onm2 && vpMatches12 == om2,
+                       "n=" + std::to_string(nm2) + " oracle=" + std::to_string(onm2));
+            }
+
+        // ---- SearchForTriangulation (:657-823): no MapPoints on half the features, mono + stereo
+        {
+            std::vector<uint8_t> hm1(n1), hm2(n2);
+            std::vector<float> ur1(n1), ur2(n2);
+            for (int i = 0; i < n1; i++) {
+                hm1[i] = (i % 2) == 0;
+                ur1[i] = (i % 3) ? -1.f : k1[i].x - 10.f;
+            }
+            for (int i = 0; i < n2; i++) {
+                hm2[i] = (i % 3) == 0;
+                ur2[i] = (i % 4) ? -1.f : k2[i].x - 12.f;
+            }
+            std::vector<float> sc = extractor.GetScaleFactors(), s2 = extractor.GetScaleSigmaSquares();
+            // fundamental matrix of a pure x-translation (epipolar lines = rows) with a small tilt
+            const float F12[9] = {0.f, -1e-4f, 0.002f, 1e-4f, 0.f, -1.f, -0.03f, 1.f, 0.5f};
+            for (int only_stereo = 0; only_stereo < 2; only_stereo++) {
+                ORBmatcher matcher(0.6f, false);   // LocalMapping.cc:225
+                KeyFrameData A, B;
+                A.keys = &k1;
+                A.descriptors = &d1;
+                A.featVec = &fv1;
+                A.hasMapPoint = &hm1;
+                A.uRight = &ur1;
+                B.keys = &k2;
+                B.descriptors = &d2;
+                B.featVec = &fv2;
+                B.hasMapPoint = &hm2;
+                B.uRight = &ur2;
+                B.scaleFactors = &sc;
+                B.levelSigma2 = &s2;
+                std::vector<std::pair<size_t, size_t> > pairs;
+                const int np = matcher.SearchForTriangulation(A, B, F12, 5000.f, 300.f, pairs, only_stereo != 0);
+                std::vector<int> op(2 * (size_t)n1 + 2);
+                const int onp = oracle_search_for_triangulation(
+                    0, only_stereo, n1, d1.buf.data(), (const OracleKeyPoint*)k1.data(), hm1.data(), ur1.data(), ofv1.fv,
+                    n2, d2.buf.data(), (const OracleKeyPoint*)k2.data(), hm2.data(), ur2.data(), ofv2.fv, F12, 5000.f,
+                    300.f, sc.data(), s2.data(), op.data(), n1 + 1);
+                bool ok = np == onp && (int)pairs.size() == np;
+                for (int i = 0; ok && i < np; i++) ok = (int)pairs[i].first == op[2 * i] && (int)pairs[i].second == op[2 * i + 1];
+                report("SearchForTriangulation_stereo" + std::to_string(only_stereo), ok,
+                       "n=" + std::to_string(np) + " oracle=" + std::to_string(onp));
+            }
+        }
+
+        // ---- window matchers: SearchForInitialization (:405-520), BirdviewMatch x2 (:1667-1899)
+        {
+            FrameGrid grid(k2, 0.f, (float)w, 0.f, (float)h);
+            FrameData F1, F2;
+            F1.keys = &k1;
+            F1.descriptors = &d1;
+            F2.keys = &k2;
+            F2.descriptors = &d2;
+            F2.grid = &grid;
+            for (int win = 0; win < 2; win++) {
+                const int windowSize = win ? 100 : 15;   // Tracking.cc:739 (init), :744 (bird)
+                ORBmatcher matcher(0.9f, true);
+                std::vector<Point2f> prev(n1);
+                for (int i = 0; i < n1; i++) prev[i] = Point2f{k1[i].x, k1[i].y};
+                std::vector<Point2f> prevB = prev;
+                std::vector<int> m12, m12b, m12c;
+                const int nm = matcher.SearchForInitialization(F1, F2, prev, m12, windowSize);
+                const int nmb = matcher.BirdviewMatch(F1, F2, m12b, prevB, windowSize);
+                const int nmc = matcher.BirdviewMatch(F1, F2, m12c, windowSize);
+                // oracle: candidates from the oracle's GetFeaturesInArea
+                for (int lvl0 = 1; lvl0 >= 0; lvl0--) {
+                    std::vector<int> off(n1 + 1, 0), idx;
+                    std::vector<int> buf(n2 + 1);
+                    for (int i = 0; i < n1; i++) {
+                        if (!(lvl0 && k1[i].octave > 0)) {
+                            const int c = oracle_features_in_area(n2, (const OracleKeyPoint*)k2.data(), 0.f, (float)w, 0.f,
+                                                                  (float)h, k1[i].x, k1[i].y, (float)windowSize,
+                                                                  k1[i].octave, k1[i].octave, buf.data(), n2 + 1);
+                            idx.insert(idx.end(), buf.begin(), buf.begin() + c);
+                        }
+                        off[i + 1] = (int)idx.size();
+                    }
+                    if (idx.empty()) idx.push_back(0);
+                    std::vector<int> om(n1 + 1, -1);
+                    const int onm = oracle_window_match(0.9f, 1, lvl0, n1, d1.buf.data(), (const OracleKeyPoint*)k1.data(),
+                                                        n2, d2.buf.data(), (const OracleKeyPoint*)k2.data(), off.data(),
+                                                        idx.data(), om.data());
+                    om.resize(n1);
+                    const std::string tag = "_win" + std::to_string(windowSize);
+                    if (lvl0) {
+                        report("SearchForInitialization" + tag, nm == onm && m12 == om,
+                               "n=" + std::to_string(nm) + " oracle=" + std::to_string(onm));
+                        report("BirdviewMatch_prev" + tag, nmb == onm && m12b == om);
+                        bool pok = true;
+                        for (int i = 0; i < n1; i++)
+                            if (om[i] >= 0) pok = pok && prev[i].x == k2[om[i]].x && prev[i].y == k2[om[i]].y;
+                        report("SearchForInitialization_prev_updated" + tag, pok);
+                    } else {
+                        report("BirdviewMatch" + tag, nmc == onm && m12c == om,
+                               "n=" + std::to_string(nmc) + " oracle=" + std::to_string(onm));
+                    }
+                }
+            }
+        }
+    } catch (const std::exception& e) {
+        report("exception", false, e.what());
+    }
+    printf("SUMMARY %d %d\n", g_pass, g_fail);
+    return g_fail ? 1 : 0;
+}

@@ -1,0 +1,73 @@
+"""The C++ host mirror (orb-slam-birdview_amd/host/: ORB_SLAM2::ORBextractor / ORBmatcher over the
+C-ABI).  GPU: tests/cpp/test_host_mirror drives the mirror the way Frame/Tracking/LocalMapping drive
+the reference classes and checks every result against the oracle, bit-exact.  CPU: the mirror
+builds, links liborbgpu and fails loudly (OrbGpuError, no CPU fallback) without a device."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "orb-slam-birdview_amd")
+CPP = os.path.join(ROOT, "tests", "cpp")
+BIN = os.path.join(CPP, "test_host_mirror")
+
+
+@pytest.fixture(scope="module")
+def mirror_bin():
+    subprocess.check_call(["make", "-s", "-C", PKG, "liborbslam_host.so"])
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    subprocess.check_call(["make", "-s", "-C", CPP])
+    return BIN
+
+
+def _run(bin_path, frames, nf, tmp_path):
+    n, h, w = frames.shape
+    raw = tmp_path / f"frames_{w}x{h}.raw"
+    raw.write_bytes(np.ascontiguousarray(frames, np.uint8).tobytes())
+    p = subprocess.run([bin_path, str(raw), str(w), str(h), str(n), str(nf)], capture_output=True, text=True,
+                       timeout=300)
+    return p.returncode, p.stdout, p.stderr
+
+
+def test_mirror_library_exports_reference_api(mirror_bin):
+    lib = ctypes.CDLL(os.path.join(PKG, "liborbslam_host.so"))
+    out = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(PKG, "liborbslam_host.so")],
+                         capture_output=True, text=True, check=True).stdout
+    for sym in ["ORB_SLAM2::ORBextractor::ORBextractor(int, float, int, int, int)",
+                "ORB_SLAM2::ORBextractor::operator()(ORB_SLAM2::ImageView const&, ORB_SLAM2::ImageView const&, "
+                "std::vector<orb_keypoint, std::allocator<orb_keypoint> >&, ORB_SLAM2::DescriptorMat&)",
+                "ORB_SLAM2::ORBmatcher::ORBmatcher(float, bool)",
+                "ORB_SLAM2::ORBmatcher::DescriptorDistance(unsigned char const*, unsigned char const*)",
+                "ORB_SLAM2::ORBmatcher::SearchByBoW(ORB_SLAM2::KeyFrameData const&, ORB_SLAM2::FrameData const&",
+                "ORB_SLAM2::ORBmatcher::SearchByBoW(ORB_SLAM2::KeyFrameData const&, ORB_SLAM2::KeyFrameData const&",
+                "ORB_SLAM2::ORBmatcher::SearchForTriangulation(",
+                "ORB_SLAM2::ORBmatcher::SearchForInitialization(",
+                "ORB_SLAM2::ORBmatcher::BirdviewMatch(",
+                "ORB_SLAM2::FrameGrid::GetFeaturesInArea("]:
+        assert sym in out, sym
+    del lib
+
+
+def test_mirror_fails_loudly_without_gpu(mirror_bin, tmp_path):
+    import orbgpu
+    if orbgpu.device_count() > 0:
+        pytest.skip("a GPU is present")
+    rc, out, _ = _run(mirror_bin, np.zeros((1, 64, 64), np.uint8), 100, tmp_path)
+    assert rc == 1
+    assert "CHECK exception FAIL orb_create" in out and "no CPU fallback" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1280, 720, 2000)])
+def test_mirror_parity_on_gpu(mirror_bin, tmp_path, w, h, nf):
+    from orbgpu.synth import synth_frame
+    a = synth_frame(w, h, 21)
+    frames = np.stack([a, np.roll(a, (3, 5), axis=(0, 1)), synth_frame(w, h, 5, "noise")])
+    rc, out, err = _run(mirror_bin, frames, nf, tmp_path)
+    fails = [l for l in out.splitlines() if " FAIL" in l]
+    assert rc == 0 and not fails, "\n".join(fails) + "\n" + err[-2000:]
+    summary = [l for l in out.splitlines() if l.startswith("SUMMARY")][0].split()
+    assert int(summary[1]) >= 20 and int(summary[2]) == 0
