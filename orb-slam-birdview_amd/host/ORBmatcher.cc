@@ -8,7 +8,7 @@
 
 #include <algorithm>
 
-namespace ORB_SLAM2 {
+namespace ORBGPU_MATCHER_NAMESPACE {
 
 const int ORBmatcher::TH_HIGH = 100;   // ORBmatcher.cc:37-39
 const int ORBmatcher::TH_LOW = 50;
@@ -74,52 +74,56 @@ struct Csr {
 };
 
 std::vector<float> angles(const FeatureSet& s) {
-    std::vector<float> a(s.N());
-    for (int i = 0; i < s.N(); i++) a[i] = (*s.keys)[i].angle;
+    std::vector<float> a(std::max(s.N(), 1), 0.f);
+    for (int i = 0; i < s.N(); i++) a[i] = s.keys[i].angle;
     return a;
 }
 
 const uint8_t* desc_ptr(const FeatureSet& s) {
     static const uint8_t dummy[32] = {0};
-    return (s.descriptors && s.descriptors->rows) ? s.descriptors->buf.data() : dummy;
+    return (s.descriptors && s.N()) ? s.descriptors : dummy;
 }
 
 const KeyPoint* keys_ptr(const FeatureSet& s) {
     static const KeyPoint dummy = {0, 0, 0, 0, 0, 0, 0};
-    return s.N() ? s.keys->data() : &dummy;
+    return (s.keys && s.N()) ? s.keys : &dummy;
 }
 
-std::vector<uint8_t> flags_or(const std::vector<uint8_t>* v, int n, uint8_t dflt) {
-    return v ? *v : std::vector<uint8_t>(std::max(n, 1), dflt);
+void require(bool ok, const char* what) {
+    if (!ok) throw OrbGpuError(ORB_ERR_ARG, what);
 }
 
-std::vector<float> floats_or(const std::vector<float>* v, int n, float dflt) {
-    return v ? *v : std::vector<float>(std::max(n, 1), dflt);
+std::vector<uint8_t> flags_or(const uint8_t* v, int n, uint8_t dflt) {
+    return v ? std::vector<uint8_t>(v, v + n) : std::vector<uint8_t>(n, dflt);
+}
+
+std::vector<float> floats_or(const float* v, int n, float dflt) {
+    return v ? std::vector<float>(v, v + n) : std::vector<float>(n, dflt);
 }
 
 }  // namespace
 
 /* ---------------- Frame grid (Frame.cc:378-412, 494-560, 877-940) ---------------- */
-FrameGrid::FrameGrid(const std::vector<KeyPoint>& keysUn, float minX, float maxX, float minY, float maxY) {
+FrameGrid::FrameGrid(const KeyPoint* keysUn, int n, float minX, float maxX, float minY, float maxY) {
     minX_ = minX;
     minY_ = minY;
     invW_ = static_cast<float>(ORBGPU_FRAME_GRID_COLS) / static_cast<float>(maxX - minX);   // Frame.cc:156-157
     invH_ = static_cast<float>(ORBGPU_FRAME_GRID_ROWS) / static_cast<float>(maxY - minY);
-    assign(keysUn);
+    assign(keysUn, n);
 }
 
-FrameGrid FrameGrid::Birdview(const std::vector<KeyPoint>& keysBird, float widthInv, float heightInv) {
+FrameGrid FrameGrid::Birdview(const KeyPoint* keysBird, int n, float widthInv, float heightInv) {
     FrameGrid g;
     g.invW_ = widthInv;
     g.invH_ = heightInv;
-    g.assign(keysBird);
+    g.assign(keysBird, n);
     return g;
 }
 
-void FrameGrid::assign(const std::vector<KeyPoint>& keys) {
-    keys_ = &keys;
+void FrameGrid::assign(const KeyPoint* keys, int n) {
+    keys_ = keys;
     cells_.assign((size_t)ORBGPU_FRAME_GRID_COLS * ORBGPU_FRAME_GRID_ROWS, std::vector<size_t>());
-    for (size_t i = 0; i < keys.size(); i++) {
+    for (int i = 0; i < n; i++) {
         // PosInGrid (Frame.cc:549-560): round((x - mnMinX) * inv)
         const int posX = (int)round((keys[i].x - minX_) * invW_);
         const int posY = (int)round((keys[i].y - minY_) * invH_);
@@ -130,7 +134,7 @@ void FrameGrid::assign(const std::vector<KeyPoint>& keys) {
 
 std::vector<size_t> FrameGrid::GetFeaturesInArea(float x, float y, float r, int minLevel, int maxLevel) const {
     std::vector<size_t> vIndices;
-    if (!keys_) return vIndices;
+    if (cells_.empty()) return vIndices;
     const int nMinCellX = std::max(0, (int)floor((x - minX_ - r) * invW_));
     if (nMinCellX >= ORBGPU_FRAME_GRID_COLS) return vIndices;
     const int nMaxCellX = std::min((int)ORBGPU_FRAME_GRID_COLS - 1, (int)ceil((x - minX_ + r) * invW_));
@@ -144,7 +148,7 @@ std::vector<size_t> FrameGrid::GetFeaturesInArea(float x, float y, float r, int 
         for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
             const std::vector<size_t>& vCell = cells_[(size_t)ix * ORBGPU_FRAME_GRID_ROWS + iy];
             for (size_t j = 0; j < vCell.size(); j++) {
-                const KeyPoint& kp = (*keys_)[vCell[j]];
+                const KeyPoint& kp = keys_[vCell[j]];
                 if (bCheckLevels) {
                     if (kp.octave < minLevel) continue;
                     if (maxLevel >= 0 && kp.octave > maxLevel) continue;
@@ -165,10 +169,10 @@ int ORBmatcher::SearchByBoW(const KeyFrameData& KF, const FrameData& F, std::vec
     const int nKF = KF.N(), nF = F.N();
     vpMapPointMatches.assign(nF, -1);   // :163 vector<MapPoint*>(F.N, NULL)
     Csr a(KF.featVec), b(F.featVec);
+    require(nKF == 0 || (KF.keys && KF.descriptors), "SearchByBoW: KF keys/descriptors");
+    require(nF == 0 || (F.keys && F.descriptors), "SearchByBoW: F keys/descriptors");
     std::vector<float> angKF = angles(KF), angF = angles(F);
-    angKF.resize(std::max(nKF, 1));
-    angF.resize(std::max(nF, 1));
-    std::vector<uint8_t> mp = flags_or(KF.hasMapPoint, nKF, 1);
+    std::vector<uint8_t> mp = flags_or(KF.hasMapPoint, std::max(nKF, 1), 1);
     std::vector<int> out(std::max(nF, 1), -1);
     int nmatches = 0;
     check(orb_search_by_bow_kf_f(matcher_ctx(), mfNNratio, mbCheckOrientation, nKF, desc_ptr(KF), angKF.data(),
@@ -182,10 +186,11 @@ int ORBmatcher::SearchByBoW(const KeyFrameData& KF1, const KeyFrameData& KF2, st
     const int n1 = KF1.N(), n2 = KF2.N();
     vpMatches12.assign(n1, -1);   // :535
     Csr a(KF1.featVec), b(KF2.featVec);
+    require(n1 == 0 || (KF1.keys && KF1.descriptors), "SearchByBoW: KF1 keys/descriptors");
+    require(n2 == 0 || (KF2.keys && KF2.descriptors), "SearchByBoW: KF2 keys/descriptors");
     std::vector<float> ang1 = angles(KF1), ang2 = angles(KF2);
-    ang1.resize(std::max(n1, 1));
-    ang2.resize(std::max(n2, 1));
-    std::vector<uint8_t> mp1 = flags_or(KF1.hasMapPoint, n1, 1), mp2 = flags_or(KF2.hasMapPoint, n2, 1);
+    std::vector<uint8_t> mp1 = flags_or(KF1.hasMapPoint, std::max(n1, 1), 1),
+                         mp2 = flags_or(KF2.hasMapPoint, std::max(n2, 1), 1);
     std::vector<int> out(std::max(n1, 1), -1);
     int nmatches = 0;
     check(orb_search_by_bow_kf_kf(matcher_ctx(), mfNNratio, mbCheckOrientation, n1, desc_ptr(KF1), ang1.data(),
@@ -201,15 +206,18 @@ int ORBmatcher::SearchForTriangulation(const KeyFrameData& KF1, const KeyFrameDa
                                        const bool bOnlyStereo) {
     const int n1 = KF1.N(), n2 = KF2.N();
     Csr a(KF1.featVec), b(KF2.featVec);
-    std::vector<uint8_t> mp1 = flags_or(KF1.hasMapPoint, n1, 0), mp2 = flags_or(KF2.hasMapPoint, n2, 0);
-    std::vector<float> ur1 = floats_or(KF1.uRight, n1, -1.f), ur2 = floats_or(KF2.uRight, n2, -1.f);
-    if (!KF2.scaleFactors || !KF2.levelSigma2) throw OrbGpuError(ORB_ERR_ARG, "SearchForTriangulation: KF2 scale tables");
+    require(n1 == 0 || (KF1.keys && KF1.descriptors), "SearchForTriangulation: KF1 keys/descriptors");
+    require(n2 == 0 || (KF2.keys && KF2.descriptors), "SearchForTriangulation: KF2 keys/descriptors");
+    require(KF2.scaleFactors && KF2.levelSigma2 && KF2.nlevels > 0, "SearchForTriangulation: KF2 scale tables");
+    std::vector<uint8_t> mp1 = flags_or(KF1.hasMapPoint, std::max(n1, 1), 0),
+                         mp2 = flags_or(KF2.hasMapPoint, std::max(n2, 1), 0);
+    std::vector<float> ur1 = floats_or(KF1.uRight, std::max(n1, 1), -1.f), ur2 = floats_or(KF2.uRight, std::max(n2, 1), -1.f);
     std::vector<int> pairs(2 * (size_t)std::max(n1, 1));
     int np = 0;
     check(orb_search_for_triangulation(matcher_ctx(), mbCheckOrientation, bOnlyStereo, n1, desc_ptr(KF1), keys_ptr(KF1),
                                        mp1.data(), ur1.data(), a.fv, n2, desc_ptr(KF2), keys_ptr(KF2), mp2.data(),
-                                       ur2.data(), b.fv, F12, ex, ey, KF2.scaleFactors->data(),
-                                       KF2.levelSigma2->data(), (int)KF2.scaleFactors->size(), pairs.data(),
+                                       ur2.data(), b.fv, F12, ex, ey, KF2.scaleFactors, KF2.levelSigma2,
+                                       KF2.nlevels, pairs.data(),
                                        std::max(n1, 1), &np),
           "SearchForTriangulation");
     vMatchedPairs.clear();   // :813-820
@@ -222,11 +230,13 @@ int ORBmatcher::window_match(bool level0_only, const FeatureSet& F1, const Featu
                              const std::vector<Point2f>* centres, int windowSize, std::vector<int>& vnMatches12) {
     const int n1 = F1.N(), n2 = F2.N();
     vnMatches12.assign(n1, -1);
-    if (!F2.grid) throw OrbGpuError(ORB_ERR_ARG, "window match: F2 grid");
+    require(F2.grid != nullptr, "window match: F2 grid");
+    require(n1 == 0 || (F1.keys && F1.descriptors), "window match: F1 keys/descriptors");
+    require(n2 == 0 || (F2.keys && F2.descriptors), "window match: F2 keys/descriptors");
     // candidate lists: F2.GetFeaturesInArea(centre, windowSize, level1, level1) per query (:425, :1686, :1806)
     std::vector<int> off(n1 + 1, 0), idx;
     for (int i1 = 0; i1 < n1; i1++) {
-        const KeyPoint& kp1 = (*F1.keys)[i1];
+        const KeyPoint& kp1 = F1.keys[i1];
         if (!(level0_only && kp1.octave > 0)) {
             const float x = centres ? (*centres)[i1].x : kp1.x, y = centres ? (*centres)[i1].y : kp1.y;
             const std::vector<size_t> v = F2.grid->GetFeaturesInArea(x, y, (float)windowSize, kp1.octave, kp1.octave);
@@ -249,7 +259,7 @@ int ORBmatcher::SearchForInitialization(const FrameData& F1, const FrameData& F2
     const int n = window_match(true, F1, F2, &vbPrevMatched, windowSize, vnMatches12);
     for (size_t i1 = 0; i1 < vnMatches12.size(); i1++)   // :514-517 update prev matched
         if (vnMatches12[i1] >= 0) {
-            const KeyPoint& k = (*F2.keys)[vnMatches12[i1]];
+            const KeyPoint& k = F2.keys[vnMatches12[i1]];
             vbPrevMatched[i1].x = k.x;
             vbPrevMatched[i1].y = k.y;
         }
@@ -261,7 +271,7 @@ int ORBmatcher::BirdviewMatch(const FrameData& F1, const FrameData& F2, std::vec
     const int n = window_match(true, F1, F2, &vPrevMatched, windowSize, vnMatches12);
     for (size_t i1 = 0; i1 < vnMatches12.size(); i1++)   // :1778-1781
         if (vnMatches12[i1] >= 0) {
-            const KeyPoint& k = (*F2.keys)[vnMatches12[i1]];
+            const KeyPoint& k = F2.keys[vnMatches12[i1]];
             vPrevMatched[i1].x = k.x;
             vPrevMatched[i1].y = k.y;
         }
@@ -273,4 +283,4 @@ int ORBmatcher::BirdviewMatch(const FrameData& F1, const FrameData& F2, std::vec
     return window_match(false, F1, F2, nullptr, windowSize, vnMatches12);
 }
 
-}  // namespace ORB_SLAM2
+}  // namespace ORBGPU_MATCHER_NAMESPACE

@@ -21,7 +21,19 @@
 
 #include "ORBextractor.h"
 
-namespace ORB_SLAM2 {
+// The matcher lives in ORB_SLAM2 like the reference's.  When integrated next to the reference's own
+// ORB_SLAM2::ORBmatcher (which keeps the projection-based searches), build with
+// -DORBGPU_MATCHER_NAMESPACE=orbgpu_host.
+#ifndef ORBGPU_MATCHER_NAMESPACE
+#define ORBGPU_MATCHER_NAMESPACE ORB_SLAM2
+#endif
+
+namespace ORBGPU_MATCHER_NAMESPACE {
+
+using ORB_SLAM2::DescriptorMat;
+using ORB_SLAM2::KeyPoint;
+using ORB_SLAM2::OrbGpuError;
+using ORB_SLAM2::Point2f;
 
 // DBoW2::FeatureVector (Thirdparty/DBoW2/DBoW2/FeatureVector.h: std::map<NodeId, std::vector<unsigned int>>)
 typedef std::map<unsigned int, std::vector<unsigned int> > FeatureVector;
@@ -35,30 +47,33 @@ class FrameGrid {
 public:
     FrameGrid() = default;
     // Frame grid: cells of (maxX-minX)/64 x (maxY-minY)/48 over mvKeysUn
-    FrameGrid(const std::vector<KeyPoint>& keysUn, float minX, float maxX, float minY, float maxY);
+    FrameGrid(const KeyPoint* keysUn, int n, float minX, float maxX, float minY, float maxY);
     // birdview grid: GridElementWidthInv/HeightInv given directly, origin (0, 0)
-    static FrameGrid Birdview(const std::vector<KeyPoint>& keysBird, float widthInv, float heightInv);
+    static FrameGrid Birdview(const KeyPoint* keysBird, int n, float widthInv, float heightInv);
     std::vector<size_t> GetFeaturesInArea(float x, float y, float r, int minLevel = -1, int maxLevel = -1) const;
 
 private:
-    void assign(const std::vector<KeyPoint>& keys);
-    const std::vector<KeyPoint>* keys_ = nullptr;
+    void assign(const KeyPoint* keys, int n);
+    const KeyPoint* keys_ = nullptr;
     float minX_ = 0, minY_ = 0, invW_ = 0, invH_ = 0;
     std::vector<std::vector<size_t> > cells_;   // [ix * ROWS + iy]
 };
 
-// The members of a Frame / KeyFrame that ORBmatcher reads.  Pointers may be NULL where a method
-// does not use the member (see each method).
+// The members of a Frame / KeyFrame that ORBmatcher reads, as zero-copy views (cv::KeyPoint and
+// orb_keypoint share one 28-byte layout; a continuous n x 32 CV_8U Mat is n*32 bytes).  Pointers
+// may be NULL where a method does not read the member (see each method).
 struct FeatureSet {
-    const std::vector<KeyPoint>* keys = nullptr;      // Frame::mvKeys / KeyFrame::mvKeysUn / mvKeysBird
-    const DescriptorMat* descriptors = nullptr;       // mDescriptors / mDescriptorsBird
+    int n = 0;                                        // N (Frame::N / KeyFrame::N / mvKeysBird.size())
+    const KeyPoint* keys = nullptr;                   // Frame::mvKeys / KeyFrame::mvKeysUn / mvKeysBird
+    const uint8_t* descriptors = nullptr;             // mDescriptors / mDescriptorsBird, row-major n x 32
     const FeatureVector* featVec = nullptr;           // mFeatVec
-    const std::vector<uint8_t>* hasMapPoint = nullptr;   // per feature: MapPoint != NULL (&& !isBad() where read)
-    const std::vector<float>* uRight = nullptr;       // mvuRight
-    const std::vector<float>* scaleFactors = nullptr; // mvScaleFactors
-    const std::vector<float>* levelSigma2 = nullptr;  // mvLevelSigma2
+    const uint8_t* hasMapPoint = nullptr;             // per feature: MapPoint != NULL (&& !isBad() where read)
+    const float* uRight = nullptr;                    // mvuRight
+    const float* scaleFactors = nullptr;              // mvScaleFactors
+    const float* levelSigma2 = nullptr;               // mvLevelSigma2
+    int nlevels = 0;                                  // mnScaleLevels (length of the two tables above)
     const FrameGrid* grid = nullptr;                  // mGrid / mGridBirdview
-    int N() const { return keys ? (int)keys->size() : 0; }
+    int N() const { return n; }
 };
 // Tags standing for the reference's Frame& and KeyFrame* arguments (so the overloads keep the
 // reference's names: SearchByBoW(KeyFrame*, Frame&) vs SearchByBoW(KeyFrame*, KeyFrame*)).
@@ -106,6 +121,6 @@ protected:
     bool mbCheckOrientation;
 };
 
-}  // namespace ORB_SLAM2
+}  // namespace ORBGPU_MATCHER_NAMESPACE
 
 #endif

@@ -74,6 +74,13 @@ struct OracleFv {
     }
 };
 
+template <class S>
+static void view(S& s, const std::vector<KeyPoint>& k, const DescriptorMat& d) {
+    s.n = (int)k.size();
+    s.keys = k.data();
+    s.descriptors = d.buf.data();
+}
+
 static std::vector<float> angles_of(const std::vector<KeyPoint>& k) {
     std::vector<float> a(k.size());
     for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
@@ -183,13 +190,11 @@ int main(int argc, char** argv) {
                 const std::string tag = std::string("_r") + std::to_string(ri) + "_ori" + std::to_string(co);
                 // SearchByBoW(KeyFrame*, Frame&, ...) (ORBmatcher.cc:159-288)
                 KeyFrameData KF;
-                KF.keys = &k1;
-                KF.descriptors = &d1;
+                view(KF, k1, d1);
                 KF.featVec = &fv1;
-                KF.hasMapPoint = &mp1;
+                KF.hasMapPoint = mp1.data();
                 FrameData F;
-                F.keys = &k2;
-                F.descriptors = &d2;
+                view(F, k2, d2);
                 F.featVec = &fv2;
                 std::vector<int> vpMapPointMatches;
                 const int nm = matcher.SearchByBoW(KF, F, vpMapPointMatches);
@@ -200,10 +205,9 @@ int main(int argc, char** argv) {
                        "n=" + std::to_string(nm) + " oracle=" + std::to_string(onm));
                 // SearchByBoW(KeyFrame*, KeyFrame*, ...) (:522-655)
                 KeyFrameData KF2;
-                KF2.keys = &k2;
-                KF2.descriptors = &d2;
+                view(KF2, k2, d2);
                 KF2.featVec = &fv2;
-                KF2.hasMapPoint = &mp2;
+                KF2.hasMapPoint = mp2.data();
                 std::vector<int> vpMatches12;
                 const int nm2 = matcher.SearchByBoW(KF, KF2, vpMatches12);
                 std::vector<int> om2(n1, -1);
@@ -232,18 +236,17 @@ int main(int argc, char** argv) {
             for (int only_stereo = 0; only_stereo < 2; only_stereo++) {
                 ORBmatcher matcher(0.6f, false);   // LocalMapping.cc:225
                 KeyFrameData A, B;
-                A.keys = &k1;
-                A.descriptors = &d1;
+                view(A, k1, d1);
                 A.featVec = &fv1;
-                A.hasMapPoint = &hm1;
-                A.uRight = &ur1;
-                B.keys = &k2;
-                B.descriptors = &d2;
+                A.hasMapPoint = hm1.data();
+                A.uRight = ur1.data();
+                view(B, k2, d2);
                 B.featVec = &fv2;
-                B.hasMapPoint = &hm2;
-                B.uRight = &ur2;
-                B.scaleFactors = &sc;
-                B.levelSigma2 = &s2;
+                B.hasMapPoint = hm2.data();
+                B.uRight = ur2.data();
+                B.scaleFactors = sc.data();
+                B.levelSigma2 = s2.data();
+                B.nlevels = (int)sc.size();
                 std::vector<std::pair<size_t, size_t> > pairs;
                 const int np = matcher.SearchForTriangulation(A, B, F12, 5000.f, 300.f, pairs, only_stereo != 0);
                 std::vector<int> op(2 * (size_t)n1 + 2);
@@ -260,12 +263,10 @@ int main(int argc, char** argv) {
 
         // ---- window matchers: SearchForInitialization (:405-520), BirdviewMatch x2 (:1667-1899)
         {
-            FrameGrid grid(k2, 0.f, (float)w, 0.f, (float)h);
+            FrameGrid grid(k2.data(), n2, 0.f, (float)w, 0.f, (float)h);
             FrameData F1, F2;
-            F1.keys = &k1;
-            F1.descriptors = &d1;
-            F2.keys = &k2;
-            F2.descriptors = &d2;
+            view(F1, k1, d1);
+            view(F2, k2, d2);
             F2.grid = &grid;
             for (int win = 0; win < 2; win++) {
                 const int windowSize = win ? 100 : 15;   // Tracking.cc:739 (init), :744 (bird)
