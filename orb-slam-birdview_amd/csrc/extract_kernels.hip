@@ -117,6 +117,73 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
     *reinterpret_cast<uint32_t*>(dst + (long long)y * g->L[level].pitch + x0) = packed;
 }
 
+/* Same arithmetic, LDS-tiled: a block produces a 128 x 16 output tile.  The tile's source span
+ * (<= 268 x 40 bytes, checked on the host: LevelGeom::rs_tiled) is staged with coalesced dword loads
+ * (byte loads if the level base/stride is not dword aligned), the coefficients of the tile's
+ * columns/rows are staged once, and each thread then produces 4 output pixels per row pass
+ * (one dword store) from LDS byte reads. */
+__global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
+                                                      const ResizeCoef* __restrict__ coef, int level,
+                                                      const uint8_t* __restrict__ frames, long long framePitch,
+                                                      int rowStride, uint8_t* __restrict__ pyr) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[kRsRows * kRsPitch];
+    __shared__ int4 s_cx[kRsTileW];
+    __shared__ int4 s_cy[kRsTileH];
+    const int f = blockIdx.z;
+    const int dw = g->L[level].w, dh = g->L[level].h;
+    const int x0 = blockIdx.x * kRsTileW, y0 = blockIdx.y * kRsTileH;
+    const int tid = threadIdx.x;
+    const LevelPtr src = level_ptr(g, level - 1, frames, framePitch, rowStride, pyr, f);
+    const int nx = min(kRsTileW, dw - x0), ny = min(kRsTileH, dh - y0);
+    if (tid < kRsTileW) {
+        const ResizeCoef c = coef[x0 + min(tid, nx - 1)];
+        s_cx[tid] = make_int4(c.s0, c.s1, c.c0, c.c1);
+    } else if (tid < kRsTileW + kRsTileH) {
+        const ResizeCoef c = coef[dw + y0 + min(tid - kRsTileW, ny - 1)];
+        s_cy[tid - kRsTileW] = make_int4(c.s0, c.s1, c.c0, c.c1);
+    }
+    // source span (the coefficient tables are monotone)
+    const int sx0 = coef[x0].s0 & ~3, sx1 = coef[x0 + nx - 1].s1;
+    const int sy0 = coef[dw + y0].s0, sy1 = coef[dw + y0 + ny - 1].s1;
+    const int nw = (sx1 - sx0 + 4) >> 2, nr = sy1 - sy0 + 1;
+    const uint8_t* base = src.p + (long long)sy0 * src.stride + sx0;
+    if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
+        for (int i = tid; i < nr * 68; i += 256) {   // 68 dwords per LDS row
+            const int r = i / 68, wd = i - r * 68;
+            if (wd < nw)
+                *reinterpret_cast<uint32_t*>(&s_src[r * kRsPitch + 4 * wd]) =
+                    *reinterpret_cast<const uint32_t*>(base + (long long)r * src.stride + 4 * wd);
+        }
+    } else {
+        const int nb = sx1 - sx0 + 1;
+        for (int i = tid; i < nr * kRsPitch; i += 256) {
+            const int r = i / kRsPitch, b = i - r * kRsPitch;
+            if (b < nb) s_src[r * kRsPitch + b] = base[(long long)r * src.stride + b];
+        }
+    }
+    __syncthreads();
+    const int tx = (tid & 31) * 4;
+    uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off;
+#pragma unroll
+    for (int pass = 0; pass < kRsTileH / 8; pass++) {
+        const int ty = pass * 8 + (tid >> 5);
+        if (ty >= ny || tx >= nx) continue;
+        const int4 cy = s_cy[ty];
+        const uint8_t* r0 = &s_src[(cy.x - sy0) * kRsPitch - sx0];
+        const uint8_t* r1 = &s_src[(cy.y - sy0) * kRsPitch - sx0];
+        uint32_t packed = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int4 cx = s_cx[min(tx + i, nx - 1)];
+            const int h0 = r0[cx.x] * cx.z + r0[cx.y] * cx.w;
+            const int h1 = r1[cx.x] * cx.z + r1[cx.y] * cx.w;
+            const int v = (((cy.z * (h0 >> 4)) >> 16) + ((cy.w * (h1 >> 4)) >> 16) + 2) >> 2;
+            packed |= (uint32_t)v << (8 * i);
+        }
+        *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + ty) * g->L[level].pitch + x0 + tx) = packed;
+    }
+}
+
 /* ------------------------------------------------------------------------------------------------
  * FAST-9/16 + NMS per cell, with the iniThFAST -> minThFAST fallback
  * (ComputeKeyPointsOctTree, ORBextractor.cc:789-828; cv::FAST semantics SURVEY Appendix A.3).
@@ -995,9 +1062,15 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     if (nframes <= 0) return hipSuccess;
     if (marker) marker(user, ORB_K_RESIZE, 1);
     for (int l = 1; l < g.nlevels; l++) {
-        dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
-        hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l, d_frames,
-                           frame_pitch, row_stride, b.d_pyr);
+        if (g.L[l].rs_tiled && !b.resize_direct) {
+            dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, kRsTileH), nframes);
+            hipLaunchKernelGGL(k_resize_tiled, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,
+                               d_frames, frame_pitch, row_stride, b.d_pyr);
+        } else {
+            dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
+            hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,
+                               d_frames, frame_pitch, row_stride, b.d_pyr);
+        }
     }
     if (marker) marker(user, ORB_K_RESIZE, 0);
     if (marker) marker(user, ORB_K_FAST, 1);

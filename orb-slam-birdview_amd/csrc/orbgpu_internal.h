@@ -19,12 +19,16 @@ constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3
 constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as aligned dwords
 constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
+constexpr int kRsTileW = 128;         // k_resize_tiled: output tile 128 x 16, 4 px per thread
+constexpr int kRsTileH = 16;
+constexpr int kRsPitch = 272;         // LDS source tile: up to 268 bytes x 40 rows (scale factors <= 2)
+constexpr int kRsRows = 40;
 
 // Per-level geometry (host-computed once per image size; lives in device memory).
 struct LevelGeom {
     int w, h;            // level size (ComputePyramid, ORBextractor.cc:1112)
     int pitch;           // row pitch of the stored level (levels >= 1)
-    int pad0;
+    int rs_tiled;        // k_resize_tiled's LDS tile holds every source span of this level (else k_resize)
     long long pyr_off;   // byte offset of the level inside a frame's pyramid slot (levels >= 1)
     int maxBX, maxBY;    // maxBorderX/Y (:775-776)
     int nCols, nRows, wCell, hCell;   // cell grid (:781-787)
@@ -75,6 +79,7 @@ struct ExtractBuffers {
     int* d_lvlCount;               // nframes * nlevels
     int* d_err;                    // 1 int: internal overflow flag
     int fast_remap;                // XCD-contiguous block->cell remap in k_fast (speed only)
+    int resize_direct;             // force the untiled k_resize (A/B switch, ORBGPU_RESIZE_DIRECT=1)
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin);
