@@ -469,6 +469,238 @@ __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const 
     }
 }
 
+/* Wave-per-cell form of the same algorithm: four (frame, cell) items per 256-thread block, one per
+ * wavefront, so every synchronisation is a wave barrier (no block barriers).  The per-wave LDS carve
+ * is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors are compacted with
+ * per-bit ballots (list order is irrelevant: emission order comes from the keep bitmap, one 64-bit
+ * row mask per domain row, emitted in raster order by one lane per row). */
+__device__ __forceinline__ int wave_excl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// q = x / n for x < 2^20 / n via a 20-bit reciprocal (wave-uniform n <= 64): two VALU ops, exact.
+__device__ __forceinline__ uint32_t recip20(uint32_t n) { return ((1u << 20) + n - 1) / n; }
+__device__ __forceinline__ uint32_t div20(uint32_t x, uint32_t m) { return __umul24(x, m) >> 20; }
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {   // per 16-bit lane a - b (v_pk_sub_i16)
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, a) - __builtin_bit_cast(short2_t, b));
+}
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {   // per 16-bit lane a + b (v_pk_add_i16)
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, a) + __builtin_bit_cast(short2_t, b));
+}
+
+// Compass prefilter (see fast_maybe) for two pixels held as 16-bit lanes: returns sign bits 15/31
+// set where the pixel may be a corner at threshold t.  Bright: (v+t) - p < 0, dark: p - (v-t) < 0;
+// the four cyclically adjacent compass pairs reduce to (b0|b8) & (b4|b12).
+__device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p4, uint32_t p8, uint32_t p12,
+                                             uint32_t tt) {
+    const uint32_t vt = pk_add16(v, tt), vmt = pk_sub16(v, tt);   // v + t, v - t (per lane)
+    const uint32_t b0 = pk_sub16(vt, p0), b4 = pk_sub16(vt, p4), b8 = pk_sub16(vt, p8), b12 = pk_sub16(vt, p12);
+    const uint32_t d0 = pk_sub16(p0, vmt), d4 = pk_sub16(p4, vmt), d8 = pk_sub16(p8, vmt), d12 = pk_sub16(p12, vmt);
+    return ((b0 | b8) & (b4 | b12)) | ((d0 | d8) & (d4 | d12));
+}
+
+__global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
+                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
+                                                   uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
+                                                   int remap) {
+    extern __shared__ __attribute__((aligned(16))) int smem_fast[];
+    uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
+    constexpr int TP = kFastTilePitch;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (4 cells each)
+    int blk = blockIdx.x;
+    if (remap) {
+        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int item = blk * 4 + wv;
+    if (item >= total) return;   // whole wave; nothing below uses a block barrier
+    const int wb = g->fast_wave_bytes;
+    uint8_t* tile = smem + (size_t)wv * wb;
+    // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*64 + dx+1]
+    uint8_t* sM = tile + ((g->fast_rows * TP + 16 + 15) & ~15);
+    uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * 64 + 15) & ~15));
+    unsigned long long* keepb =
+        reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(sList) + ((g->fast_list * 2 + 15) & ~15));
+    const int tmin = min(g->iniTh, g->minTh);
+    const FastCell c = fast_cell(g, item, frames, framePitch, rowStride, pyr);
+    int* cntOut = cellCount + (long long)c.f * g->ncells + c.cell;
+    if (!c.valid) {
+        if (lane == 0) *cntOut = 0;
+        return;
+    }
+    const int dw = c.dw, dh = c.dh;
+    // ---- ROI -> LDS (rows TP apart), eight dword loads in flight per lane; zero the score map
+    int xoff = 0;
+    if (c.aligned) {
+        const int n = c.rh * c.nw;
+        const uint32_t mnw = recip20(c.nw);
+        for (int b0 = 0; b0 < n; b0 += 8 * 64) {
+            uint32_t v[8];
+            int dsto[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int idx = b0 + k * 64 + lane;
+                const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
+                dsto[k] = idx < n ? yy * TP + ww * 4 : -1;
+                v[k] = idx < n ? *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4)
+                               : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (dsto[k] >= 0) *reinterpret_cast<uint32_t*>(&tile[dsto[k]]) = v[k];
+        }
+        xoff = c.iniX & 3;
+    } else {
+        const uint32_t mrw = recip20(c.rw);
+        for (int idx = lane; idx < c.rh * c.rw; idx += 64) {
+            const int yy = (int)div20(idx, mrw), xx = idx - yy * c.rw;
+            tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
+        }
+    }
+    for (int i = lane; i < (dh + 2) * 16; i += 64) reinterpret_cast<uint32_t*>(sM)[i] = 0u;
+    if (lane < dh) keepb[lane] = 0ull;
+    wave_lds_sync();
+    // ---- stage 1: compass prefilter, 4 pixels per lane in packed 16-bit lanes; lane -> (run, row)
+    // fixed for the cell (rows advance by 64 / nruns per iteration), per-bit ballot compaction
+    const int nruns = (dw + 3) >> 2;
+    const int rpi = 64 / nruns;                          // rows per iteration
+    const int lrow = (int)div20(lane, recip20(nruns));
+    const int x0 = 4 * (lane - lrow * nruns);
+    const bool lane_on = lrow < rpi;
+    const uint32_t tt = (uint32_t)tmin | ((uint32_t)tmin << 16);
+    const uint32_t xvalid = x0 + 4 <= dw ? 0xFu : (1u << max(dw - x0, 0)) - 1u;
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
+    int nlist = 0;
+    for (int r0 = 0; r0 < dh; r0 += rpi) {
+        const int dy = r0 + lrow;
+        int pm = 0;
+        if (lane_on && dy < dh) {
+            const int sc = (dy + 3) * TP + x0 + xoff;       // centre row, from pixel x0-3
+            const int s0 = (dy + 6) * TP + x0 + 3 + xoff;   // row +3
+            const int s8 = dy * TP + x0 + 3 + xoff;         // row -3
+            const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
+            const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3];
+            const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);   // pixels x0-3 .. x0
+            const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);   // x0+1 .. x0+4
+            const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);   // x0+5 .. x0+8
+            const uint32_t P0 = __builtin_amdgcn_alignbyte(t32[d0 + 1], t32[d0], s0 & 3);
+            const uint32_t P8 = __builtin_amdgcn_alignbyte(t32[d8 + 1], t32[d8], s8 & 3);
+            const uint32_t V = __builtin_amdgcn_alignbyte(A1, A0, 3);     // centres x0 .. x0+3
+            const uint32_t P4 = __builtin_amdgcn_alignbyte(A2, A1, 2);    // x0+3 .. x0+6
+            const uint32_t P12 = A0;                                      // x0-3 .. x0
+            constexpr uint32_t LO = 0x00FF00FFu;
+            const uint32_t re = compass2(V & LO, P0 & LO, P4 & LO, P8 & LO, P12 & LO, tt);                 // px 0, 2
+            const uint32_t ro = compass2((V >> 8) & LO, (P0 >> 8) & LO, (P4 >> 8) & LO, (P8 >> 8) & LO,
+                                         (P12 >> 8) & LO, tt);                                          // px 1, 3
+            pm = (int)((((re >> 15) & 1u) | ((ro >> 14) & 2u) | ((re >> 29) & 4u) | ((ro >> 28) & 8u)) & xvalid);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const bool bit = (pm >> i) & 1;
+            const unsigned long long m = __ballot(bit);
+            if (bit) sList[nlist + lanes_below(m)] = (uint16_t)(dy * 64 + x0 + i);
+            nlist += __popcll(m);
+        }
+    }
+    wave_lds_sync();
+    // ---- stage 2: exact arc strength for the survivors; corners at tmin are compacted in place
+    // (each chunk is read into registers before any lane writes, and writes land at or before it)
+    const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
+    int ncorner = 0;
+    for (int b0 = 0; b0 < nlist; b0 += 64) {
+        const int i = b0 + lane;
+        int p = 0, m = 0;
+        if (i < nlist) {
+            p = sList[i];
+            m = fast_arc_strength(t0 + (p >> 6) * TP + (p & 63));
+            sM[p + 65] = (uint8_t)m;
+        }
+        const bool corner = m > tmin;
+        const unsigned long long cm = __ballot(corner);
+        if (corner) sList[ncorner + lanes_below(cm)] = (uint16_t)p;
+        ncorner += __popcll(cm);
+    }
+    wave_lds_sync();
+    // ---- cell-local NMS at iniThFAST, then the minThFAST fallback if nothing survived (:812-816).
+    // Neighbours outside the domain read the zero border; non-corners at th count 0.
+    int th = g->iniTh;
+    int kept = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        int mine = 0;
+        for (int i = lane; i < ncorner; i += 64) {
+            const int p = sList[i];
+            const uint8_t* q = sM + p + 65;
+            const int m = q[0];
+            if (m <= th) continue;
+            const int s = m - 1;
+            bool k = true;
+#pragma unroll
+            for (int oy = -1; oy <= 1; oy++) {
+#pragma unroll
+                for (int ox = -1; ox <= 1; ox++) {
+                    if (ox == 0 && oy == 0) continue;
+                    const int mn = q[oy * 64 + ox];
+                    const int sn = mn > th ? mn - 1 : 0;
+                    k = k && (s > sn);
+                }
+            }
+            if (k) {
+                atomicOr(&keepb[p >> 6], 1ull << (p & 63));
+                mine++;
+            }
+        }
+        kept = wave_sum(mine);
+        if (kept > 0 || th == g->minTh) break;
+        th = g->minTh;
+    }
+    wave_lds_sync();
+    // ---- emission in raster order: lane = domain row
+    const LevelGeom& L = g->L[c.l];
+    uint32_t* out = cands + (long long)c.f * g->ncand + L.cand_base + (long long)(c.cell - L.cell_base) * L.cell_cap;
+    unsigned long long bits = lane < dh ? keepb[lane] : 0ull;
+    int pos = wave_excl_scan(__popcll(bits));
+    const uint32_t yr = (uint32_t)(lane + 3 + c.ci * L.hCell);
+    while (bits) {
+        const int dx = __ffsll((long long)bits) - 1;
+        bits &= bits - 1;
+        const uint32_t xr = (uint32_t)(dx + 3 + c.cj * L.wCell);
+        out[pos++] = xr | (yr << 12) | ((uint32_t)(sM[(lane + 1) * 64 + dx + 1] - 1) << 24);
+    }
+    if (lane == 0) *cntOut = kept;
+}
+
+void fast_wave_layout(Geom& g) {
+    int rows = 1, drows = 1, list = 1;
+    for (int l = 0; l < g.nlevels; l++) {
+        const LevelGeom& L = g.L[l];
+        rows = std::max(rows, L.hCell + 6);
+        drows = std::max(drows, L.hCell);
+        list = std::max(list, L.hCell * L.wCell);
+    }
+    g.fast_rows = rows;
+    g.fast_drows = drows;
+    g.fast_list = list;
+    g.fast_wave_bytes = ((rows * kFastTilePitch + 16 + 15) & ~15) + (((drows + 2) * 64 + 15) & ~15) +
+                        ((list * 2 + 15) & ~15) + drows * 8;
+    g.fast_wave_bytes = (g.fast_wave_bytes + 15) & ~15;
+}
+
 /* ------------------------------------------------------------------------------------------------
  * DistributeOctTree (ORBextractor.cc:539-763) — one workgroup per (level, frame).
  *
@@ -1075,8 +1307,13 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     if (marker) marker(user, ORB_K_RESIZE, 0);
     if (marker) marker(user, ORB_K_FAST, 1);
     const int fast_items = g.ncells * nframes;
-    hipLaunchKernelGGL(k_fast, dim3(fast_items), dim3(256), 0, stream, b.d_geom, d_frames,
-                       frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
+    if (b.fast_block || (size_t)g.fast_wave_bytes * 4 > 65536)   // very large cells: block-per-cell kernel
+        hipLaunchKernelGGL(k_fast, dim3(fast_items), dim3(256), 0, stream, b.d_geom, d_frames,
+                           frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
+    else
+        hipLaunchKernelGGL(k_fast_wave, dim3(cdiv(fast_items, 4)), dim3(256), (size_t)g.fast_wave_bytes * 4, stream,
+                           b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items,
+                           b.fast_remap);
     if (marker) marker(user, ORB_K_FAST, 0);
     if (marker) marker(user, ORB_K_OCTREE, 1);
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, nframes), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap),

@@ -173,6 +173,7 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
     int nc = std::max(maxN + 8, 4 * maxNini + 8);
     nc = (nc + 63) & ~63;
     g.node_cap = nc;
+    fast_wave_layout(g);
     if (octree_lds_bytes(nc) > 160 * 1024) return ORB_ERR_GEOMETRY;
     return ORB_OK;
 }
@@ -247,6 +248,7 @@ ExtractBuffers Ctx::buffers() const {
     b.d_err = d_err;
     b.fast_remap = fast_remap ? 1 : 0;
     b.resize_direct = resize_direct ? 1 : 0;
+    b.fast_block = fast_block ? 1 : 0;
     return b;
 }
 
@@ -325,6 +327,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         c->num_cu = 256;
     if (const char* e = std::getenv("ORBGPU_FAST_REMAP")) c->fast_remap = e[0] == '1';
     if (const char* e = std::getenv("ORBGPU_RESIZE_DIRECT")) c->resize_direct = e[0] == '1';
+    if (const char* e = std::getenv("ORBGPU_FAST_BLOCK")) c->fast_block = e[0] == '1';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);

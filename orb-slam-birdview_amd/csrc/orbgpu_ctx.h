@@ -20,6 +20,7 @@ struct Ctx {
     int num_cu = 256;
     bool fast_remap = true;   // ORBGPU_FAST_REMAP=0 disables the XCD-contiguous cell remap (A/B switch)
     bool resize_direct = false;   // ORBGPU_RESIZE_DIRECT=1 forces the untiled resize kernel (A/B switch)
+    bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
     hipStream_t stream = nullptr;
 
     // ORBextractor tables (ORBextractor.cc:410-470)

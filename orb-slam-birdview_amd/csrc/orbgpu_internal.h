@@ -54,6 +54,10 @@ struct Geom {
     int iniTh, minTh;
     int node_cap;        // octree LDS node capacity
     int max_level_cand;  // max cand_cap over levels (octree key scratch per level)
+    int fast_rows;       // k_fast_wave per-wave LDS carve (max over levels): ROI rows,
+    int fast_drows;      //   detection-domain rows,
+    int fast_list;       //   prefilter-survivor list entries (domain pixels)
+    int fast_wave_bytes; //   bytes per wave (tile | arc strength | list | keep bits)
     int umax[16];        // ORBextractor.cc:454-469
     int gk[8];           // 7-tap Gaussian, sigma 2, 8-bit fixed point (getGaussianKernel x 256)
     LevelGeom L[ORBGPU_MAX_LEVELS];
@@ -80,6 +84,7 @@ struct ExtractBuffers {
     int* d_err;                    // 1 int: internal overflow flag
     int fast_remap;                // XCD-contiguous block->cell remap in k_fast (speed only)
     int resize_direct;             // force the untiled k_resize (A/B switch, ORBGPU_RESIZE_DIRECT=1)
+    int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin);
@@ -112,5 +117,6 @@ hipError_t launch_triangulation(const uint8_t* d_desc1, const orb_keypoint* d_kp
                                 hipStream_t stream);
 
 size_t octree_lds_bytes(int node_cap);
+void fast_wave_layout(Geom& g);   // fills fast_rows/drows/list/wave_bytes from the level grids
 
 }  // namespace orbgpu
