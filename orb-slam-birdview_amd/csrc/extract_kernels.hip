@@ -1054,9 +1054,10 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap) {
     // per wave: 43x48 window (+16 B pad; reused for the transposed 37x40 blurred patch) and the
-    // transposed row-pass sums RT[rx][wy] (u16, 40 x 48)
+    // transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch; pitch 50 spreads the transposed
+    // stores of the 10 column groups over distinct banks)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kDescWin * kDescWinPitch + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][40 * 48];
+    __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][40 * kRtPitch];
     const int f = blockIdx.y;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nl = g->nlevels;
@@ -1188,10 +1189,10 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                 r23 = P[j + 2] * K[j] + r23;
             }
             const int rx = 4 * gq;
-            rt[(rx + 0) * 48 + wy] = r01.x;
-            rt[(rx + 1) * 48 + wy] = r01.y;
-            rt[(rx + 2) * 48 + wy] = r23.x;
-            rt[(rx + 3) * 48 + wy] = r23.y;
+            rt[(rx + 0) * kRtPitch + wy] = r01.x;
+            rt[(rx + 1) * kRtPitch + wy] = r01.y;
+            rt[(rx + 2) * kRtPitch + wy] = r23.x;
+            rt[(rx + 3) * kRtPitch + wy] = r23.y;
         }
     }
     wave_lds_sync();
@@ -1213,7 +1214,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         outa[r] = -1;
         if (it < kDescBlur * 10) {
             const int bx = it / 10, gq = it - bx * 10;
-            const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + bx * 48 + 4 * gq);
+            const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + bx * kRtPitch + 4 * gq);
             ushort2_t D[5];
 #pragma unroll
             for (int i = 0; i < 5; i++) D[i] = __builtin_bit_cast(ushort2_t, rp[i]);

@@ -19,6 +19,7 @@ constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3
 constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as aligned dwords
 constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
+constexpr int kRtPitch = 50;          // k_describe row-pass sums, u16 per transposed row
 constexpr int kRsTileW = 128;         // k_resize_tiled: output tile 128 x 16, 4 px per thread
 constexpr int kRsTileH = 16;
 constexpr int kRsPitch = 272;         // LDS source tile: up to 268 bytes x 40 rows (scale factors <= 2)
