@@ -195,8 +195,8 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
  * buffers do for a ROI).  Survivors are emitted in raster order (FAST emission order), packed
  * x_rel | y_rel<<12 | score<<24 with coordinates relative to minBorder (:822-823).
  * --------------------------------------------------------------------------------------------- */
+template <int P = kFastTilePitch>
 __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
-    constexpr int P = kFastTilePitch;
     const int v = c[0];
     int d[16];
     d[0] = v - c[3 * P];
@@ -514,13 +514,13 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
     return ((b0 | b8) & (b4 | b12)) | ((d0 | d8) & (d4 | d12));
 }
 
+template <int TP, int SP>
 __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
                                                    int remap) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
-    constexpr int TP = kFastTilePitch;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (4 cells each)
     int blk = blockIdx.x;
@@ -532,9 +532,9 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     if (item >= total) return;   // whole wave; nothing below uses a block barrier
     const int wb = g->fast_wave_bytes;
     uint8_t* tile = smem + (size_t)wv * wb;
-    // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*64 + dx+1]
+    // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*SP + dx+1]
     uint8_t* sM = tile + ((g->fast_rows * TP + 16 + 15) & ~15);
-    uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * 64 + 15) & ~15));
+    uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * SP + 15) & ~15));
     unsigned long long* keepb =
         reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(sList) + ((g->fast_list * 2 + 15) & ~15));
     const int tmin = min(g->iniTh, g->minTh);
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
             tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
         }
     }
-    for (int i = lane; i < (dh + 2) * 16; i += 64) reinterpret_cast<uint32_t*>(sM)[i] = 0u;
+    for (int i = lane; i < (dh + 2) * (SP / 4); i += 64) reinterpret_cast<uint32_t*>(sM)[i] = 0u;
     if (lane < dh) keepb[lane] = 0ull;
     wave_lds_sync();
     // ---- stage 1: compass prefilter, 4 pixels per lane in packed 16-bit lanes; lane -> (run, row)
@@ -628,8 +628,8 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         int p = 0, m = 0;
         if (i < nlist) {
             p = sList[i];
-            m = fast_arc_strength(t0 + (p >> 6) * TP + (p & 63));
-            sM[p + 65] = (uint8_t)m;
+            m = fast_arc_strength<TP>(t0 + (p >> 6) * TP + (p & 63));
+            sM[(p >> 6) * SP + (p & 63) + SP + 1] = (uint8_t)m;
         }
         const bool corner = m > tmin;
         const unsigned long long cm = __ballot(corner);
@@ -645,7 +645,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         int mine = 0;
         for (int i = lane; i < ncorner; i += 64) {
             const int p = sList[i];
-            const uint8_t* q = sM + p + 65;
+            const uint8_t* q = sM + (p >> 6) * SP + (p & 63) + SP + 1;
             const int m = q[0];
             if (m <= th) continue;
             const int s = m - 1;
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
 #pragma unroll
                 for (int ox = -1; ox <= 1; ox++) {
                     if (ox == 0 && oy == 0) continue;
-                    const int mn = q[oy * 64 + ox];
+                    const int mn = q[oy * SP + ox];
                     const int sn = mn > th ? mn - 1 : 0;
                     k = k && (s > sn);
                 }
@@ -680,24 +680,30 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         const int dx = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
         const uint32_t xr = (uint32_t)(dx + 3 + c.cj * L.wCell);
-        out[pos++] = xr | (yr << 12) | ((uint32_t)(sM[(lane + 1) * 64 + dx + 1] - 1) << 24);
+        out[pos++] = xr | (yr << 12) | ((uint32_t)(sM[(lane + 1) * SP + dx + 1] - 1) << 24);
     }
     if (lane == 0) *cntOut = kept;
 }
 
+// Per-wave LDS carve of k_fast_wave.  Cells at most 36 px wide (every BASELINE config) use the
+// compact pitches <56, 40>: the tile row must hold the prefilter's dword window (4*ceil(dw/4) + 14
+// bytes) and the ROI's dwords, the score map a zero column either side of the domain.
 void fast_wave_layout(Geom& g) {
-    int rows = 1, drows = 1, list = 1;
+    int rows = 1, drows = 1, list = 1, maxw = 1;
     for (int l = 0; l < g.nlevels; l++) {
         const LevelGeom& L = g.L[l];
         rows = std::max(rows, L.hCell + 6);
         drows = std::max(drows, L.hCell);
         list = std::max(list, L.hCell * L.wCell);
+        maxw = std::max(maxw, L.wCell);
     }
     g.fast_rows = rows;
     g.fast_drows = drows;
     g.fast_list = list;
-    g.fast_wave_bytes = ((rows * kFastTilePitch + 16 + 15) & ~15) + (((drows + 2) * 64 + 15) & ~15) +
-                        ((list * 2 + 15) & ~15) + drows * 8;
+    g.fast_compact = maxw <= 36 ? 1 : 0;
+    const int tp = g.fast_compact ? 56 : kFastTilePitch, sp = g.fast_compact ? 40 : 64;
+    g.fast_wave_bytes = ((rows * tp + 16 + 15) & ~15) + (((drows + 2) * sp + 15) & ~15) + ((list * 2 + 15) & ~15) +
+                        drows * 8;
     g.fast_wave_bytes = (g.fast_wave_bytes + 15) & ~15;
 }
 
@@ -1293,7 +1299,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                           int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
     if (nframes <= 0) return hipSuccess;
-    if (marker) marker(user, ORB_K_RESIZE, 1);
+    if (marker) marker(user, ORB_K_RESIZE, 1, stream);
     for (int l = 1; l < g.nlevels; l++) {
         if (g.L[l].rs_tiled && !b.resize_direct) {
             dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, kRsTileH), nframes);
@@ -1305,26 +1311,30 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                                d_frames, frame_pitch, row_stride, b.d_pyr);
         }
     }
-    if (marker) marker(user, ORB_K_RESIZE, 0);
-    if (marker) marker(user, ORB_K_FAST, 1);
+    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
+    if (marker) marker(user, ORB_K_FAST, 1, stream);
     const int fast_items = g.ncells * nframes;
     if (b.fast_block || (size_t)g.fast_wave_bytes * 4 > 65536)   // very large cells: block-per-cell kernel
         hipLaunchKernelGGL(k_fast, dim3(fast_items), dim3(256), 0, stream, b.d_geom, d_frames,
                            frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
+    else if (g.fast_compact)
+        hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(fast_items, 4)), dim3(256), (size_t)g.fast_wave_bytes * 4,
+                           stream, b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount,
+                           fast_items, b.fast_remap);
     else
-        hipLaunchKernelGGL(k_fast_wave, dim3(cdiv(fast_items, 4)), dim3(256), (size_t)g.fast_wave_bytes * 4, stream,
-                           b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items,
-                           b.fast_remap);
-    if (marker) marker(user, ORB_K_FAST, 0);
-    if (marker) marker(user, ORB_K_OCTREE, 1);
+        hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(fast_items, 4)), dim3(256),
+                           (size_t)g.fast_wave_bytes * 4, stream, b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr,
+                           b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
+    if (marker) marker(user, ORB_K_FAST, 0, stream);
+    if (marker) marker(user, ORB_K_OCTREE, 1, stream);
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, nframes), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap),
                        stream, b.d_geom, b.d_cands, b.d_cellCount, b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount,
                        b.d_err);
-    if (marker) marker(user, ORB_K_OCTREE, 0);
-    if (marker) marker(user, ORB_K_DESCRIBE, 1);
+    if (marker) marker(user, ORB_K_OCTREE, 0, stream);
+    if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
     hipLaunchKernelGGL(k_describe, dim3(cdiv(g.nkpcap, 4), nframes), dim3(256), 0, stream, b.d_geom, d_frames,
                        frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap);
-    if (marker) marker(user, ORB_K_DESCRIBE, 0);
+    if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);
     return hipGetLastError();
 }
 

@@ -153,10 +153,10 @@ struct TopkSession {
         hipError_t e;
         if (thr && (e = hipMemcpyAsync(d_thr, thr, (size_t)nt * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
             return set_error("upload thresholds", e), ORB_ERR_HIP;
-        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
         e = launch_hamming_topk(d_q + (size_t)from * 32, n, d_t, nt, d_rng + from, d_cand, thr ? d_thr : nullptr, K,
                                 d_dist + (size_t)from * K, d_idx + (size_t)from * K, d_nvalid + from, c->stream);
-        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("hamming kernel", e), ORB_ERR_HIP;
         if ((e = hipMemcpyAsync(dist.data() + (size_t)from * K, d_dist + (size_t)from * K, (size_t)n * K * 4,
                                 hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
@@ -251,10 +251,10 @@ int orb_hamming_topk(orb_ctx* h, const uint8_t* q, int nq, const uint8_t* t, int
         (train_thr && (e = hipMemcpyAsync(d_thr, train_thr, (size_t)nt * 4, hipMemcpyHostToDevice, c->stream)) !=
                           hipSuccess))
         return set_error("upload", e), ORB_ERR_HIP;
-    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_topk(d_q, nq, d_t, nt, cand_off ? d_rng : nullptr, d_cand, train_thr ? d_thr : nullptr, k,
                             d_dist, d_idx, d_nv, c->stream);
-    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
     if (e != hipSuccess) return set_error("hamming kernel", e), ORB_ERR_HIP;
     if ((e = hipMemcpyAsync(out_dist, d_dist, (size_t)nq * k * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(out_idx, d_idx, (size_t)nq * k * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
@@ -275,9 +275,9 @@ int orb_hamming_top2_device(orb_ctx* h, const uint8_t* d_q, int nq, const uint8_
     hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(int4)) + 256);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     int4* part = a.take<int4>((size_t)ns * nq);
-    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2(d_q, nq, d_t, nt, d_best, d_best_idx, d_second, part, c->stream);
-    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+    if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
     return e == hipSuccess ? ORB_OK : (set_error("top2 kernel", e), ORB_ERR_HIP);
 }
 
@@ -442,9 +442,9 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
             tp.sigma2[l] = sigma2_2[l];
         }
         tp.only_stereo = only_stereo;
-        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
         e = launch_triangulation(d_d1, d_k1, d_u1, d_d2, d_k2, d_m2, d_u2, d_q, d_r, d_c, nitems, tp, d_b, c->stream);
-        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
         if ((e = hipMemcpyAsync(best.data(), d_b, (size_t)nitems * 4, hipMemcpyDeviceToHost, c->stream)) !=
                 hipSuccess ||

@@ -252,12 +252,12 @@ ExtractBuffers Ctx::buffers() const {
     return b;
 }
 
-void Ctx::marker(void* user, int id, int begin) {
+void Ctx::marker(void* user, int id, int begin, hipStream_t s) {
     Ctx* c = (Ctx*)user;
     if (!c->prof_on) return;
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) return;
-    (void)hipEventRecord(ev, c->stream);
+    (void)hipEventRecord(ev, s);
     if (begin) c->prof_open[id] = ev;
     else c->prof_pairs.push_back({id, c->prof_open[id], ev});
 }
@@ -266,9 +266,36 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
                      uint8_t* d_desc, int* d_counts, int kp_cap) {
     hipError_t e = hipMemsetAsync(d_err, 0, sizeof(int), stream);
     if (e != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
-    e = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
-                       stream, &Ctx::marker, this);
-    if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
+    const int ns = std::min(std::min(nsub, kMaxSubStreams), nframes);
+    if (ns <= 1) {
+        e = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
+                           stream, &Ctx::marker, this);
+        if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
+    } else {
+        // fork: sub-batch s (frames [f0, f0+nf)) runs on sub[s] with its own frame slots; join on `stream`
+        if ((e = hipEventRecord(ev_fork, stream)) != hipSuccess) return set_error("event record", e), ORB_ERR_HIP;
+        const Geom& g = geom;
+        const size_t nl = g.nlevels;
+        for (int si = 0; si < ns; si++) {
+            const int f0 = (int)((long long)nframes * si / ns), f1 = (int)((long long)nframes * (si + 1) / ns);
+            if ((e = hipStreamWaitEvent(sub[si], ev_fork, 0)) != hipSuccess) return set_error("wait", e), ORB_ERR_HIP;
+            ExtractBuffers b = buffers();
+            b.d_pyr += (size_t)f0 * g.pyr_bytes;
+            b.d_cands += (size_t)f0 * g.ncand;
+            b.d_cellCount += (size_t)f0 * g.ncells;
+            b.d_keys += (size_t)f0 * nl * g.max_level_cand;
+            b.d_knode += (size_t)f0 * nl * g.max_level_cand;
+            b.d_lvlKps += (size_t)f0 * g.nkpcap;
+            b.d_lvlCount += (size_t)f0 * nl;
+            e = launch_extract(g, b, d_frames + (size_t)f0 * frame_pitch, frame_pitch, row_stride, f1 - f0,
+                               d_kps + (size_t)f0 * kp_cap, d_desc + (size_t)f0 * kp_cap * 32, d_counts + f0, kp_cap,
+                               sub[si], &Ctx::marker, this);
+            if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
+            if ((e = hipEventRecord(ev_join[si], sub[si])) != hipSuccess ||
+                (e = hipStreamWaitEvent(stream, ev_join[si], 0)) != hipSuccess)
+                return set_error("join", e), ORB_ERR_HIP;
+        }
+    }
     last_frames = d_frames;
     last_frame_pitch = frame_pitch;
     last_row_stride = row_stride;
@@ -333,6 +360,16 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         set_error("hipStreamCreate", e);
         return fail(ORB_ERR_HIP);
     }
+    if (const char* ev = std::getenv("ORBGPU_STREAMS")) c->nsub = std::min(std::max(std::atoi(ev), 1), kMaxSubStreams);
+    bool sub_ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < kMaxSubStreams && sub_ok; i++)
+        sub_ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) == hipSuccess;
+    if (!sub_ok) {
+        orb_destroy(reinterpret_cast<orb_ctx*>(c));
+        set_error("hipStreamCreate (sub-batch streams)", hipErrorOutOfMemory);
+        return fail(ORB_ERR_HIP);
+    }
     compute_tables(c);
     if (!c->umax_ok) {
         orb_destroy(reinterpret_cast<orb_ctx*>(c));
@@ -366,6 +403,11 @@ void orb_destroy(orb_ctx* h) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    for (int i = 0; i < kMaxSubStreams; i++) {
+        if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
+        if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -22,6 +22,11 @@ struct Ctx {
     bool resize_direct = false;   // ORBGPU_RESIZE_DIRECT=1 forces the untiled resize kernel (A/B switch)
     bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
     hipStream_t stream = nullptr;
+    // a batch of frames is split over `nsub` streams so that one sub-batch's low-occupancy phases
+    // (short pyramid levels, the per-level octree) overlap another's kernels (ORBGPU_STREAMS, 1..4)
+    int nsub = 1;   // measured: 2 and 4 are slower at B = 64 (every phase already fills the GPU)
+    hipStream_t sub[kMaxSubStreams]{};
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxSubStreams]{};
 
     // ORBextractor tables (ORBextractor.cc:410-470)
     float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},
@@ -91,7 +96,7 @@ struct Ctx {
     ExtractBuffers buffers() const;
     int run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
                     uint8_t* d_desc, int* d_counts, int kp_cap);
-    static void marker(void* user, int id, int begin);
+    static void marker(void* user, int id, int begin, hipStream_t s);
 };
 
 }  // namespace orbgpu

@@ -59,6 +59,7 @@ struct Geom {
     int fast_drows;      //   detection-domain rows,
     int fast_list;       //   prefilter-survivor list entries (domain pixels)
     int fast_wave_bytes; //   bytes per wave (tile | arc strength | list | keep bits)
+    int fast_compact;    //   every cell <= 36 px wide: compact LDS pitches (tile 56, score map 40)
     int umax[16];        // ORBextractor.cc:454-469
     int gk[8];           // 7-tap Gaussian, sigma 2, 8-bit fixed point (getGaussianKernel x 256)
     LevelGeom L[ORBGPU_MAX_LEVELS];
@@ -88,7 +89,8 @@ struct ExtractBuffers {
     int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
 };
 
-typedef void (*KernelMarker)(void* user, int kernel_id, int begin);
+typedef void (*KernelMarker)(void* user, int kernel_id, int begin, hipStream_t stream);
+constexpr int kMaxSubStreams = 4;   // a batch is split over up to this many streams (kernel overlap)
 
 hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
