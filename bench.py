@@ -35,7 +35,7 @@ CONFIGS = {   # BASELINE.json configs; C3 is the headline single-GPU workload
     "c5": dict(w=1280, h=720, nfeatures=4000, name="C5 1280x720 synthetic, 4000 features, 8 levels"),
 }
 PEAK_HBM_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-KNAMES = ["resize", "fast", "octree", "describe", "hamming"]
+KNAMES = ["resize", "fast", "octree", "describe", "hamming", "stereo"]   # ORB_K_* order
 
 
 # ---------------------------------------------------------------- distributed plumbing

@@ -104,7 +104,7 @@ int   orb_memset_device(orb_ctx* ctx, void* dst, int value, size_t bytes);
 
 /* ---- per-kernel timing with HIP events on the context stream (bench roofline) ---- */
 enum { ORB_K_RESIZE = 0, ORB_K_FAST = 1, ORB_K_OCTREE = 2, ORB_K_DESCRIBE = 3, ORB_K_HAMMING = 4,
-       ORB_K_COUNT = 5 };
+       ORB_K_STEREO = 5, ORB_K_COUNT = 6 };
 int orb_profile_enable(orb_ctx* ctx, int on);   /* clears accumulated times */
 int orb_profile_read(orb_ctx* ctx, double* ms_total /*ORB_K_COUNT*/, int* launches /*ORB_K_COUNT*/);
 
@@ -190,6 +190,24 @@ int orb_window_match(orb_ctx* ctx, float nnratio, int check_ori, int level0_only
  * C++ mirror uses to build window candidate lists. Returns count or -(needed)-1. */
 int orb_features_in_area(int n, const orb_keypoint* kps_un, float min_x, float max_x, float min_y, float max_y,
                          float x, float y, float r, int min_level, int max_level, int* out, int cap);
+
+/* ======================= Frame::ComputeStereoMatches ======================= */
+
+/* void Frame::ComputeStereoMatches()  Frame.cc:662-836, for one rectified pair.  `left` / `right` are
+ * the contexts that extracted the left / right image last (orb_extract; the reference's
+ * mpORBextractorLeft/Right, whose mvImagePyramid the window search reads) — same device, same image
+ * size.  kpsL/descL = mvKeys/mDescriptors (nL), kpsR/descR = mvKeysRight/mDescriptorsRight (nR);
+ * mb = baseline, mbf = baseline * fx.  uright / depth (nL each) receive mvuRight / mvDepth
+ * (-1 = no match); *nmatched = number of left keypoints with a depth.  Synchronous. */
+int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_keypoint* kpsL, const uint8_t* descL,
+                               int nR, const orb_keypoint* kpsR, const uint8_t* descR, float mb, float mbf,
+                               float* uright, float* depth, int* nmatched);
+
+/* Device-resident batched form: frames (2p, 2p+1) of the last orb_extract_batch_device on ctx are
+ * the (left, right) images of pair p.  Outputs at d_uright/d_depth[p * kp_cap + i] (kp_cap of that
+ * batch) and d_nmatched[p].  Asynchronous on the context stream. */
+int orb_stereo_batch_device(orb_ctx* ctx, int npairs, float mb, float mbf, float* d_uright, float* d_depth,
+                            int* d_nmatched);
 
 #ifdef __cplusplus
 }

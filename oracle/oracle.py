@@ -66,6 +66,7 @@ def lib():
                                                       FeatVec, vp, cf, cf, vp, vp, vp, ci]
         L.oracle_window_match.argtypes = [cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp]
         L.oracle_features_in_area.argtypes = [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]
+        L.oracle_stereo_matches.argtypes = [vp, vp, ci, vp, vp, ci, vp, vp, cf, cf, vp, vp]
         _LIB = L
     return _LIB
 
@@ -265,3 +266,17 @@ def features_in_area(kps_un, min_x, max_x, min_y, max_y, x, y, r, min_level=-1, 
     n = lib().oracle_features_in_area(len(k), _p(k), min_x, max_x, min_y, max_y, x, y, r, min_level, max_level,
                                       _p(out), len(out))
     return out[:n]
+
+
+def stereo_matches(left, right, kpsL, descL, kpsR, descR, mb, mbf):
+    """Frame::ComputeStereoMatches (Frame.cc:662-836) on two OracleExtractors that ran on the
+    rectified left / right images.  Returns (mvuRight, mvDepth, n_with_depth)."""
+    kl = np.ascontiguousarray(kpsL, KP_DTYPE)
+    kr = np.ascontiguousarray(kpsR, KP_DTYPE)
+    dl = np.ascontiguousarray(descL, np.uint8)
+    dr = np.ascontiguousarray(descR, np.uint8)
+    u = np.zeros(max(len(kl), 1), np.float32)
+    d = np.zeros(max(len(kl), 1), np.float32)
+    n = lib().oracle_stereo_matches(left.h, right.h, len(kl), _p(kl), _p(dl), len(kr), _p(kr), _p(dr), mb, mbf,
+                                    _p(u), _p(d))
+    return u[:len(kl)], d[:len(kl)], n

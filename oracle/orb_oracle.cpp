@@ -1071,4 +1071,134 @@ int oracle_features_in_area(int n, const OracleKeyPoint* kpsUn_, float mnMinX, f
     return (int)v.size();
 }
 
+/* Frame::ComputeStereoMatches  Frame.cc:662-836.  left/right: oracle extractors that ran on the
+ * rectified left/right images (their pyramids are mpORBextractorLeft/Right->mvImagePyramid);
+ * kpsL/descL = mvKeys/mDescriptors, kpsR/descR = mvKeysRight/mDescriptorsRight; scale tables of
+ * the left extractor (Frame copies them, Frame.cc:104-109).  Writes mvuRight / mvDepth (N each). */
+int oracle_stereo_matches(void* left, void* right, int N, const OracleKeyPoint* kpsL_, const uint8_t* descL, int Nr,
+                          const OracleKeyPoint* kpsR_, const uint8_t* descR, float mb, float mbf, float* mvuRight,
+                          float* mvDepth) {
+    const Extractor* eL = (const Extractor*)left;
+    const Extractor* eR = (const Extractor*)right;
+    const KP* mvKeys = (const KP*)kpsL_;
+    const KP* mvKeysRight = (const KP*)kpsR_;
+    const std::vector<float>& mvScaleFactors = eL->mvScaleFactor;
+    const std::vector<float>& mvInvScaleFactors = eL->mvInvScaleFactor;
+    for (int i = 0; i < N; i++) {   // :664-665
+        mvuRight[i] = -1.0f;
+        mvDepth[i] = -1.0f;
+    }
+    const int TH_HIGH = 100;
+    const int thOrbDist = (TH_HIGH + TH_LOW) / 2;   // :667
+    const int nRows = eL->pyr[0].h;                  // :669
+    std::vector<std::vector<size_t>> vRowIndices(nRows, std::vector<size_t>());
+    for (int iR = 0; iR < Nr; iR++) {   // :678-689
+        const KP& kp = mvKeysRight[iR];
+        const float& kpY = kp.y;
+        const float r = 2.0f * mvScaleFactors[mvKeysRight[iR].octave];
+        const int maxr = (int)std::ceil(kpY + r);
+        const int minr = (int)std::floor(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) vRowIndices[yi].push_back(iR);   // (reference indexes unchecked)
+    }
+    const float minZ = mb;   // :692-694
+    const float minD = 0;
+    const float maxD = mbf / minZ;
+    std::vector<std::pair<int, int>> vDistIdx;
+    vDistIdx.reserve(N);
+    for (int iL = 0; iL < N; iL++) {
+        const KP& kpL = mvKeys[iL];
+        const int& levelL = kpL.octave;
+        const float& vL = kpL.y;
+        const float& uL = kpL.x;
+        const std::vector<size_t>& vCandidates = vRowIndices[(size_t)vL];   // :707 float index, truncated
+        if (vCandidates.empty()) continue;
+        const float minU = uL - maxD;
+        const float maxU = uL - minD;
+        if (maxU < 0) continue;
+        int bestDist = TH_HIGH;
+        size_t bestIdxR = 0;
+        const uint8_t* dL = descL + (size_t)iL * 32;
+        for (size_t iC = 0; iC < vCandidates.size(); iC++) {   // :724-745
+            const size_t iR = vCandidates[iC];
+            const KP& kpR = mvKeysRight[iR];
+            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+            const float& uR = kpR.x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = DescriptorDistance(dL, descR + iR * 32);
+                if (dist < bestDist) {
+                    bestDist = dist;
+                    bestIdxR = iR;
+                }
+            }
+        }
+        if (bestDist < thOrbDist) {   // :748-834
+            const float uR0 = mvKeysRight[bestIdxR].x;
+            const float scaleFactor = mvInvScaleFactors[kpL.octave];
+            const float scaleduL = std::round(kpL.x * scaleFactor);
+            const float scaledvL = std::round(kpL.y * scaleFactor);
+            const float scaleduR0 = std::round(uR0 * scaleFactor);
+            const int w = 5;
+            const Img& PL = eL->pyr[kpL.octave];
+            const Img& PR = eR->pyr[kpL.octave];
+            const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
+            const float cL = (float)PL.row(yl0 + w)[xl0 + w];
+            int bestDist2 = INT_MAX;
+            int bestincR = 0;
+            const int L = 5;
+            float vDists[2 * L + 1];
+            const float iniu = scaleduR0 + L - w;
+            const float endu = scaleduR0 + L + w + 1;
+            if (iniu < 0 || endu >= PR.w) continue;
+            for (int incR = -L; incR <= +L; incR++) {
+                const int xr0 = (int)scaleduR0 + incR - w;
+                const float cR = (float)PR.row(yl0 + w)[xr0 + w];
+                // cv::norm(IL, IR, NORM_L1) on centred float patches: exact integer sum (|values| <= 510)
+                double acc = 0;
+                for (int yy = 0; yy < 2 * w + 1; yy++)
+                    for (int xx = 0; xx < 2 * w + 1; xx++) {
+                        const float a = (float)PL.row(yl0 + yy)[xl0 + xx] - cL;
+                        const float b = (float)PR.row(yl0 + yy)[xr0 + xx] - cR;
+                        acc += std::fabs((double)(a - b));
+                    }
+                const float dist = (float)acc;
+                if (dist < bestDist2) {
+                    bestDist2 = (int)dist;
+                    bestincR = incR;
+                }
+                vDists[L + incR] = dist;
+            }
+            if (bestincR == -L || bestincR == L) continue;
+            const float dist1 = vDists[L + bestincR - 1];
+            const float dist2 = vDists[L + bestincR];
+            const float dist3 = vDists[L + bestincR + 1];
+            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            if (deltaR < -1 || deltaR > 1) continue;
+            float bestuR = mvScaleFactors[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+            float disparity = (uL - bestuR);
+            if (disparity >= minD && disparity < maxD) {
+                if (disparity <= 0) {
+                    disparity = 0.01;
+                    bestuR = uL - 0.01;
+                }
+                mvDepth[iL] = mbf / disparity;
+                mvuRight[iL] = bestuR;
+                vDistIdx.push_back(std::pair<int, int>(bestDist2, iL));
+            }
+        }
+    }
+    if (vDistIdx.empty()) return 0;   // (the reference reads vDistIdx[0] of an empty vector: UB)
+    std::sort(vDistIdx.begin(), vDistIdx.end());   // :822-835
+    const float median = vDistIdx[vDistIdx.size() / 2].first;
+    const float thDist = 1.5f * 1.4f * median;
+    int nvalid = (int)vDistIdx.size();
+    for (int i = (int)vDistIdx.size() - 1; i >= 0; i--) {
+        if (vDistIdx[i].first < thDist) break;
+        mvuRight[vDistIdx[i].second] = -1;
+        mvDepth[vDistIdx[i].second] = -1;
+        nvalid--;
+    }
+    return nvalid;
+}
+
 }  // extern "C"

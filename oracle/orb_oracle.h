@@ -123,6 +123,13 @@ int oracle_features_in_area(int n, const OracleKeyPoint* kpsUn,
                             float x, float y, float r, int minLevel, int maxLevel,
                             int* out, int cap);
 
+/* Frame::ComputeStereoMatches (Frame.cc:662-836) on the pyramids of two oracle extractors that ran on
+ * the rectified left / right images.  Writes mvuRight / mvDepth (N each, -1 = no match); returns the
+ * number of left keypoints with a depth. */
+int oracle_stereo_matches(void* left, void* right, int N, const OracleKeyPoint* kpsL, const uint8_t* descL, int Nr,
+                          const OracleKeyPoint* kpsR, const uint8_t* descR, float mb, float mbf, float* mvuRight,
+                          float* mvDepth);
+
 #ifdef __cplusplus
 }
 #endif

@@ -300,6 +300,10 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     last_frame_pitch = frame_pitch;
     last_row_stride = row_stride;
     last_nframes = nframes;
+    last_kps = d_kps;
+    last_desc = d_desc;
+    last_counts = d_counts;
+    last_kp_cap = kp_cap;
     level_cache_valid = 0;
     return ORB_OK;
 }

@@ -83,6 +83,10 @@ struct Ctx {
     long long last_frame_pitch = 0;
     int last_row_stride = 0;
     int last_nframes = 0;
+    const orb_keypoint* last_kps = nullptr;   // outputs of the last batch (stereo matching reads them)
+    const uint8_t* last_desc = nullptr;
+    const int* last_counts = nullptr;
+    int last_kp_cap = 0;
     unsigned level_cache_valid = 0;
     std::vector<uint8_t> level_host[ORBGPU_MAX_LEVELS];
 

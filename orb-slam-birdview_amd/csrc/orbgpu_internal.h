@@ -119,6 +119,23 @@ hipError_t launch_triangulation(const uint8_t* d_desc1, const orb_keypoint* d_kp
                                 const int* d_cand_idx, int nitems, const TriParams& tp, int* d_best,
                                 hipStream_t stream);
 
+// Frame::ComputeStereoMatches (stereo.hip).  One side of a rectified pair: its pyramid (level 0 in
+// `frames`, levels >= 1 in `pyr`) and extraction outputs, for pair p at frame frame0 + p*frame_step.
+struct StereoSide {
+    const uint8_t* frames;
+    long long frame_pitch;
+    int row_stride;
+    const uint8_t* pyr;
+    int frame0, frame_step;
+    const orb_keypoint* kps;   // pair p: kps + (frame0 + p*frame_step) * kp_stride
+    const uint8_t* desc;       // same slots, 32 B each
+    const int* counts;         // counts[frame]
+    long long kp_stride;
+};
+hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L, const StereoSide& R, int npairs,
+                         float mb, float mbf, float* d_uright, float* d_depth, int* d_sad, long long out_stride,
+                         int* d_nmatched, hipStream_t stream);
+
 size_t octree_lds_bytes(int node_cap);
 void fast_wave_layout(Geom& g);   // fills fast_rows/drows/list/wave_bytes from the level grids
 

@@ -1,0 +1,370 @@
+// Frame::ComputeStereoMatches (Frame.cc:662-836) on gfx950: the first consumer of the extractor's
+// outputs.  Reads the left/right pyramids where the extractor left them in HBM,
+// so mvImagePyramid never has to be copied to the host for stereo.
+//
+//   k_stereo      one wavefront per left keypoint: row-band / octave / disparity-range filtered
+//                 Hamming search over the right keypoints (first minimum, as the strict '<' of
+//                 :737-741), then the 11x11 centred-L1 window search over 11 offsets (:758-788),
+//                 parabola refinement and the disparity checks (:790-819)
+//   k_stereo_cut  one workgroup per pair: median of the accepted window distances and the
+//                 1.5*1.4*median outlier cut (:822-835)
+//
+// All window arithmetic is integer (cv::norm NORM_L1 of integer-valued float patches is an exact
+// integer); the parabola and depth use the reference's float expressions, uncontracted.
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include "orbgpu_ctx.h"
+
+namespace orbgpu {
+namespace {
+
+constexpr int kThHigh = 100;                      // ORBmatcher.cc:37
+constexpr int kThOrbDist = (kThHigh + 50) / 2;    // Frame.cc:667
+constexpr int kWin = 5;                           // :758 w
+constexpr int kRange = 5;                         // :765 L
+
+__device__ __forceinline__ const uint8_t* level_base(const Geom* __restrict__ g, const StereoSide& s, int f, int l,
+                                                     int& stride) {
+    if (l == 0) {
+        stride = s.row_stride;
+        return s.frames + (long long)f * s.frame_pitch;
+    }
+    stride = g->L[l].pitch;
+    return s.pyr + (long long)f * g->pyr_bytes + g->L[l].pyr_off;
+}
+
+__device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_stereo(const Geom* __restrict__ g, StereoSide L, StereoSide R, float mb,
+                                                float mbf, float* __restrict__ uright, float* __restrict__ depth,
+                                                int* __restrict__ sad, long long out_stride) {
+    __shared__ int s_part[4][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int p = blockIdx.y;
+    const int iL = blockIdx.x * 4 + wv;
+    const int fL = L.frame0 + p * L.frame_step, fR = R.frame0 + p * R.frame_step;
+    const int nL = L.counts[fL], nR = R.counts[fR];
+    if (iL >= nL) return;
+    const orb_keypoint* kR = R.kps + (long long)fR * R.kp_stride;
+    const orb_keypoint kpL = L.kps[(long long)fL * L.kp_stride + iL];
+    const uint4* qp = reinterpret_cast<const uint4*>(L.desc + ((long long)fL * L.kp_stride + iL) * 32);
+    const uint4 qa = qp[0], qb = qp[1];
+    const uint4* dR = reinterpret_cast<const uint4*>(R.desc + (long long)fR * R.kp_stride * 32);
+    const float minD = 0, maxD = mbf / mb;   // :692-694 (minZ = mb)
+    const float uL = kpL.x, vL = kpL.y;
+    const float minU = uL - maxD, maxU = uL - minD;
+    const int yL = (int)vL;                  // vRowIndices[vL]: float index truncated (:707)
+    const int levelL = kpL.octave;
+
+    // ---- descriptor search over the right keypoints whose row band covers yL (:676-689, :716-745)
+    unsigned best = 0xFFFFFFFFu;   // dist << 16 | iR: the first minimum in iR order
+    if (maxU >= 0) {
+        for (int iR = lane; iR < nR; iR += 64) {
+            const orb_keypoint kr = kR[iR];
+            const float r = 2.0f * g->L[kr.octave].scale;
+            const int maxr = (int)ceilf(kr.y + r), minr = (int)floorf(kr.y - r);
+            if (yL < minr || yL > maxr) continue;
+            if (kr.octave < levelL - 1 || kr.octave > levelL + 1) continue;
+            if (!(kr.x >= minU && kr.x <= maxU)) continue;
+            const int dist = hamming256(qa, qb, dR[2 * iR], dR[2 * iR + 1]);
+            if (dist < kThHigh) best = min(best, ((unsigned)dist << 16) | (unsigned)iR);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (unsigned)__shfl_xor((int)best, o));
+
+    float outU = -1.0f, outD = -1.0f;
+    int outS = -1;
+    if (best != 0xFFFFFFFFu && (int)(best >> 16) < kThOrbDist) {
+        // ---- sliding-window search at the keypoint's scale (:750-788)
+        const int bestIdxR = (int)(best & 0xFFFF);
+        const float uR0 = kR[bestIdxR].x;
+        const float scaleFactor = 1.0f / g->L[levelL].scale;   // mvInvScaleFactors (ORBextractor.cc:428-429)
+        const float scaleduL = roundf(uL * scaleFactor);
+        const float scaledvL = roundf(vL * scaleFactor);
+        const float scaleduR0 = roundf(uR0 * scaleFactor);
+        const float iniu = scaleduR0 + kRange - kWin;
+        const float endu = scaleduR0 + kRange + kWin + 1;
+        const int cols = g->L[levelL].w;
+        if (!(iniu < 0 || endu >= cols)) {
+            int sL, sR;
+            const uint8_t* PL = level_base(g, L, fL, levelL, sL);
+            const uint8_t* PR = level_base(g, R, fR, levelL, sR);
+            const int y0 = (int)scaledvL - kWin, xl0 = (int)scaleduL - kWin, xr0 = (int)scaleduR0 - kWin;
+            const int cL = PL[(long long)(y0 + kWin) * sL + xl0 + kWin];
+            // lane j < 55: offset incR = j/5 - 5, row group j%5 (rows {0-2}, {3-4}, ..., {9-10})
+            int acc = 0;
+            if (lane < 55) {
+                const int inc = lane / 5 - kRange, rg = lane - (lane / 5) * 5;
+                const int r0 = rg == 0 ? 0 : 2 * rg + 1, r1 = 2 * rg + 3;
+                const int xr = xr0 + inc;
+                const int cR = PR[(long long)(y0 + kWin) * sR + xr + kWin];
+                for (int yy = r0; yy < r1; yy++) {
+                    const uint8_t* rl = PL + (long long)(y0 + yy) * sL + xl0;
+                    const uint8_t* rr = PR + (long long)(y0 + yy) * sR + xr;
+#pragma unroll
+                    for (int xx = 0; xx < 2 * kWin + 1; xx++)   // |(l - cL) - (r - cR)| = |(l + cR) - (r + cL)|
+                        acc += abs((rl[xx] + cR) - (rr[xx] + cL));
+                }
+            }
+            s_part[wv][lane] = acc;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane == 0) {
+                float vDists[2 * kRange + 1];
+                int bestDist = INT_MAX, bestincR = 0;
+                for (int k = 0; k < 2 * kRange + 1; k++) {
+                    const int* q = &s_part[wv][5 * k];
+                    const float dist = (float)(q[0] + q[1] + q[2] + q[3] + q[4]);
+                    if (dist < bestDist) {
+                        bestDist = (int)dist;
+                        bestincR = k - kRange;
+                    }
+                    vDists[k] = dist;
+                }
+                if (bestincR != -kRange && bestincR != kRange) {
+                    // ---- sub-pixel parabola (:793-801) and disparity checks (:803-819)
+                    const float dist1 = vDists[kRange + bestincR - 1];
+                    const float dist2 = vDists[kRange + bestincR];
+                    const float dist3 = vDists[kRange + bestincR + 1];
+                    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+                    if (!(deltaR < -1 || deltaR > 1)) {
+                        float bestuR = g->L[levelL].scale * ((float)scaleduR0 + (float)bestincR + deltaR);
+                        float disparity = (uL - bestuR);
+                        if (disparity >= minD && disparity < maxD) {
+                            if (disparity <= 0) {
+                                disparity = 0.01f;
+                                bestuR = (float)((double)uL - 0.01);
+                            }
+                            outD = mbf / disparity;
+                            outU = bestuR;
+                            outS = bestDist;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        const long long o = (long long)p * out_stride + iL;
+        uright[o] = outU;
+        depth[o] = outD;
+        sad[o] = outS;
+    }
+}
+
+// Median cut (:822-835): sort the accepted window distances (bitonic, LDS), thDist =
+// 1.5f*1.4f*median, reject every accepted keypoint whose distance is >= thDist.
+__global__ __launch_bounds__(256) void k_stereo_cut(StereoSide L, float* __restrict__ uright,
+                                                    float* __restrict__ depth, int* __restrict__ sad,
+                                                    long long out_stride, int np2, int* __restrict__ nmatched) {
+    extern __shared__ int s_keys[];
+    __shared__ int s_cnt, s_kept;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int nL = L.counts[L.frame0 + p * L.frame_step];
+    float* ur = uright + (long long)p * out_stride;
+    float* dp = depth + (long long)p * out_stride;
+    int* sd = sad + (long long)p * out_stride;
+    if (tid == 0) {
+        s_cnt = 0;
+        s_kept = 0;
+    }
+    for (int i = tid; i < np2; i += 256) s_keys[i] = INT_MAX;
+    __syncthreads();
+    for (int i = tid; i < nL; i += 256) {
+        const int v = sd[i];
+        if (v >= 0) s_keys[atomicAdd(&s_cnt, 1)] = v;
+    }
+    __syncthreads();
+    const int cnt = s_cnt;
+    if (cnt == 0) {   // (the reference reads vDistIdx[0] of an empty vector)
+        if (tid == 0) nmatched[p] = 0;
+        return;
+    }
+    for (int k = 2; k <= np2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < np2; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int a = s_keys[i], b = s_keys[ixj];
+                    const bool up = (i & k) == 0;
+                    if (up ? a > b : a < b) {
+                        s_keys[i] = b;
+                        s_keys[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const float median = (float)s_keys[cnt / 2];
+    const float thDist = 1.5f * 1.4f * median;
+    int kept = 0;
+    for (int i = tid; i < nL; i += 256) {
+        const int v = sd[i];
+        if (v < 0) continue;
+        if ((float)v < thDist) {
+            kept++;
+        } else {
+            ur[i] = -1.0f;
+            dp[i] = -1.0f;
+        }
+    }
+    if (kept) atomicAdd(&s_kept, kept);
+    __syncthreads();
+    if (tid == 0) nmatched[p] = s_kept;
+}
+
+hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L, const StereoSide& R, int npairs,
+                         float mb, float mbf, float* d_uright, float* d_depth, int* d_sad, long long out_stride,
+                         int* d_nmatched, hipStream_t stream) {
+    if (npairs <= 0) return hipSuccess;
+    const int cap = (int)out_stride;
+    hipLaunchKernelGGL(k_stereo, dim3((cap + 3) / 4, npairs), dim3(256), 0, stream, d_geom, L, R, mb, mbf, d_uright,
+                       d_depth, d_sad, out_stride);
+    int np2 = 1;
+    while (np2 < cap) np2 <<= 1;
+    if ((size_t)np2 * 4 > 64 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_stereo_cut, dim3(npairs), dim3(256), (size_t)np2 * 4, stream, L, d_uright, d_depth, d_sad,
+                       out_stride, np2, d_nmatched);
+    (void)g;
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu
+
+using namespace orbgpu;
+
+#define CTX_GUARD(ctx)                                                              \
+    if (!(ctx)) {                                                                   \
+        set_error("NULL context", hipSuccess);                                      \
+        return ORB_ERR_ARG;                                                         \
+    }                                                                               \
+    {                                                                               \
+        hipError_t _e = hipSetDevice((ctx)->device);                                \
+        if (_e != hipSuccess) return set_error("hipSetDevice", _e), ORB_ERR_HIP;    \
+    }
+
+static bool same_geometry(const Ctx* a, const Ctx* b) {
+    if (!a->have_geom || !b->have_geom) return false;
+    const Geom &x = a->geom, &y = b->geom;
+    if (x.W != y.W || x.H != y.H || x.nlevels != y.nlevels) return false;
+    for (int l = 0; l < x.nlevels; l++)
+        if (x.L[l].w != y.L[l].w || x.L[l].h != y.L[l].h || x.L[l].pitch != y.L[l].pitch ||
+            x.L[l].pyr_off != y.L[l].pyr_off || x.L[l].scale != y.L[l].scale)
+            return false;
+    return true;
+}
+
+extern "C" {
+
+int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_keypoint* kpsL, const uint8_t* descL,
+                               int nR, const orb_keypoint* kpsR, const uint8_t* descR, float mb, float mbf,
+                               float* uright, float* depth, int* nmatched) {
+    Ctx* cl = reinterpret_cast<Ctx*>(left);
+    Ctx* cr = reinterpret_cast<Ctx*>(right);
+    CTX_GUARD(cl);
+    if (!cr || nL < 0 || nR < 0 || (nL && (!kpsL || !descL || !uright || !depth)) || (nR && (!kpsR || !descR)))
+        return set_error("orb_compute_stereo_matches: bad arguments", hipSuccess), ORB_ERR_ARG;
+    if (cl->device != cr->device)
+        return set_error("orb_compute_stereo_matches: contexts on different devices", hipSuccess), ORB_ERR_ARG;
+    if (cl->last_nframes < 1 || cr->last_nframes < 1 || !same_geometry(cl, cr))
+        return set_error("orb_compute_stereo_matches: both contexts must have extracted an image of one size",
+                         hipSuccess),
+               ORB_ERR_ARG;
+    if (nL == 0) {
+        if (nmatched) *nmatched = 0;
+        return ORB_OK;
+    }
+    hipError_t e;
+    if ((e = hipStreamSynchronize(cr->stream)) != hipSuccess) return set_error("sync right", e), ORB_ERR_HIP;
+    const int cap = std::max(nL, 1);
+    const size_t A = 256;
+    auto al = [&](size_t x) { return (x + A - 1) & ~(A - 1); };
+    const size_t need = al((size_t)nL * 28) + al((size_t)nL * 32) + al((size_t)std::max(nR, 1) * 28) +
+                        al((size_t)std::max(nR, 1) * 32) + al(16) + 3 * al((size_t)cap * 4) + al(4) + A;
+    if (need > cl->scratch_cap || !cl->d_scratch) {
+        if (cl->d_scratch) (void)hipFree(cl->d_scratch);
+        cl->d_scratch = nullptr;
+        cl->scratch_cap = 0;
+        if ((e = hipMalloc((void**)&cl->d_scratch, need)) != hipSuccess) return set_error("stereo scratch", e), ORB_ERR_NOMEM;
+        cl->scratch_cap = need;
+    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        uint8_t* q = cl->d_scratch + off;
+        off += al(bytes);
+        return q;
+    };
+    orb_keypoint* d_kL = (orb_keypoint*)take((size_t)nL * 28);
+    uint8_t* d_dL = take((size_t)nL * 32);
+    orb_keypoint* d_kR = (orb_keypoint*)take((size_t)std::max(nR, 1) * 28);
+    uint8_t* d_dR = take((size_t)std::max(nR, 1) * 32);
+    int* d_cnt = (int*)take(16);
+    float* d_u = (float*)take((size_t)cap * 4);
+    float* d_d = (float*)take((size_t)cap * 4);
+    int* d_s = (int*)take((size_t)cap * 4);
+    int* d_nm = (int*)take(4);
+    const int cnt[2] = {nL, nR};
+    if ((e = hipMemcpyAsync(d_kL, kpsL, (size_t)nL * 28, hipMemcpyHostToDevice, cl->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_dL, descL, (size_t)nL * 32, hipMemcpyHostToDevice, cl->stream)) != hipSuccess ||
+        (nR && (e = hipMemcpyAsync(d_kR, kpsR, (size_t)nR * 28, hipMemcpyHostToDevice, cl->stream)) != hipSuccess) ||
+        (nR && (e = hipMemcpyAsync(d_dR, descR, (size_t)nR * 32, hipMemcpyHostToDevice, cl->stream)) != hipSuccess) ||
+        (e = hipMemcpyAsync(d_cnt, cnt, sizeof cnt, hipMemcpyHostToDevice, cl->stream)) != hipSuccess)
+        return set_error("stereo upload", e), ORB_ERR_HIP;
+    StereoSide SL{cl->last_frames, cl->last_frame_pitch, cl->last_row_stride, cl->d_pyr, 0, 0, d_kL, d_dL, d_cnt, 0};
+    StereoSide SR{cr->last_frames, cr->last_frame_pitch, cr->last_row_stride, cr->d_pyr, 0, 0, d_kR, d_dR, d_cnt + 1, 0};
+    if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 1, cl->stream);
+    e = launch_stereo(cl->d_geom, cl->geom, SL, SR, 1, mb, mbf, d_u, d_d, d_s, cap, d_nm, cl->stream);
+    if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 0, cl->stream);
+    if (e != hipSuccess) return set_error("stereo kernels", e), ORB_ERR_HIP;
+    int nm = 0;
+    if ((e = hipMemcpyAsync(uright, d_u, (size_t)nL * 4, hipMemcpyDeviceToHost, cl->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(depth, d_d, (size_t)nL * 4, hipMemcpyDeviceToHost, cl->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(&nm, d_nm, 4, hipMemcpyDeviceToHost, cl->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(cl->stream)) != hipSuccess)
+        return set_error("stereo download", e), ORB_ERR_HIP;
+    if (nmatched) *nmatched = nm;
+    return ORB_OK;
+}
+
+int orb_stereo_batch_device(orb_ctx* h, int npairs, float mb, float mbf, float* d_uright, float* d_depth,
+                            int* d_nmatched) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (npairs <= 0 || !d_uright || !d_depth || !d_nmatched)
+        return set_error("orb_stereo_batch_device: bad arguments", hipSuccess), ORB_ERR_ARG;
+    if (!c->last_kps || c->last_nframes < 2 * npairs)
+        return set_error("orb_stereo_batch_device: the last batch holds fewer than 2*npairs frames", hipSuccess),
+               ORB_ERR_ARG;
+    const int cap = c->last_kp_cap;
+    const size_t need = (size_t)npairs * cap * 4 + 256;
+    hipError_t e;
+    if (need > c->scratch_cap || !c->d_scratch) {
+        if (c->d_scratch) (void)hipFree(c->d_scratch);
+        c->d_scratch = nullptr;
+        c->scratch_cap = 0;
+        if ((e = hipMalloc((void**)&c->d_scratch, need)) != hipSuccess) return set_error("stereo scratch", e), ORB_ERR_NOMEM;
+        c->scratch_cap = need;
+    }
+    StereoSide SL{c->last_frames, c->last_frame_pitch, c->last_row_stride, c->d_pyr, 0, 2, c->last_kps, c->last_desc,
+                  c->last_counts, cap};
+    StereoSide SR = SL;
+    SR.frame0 = 1;
+    if (c->prof_on) Ctx::marker(c, ORB_K_STEREO, 1, c->stream);
+    e = launch_stereo(c->d_geom, c->geom, SL, SR, npairs, mb, mbf, d_uright, d_depth, (int*)c->d_scratch, cap,
+                      d_nmatched, c->stream);
+    if (c->prof_on) Ctx::marker(c, ORB_K_STEREO, 0, c->stream);
+    if (e != hipSuccess) return set_error("stereo kernels", e), ORB_ERR_HIP;
+    return ORB_OK;
+}
+
+}  // extern "C"

@@ -13,7 +13,7 @@ import numpy as np
 from ._lib import OrbError, OrbFeatVec, OrbParams, check, lib
 
 __all__ = ["ORBextractor", "ORBmatcher", "BatchExtractor", "KP_DTYPE", "OrbError", "device_count",
-           "features_in_area"]
+           "features_in_area", "compute_stereo_matches"]
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -201,10 +201,15 @@ class BatchExtractor(_Ctx):
         check(lib().orb_profile_enable(self.h, int(on)), "orb_profile_enable")
 
     def profile_read(self):
-        ms = np.zeros(5, np.float64)
-        n = np.zeros(5, np.int32)
+        ms = np.zeros(6, np.float64)   # ORB_K_COUNT
+        n = np.zeros(6, np.int32)
         check(lib().orb_profile_read(self.h, _p(ms), _p(n)), "orb_profile_read")
         return ms, n
+
+    def stereo(self, npairs, mb, mbf, d_uright, d_depth, d_nmatched):
+        """Frame::ComputeStereoMatches for frame pairs (2p, 2p+1) of the last launch, on the device."""
+        check(lib().orb_stereo_batch_device(self.h, npairs, mb, mbf, d_uright, d_depth, d_nmatched),
+              "orb_stereo_batch_device")
 
     def hamming_top2(self, d_q, nq, d_t, nt, d_best, d_idx, d_second):
         check(lib().orb_hamming_top2_device(self.h, d_q, nq, d_t, nt, d_best, d_idx, d_second),
@@ -229,6 +234,21 @@ def _featvec(fv):
     idx = np.ascontiguousarray(np.concatenate(groups) if groups else np.zeros(1, np.int32), np.int32)
     s = OrbFeatVec(len(ids), ids.ctypes.data if len(ids) else None, off.ctypes.data, idx.ctypes.data)
     return s, (ids, off, idx)
+
+
+def compute_stereo_matches(left, right, kpsL, descL, kpsR, descR, mb, mbf):
+    """Frame::ComputeStereoMatches (Frame.cc:662-836): left / right are the ORBextractors that
+    extracted the rectified left / right images last.  Returns (mvuRight, mvDepth, n_with_depth)."""
+    kl = np.ascontiguousarray(kpsL, KP_DTYPE)
+    kr = np.ascontiguousarray(kpsR, KP_DTYPE)
+    dl = np.ascontiguousarray(descL, np.uint8)
+    dr = np.ascontiguousarray(descR, np.uint8)
+    u = np.zeros(max(len(kl), 1), np.float32)
+    d = np.zeros(max(len(kl), 1), np.float32)
+    n = ctypes.c_int(0)
+    check(lib().orb_compute_stereo_matches(left.h, right.h, len(kl), _p(kl), _p(dl), len(kr), _p(kr), _p(dr), mb, mbf,
+                                           _p(u), _p(d), ctypes.byref(n)), "orb_compute_stereo_matches")
+    return u[:len(kl)], d[:len(kl)], n.value
 
 
 def features_in_area(kps_un, min_x, max_x, min_y, max_y, x, y, r, min_level=-1, max_level=-1):

@@ -62,6 +62,8 @@ SIGNATURES = {
                                           OrbFeatVec, vp, cf, cf, vp, vp, ci, vp, ci, ctypes.POINTER(ci)]),
     "orb_window_match": (ci, [vp, cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, ctypes.POINTER(ci)]),
     "orb_features_in_area": (ci, [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]),
+    "orb_compute_stereo_matches": (ci, [vp, vp, ci, vp, vp, ci, vp, vp, cf, cf, vp, vp, ctypes.POINTER(ci)]),
+    "orb_stereo_batch_device": (ci, [vp, ci, cf, cf, vp, vp, vp]),
 }
 
 STATUS = {0: "ORB_OK", -1: "ORB_ERR_ARG", -2: "ORB_ERR_HIP", -3: "ORB_ERR_CAPACITY",

@@ -19,6 +19,7 @@
 #include "../../oracle/orb_oracle.h"
 #include "../../orb-slam-birdview_amd/host/ORBextractor.h"
 #include "../../orb-slam-birdview_amd/host/ORBmatcher.h"
+#include "../../orb-slam-birdview_amd/host/Stereo.h"
 
 using namespace ORB_SLAM2;
 
@@ -312,6 +313,32 @@ int main(int argc, char** argv) {
                     }
                 }
             }
+        }
+        // ---- Frame::ComputeStereoMatches (Frame.cc:662-836): frame 0 = left, frame 1 = right
+        {
+            ORBextractor left(nf, 1.2f, 8, 20, 7), right(nf, 1.2f, 8, 20, 7);
+            std::vector<KeyPoint> kl, kr;
+            DescriptorMat dl, dr;
+            left(ImageView(frames.data(), w, h), ImageView(), kl, dl);
+            right(ImageView(frames.data() + (size_t)w * h, w, h), ImageView(), kr, dr);
+            std::vector<float> mvuRight, mvDepth;
+            const float mb = 0.12f, mbf = 0.12f * 500.0f;
+            const int n = ComputeStereoMatches(left, right, kl, dl, kr, dr, mb, mbf, mvuRight, mvDepth);
+            void* ol = oracle_create(nf, 1.2f, 8, 20, 7, 0);
+            void* orr = oracle_create(nf, 1.2f, 8, 20, 7, 0);
+            oracle_run(ol, frames.data(), w, h, w);
+            oracle_run(orr, frames.data() + (size_t)w * h, w, h, w);
+            std::vector<float> ou(kl.size() + 1), od(kl.size() + 1);
+            const int on = oracle_stereo_matches(ol, orr, (int)kl.size(), (const OracleKeyPoint*)kl.data(), dl.buf.data(),
+                                                 (int)kr.size(), (const OracleKeyPoint*)kr.data(), dr.buf.data(), mb, mbf,
+                                                 ou.data(), od.data());
+            oracle_destroy(ol);
+            oracle_destroy(orr);
+            ou.resize(kl.size());
+            od.resize(kl.size());
+            const bool ok = n == on && memcmp(mvuRight.data(), ou.data(), ou.size() * 4) == 0 &&
+                            memcmp(mvDepth.data(), od.data(), od.size() * 4) == 0;
+            report("ComputeStereoMatches", ok, "n=" + std::to_string(n) + " oracle=" + std::to_string(on));
         }
     } catch (const std::exception& e) {
         report("exception", false, e.what());

@@ -46,7 +46,8 @@ def test_mirror_library_exports_reference_api(mirror_bin):
                 "ORB_SLAM2::ORBmatcher::SearchForTriangulation(",
                 "ORB_SLAM2::ORBmatcher::SearchForInitialization(",
                 "ORB_SLAM2::ORBmatcher::BirdviewMatch(",
-                "ORB_SLAM2::FrameGrid::GetFeaturesInArea("]:
+                "ORB_SLAM2::FrameGrid::GetFeaturesInArea(",
+                "ORB_SLAM2::ComputeStereoMatches("]:
         assert sym in out, sym
     del lib
 
@@ -64,8 +65,10 @@ def test_mirror_fails_loudly_without_gpu(mirror_bin, tmp_path):
 @pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1280, 720, 2000)])
 def test_mirror_parity_on_gpu(mirror_bin, tmp_path, w, h, nf):
     from orbgpu.synth import synth_frame
+    from orbgpu.synth import synth_stereo_right
     a = synth_frame(w, h, 21)
-    frames = np.stack([a, np.roll(a, (3, 5), axis=(0, 1)), synth_frame(w, h, 5, "noise")])
+    # frame 1: a rectified right view of frame 0 (matchers and ComputeStereoMatches use the pair)
+    frames = np.stack([a, synth_stereo_right(a, 21), synth_frame(w, h, 5, "noise")])
     rc, out, err = _run(mirror_bin, frames, nf, tmp_path)
     fails = [l for l in out.splitlines() if " FAIL" in l]
     assert rc == 0 and not fails, "\n".join(fails) + "\n" + err[-2000:]

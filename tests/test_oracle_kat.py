@@ -232,3 +232,40 @@ def test_oracle_matches_golden(oracle_mod, name):
     k, d = oracle_mod.OracleExtractor(nf)(img)
     assert k.tobytes() == g["kps"].tobytes()
     assert np.array_equal(d, g["desc"])
+
+
+def test_oracle_stereo_golden(oracle_mod):
+    """Frame::ComputeStereoMatches restatement (Frame.cc:662-836) against its committed vectors."""
+    import hashlib
+    from orbgpu.synth import synth_frame, synth_stereo_right
+    g = _golden("stereo_640x480.npz")
+    w, h, nf, idx = [int(v) for v in g["cfg"]]
+    left = synth_frame(w, h, idx)
+    right = synth_stereo_right(left, idx)
+    assert hashlib.sha256(left.tobytes()).hexdigest() == str(g["left_sha256"])
+    assert hashlib.sha256(right.tobytes()).hexdigest() == str(g["right_sha256"])
+    ol, orr = oracle_mod.OracleExtractor(nf), oracle_mod.OracleExtractor(nf)
+    kl, dl = ol(left)
+    kr, dr = orr(right)
+    u, d, n = oracle_mod.stereo_matches(ol, orr, kl, dl, kr, dr, float(g["mb"]), float(g["mbf"]))
+    assert n == int(g["n"]) and u.tobytes() == g["uright"].tobytes() and d.tobytes() == g["depth"].tobytes()
+
+
+def test_oracle_stereo_kat(oracle_mod):
+    """Identical views: every window distance is 0, the median is 0 and the 1.5*1.4*median cut
+    (Frame.cc:822-835) rejects every match; accepted depths satisfy depth = mbf / (uL - uR)."""
+    from orbgpu.synth import synth_frame, synth_stereo_right
+    left = synth_frame(320, 240, 4)
+    ol, orr = oracle_mod.OracleExtractor(500), oracle_mod.OracleExtractor(500)
+    kl, dl = ol(left)
+    kr, dr = orr(left.copy())
+    u, d, n = oracle_mod.stereo_matches(ol, orr, kl, dl, kr, dr, 0.1, 50.0)
+    assert n == 0 and (u == -1).all() and (d == -1).all()
+    right = synth_stereo_right(left, 4)
+    kr, dr = orr(right)
+    u, d, n = oracle_mod.stereo_matches(ol, orr, kl, dl, kr, dr, 0.1, 50.0)
+    ok = u >= 0
+    assert n == ok.sum() > 0
+    disp = kl["x"][ok] - u[ok]
+    assert np.all(disp >= 0) and np.all(disp < 500.0)
+    assert np.array_equal(d[ok], (np.float32(50.0) / disp.astype(np.float32)).astype(np.float32))

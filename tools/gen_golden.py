@@ -34,5 +34,23 @@ def main():
         print(name, len(k))
 
 
+def stereo():
+    """Frame::ComputeStereoMatches on a seeded synthetic stereo pair (oracle), 640x480 / 1000 features."""
+    from orbgpu.synth import synth_stereo_right
+    left = synth_frame(640, 480, 3)
+    right = synth_stereo_right(left, 3)
+    ol, orr = oracle.OracleExtractor(1000), oracle.OracleExtractor(1000)
+    kl, dl = ol(left)
+    kr, dr = orr(right)
+    u, d, n = oracle.stereo_matches(ol, orr, kl, dl, kr, dr, 0.12, 0.12 * 500.0)
+    np.savez_compressed(os.path.join(OUT, "stereo_640x480.npz"), cfg=np.array([640, 480, 1000, 3]),
+                        mb=np.float32(0.12), mbf=np.float32(0.12 * 500.0),
+                        left_sha256=np.array(hashlib.sha256(left.tobytes()).hexdigest()),
+                        right_sha256=np.array(hashlib.sha256(right.tobytes()).hexdigest()),
+                        uright=u, depth=d, n=np.int32(n))
+    print("stereo_640x480.npz", n)
+
+
 if __name__ == "__main__":
     main()
+    stereo()
