@@ -205,23 +205,22 @@ def main():
     tmax, total_kps = reduce_max_sum(dist, local_time, local_kps)
     _, total_frames = reduce_max_sum(dist, 0.0, float(B * args.steps))
 
-    # ---- Hamming: all-pairs top-2 between consecutive frames' descriptors (device-resident)
+    # ---- Hamming: all-pairs top-2 between consecutive frames' descriptors (device-resident, one
+    # launch for all B-1 pairs: orb_hamming_top2_frames_device, counts read on the device)
     ham = None
     if not args.no_hamming:
         counts = ex.counts()
         L = orbgpu._lib.lib()
-        nq = int(counts.min())
-        dbest = [ex._alloc(nq * 4) for _ in range(3)]
         pairs = B - 1
+        qf, tf = list(range(pairs)), list(range(1, B))
+        dbest = [ex._alloc(pairs * ex.kp_cap * 4) for _ in range(3)]
 
         def ham_step():
-            for f in range(pairs):
-                ex.hamming_top2(ex.d_desc + f * ex.kp_cap * 32, nq, ex.d_desc + (f + 1) * ex.kp_cap * 32, nq,
-                                *dbest)
+            ex.hamming_top2_frames(qf, tf, *dbest)
         ham_step()
         sync()
         ex.profile(True)
-        hs = max(2, args.steps // 4)
+        hs = max(2, args.steps)
         barrier(dist)
         th0 = time.perf_counter()
         for _ in range(hs):
@@ -232,14 +231,19 @@ def main():
         ex.profile(False)
         for p in dbest:
             L.orb_device_free(ex.h, p)
-        evals = float(nq) * nq * pairs * hs
+        evals_step = float(sum(int(counts[a]) * int(counts[b]) for a, b in zip(qf, tf)))
+        evals = evals_step * hs
         htmax, hevals = reduce_max_sum(dist, th1 - th0, evals)
         kt = hms[4] / 1e3 / max(hl[4], 1)
-        ham = {"matches_per_s": round(hevals / htmax, 1), "queries_per_s": round(hevals / nq / htmax, 1),
-               "pair": f"{nq}x{nq} descriptors (frame f vs f+1), {pairs} pairs per step per GPU",
+        PEAK_VALU = 256 * 128 * 2.4e9   # lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
+        ham = {"matches_per_s": round(hevals / htmax, 1),
+               "queries_per_s": round(hevals / float(np.mean(counts)) / htmax, 1),
+               "pair": f"frame f vs f+1 descriptors (~{int(np.mean(counts))} each), {pairs} pairs per launch",
                "kernel_avg_us": round(kt * 1e6, 2),
-               "kernel_valu_ops_per_s": round(16.0 * nq * nq / kt, 1) if kt > 0 else None,
-               "kernel_hbm_gbs": round((32.0 * 2 * nq + 12 * nq) / kt / 1e9, 2) if kt > 0 else None}
+               "kernel_valu_ops_per_s": round(16.0 * evals_step / kt, 1) if kt > 0 else None,
+               "valu_frac": round(16.0 * evals_step / kt / PEAK_VALU, 4) if kt > 0 else None,
+               "kernel_hbm_gbs": round((32.0 * 2 * float(counts.sum()) + 12 * float(counts.sum())) / kt / 1e9, 2)
+               if kt > 0 else None}
 
     # ---- roofline of the dominant kernel (per-step algorithmic bytes / per-step kernel time)
     per_frame_kps = kps_per_step / B

@@ -138,6 +138,15 @@ int orb_hamming_topk(orb_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, i
 int orb_hamming_top2_device(orb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
                             int* d_best, int* d_best_idx, int* d_second);
 
+/* Batched device form over the descriptor slots of an extraction batch (orb_extract_batch_device's
+ * d_desc / d_counts / kp_cap): pair p matches the descriptors of frame q_frames[p] against those of
+ * frame t_frames[p] (host arrays), all pairs in one launch, counts read on the device.  Outputs at
+ * d_best / d_best_idx / d_second[p * kp_cap + i].  kp_cap <= 65535.  Asynchronous.  This is the
+ * brute-force SearchByBoW inner loop of BASELINE config C4 (one vocabulary node holding everything). */
+int orb_hamming_top2_frames_device(orb_ctx* ctx, const uint8_t* d_desc, const int* d_counts, int kp_cap, int npairs,
+                                   const int* q_frames, const int* t_frames, int* d_best, int* d_best_idx,
+                                   int* d_second);
+
 /* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21) as CSR. */
 typedef struct {
     int nnodes;

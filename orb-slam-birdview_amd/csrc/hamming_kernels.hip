@@ -2,6 +2,8 @@
 // 8 x (v_xor_b32 + v_bcnt_u32_b32): bitwise VALU work, no MFMA.  The selection logic that depends
 // on the order of earlier accepted matches (SearchByBoW's taken set, SearchForInitialization's
 // vMatchedDistance) is replayed on the host from these exact top-k lists (matcher.cpp).
+#include <algorithm>
+
 #include "orbgpu_internal.h"
 
 namespace orbgpu {
@@ -89,65 +91,92 @@ __global__ __launch_bounds__(256) void k_topk(const uint8_t* __restrict__ q, int
     if (lane == 0 && out_nvalid) out_nvalid[qi] = nvalid;
 }
 
-/* All-pairs top-2 (best, its index — first on ties — and second best), thread per query, train
- * descriptors streamed through LDS in 256-row tiles and read as wave-uniform broadcasts.  The
- * train set is split over gridDim.y slices for occupancy; slices are merged by k_top2_merge. */
-__global__ __launch_bounds__(256) void k_top2_tiles(const uint8_t* __restrict__ q, int nq,
-                                                    const uint8_t* __restrict__ t, int nt, int slice,
-                                                    int4* __restrict__ part) {
-    __shared__ uint4 s_t[256 * 2];
-    const int qi = blockIdx.x * 256 + threadIdx.x;
-    const int sl = blockIdx.y;
-    const int t0 = sl * slice, t1 = min(nt, t0 + slice);
+/* Batched all-pairs top-2 over many (query set, train set) pairs in one launch.  Lane = query, one
+ * wavefront = 64 queries x one train slice; the train descriptors of the slice are wave-uniform and
+ * read through the scalar cache (s_load), so the inner loop is 8 v_xor + 8 v_bcnt (accumulating)
+ * and a 3-op top-2 update on keys dist << 16 | train index: min keeps the first index on ties, and
+ * second = min(second, max(best, key)) is the second-smallest key.  Slices are merged by
+ * k_top2b_merge (keys compose the same way).  Counts may be read on the device (an extraction
+ * batch's d_counts), so a whole batch of frame pairs needs no host round trip. */
+__global__ __launch_bounds__(256) void k_top2_batch(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
+                                                    int* __restrict__ idx_o, int* __restrict__ second_o) {
+    const int p = blockIdx.z, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
+    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
+    const int qw = (blockIdx.x * 4 + wv) * 64;
+    if (qw >= nq) return;   // whole wave (no block barriers below)
+    const int qi = qw + lane;
+    const int t0 = blockIdx.y * a.slice, t1 = min(nt, t0 + a.slice);
     uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
     if (qi < nq) {
-        const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)qi * 32);
+        const uint4* qp = reinterpret_cast<const uint4*>(a.q + ((long long)fr.x * a.q_stride + qi) * 32);
         qa = qp[0];
         qb = qp[1];
     }
-    int best = 257, bidx = -1, second = 257;
-    for (int tb = t0; tb < t1; tb += 256) {
-        const int n = min(256, t1 - tb);
-        __syncthreads();
-        if ((int)threadIdx.x < n) {
-            const uint4* tp = reinterpret_cast<const uint4*>(t + (long long)(tb + threadIdx.x) * 32);
-            s_t[2 * threadIdx.x] = tp[0];
-            s_t[2 * threadIdx.x + 1] = tp[1];
-        }
-        __syncthreads();
-        for (int j = 0; j < n; j++) {
-            const int d = hamming256(qa, qb, s_t[2 * j], s_t[2 * j + 1]);
-            if (d < best) {
-                second = best;
-                best = d;
-                bidx = tb + j;
-            } else if (d < second) {
-                second = d;
-            }
-        }
+    const uint4* __restrict__ T = reinterpret_cast<const uint4*>(a.t + (long long)fr.y * a.t_stride * 32);
+    unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
+#pragma unroll 4
+    for (int j = t0; j < t1; j++) {
+        const uint4 x = T[2 * j], y = T[2 * j + 1];
+        const unsigned d = __popc(qa.x ^ x.x) + __popc(qa.y ^ x.y) + __popc(qa.z ^ x.z) + __popc(qa.w ^ x.w) +
+            __popc(qb.x ^ y.x) + __popc(qb.y ^ y.y) + __popc(qb.z ^ y.z) + __popc(qb.w ^ y.w);
+        const unsigned key = (d << 16) | (unsigned)j;
+        s2 = min(s2, max(b, key));
+        b = min(b, key);
     }
-    if (qi < nq) part[(long long)sl * nq + qi] = make_int4(best, bidx, second, 0);
+    if (qi >= nq) return;
+    const long long o = (long long)p * a.out_stride + qi;
+    if (gridDim.y == 1) {
+        best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
+        idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
+        second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
+    } else {
+        part[((long long)p * gridDim.y + blockIdx.y) * a.out_stride + qi] = make_uint2(b, s2);
+    }
 }
 
-__global__ __launch_bounds__(256) void k_top2_merge(const int4* __restrict__ part, int nq, int nslices,
-                                                    int* __restrict__ best_o, int* __restrict__ idx_o,
-                                                    int* __restrict__ second_o) {
+__global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, const uint2* __restrict__ part,
+                                                     int* __restrict__ best_o, int* __restrict__ idx_o,
+                                                     int* __restrict__ second_o) {
+    const int p = blockIdx.y;
+    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
+    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
     const int qi = blockIdx.x * 256 + threadIdx.x;
     if (qi >= nq) return;
-    int4 acc = part[qi];
-    for (int s = 1; s < nslices; s++) {
-        const int4 p = part[(long long)s * nq + qi];
-        if (p.x < acc.x) {            // later slice wins only on a strictly smaller distance
-            acc.z = min(acc.x, p.z);
-            acc.x = p.x;
-            acc.y = p.y;
-        } else {
-            acc.z = min(acc.z, p.x);
-        }
+    const int used = min(nslices, (nt + a.slice - 1) / a.slice);   // slices past nt were never written
+    unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
+    for (int s = 0; s < used; s++) {
+        const uint2 v = part[((long long)p * nslices + s) * a.out_stride + qi];
+        s2 = min(min(s2, v.y), max(b, v.x));
+        b = min(b, v.x);
     }
-    best_o[qi] = acc.x;
-    idx_o[qi] = acc.y;
-    second_o[qi] = acc.z;
+    const long long o = (long long)p * a.out_stride + qi;
+    best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
+    idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
+    second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
+}
+
+int top2_batch_slices(int npairs, int max_nq, int max_nt) {
+    const int qwaves = std::max(1, (max_nq + 63) / 64);
+    int ns = (8192 + npairs * qwaves - 1) / (npairs * qwaves);   // aim for >= 8192 wavefronts
+    ns = std::min(ns, std::max(1, (max_nt + 31) / 32));          // >= 32 trains per slice
+    return std::max(ns, 1);
+}
+
+hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq, int max_nt, int* d_best,
+                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream) {
+    if (npairs <= 0 || max_nq <= 0) return hipSuccess;
+    if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
+    Top2Batch a = a0;
+    const int ns = top2_batch_slices(npairs, max_nq, max_nt);
+    a.slice = std::max(1, (max_nt + ns - 1) / ns);
+    const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
+    hipLaunchKernelGGL(k_top2_batch, dim3((max_nq + 255) / 256, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best,
+                       d_best_idx, d_second);
+    if (nsu > 1)
+        hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,
+                           d_best, d_best_idx, d_second);
+    return hipGetLastError();
 }
 
 /* SearchForTriangulation inner loop (ORBmatcher.cc:712-761) for one (idx1, node) item per
@@ -214,25 +243,6 @@ hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, i
     if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_topk, dim3((nq + 3) / 4), dim3(256), 0, stream, d_q, nq, d_t, nt, d_ranges, d_cand_idx,
                        d_thr, k, d_dist, d_idx, d_nvalid);
-    return hipGetLastError();
-}
-
-int top2_slices(int nq, int nt) {
-    const int qblocks = (nq + 255) / 256;
-    int nslices = 1;
-    while (qblocks * nslices < 1024 && nt / (nslices * 2) >= 256) nslices *= 2;
-    return nslices;
-}
-
-hipError_t launch_hamming_top2(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int* d_best, int* d_best_idx,
-                               int* d_second, int4* d_part, hipStream_t stream) {
-    if (nq <= 0) return hipSuccess;
-    const int qblocks = (nq + 255) / 256;
-    const int nslices = top2_slices(nq, nt);
-    const int slice = (nt + nslices - 1) / nslices;
-    hipLaunchKernelGGL(k_top2_tiles, dim3(qblocks, nslices), dim3(256), 0, stream, d_q, nq, d_t, nt, slice, d_part);
-    hipLaunchKernelGGL(k_top2_merge, dim3(qblocks), dim3(256), 0, stream, d_part, nq, nslices, d_best, d_best_idx,
-                       d_second);
     return hipGetLastError();
 }
 

@@ -230,6 +230,8 @@ int Ctx::ensure_frames(int nframes) {
         set_error("device allocation for the extractor", e);
         return ORB_ERR_NOMEM;
     }
+    // the overflow flag is read by orb_sync even before the first extraction
+    if ((e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
     return ORB_OK;
 }
 

@@ -74,6 +74,7 @@ struct Ctx {
     size_t counts_cap = 0;
     void* h_pinned = nullptr;
 
+    std::vector<int2> frames_host;   // staging for orb_hamming_top2_frames_device pair lists
     // matcher scratch arena (bytes)
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;

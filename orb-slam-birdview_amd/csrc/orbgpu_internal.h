@@ -101,9 +101,23 @@ hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, i
                                const int* d_cand_idx, const int* d_thr, int k, int* d_dist, int* d_idx,
                                int* d_nvalid, hipStream_t stream);
 
-int top2_slices(int nq, int nt);   // train slices of the all-pairs top-2 (scratch = slices*nq int4)
-hipError_t launch_hamming_top2(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int* d_best,
-                               int* d_best_idx, int* d_second, int4* d_part, hipStream_t stream);
+
+// Batched all-pairs top-2 (k_top2_batch): pair p = (query frame frames[p].x, train frame frames[p].y)
+// of descriptor arrays q / t with q_stride / t_stride descriptors per frame; counts[frame] on the
+// device, or nq / nt for every pair when counts == NULL (frames == NULL: one pair, frame 0).
+struct Top2Batch {
+    const uint8_t* q;
+    const uint8_t* t;
+    long long q_stride, t_stride;
+    const int* counts;
+    int nq, nt;
+    const int2* frames;
+    int slice;
+    long long out_stride;   // outputs / partials of pair p at p * out_stride + query
+};
+int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
+hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
+                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream);
 
 struct TriParams {
     float F[9];

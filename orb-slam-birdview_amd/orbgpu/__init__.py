@@ -211,6 +211,13 @@ class BatchExtractor(_Ctx):
         check(lib().orb_stereo_batch_device(self.h, npairs, mb, mbf, d_uright, d_depth, d_nmatched),
               "orb_stereo_batch_device")
 
+    def hamming_top2_frames(self, q_frames, t_frames, d_best, d_idx, d_second):
+        """All-pairs top-2 between frames q_frames[p] and t_frames[p] of the last launch, one launch."""
+        qf = np.ascontiguousarray(q_frames, np.int32)
+        tf = np.ascontiguousarray(t_frames, np.int32)
+        check(lib().orb_hamming_top2_frames_device(self.h, self.d_desc, self.d_counts, self.kp_cap, len(qf), _p(qf),
+                                                   _p(tf), d_best, d_idx, d_second), "orb_hamming_top2_frames_device")
+
     def hamming_top2(self, d_q, nq, d_t, nt, d_best, d_idx, d_second):
         check(lib().orb_hamming_top2_device(self.h, d_q, nq, d_t, nt, d_best, d_idx, d_second),
               "orb_hamming_top2_device")

@@ -54,6 +54,7 @@ SIGNATURES = {
     "orb_descriptor_distance": (ci, [vp, vp]),
     "orb_hamming_topk": (ci, [vp, vp, ci, vp, ci, vp, vp, vp, ci, vp, vp, vp]),
     "orb_hamming_top2_device": (ci, [vp, vp, ci, vp, ci, vp, vp, vp]),
+    "orb_hamming_top2_frames_device": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, vp, vp]),
     "orb_search_by_bow_kf_f": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp, vp, OrbFeatVec, vp,
                                     ctypes.POINTER(ci)]),
     "orb_search_by_bow_kf_kf": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, OrbFeatVec, vp,

@@ -214,3 +214,65 @@ def test_window_match(orbgpu_mod, oracle_mod, frames, level0_only, window):
         on, om = oracle_mod.window_match(ratio, True, level0_only, da, ka, db, kb, off, cand)
         assert n == on and np.array_equal(mm, om)
         assert n > 20
+
+
+@pytest.mark.parametrize("nt", [1, 40, 700])
+def test_top2_device_small_train_sets(orbgpu_mod, nt):
+    """Edge sizes of the batched kernel: one train, a single slice, and a query count that is not a
+    multiple of 64 (partial last wavefront)."""
+    from orbgpu import _lib
+    rng = np.random.default_rng(nt)
+    nq = 77
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    b = orbgpu_mod.BatchExtractor(1000, 640, 480, 1)
+    L = _lib.lib()
+    dq, dt = b._alloc(q.nbytes), b._alloc(t.nbytes)
+    out = [b._alloc(nq * 4) for _ in range(3)]
+    L.orb_memcpy_h2d(b.h, dq, q.ctypes.data, q.nbytes)
+    L.orb_memcpy_h2d(b.h, dt, t.ctypes.data, t.nbytes)
+    b.hamming_top2(dq, nq, dt, nt, *out)
+    b.sync()
+    res = [np.zeros(nq, np.int32) for _ in range(3)]
+    for r, d in zip(res, out):
+        L.orb_memcpy_d2h(b.h, r.ctypes.data, d, nq * 4)
+    D = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    srt = np.sort(D, 1)
+    assert np.array_equal(res[0], srt[:, 0]) and np.array_equal(res[1], D.argmin(1))
+    assert np.array_equal(res[2], srt[:, 1] if nt > 1 else np.full(nq, 257))
+    for p in [dq, dt] + out:
+        L.orb_device_free(b.h, p)
+
+
+def test_top2_frames_batch_vs_numpy(orbgpu_mod):
+    """orb_hamming_top2_frames_device: many frame pairs of an extraction batch in one launch, counts
+    read on the device — vs numpy on the downloaded descriptors."""
+    from orbgpu import _lib
+    from orbgpu.synth import synth_batch
+    B = 6
+    bx = orbgpu_mod.BatchExtractor(1000, 640, 480, B)
+    bx.upload(synth_batch(640, 480, B, first=30))
+    bx.launch()
+    bx.sync()
+    cap = bx.kp_cap
+    qf, tf = [0, 1, 2, 3, 4, 5, 2], [1, 2, 3, 4, 5, 0, 2]
+    L = _lib.lib()
+    out = [bx._alloc(len(qf) * cap * 4) for _ in range(3)]
+    bx.hamming_top2_frames(qf, tf, *out)
+    bx.sync()
+    res = [np.zeros(len(qf) * cap, np.int32) for _ in range(3)]
+    for r, d in zip(res, out):
+        L.orb_memcpy_d2h(bx.h, r.ctypes.data, d, r.nbytes)
+    for p, (a, b) in enumerate(zip(qf, tf)):
+        _, da = bx.results(a)
+        _, db = bx.results(b)
+        D = np.unpackbits(da[:, None, :] ^ db[None, :, :], axis=2).sum(2)
+        srt = np.sort(D, 1)
+        n = len(da)
+        sl = slice(p * cap, p * cap + n)
+        assert np.array_equal(res[0][sl], srt[:, 0])
+        assert np.array_equal(res[1][sl], D.argmin(1))
+        assert np.array_equal(res[2][sl], srt[:, 1])
+    for d in out:
+        L.orb_device_free(bx.h, d)
+    bx.close()
