@@ -103,15 +103,20 @@ def algorithmic_bytes(w, h, kps_per_frame, cands_per_frame):
     }
 
 
-def read_pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (or None)."""
+PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
+
+
+def read_pmc(kernel):
+    """(HBM bytes per launch, VALU instructions per launch, source commit) of `kernel` from the
+    committed rocprofv3 PMC summary (tools/pmc.sh -> profiles/pmc_traffic.json), or Nones."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d["per_launch_bytes"].get(kernel)
     except Exception:
-        return None
+        return None, None, None
+    sq = d.get("sq_per_launch", {}).get(kernel, {})
+    return d.get("per_launch_bytes", {}).get(kernel), sq.get("SQ_INSTS_VALU"), d.get("commit")
 
 
 # ---------------------------------------------------------------- CPU baseline (oracle, rank 0, N=1)
@@ -158,6 +163,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hamming", action="store_true")
+    ap.add_argument("--no-stereo", action="store_true")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -235,13 +241,12 @@ def main():
         evals = evals_step * hs
         htmax, hevals = reduce_max_sum(dist, th1 - th0, evals)
         kt = hms[4] / 1e3 / max(hl[4], 1)
-        PEAK_VALU = 256 * 128 * 2.4e9   # lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
         ham = {"matches_per_s": round(hevals / htmax, 1),
                "queries_per_s": round(hevals / float(np.mean(counts)) / htmax, 1),
                "pair": f"frame f vs f+1 descriptors (~{int(np.mean(counts))} each), {pairs} pairs per launch",
                "kernel_avg_us": round(kt * 1e6, 2),
                "kernel_valu_ops_per_s": round(16.0 * evals_step / kt, 1) if kt > 0 else None,
-               "valu_frac": round(16.0 * evals_step / kt / PEAK_VALU, 4) if kt > 0 else None,
+               "valu_frac": round(16.0 * evals_step / kt / PEAK_VALU_LANE_OPS, 4) if kt > 0 else None,
                "kernel_hbm_gbs": round((32.0 * 2 * float(counts.sum()) + 12 * float(counts.sum())) / kt / 1e9, 2)
                if kt > 0 else None}
 
@@ -259,16 +264,65 @@ def main():
     dom_s = ms_per_step_k[dom] / 1e3
     achieved = dom_bytes / dom_s / 1e9
     launches_per_step = klaunch[KNAMES.index(dom)] / steps
-    traffic = read_pmc_traffic(dom)
+    traffic, valu_insts, pmc_commit = read_pmc(dom)
     sum_k_s = sum(ms_per_step_k.values()) / 1e3
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5),
                 "traffic": (round(traffic) if traffic is not None else None),   # HBM bytes per launch (PMC)
                 "algorithmic_bytes_per_frame": int(ab[dom]), "launches_per_step": launches_per_step,
                 "kernel_avg_launch_us": round(dom_s / launches_per_step * 1e6, 2),
+                # the kernel's real limiter is VALU issue: PMC SQ_INSTS_VALU x 64 lanes per launch / launch time
+                "valu": ({"achieved_lane_ops_per_s": round(valu_insts * 64 / (dom_s / launches_per_step), 1),
+                          "peak_lane_ops_per_s": PEAK_VALU_LANE_OPS,
+                          "frac": round(valu_insts * 64 / (dom_s / launches_per_step) / PEAK_VALU_LANE_OPS, 4),
+                          "valu_insts_per_launch": valu_insts, "pmc_commit": pmc_commit}
+                         if valu_insts else None),
                 "pipeline": {"bytes_per_frame": int(ab["pipeline"]),
                              "achieved": round(ab["pipeline"] * B / sum_k_s / 1e9, 2),
                              "frac": round(ab["pipeline"] * B / sum_k_s / 1e9 / PEAK_HBM_GBS, 5)}}
+
+    # ---- Frame::ComputeStereoMatches on the GPU (BASELINE C4's stereo leg): a
+    # separate batch of rectified synthetic pairs (frames 2p, 2p+1) extracted once, then the stereo
+    # kernels timed alone over all pairs per launch (pyramids and keypoints resident in HBM)
+    stereo = None
+    if not args.no_stereo:
+        from orbgpu.synth import synth_stereo_right
+        npairs = max(1, B // 4)
+        sf = []
+        for i in range(npairs):
+            left = frames[i]
+            sf += [left, synth_stereo_right(left, first + i)]
+        sx = orbgpu.BatchExtractor(nf, w, h, 2 * npairs, device=local)
+        sx.upload(np.stack(sf))
+        sx.launch()
+        sx.sync()
+        cap = sx.kp_cap
+        du, dd, dn = sx._alloc(npairs * cap * 4), sx._alloc(npairs * cap * 4), sx._alloc(npairs * 4)
+        mb, mbf = 0.54, 0.54 * 721.5   # KITTI-like baseline (m) and baseline * fx
+        sx.stereo(npairs, mb, mbf, du, dd, dn)
+        sx.sync()
+        sx.profile(True)
+        ss = max(2, args.steps)
+        barrier(dist)
+        ts0 = time.perf_counter()
+        for _ in range(ss):
+            sx.stereo(npairs, mb, mbf, du, dd, dn)
+        sx.sync()
+        ts1 = time.perf_counter()
+        sms, sl = sx.profile_read()
+        sx.profile(False)
+        nmatched = np.zeros(npairs, np.int32)
+        orbgpu._lib.check(orbgpu._lib.lib().orb_memcpy_d2h(sx.h, nmatched.ctypes.data, dn, nmatched.nbytes))
+        stmax, spairs = reduce_max_sum(dist, ts1 - ts0, float(npairs * ss))
+        st_k = sms[5] / 1e3 / max(sl[5], 1)
+        stereo = {"pairs_per_s": round(spairs / stmax, 1), "pairs_per_launch": npairs,
+                  "kernel_avg_us": round(st_k * 1e6, 2),
+                  "left_keypoints_with_depth_per_pair": round(float(nmatched.mean()), 1),
+                  "note": "stereo kernels only (k_stereo + k_stereo_cut), inputs resident; "
+                          "synthetic rectified pairs, disparity 0-64 px per 16-row band"}
+        for ptr in (du, dd, dn):
+            orbgpu._lib.lib().orb_device_free(sx.h, ptr)
+        sx.close()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -285,7 +339,7 @@ def main():
                "frames_per_s": round(total_frames / tmax, 1),
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
-               "roofline": roofline, "cpu_baseline": cpu, "hamming": ham}
+               "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo}
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)

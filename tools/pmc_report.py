@@ -19,8 +19,9 @@ import re
 import sys
 from collections import defaultdict
 
-SHORT = {"k_fast": "fast", "k_resize": "resize", "k_octree": "octree", "k_describe": "describe",
-         "k_top2_tiles": "hamming", "k_top2_merge": "hamming_merge", "k_calib_read_u8": "calib_read_u8",
+SHORT = {"k_fast": "fast", "k_fast_wave": "fast", "k_resize": "resize", "k_resize_tiled": "resize",
+         "k_octree": "octree", "k_describe": "describe", "k_top2_batch": "hamming", "k_top2b_merge": "hamming_merge",
+         "k_stereo": "stereo", "k_stereo_cut": "stereo_cut", "k_calib_read_u8": "calib_read_u8",
          "k_calib_read_u32": "calib_read_u32", "k_calib_read_u128": "calib_read_u128",
          "k_calib_write_u32": "calib_write_u32"}
 
@@ -84,6 +85,18 @@ def main():
         wb = sum(bw.get(k, [0])) / max(1, len(bw.get(k, []))) * 1024
         out["raw_bytes_per_launch"][k] = {"fetch": fb, "write": wb, "dispatches": len(bf.get(k, []))}
         out["per_launch_bytes"][k] = fb * rf + wb * wf
+    # SQ issue counters per launch (VALU roofline; SQ_*_CYCLES are quad-cycles)
+    out["sq_per_launch"] = {}
+    for fn in glob.glob(os.path.join(root, "bench_SQ", "**", "*counter_collection*.csv"), recursive=True):
+        acc = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                k = short_name(row.get("Kernel_Name", ""))
+                if k is None:
+                    continue
+                acc[k][row["Counter_Name"]][row.get("Dispatch_Id", "0")] += float(row["Counter_Value"])
+        for k, cs in acc.items():
+            out["sq_per_launch"][k] = {c: sum(d.values()) / len(d) for c, d in cs.items()}
     print(json.dumps(out, indent=1))
 
 
