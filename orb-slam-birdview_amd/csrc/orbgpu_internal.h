@@ -146,8 +146,9 @@ struct StereoSide {
     const int* counts;         // counts[frame]
     long long kp_stride;
 };
+size_t stereo_scratch_ints(const Geom& g, int npairs, long long out_stride);
 hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L, const StereoSide& R, int npairs,
-                         float mb, float mbf, float* d_uright, float* d_depth, int* d_sad, long long out_stride,
+                         float mb, float mbf, float* d_uright, float* d_depth, int* d_scratch, long long out_stride,
                          int* d_nmatched, hipStream_t stream);
 
 size_t octree_lds_bytes(int node_cap);

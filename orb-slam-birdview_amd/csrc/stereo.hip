@@ -41,11 +41,73 @@ __device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, cons
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// Exclusive scan of one int per thread over a 256-thread block; s_w holds 4 wave totals.
+__device__ __forceinline__ int block256_scan(int v, int* s_w, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        before += w < wave ? s_w[w] : 0;
+        total += s_w[w];
+    }
+    __syncthreads();
+    return before + x - v;
+}
+
 }  // namespace
+
+// Right keypoints bucketed by image row (counting sort in LDS, one workgroup per pair): the
+// descriptor search of a left keypoint then visits only the rows its band can reach instead of
+// every right keypoint.  Order inside a row is irrelevant (the search minimises dist << 16 | iR).
+__global__ __launch_bounds__(256) void k_stereo_bucket(const Geom* __restrict__ g, StereoSide R,
+                                                       int* __restrict__ rows, int* __restrict__ sorted,
+                                                       long long row_stride, long long out_stride) {
+    extern __shared__ int s_hist[];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int fR = R.frame0 + p * R.frame_step;
+    const int nR = R.counts[fR], H = g->L[0].h;
+    const orb_keypoint* kR = R.kps + (long long)fR * R.kp_stride;
+    int* rs = rows + (long long)p * row_stride;
+    int* srt = sorted + (long long)p * out_stride;
+    for (int i = tid; i <= H; i += 256) s_hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < nR; i += 256) atomicAdd(&s_hist[min(max((int)floorf(kR[i].y), 0), H - 1)], 1);
+    __syncthreads();
+    {   // exclusive scan over the H + 1 rows: a contiguous chunk per thread
+        __shared__ int s_w[4];
+        const int chunk = (H + 1 + 255) / 256, r0 = min(tid * chunk, H + 1), r1 = min(r0 + chunk, H + 1);
+        int local = 0;
+        for (int r = r0; r < r1; r++) local += s_hist[r];
+        int total;
+        int acc = block256_scan(local, s_w, total);
+        for (int r = r0; r < r1; r++) {
+            const int v = s_hist[r];
+            s_hist[r] = acc;
+            rs[r] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nR; i += 256) {
+        const int r = min(max((int)floorf(kR[i].y), 0), H - 1);
+        srt[atomicAdd(&s_hist[r], 1)] = i;
+    }
+}
 
 __global__ __launch_bounds__(256) void k_stereo(const Geom* __restrict__ g, StereoSide L, StereoSide R, float mb,
                                                 float mbf, float* __restrict__ uright, float* __restrict__ depth,
-                                                int* __restrict__ sad, long long out_stride) {
+                                                int* __restrict__ sad, long long out_stride,
+                                                const int* __restrict__ rows, const int* __restrict__ sorted,
+                                                long long row_stride) {
     __shared__ int s_part[4][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int p = blockIdx.y;
@@ -67,7 +129,15 @@ __global__ __launch_bounds__(256) void k_stereo(const Geom* __restrict__ g, Ster
     // ---- descriptor search over the right keypoints whose row band covers yL (:676-689, :716-745)
     unsigned best = 0xFFFFFFFFu;   // dist << 16 | iR: the first minimum in iR order
     if (maxU >= 0) {
-        for (int iR = lane; iR < nR; iR += 64) {
+        // a right keypoint reaches rows [floor(y - r), ceil(y + r)], r = 2 * scale <= 2 * scale_max
+        const int reach = (int)ceilf(2.0f * g->L[g->nlevels - 1].scale) + 1;
+        const int H = g->L[0].h;
+        const int* rs = rows + (long long)p * row_stride;
+        const int c0 = rs[max(yL - reach, 0)], c1 = rs[min(yL + reach, H - 1) + 1];
+        const int* srt = sorted + (long long)p * out_stride;
+        (void)nR;
+        for (int c = c0 + lane; c < c1; c += 64) {
+            const int iR = srt[c];
             const orb_keypoint kr = kR[iR];
             const float r = 2.0f * g->L[kr.octave].scale;
             const int maxr = (int)ceilf(kr.y + r), minr = (int)floorf(kr.y - r);
@@ -162,51 +232,60 @@ __global__ __launch_bounds__(256) void k_stereo(const Geom* __restrict__ g, Ster
     }
 }
 
-// Median cut (:822-835): sort the accepted window distances (bitonic, LDS), thDist =
-// 1.5f*1.4f*median, reject every accepted keypoint whose distance is >= thDist.
+// Median cut (:822-835): the median of the accepted window distances (values < 2^16: 121 * 510
+// at most) by a two-pass 8-bit radix select, thDist = 1.5f*1.4f*median, and every accepted
+// keypoint whose distance is >= thDist rejected.  vDistIdx is sorted by (dist, iL), so its element
+// cnt/2 has the (cnt/2)-th smallest distance — which is all the cut uses.
 __global__ __launch_bounds__(256) void k_stereo_cut(StereoSide L, float* __restrict__ uright,
-                                                    float* __restrict__ depth, int* __restrict__ sad,
-                                                    long long out_stride, int np2, int* __restrict__ nmatched) {
-    extern __shared__ int s_keys[];
-    __shared__ int s_cnt, s_kept;
+                                                    float* __restrict__ depth, const int* __restrict__ sad,
+                                                    long long out_stride, int* __restrict__ nmatched) {
+    __shared__ int s_hist[256];
+    __shared__ int s_w[4];
+    __shared__ int s_sel[2];
+    __shared__ int s_kept;
     const int p = blockIdx.x, tid = threadIdx.x;
     const int nL = L.counts[L.frame0 + p * L.frame_step];
     float* ur = uright + (long long)p * out_stride;
     float* dp = depth + (long long)p * out_stride;
-    int* sd = sad + (long long)p * out_stride;
-    if (tid == 0) {
-        s_cnt = 0;
-        s_kept = 0;
-    }
-    for (int i = tid; i < np2; i += 256) s_keys[i] = INT_MAX;
-    __syncthreads();
-    for (int i = tid; i < nL; i += 256) {
-        const int v = sd[i];
-        if (v >= 0) s_keys[atomicAdd(&s_cnt, 1)] = v;
-    }
-    __syncthreads();
-    const int cnt = s_cnt;
-    if (cnt == 0) {   // (the reference reads vDistIdx[0] of an empty vector)
-        if (tid == 0) nmatched[p] = 0;
-        return;
-    }
-    for (int k = 2; k <= np2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < np2; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const int a = s_keys[i], b = s_keys[ixj];
-                    const bool up = (i & k) == 0;
-                    if (up ? a > b : a < b) {
-                        s_keys[i] = b;
-                        s_keys[ixj] = a;
-                    }
-                }
-            }
-            __syncthreads();
+    const int* sd = sad + (long long)p * out_stride;
+    int cnt = 0, hi = 0, k = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        s_hist[tid] = 0;
+        if (tid == 0) s_kept = 0;
+        __syncthreads();
+        int mine = 0;
+        for (int i = tid; i < nL; i += 256) {
+            const int v = sd[i];
+            if (v < 0 || (pass == 1 && (v >> 8) != hi)) continue;
+            atomicAdd(&s_hist[pass == 0 ? (v >> 8) & 255 : v & 255], 1);
+            mine++;
         }
-    const float median = (float)s_keys[cnt / 2];
+        if (mine) atomicAdd(&s_kept, mine);
+        __syncthreads();
+        if (pass == 0) {
+            cnt = s_kept;
+            if (cnt == 0) {   // (the reference reads vDistIdx[0] of an empty vector)
+                if (tid == 0) nmatched[p] = 0;
+                return;
+            }
+            k = cnt / 2;
+        }
+        const int hcount = s_hist[tid];
+        int total;
+        const int before = block256_scan(hcount, s_w, total);
+        if (before <= k && k < before + hcount) {
+            s_sel[0] = tid;
+            s_sel[1] = k - before;
+        }
+        __syncthreads();
+        if (pass == 0) hi = s_sel[0];
+        k = s_sel[1];
+        __syncthreads();
+    }
+    const float median = (float)((hi << 8) | s_sel[0]);
     const float thDist = 1.5f * 1.4f * median;
+    if (tid == 0) s_kept = 0;
+    __syncthreads();
     int kept = 0;
     for (int i = tid; i < nL; i += 256) {
         const int v = sd[i];
@@ -223,18 +302,26 @@ __global__ __launch_bounds__(256) void k_stereo_cut(StereoSide L, float* __restr
     if (tid == 0) nmatched[p] = s_kept;
 }
 
+size_t stereo_scratch_ints(const Geom& g, int npairs, long long out_stride) {
+    return (size_t)npairs * ((size_t)out_stride * 2 + g.L[0].h + 2);   // sad + sorted + row offsets
+}
+
 hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L, const StereoSide& R, int npairs,
-                         float mb, float mbf, float* d_uright, float* d_depth, int* d_sad, long long out_stride,
+                         float mb, float mbf, float* d_uright, float* d_depth, int* d_scratch, long long out_stride,
                          int* d_nmatched, hipStream_t stream) {
     if (npairs <= 0) return hipSuccess;
     const int cap = (int)out_stride;
+    const long long row_stride = g.L[0].h + 2;
+    int* d_sad = d_scratch;
+    int* d_sorted = d_sad + (size_t)npairs * out_stride;
+    int* d_rows = d_sorted + (size_t)npairs * out_stride;
+    if ((size_t)(g.L[0].h + 1) * 4 > 64 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_stereo_bucket, dim3(npairs), dim3(256), (size_t)(g.L[0].h + 1) * 4, stream, d_geom, R, d_rows,
+                       d_sorted, row_stride, out_stride);
     hipLaunchKernelGGL(k_stereo, dim3((cap + 3) / 4, npairs), dim3(256), 0, stream, d_geom, L, R, mb, mbf, d_uright,
-                       d_depth, d_sad, out_stride);
-    int np2 = 1;
-    while (np2 < cap) np2 <<= 1;
-    if ((size_t)np2 * 4 > 64 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_stereo_cut, dim3(npairs), dim3(256), (size_t)np2 * 4, stream, L, d_uright, d_depth, d_sad,
-                       out_stride, np2, d_nmatched);
+                       d_depth, d_sad, out_stride, d_rows, d_sorted, row_stride);
+    hipLaunchKernelGGL(k_stereo_cut, dim3(npairs), dim3(256), 0, stream, L, d_uright, d_depth, d_sad, out_stride,
+                       d_nmatched);
     (void)g;
     return hipGetLastError();
 }
@@ -289,8 +376,10 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     const int cap = std::max(nL, 1);
     const size_t A = 256;
     auto al = [&](size_t x) { return (x + A - 1) & ~(A - 1); };
+    const int scap = std::max(cap, nR);   // slots: sad (left) and sorted right indices share one stride
     const size_t need = al((size_t)nL * 28) + al((size_t)nL * 32) + al((size_t)std::max(nR, 1) * 28) +
-                        al((size_t)std::max(nR, 1) * 32) + al(16) + 3 * al((size_t)cap * 4) + al(4) + A;
+                        al((size_t)std::max(nR, 1) * 32) + al(16) + 2 * al((size_t)cap * 4) +
+                        al(stereo_scratch_ints(cl->geom, 1, scap) * 4) + al(4) + A;
     if (need > cl->scratch_cap || !cl->d_scratch) {
         if (cl->d_scratch) (void)hipFree(cl->d_scratch);
         cl->d_scratch = nullptr;
@@ -311,7 +400,7 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     int* d_cnt = (int*)take(16);
     float* d_u = (float*)take((size_t)cap * 4);
     float* d_d = (float*)take((size_t)cap * 4);
-    int* d_s = (int*)take((size_t)cap * 4);
+    int* d_s = (int*)take(stereo_scratch_ints(cl->geom, 1, scap) * 4);
     int* d_nm = (int*)take(4);
     const int cnt[2] = {nL, nR};
     if ((e = hipMemcpyAsync(d_kL, kpsL, (size_t)nL * 28, hipMemcpyHostToDevice, cl->stream)) != hipSuccess ||
@@ -323,7 +412,7 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     StereoSide SL{cl->last_frames, cl->last_frame_pitch, cl->last_row_stride, cl->d_pyr, 0, 0, d_kL, d_dL, d_cnt, 0};
     StereoSide SR{cr->last_frames, cr->last_frame_pitch, cr->last_row_stride, cr->d_pyr, 0, 0, d_kR, d_dR, d_cnt + 1, 0};
     if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 1, cl->stream);
-    e = launch_stereo(cl->d_geom, cl->geom, SL, SR, 1, mb, mbf, d_u, d_d, d_s, cap, d_nm, cl->stream);
+    e = launch_stereo(cl->d_geom, cl->geom, SL, SR, 1, mb, mbf, d_u, d_d, d_s, scap, d_nm, cl->stream);
     if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 0, cl->stream);
     if (e != hipSuccess) return set_error("stereo kernels", e), ORB_ERR_HIP;
     int nm = 0;
@@ -346,7 +435,7 @@ int orb_stereo_batch_device(orb_ctx* h, int npairs, float mb, float mbf, float* 
         return set_error("orb_stereo_batch_device: the last batch holds fewer than 2*npairs frames", hipSuccess),
                ORB_ERR_ARG;
     const int cap = c->last_kp_cap;
-    const size_t need = (size_t)npairs * cap * 4 + 256;
+    const size_t need = stereo_scratch_ints(c->geom, npairs, cap) * 4 + 256;
     hipError_t e;
     if (need > c->scratch_cap || !c->d_scratch) {
         if (c->d_scratch) (void)hipFree(c->d_scratch);
