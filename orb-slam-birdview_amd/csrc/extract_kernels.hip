@@ -743,12 +743,13 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
                                                            uint32_t* __restrict__ keysAll,
                                                            uint16_t* __restrict__ knodeAll,
                                                            uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
-                                                           int* __restrict__ err) {
+                                                           int* __restrict__ err, int lds_keys) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int NC = g->node_cap;
     const int tid = threadIdx.x;
     constexpr int NT = kOctreeThreads;
-    const int l = blockIdx.x, f = blockIdx.y;
+    // frames along x so that every frame's level-0 block (the longest) is dispatched first
+    const int f = blockIdx.x, l = blockIdx.y;
     const LevelGeom& L = g->L[l];
     // LDS carve: A table, B table (also the sort buffer), quad, rank, info, ord, nchr, scalars.
     uint32_t* rxA = (uint32_t*)smem;
@@ -770,14 +771,29 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
     int NC2 = 1;
     while (NC2 < NC) NC2 <<= 1;
 
-    uint32_t* keys = keysAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
-    uint16_t* knode = knodeAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
     uint32_t* outK = lvlKps + (long long)f * g->nkpcap + L.kp_base;
 
-    // 1. gather candidates in cell order (vToDistributeKeys, :818-825)
+    // 1. gather candidates in cell order (vToDistributeKeys, :818-825).  The keys and their node
+    // indices live in LDS after the node tables when they fit (every round re-reads them), else in
+    // the per-level global scratch.
     const int ncl = L.nCols * L.nRows;
     const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
     const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
+    int Ctot = 0;
+    {
+        int mine = 0;
+        for (int c = tid; c < ncl; c += NT) mine += cc[c];
+        (void)block_excl_scan(mine, sc, Ctot);
+    }
+    uint32_t* keys;
+    uint16_t* knode;
+    if (Ctot <= lds_keys) {
+        keys = reinterpret_cast<uint32_t*>(sv + 8);
+        knode = reinterpret_cast<uint16_t*>(keys + lds_keys);
+    } else {
+        keys = keysAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
+        knode = knodeAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
+    }
     int C = 0;
     for (int c0 = 0; c0 < ncl; c0 += NT) {
         const int c = c0 + tid;
@@ -1295,6 +1311,13 @@ static inline unsigned cdiv(unsigned a, unsigned b) { return (a + b - 1) / b; }
 
 size_t octree_lds_bytes(int node_cap) { return (size_t)node_cap * (16 * 4) + (32 + 8) * 4; }
 
+// Keys (u32 + u16 node index) that fit in LDS after the node tables with the block at <= 78 KiB, so
+// that two octree workgroups share a CU.
+static int octree_lds_keys(int node_cap) {
+    const long long room = 78 * 1024 - (long long)octree_lds_bytes(node_cap);
+    return room > 0 ? (int)((room / 6) & ~7LL) : 0;
+}
+
 hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                           int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
@@ -1327,9 +1350,12 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                            b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
     if (marker) marker(user, ORB_K_FAST, 0, stream);
     if (marker) marker(user, ORB_K_OCTREE, 1, stream);
-    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, nframes), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap),
-                       stream, b.d_geom, b.d_cands, b.d_cellCount, b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount,
-                       b.d_err);
+    {
+        const int lk = octree_lds_keys(g.node_cap);
+        hipLaunchKernelGGL(k_octree, dim3(nframes, g.nlevels), dim3(kOctreeThreads),
+                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, stream, b.d_geom, b.d_cands, b.d_cellCount,
+                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk);
+    }
     if (marker) marker(user, ORB_K_OCTREE, 0, stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
     hipLaunchKernelGGL(k_describe, dim3(cdiv(g.nkpcap, 4), nframes), dim3(256), 0, stream, b.d_geom, d_frames,
