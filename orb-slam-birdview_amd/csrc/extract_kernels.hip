@@ -122,11 +122,12 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
  * (byte loads if the level base/stride is not dword aligned), the coefficients of the tile's
  * columns/rows are staged once, and each thread then produces 4 output pixels per row pass
  * (one dword store) from LDS byte reads. */
+template <int kRsTileH>
 __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
                                                       const ResizeCoef* __restrict__ coef, int level,
                                                       const uint8_t* __restrict__ frames, long long framePitch,
                                                       int rowStride, uint8_t* __restrict__ pyr) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[kRsRows * kRsPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[rs_rows(kRsTileH) * kRsPitch];
     __shared__ int4 s_cx[kRsTileW];
     __shared__ int4 s_cy[kRsTileH];
     const int f = blockIdx.z;
@@ -138,9 +139,10 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
     if (tid < kRsTileW) {
         const ResizeCoef c = coef[x0 + min(tid, nx - 1)];
         s_cx[tid] = make_int4(c.s0, c.s1, c.c0, c.c1);
-    } else if (tid < kRsTileW + kRsTileH) {
-        const ResizeCoef c = coef[dw + y0 + min(tid - kRsTileW, ny - 1)];
-        s_cy[tid - kRsTileW] = make_int4(c.s0, c.s1, c.c0, c.c1);
+    }
+    for (int i = tid; i < kRsTileH; i += 256) {
+        const ResizeCoef c = coef[dw + y0 + min(i, ny - 1)];
+        s_cy[i] = make_int4(c.s0, c.s1, c.c0, c.c1);
     }
     // source span (the coefficient tables are monotone)
     const int sx0 = coef[x0].s0 & ~3, sx1 = coef[x0 + nx - 1].s1;
@@ -1324,10 +1326,24 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     if (nframes <= 0) return hipSuccess;
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);
     for (int l = 1; l < g.nlevels; l++) {
-        if (g.L[l].rs_tiled && !b.resize_direct) {
-            dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, kRsTileH), nframes);
-            hipLaunchKernelGGL(k_resize_tiled, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,
-                               d_frames, frame_pitch, row_stride, b.d_pyr);
+        const int t = g.L[l].rs_tiled;
+        const int want = b.resize_th >= 64 ? 2 : b.resize_th >= 32 ? 1 : 0;
+        int sel = -1;
+        for (int i = want; i >= 0 && sel < 0; i--)
+            if (t & (1 << i)) sel = i;
+        if (sel >= 0 && !b.resize_direct) {
+            const int th = 16 << sel;
+            dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
+            const ResizeCoef* cf = b.d_rcoef + b.rcoef_off[l];
+            if (sel == 2)
+                hipLaunchKernelGGL(k_resize_tiled<64>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames,
+                                   frame_pitch, row_stride, b.d_pyr);
+            else if (sel == 1)
+                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames,
+                                   frame_pitch, row_stride, b.d_pyr);
+            else
+                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames,
+                                   frame_pitch, row_stride, b.d_pyr);
         } else {
             dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
             hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,

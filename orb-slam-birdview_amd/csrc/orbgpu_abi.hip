@@ -122,19 +122,24 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
             rcoef_off[l] = (int)coefs.size();
             resize_coefs(g.L[l - 1].w, L.w, coefs, false);
             resize_coefs(g.L[l - 1].h, L.h, coefs, true);
-            // k_resize_tiled stages each tile's source span in a fixed LDS tile: check it fits
+            // k_resize_tiled<TH> stages each tile's source span in a fixed LDS tile: check it fits
             const ResizeCoef* cx = &coefs[rcoef_off[l]];
             const ResizeCoef* cy = cx + L.w;
-            bool fits = true;
-            for (int x0 = 0; x0 < L.w && fits; x0 += kRsTileW) {
+            bool xfits = true;
+            for (int x0 = 0; x0 < L.w && xfits; x0 += kRsTileW) {
                 const int x1 = std::min(x0 + kRsTileW, L.w) - 1;
-                fits = cx[x1].s1 - (cx[x0].s0 & ~3) + 1 <= kRsPitch - 4;
+                xfits = cx[x1].s1 - (cx[x0].s0 & ~3) + 1 <= kRsPitch - 4;
             }
-            for (int y0 = 0; y0 < L.h && fits; y0 += kRsTileH) {
-                const int y1 = std::min(y0 + kRsTileH, L.h) - 1;
-                fits = cy[y1].s1 - cy[y0].s0 + 1 <= kRsRows;
+            L.rs_tiled = 0;
+            for (int i = 0; i < 3 && xfits; i++) {
+                const int th = 16 << i;
+                bool fits = true;
+                for (int y0 = 0; y0 < L.h && fits; y0 += th) {
+                    const int y1 = std::min(y0 + th, L.h) - 1;
+                    fits = cy[y1].s1 - cy[y0].s0 + 1 <= rs_rows(th);
+                }
+                if (fits) L.rs_tiled |= 1 << i;
             }
-            L.rs_tiled = fits ? 1 : 0;
         }
         L.maxBX = L.w - kEdgeThreshold + 3;
         L.maxBY = L.h - kEdgeThreshold + 3;
@@ -250,6 +255,7 @@ ExtractBuffers Ctx::buffers() const {
     b.d_err = d_err;
     b.fast_remap = fast_remap ? 1 : 0;
     b.resize_direct = resize_direct ? 1 : 0;
+    b.resize_th = resize_th;
     b.fast_block = fast_block ? 1 : 0;
     return b;
 }
@@ -360,6 +366,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         c->num_cu = 256;
     if (const char* e = std::getenv("ORBGPU_FAST_REMAP")) c->fast_remap = e[0] == '1';
     if (const char* e = std::getenv("ORBGPU_RESIZE_DIRECT")) c->resize_direct = e[0] == '1';
+    if (const char* e = std::getenv("ORBGPU_RESIZE_TH")) c->resize_th = std::atoi(e);
     if (const char* e = std::getenv("ORBGPU_FAST_BLOCK")) c->fast_block = e[0] == '1';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;

@@ -20,6 +20,7 @@ struct Ctx {
     int num_cu = 256;
     bool fast_remap = true;   // ORBGPU_FAST_REMAP=0 disables the XCD-contiguous cell remap (A/B switch)
     bool resize_direct = false;   // ORBGPU_RESIZE_DIRECT=1 forces the untiled resize kernel (A/B switch)
+    int resize_th = 16;           // rows per resize tile (ORBGPU_RESIZE_TH = 16 | 32 | 64; 16 measured fastest)
     bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
     hipStream_t stream = nullptr;
     // a batch of frames is split over `nsub` streams so that one sub-batch's low-occupancy phases

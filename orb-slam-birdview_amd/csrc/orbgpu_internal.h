@@ -20,16 +20,15 @@ constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as 
 constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
 constexpr int kRtPitch = 50;          // k_describe row-pass sums, u16 per transposed row
-constexpr int kRsTileW = 128;         // k_resize_tiled: output tile 128 x 16, 4 px per thread
-constexpr int kRsTileH = 16;
-constexpr int kRsPitch = 272;         // LDS source tile: up to 268 bytes x 40 rows (scale factors <= 2)
-constexpr int kRsRows = 40;
+constexpr int kRsTileW = 128;         // k_resize_tiled<TH>: output tile 128 x TH, 4 px per thread
+constexpr int kRsPitch = 272;         // LDS source tile: up to 268 bytes x (2*TH + 8) rows (scale factors <= 2)
+constexpr int rs_rows(int th) { return 2 * th + 8; }
 
 // Per-level geometry (host-computed once per image size; lives in device memory).
 struct LevelGeom {
     int w, h;            // level size (ComputePyramid, ORBextractor.cc:1112)
     int pitch;           // row pitch of the stored level (levels >= 1)
-    int rs_tiled;        // k_resize_tiled's LDS tile holds every source span of this level (else k_resize)
+    int rs_tiled;        // bit i: k_resize_tiled<16 << i>'s LDS tile holds every source span (else k_resize)
     long long pyr_off;   // byte offset of the level inside a frame's pyramid slot (levels >= 1)
     int maxBX, maxBY;    // maxBorderX/Y (:775-776)
     int nCols, nRows, wCell, hCell;   // cell grid (:781-787)
@@ -86,6 +85,7 @@ struct ExtractBuffers {
     int* d_err;                    // 1 int: internal overflow flag
     int fast_remap;                // XCD-contiguous block->cell remap in k_fast (speed only)
     int resize_direct;             // force the untiled k_resize (A/B switch, ORBGPU_RESIZE_DIRECT=1)
+    int resize_th;                 // output rows per k_resize_tiled tile: 16, 32 or 64 (ORBGPU_RESIZE_TH)
     int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
 };
 
