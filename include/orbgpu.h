@@ -218,6 +218,36 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
 int orb_stereo_batch_device(orb_ctx* ctx, int npairs, float mb, float mbf, float* d_uright, float* d_depth,
                             int* d_nmatched);
 
+/* ======================= DBoW2 vocabulary transform ======================= */
+
+typedef struct orb_vocab orb_vocab;
+
+/* TemplatedVocabulary::loadFromBinaryFile (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1466-1510)
+ * of an ORB vocabulary (ORBvoc.bin format: header nb_nodes, size_node = 41, k, L, scoring,
+ * weighting; records parent:int32 | desc[32] | weight:float | isLeaf:u8), onto ctx's device. */
+int  orb_vocab_load(orb_ctx* ctx, const char* path, orb_vocab** out);
+void orb_vocab_destroy(orb_vocab* v);
+int  orb_vocab_info(const orb_vocab* v, int* k, int* L, int* scoring, int* weighting, int* nnodes, int* nwords);
+
+/* Per-feature part of TemplatedVocabulary::transform (:1240-1277): word id, word weight and the node
+ * `levelsup` levels above the leaf (FeatureVector key) of each of n descriptors, on the GPU.  Host
+ * pointers, synchronous. */
+int orb_vocab_transform(orb_ctx* ctx, const orb_vocab* v, const uint8_t* desc, int n, int levelsup, int* word_id,
+                        float* weight, uint32_t* node_id);
+
+/* Same for frames 0..nframes-1 of the last orb_extract_batch_device on ctx: outputs at
+ * [f * kp_cap + i] (device pointers), counts from that batch.  Asynchronous. */
+int orb_vocab_transform_batch_device(orb_ctx* ctx, const orb_vocab* v, int nframes, int levelsup, int* d_word,
+                                     float* d_weight, uint32_t* d_node);
+
+/* Host assembly of TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup)
+ * (:1139-1210) from the per-feature triples, in feature order: BowVector as nbow (word, value)
+ * pairs ascending by word; FeatureVector as nfv nodes ascending with CSR fv_off (nfv+1) / fv_idx.
+ * Every output array needs room for n entries (fv_off n+1). */
+int orb_vocab_bow(const orb_vocab* v, int n, const int* word_id, const float* weight, const uint32_t* node_id,
+                  int* bow_words, double* bow_values, int* nbow, uint32_t* fv_nodes, int* fv_off, int* fv_idx,
+                  int* nfv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,12 @@ def lib():
         L.oracle_window_match.argtypes = [cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp]
         L.oracle_features_in_area.argtypes = [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]
         L.oracle_stereo_matches.argtypes = [vp, vp, ci, vp, vp, ci, vp, vp, cf, cf, vp, vp]
+        L.oracle_vocab_load.restype = vp
+        L.oracle_vocab_load.argtypes = [ctypes.c_char_p]
+        L.oracle_vocab_destroy.argtypes = [vp]
+        L.oracle_vocab_info.argtypes = [vp] * 7
+        L.oracle_vocab_transform_each.argtypes = [vp, vp, ci, ci, vp, vp, vp]
+        L.oracle_vocab_transform.argtypes = [vp, vp, ci, ci, vp, vp, vp, vp, vp, vp, vp]
         _LIB = L
     return _LIB
 
@@ -280,3 +286,43 @@ def stereo_matches(left, right, kpsL, descL, kpsR, descR, mb, mbf):
     n = lib().oracle_stereo_matches(left.h, right.h, len(kl), _p(kl), _p(dl), len(kr), _p(kr), _p(dr), mb, mbf,
                                     _p(u), _p(d))
     return u[:len(kl)], d[:len(kl)], n
+
+
+class OracleVocabulary:
+    """Restated DBoW2 vocabulary: loadFromBinaryFile + transform (TemplatedVocabulary.h)."""
+
+    def __init__(self, path):
+        self.h = lib().oracle_vocab_load(path.encode())
+        assert self.h, path
+        vals = [ctypes.c_int() for _ in range(6)]
+        lib().oracle_vocab_info(self.h, *[ctypes.byref(x) for x in vals])
+        self.k, self.L, self.scoring, self.weighting, self.nnodes, self.nwords = [x.value for x in vals]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_vocab_destroy(self.h)
+            self.h = None
+
+    def transform_each(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        w = np.zeros(max(n, 1), np.int32)
+        wt = np.zeros(max(n, 1), np.float64)
+        nd = np.zeros(max(n, 1), np.uint32)
+        lib().oracle_vocab_transform_each(self.h, _p(d), n, levelsup, _p(w), _p(wt), _p(nd))
+        return w[:n], wt[:n], nd[:n]
+
+    def transform(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        bw = np.zeros(max(n, 1), np.int32)
+        bv = np.zeros(max(n, 1), np.float64)
+        fn = np.zeros(max(n, 1), np.uint32)
+        fo = np.zeros(n + 1, np.int32)
+        fi = np.zeros(max(n, 1), np.int32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        lib().oracle_vocab_transform(self.h, _p(d), n, levelsup, _p(bw), _p(bv), ctypes.byref(nb), _p(fn), _p(fo),
+                                     _p(fi), ctypes.byref(nf))
+        bow = {int(bw[i]): float(bv[i]) for i in range(nb.value)}
+        fv = {int(fn[j]): fi[fo[j]:fo[j + 1]].tolist() for j in range(nf.value)}
+        return bow, fv

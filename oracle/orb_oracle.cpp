@@ -13,6 +13,8 @@
 #include <cmath>
 #include <cstring>
 #include <list>
+#include <map>
+#include <cstdio>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -1199,6 +1201,162 @@ int oracle_stereo_matches(void* left, void* right, int N, const OracleKeyPoint* 
         nvalid--;
     }
     return nvalid;
+}
+
+/* ---------------- DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary.h:32) ----------------
+ * loadFromBinaryFile  Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1466-1510 (including its
+ * while(!f.eof()) quirk: the last record is read twice, adding a duplicate last child that can never
+ * win a strict '<' descent), transform(feature, ...)  :1240-1277, transform(features, BowVector&,
+ * FeatureVector&, levelsup)  :1139-1210, BowVector::addWeight/addIfNotExist/normalize
+ * (BowVector.cpp:34-86), FeatureVector::addFeature (FeatureVector.cpp:31-45). */
+struct OVNode {
+    int parent = 0;
+    std::vector<int> children;
+    uint8_t desc[32] = {0};
+    double weight = 0;
+    int word_id = -1;
+    bool isLeaf() const { return children.empty(); }
+};
+struct OVocab {
+    int k = 0, L = 0, scoring = 0, weighting = 0;
+    std::vector<OVNode> nodes;
+    int nwords = 0;
+};
+
+void* oracle_vocab_load(const char* path) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return nullptr;
+    OVocab* v = new OVocab();
+    unsigned int nb_nodes = 0, size_node = 0;
+    if (fread(&nb_nodes, 4, 1, f) != 1 || fread(&size_node, 4, 1, f) != 1 || fread(&v->k, 4, 1, f) != 1 ||
+        fread(&v->L, 4, 1, f) != 1 || fread(&v->scoring, 4, 1, f) != 1 || fread(&v->weighting, 4, 1, f) != 1 ||
+        size_node != 41) {
+        fclose(f);
+        delete v;
+        return nullptr;
+    }
+    v->nodes.resize(nb_nodes + 1);
+    std::vector<char> buf(size_node, 0);
+    int nid = 1;
+    for (;;) {   // while (!f.eof()): a failed read leaves buf as it was and still creates a node
+        const size_t got = fread(buf.data(), 1, size_node, f);
+        if (nid >= (int)v->nodes.size()) break;
+        OVNode& n = v->nodes[nid];
+        std::memcpy(&n.parent, buf.data(), 4);
+        v->nodes[n.parent].children.push_back(nid);
+        std::memcpy(n.desc, buf.data() + 4, 32);
+        float w;
+        std::memcpy(&w, buf.data() + 36, 4);
+        n.weight = w;
+        if (buf[40]) n.word_id = v->nwords++;
+        nid += 1;
+        if (got < size_node) break;   // eof reached on this read: the loop ends after this node
+    }
+    fclose(f);
+    return v;
+}
+
+void oracle_vocab_destroy(void* h) { delete (OVocab*)h; }
+
+int oracle_vocab_info(void* h, int* k, int* L, int* scoring, int* weighting, int* nnodes, int* nwords) {
+    const OVocab* v = (const OVocab*)h;
+    *k = v->k;
+    *L = v->L;
+    *scoring = v->scoring;
+    *weighting = v->weighting;
+    *nnodes = (int)v->nodes.size();
+    *nwords = v->nwords;
+    return 0;
+}
+
+/* transform(feature, word_id, weight, nid, levelsup) for each of n descriptors. */
+void oracle_vocab_transform_each(void* h, const uint8_t* desc, int n, int levelsup, int* word_id, double* weight,
+                                 uint32_t* nid_out) {
+    const OVocab* v = (const OVocab*)h;
+    for (int i = 0; i < n; i++) {
+        const uint8_t* feature = desc + (size_t)i * 32;
+        const int nid_level = v->L - levelsup;
+        uint32_t nid = 0;   // (uninitialised in the reference when a leaf comes before nid_level)
+        if (nid_level <= 0) nid = 0;
+        int final_id = 0;
+        int current_level = 0;
+        do {
+            ++current_level;
+            const std::vector<int>& nodes = v->nodes[final_id].children;
+            final_id = nodes[0];
+            double best_d = DescriptorDistance(feature, v->nodes[final_id].desc);
+            for (size_t c = 1; c < nodes.size(); c++) {
+                const int id = nodes[c];
+                const double d = DescriptorDistance(feature, v->nodes[id].desc);
+                if (d < best_d) {
+                    best_d = d;
+                    final_id = id;
+                }
+            }
+            if (current_level == nid_level) nid = (uint32_t)final_id;
+        } while (!v->nodes[final_id].isLeaf());
+        word_id[i] = v->nodes[final_id].word_id;
+        weight[i] = v->nodes[final_id].weight;
+        nid_out[i] = nid;
+    }
+}
+
+/* transform(features, BowVector&, FeatureVector&, levelsup).  BowVector out: nbow (word, value)
+ * pairs ascending by word; FeatureVector out: nfv nodes ascending, fv_off (nfv+1) / fv_idx CSR.
+ * Returns 0, or -1 if a capacity is too small (caps: n each). */
+int oracle_vocab_transform(void* h, const uint8_t* desc, int n, int levelsup, int* bow_words, double* bow_values,
+                           int* nbow, uint32_t* fv_nodes, int* fv_off, int* fv_idx, int* nfv) {
+    const OVocab* v = (const OVocab*)h;
+    std::map<int, double> bow;
+    std::map<uint32_t, std::vector<int>> fv;
+    if (v->nwords > 0) {   // if(empty()) return;  TemplatedVocabulary.h:1146-1149
+        // scoring -> (must normalise, norm): L1, L2, ChiSquare, KL, Bhattacharyya: true; DotProduct: false
+        const bool must = v->scoring != 5;
+        const bool l1 = v->scoring != 1;
+        std::vector<int> wid(n);
+        std::vector<double> w(n);
+        std::vector<uint32_t> nid(n);
+        oracle_vocab_transform_each(h, desc, n, levelsup, wid.data(), w.data(), nid.data());
+        const bool tf = v->weighting == 0 || v->weighting == 1;   // TF_IDF, TF
+        for (int i = 0; i < n; i++) {
+            if (w[i] > 0) {
+                if (tf) bow[wid[i]] += w[i];                       // addWeight
+                else if (!bow.count(wid[i])) bow[wid[i]] = w[i];   // addIfNotExist
+                fv[nid[i]].push_back(i);
+            }
+        }
+        if (tf && !bow.empty() && !must) {
+            const double nd = (double)bow.size();
+            for (auto& e : bow) e.second /= nd;
+        }
+        if (must) {   // BowVector::normalize
+            double norm = 0.0;
+            if (l1)
+                for (auto& e : bow) norm += std::fabs(e.second);
+            else {
+                for (auto& e : bow) norm += e.second * e.second;
+                norm = std::sqrt(norm);
+            }
+            if (norm > 0.0)
+                for (auto& e : bow) e.second /= norm;
+        }
+    }
+    int b = 0;
+    for (auto& e : bow) {
+        bow_words[b] = e.first;
+        bow_values[b] = e.second;
+        b++;
+    }
+    *nbow = b;
+    int j = 0, o = 0;
+    fv_off[0] = 0;
+    for (auto& e : fv) {
+        fv_nodes[j] = e.first;
+        for (int i : e.second) fv_idx[o++] = i;
+        fv_off[++j] = o;
+    }
+    *nfv = j;
+    return 0;
 }
 
 }  // extern "C"

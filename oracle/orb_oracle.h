@@ -130,6 +130,16 @@ int oracle_stereo_matches(void* left, void* right, int N, const OracleKeyPoint* 
                           const OracleKeyPoint* kpsR, const uint8_t* descR, float mb, float mbf, float* mvuRight,
                           float* mvDepth);
 
+/* DBoW2 vocabulary (TemplatedVocabulary.h): binary loader (:1466-1510), per-feature descent
+ * (:1240-1277) and the BowVector / FeatureVector transform (:1139-1210).  NULL on a bad file. */
+void* oracle_vocab_load(const char* path);
+void  oracle_vocab_destroy(void* h);
+int   oracle_vocab_info(void* h, int* k, int* L, int* scoring, int* weighting, int* nnodes, int* nwords);
+void  oracle_vocab_transform_each(void* h, const uint8_t* desc, int n, int levelsup, int* word_id, double* weight,
+                                  uint32_t* nid);
+int   oracle_vocab_transform(void* h, const uint8_t* desc, int n, int levelsup, int* bow_words, double* bow_values,
+                             int* nbow, uint32_t* fv_nodes, int* fv_off, int* fv_idx, int* nfv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,7 @@ import numpy as np
 from ._lib import OrbError, OrbFeatVec, OrbParams, check, lib
 
 __all__ = ["ORBextractor", "ORBmatcher", "BatchExtractor", "KP_DTYPE", "OrbError", "device_count",
-           "features_in_area", "compute_stereo_matches"]
+           "features_in_area", "compute_stereo_matches", "ORBVocabulary"]
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -369,3 +369,64 @@ class ORBmatcher:
     def BirdviewMatch(self, desc1, kps1, desc2, kps2, cand_off, cand_idx):
         """BirdviewMatch(const Frame&, const Frame&, vector<int>&, int) (ORBmatcher.cc:1790-1899)."""
         return self._window(False, desc1, kps1, desc2, kps2, cand_off, cand_idx)
+
+
+class ORBVocabulary:
+    """DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> (include/ORBVocabulary.h:32) on the GPU:
+    loadFromBinaryFile (TemplatedVocabulary.h:1466-1510) and transform(features, BowVector&,
+    FeatureVector&, levelsup) (:1139-1210).  BowVector -> {word: value}, FeatureVector -> {node: [i]}."""
+
+    def __init__(self, device=0):
+        self._ctx = _Ctx(1000, 1.2, 8, 20, 7, device)
+        self.v = None
+
+    def loadFromBinaryFile(self, path):
+        if self.v:
+            lib().orb_vocab_destroy(self.v)
+            self.v = None
+        out = ctypes.c_void_p()
+        check(lib().orb_vocab_load(self._ctx.h, path.encode(), ctypes.byref(out)), "orb_vocab_load")
+        self.v = out
+        vals = [ctypes.c_int() for _ in range(6)]
+        check(lib().orb_vocab_info(self.v, *[ctypes.byref(x) for x in vals]), "orb_vocab_info")
+        self.k, self.L, self.scoring, self.weighting, self.nnodes, self.nwords = [x.value for x in vals]
+        return True
+
+    def transform_each(self, desc, levelsup=4):
+        """Per-feature (word id, weight, node id levelsup above the leaf)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        w = np.zeros(max(n, 1), np.int32)
+        wt = np.zeros(max(n, 1), np.float32)
+        nd = np.zeros(max(n, 1), np.uint32)
+        check(lib().orb_vocab_transform(self._ctx.h, self.v, _p(d), n, levelsup, _p(w), _p(wt), _p(nd)),
+              "orb_vocab_transform")
+        return w[:n], wt[:n], nd[:n]
+
+    def bow(self, word, weight, node):
+        n = len(word)
+        bw = np.zeros(max(n, 1), np.int32)
+        bv = np.zeros(max(n, 1), np.float64)
+        fn = np.zeros(max(n, 1), np.uint32)
+        fo = np.zeros(n + 1, np.int32)
+        fi = np.zeros(max(n, 1), np.int32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        args = [np.ascontiguousarray(word, np.int32), np.ascontiguousarray(weight, np.float32),
+                np.ascontiguousarray(node, np.uint32)]
+        check(lib().orb_vocab_bow(self.v, n, *[_p(a) for a in args], _p(bw), _p(bv), ctypes.byref(nb), _p(fn),
+                                  _p(fo), _p(fi), ctypes.byref(nf)), "orb_vocab_bow")
+        bowv = {int(bw[i]): float(bv[i]) for i in range(nb.value)}
+        fv = {int(fn[j]): fi[fo[j]:fo[j + 1]].tolist() for j in range(nf.value)}
+        return bowv, fv
+
+    def transform(self, desc, levelsup=4):
+        """transform(features, BowVector&, FeatureVector&, levelsup) -> (bow, featvec)."""
+        return self.bow(*self.transform_each(desc, levelsup))
+
+    def close(self):
+        if getattr(self, "v", None):
+            lib().orb_vocab_destroy(self.v)
+            self.v = None
+
+    def __del__(self):
+        self.close()

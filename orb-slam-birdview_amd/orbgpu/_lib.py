@@ -65,6 +65,12 @@ SIGNATURES = {
     "orb_features_in_area": (ci, [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]),
     "orb_compute_stereo_matches": (ci, [vp, vp, ci, vp, vp, ci, vp, vp, cf, cf, vp, vp, ctypes.POINTER(ci)]),
     "orb_stereo_batch_device": (ci, [vp, ci, cf, cf, vp, vp, vp]),
+    "orb_vocab_load": (ci, [vp, ctypes.c_char_p, ctypes.POINTER(vp)]),
+    "orb_vocab_destroy": (None, [vp]),
+    "orb_vocab_info": (ci, [vp, vp, vp, vp, vp, vp, vp]),
+    "orb_vocab_transform": (ci, [vp, vp, vp, ci, ci, vp, vp, vp]),
+    "orb_vocab_transform_batch_device": (ci, [vp, vp, ci, ci, vp, vp, vp]),
+    "orb_vocab_bow": (ci, [vp, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
 }
 
 STATUS = {0: "ORB_OK", -1: "ORB_ERR_ARG", -2: "ORB_ERR_HIP", -3: "ORB_ERR_CAPACITY",

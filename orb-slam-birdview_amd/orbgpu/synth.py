@@ -101,3 +101,41 @@ def synth_stereo_right(left, idx=0, max_disp=64):
 
 def synth_batch(w, h, n, first=0, kind="scene"):
     return np.stack([synth_frame(w, h, first + i, kind) for i in range(n)])
+
+
+def write_synth_vocab(path, k=10, L=3, seed=0, scoring=0, weighting=0, stop_frac=0.05):
+    """Write a synthetic DBoW2 ORB vocabulary in ORBvoc.bin's binary format
+    (TemplatedVocabulary::saveToBinaryFile, TemplatedVocabulary.h:1512-1531): a complete k-ary tree of
+    depth L, nodes numbered breadth-first (children of a node consecutive, as DBoW2's k-means build
+    numbers them), each child descriptor = its parent's with ~1/4 of the bits flipped, leaf weights
+    U(0.1, 3) with `stop_frac` of them 0 (stopped words).  The real ORBvoc.bin is not in the
+    container; tests and the bench use this instead.  Returns (nb_nodes, nwords)."""
+    import struct
+    rng = np.random.default_rng(seed)
+    desc = [rng.integers(0, 256, 32, dtype=np.uint8)]   # root (not stored)
+    parent = [0]
+    level = [0]
+    frontier = [0]
+    for lv in range(1, L + 1):
+        nxt = []
+        for p in frontier:
+            for _ in range(k):
+                flip = rng.random(256) < 0.25
+                bits = np.unpackbits(desc[p]) ^ flip.astype(np.uint8)
+                desc.append(np.packbits(bits))
+                parent.append(p)
+                level.append(lv)
+                nxt.append(len(desc) - 1)
+        frontier = nxt
+    nb_nodes = len(desc)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<6i", nb_nodes, 4 + 32 + 4 + 1, k, L, scoring, weighting))
+        nwords = 0
+        for i in range(1, nb_nodes):
+            leaf = level[i] == L
+            w = 0.0
+            if leaf:
+                nwords += 1
+                w = 0.0 if rng.random() < stop_frac else float(rng.uniform(0.1, 3.0))
+            f.write(struct.pack("<i", parent[i]) + desc[i].tobytes() + struct.pack("<f", w) + bytes([1 if leaf else 0]))
+    return nb_nodes, nwords

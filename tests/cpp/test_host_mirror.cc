@@ -3,7 +3,7 @@
 // own code drives these classes: construct an extractor, call operator(), read the getters and
 // mvImagePyramid, run each ORBmatcher search on two extracted views.
 //
-// usage: test_host_mirror <frames.raw> <w> <h> <nframes> <nfeatures>
+// usage: test_host_mirror <frames.raw> <w> <h> <nframes> <nfeatures> [vocabulary.bin]
 //   frames.raw holds nframes gray w x h frames back to back (written by tests/test_host_mirror.py).
 // Prints one "CHECK <name> PASS|FAIL <detail>" line per check and "SUMMARY <npass> <nfail>";
 // exit status 0 iff every check passed.
@@ -20,6 +20,7 @@
 #include "../../orb-slam-birdview_amd/host/ORBextractor.h"
 #include "../../orb-slam-birdview_amd/host/ORBmatcher.h"
 #include "../../orb-slam-birdview_amd/host/Stereo.h"
+#include "../../orb-slam-birdview_amd/host/ORBVocabulary.h"
 
 using namespace ORB_SLAM2;
 
@@ -339,6 +340,39 @@ int main(int argc, char** argv) {
             const bool ok = n == on && memcmp(mvuRight.data(), ou.data(), ou.size() * 4) == 0 &&
                             memcmp(mvDepth.data(), od.data(), od.size() * 4) == 0;
             report("ComputeStereoMatches", ok, "n=" + std::to_string(n) + " oracle=" + std::to_string(on));
+        }
+        // ---- Frame::ComputeBoW (Frame.cc:562-569): ORBVocabulary::transform(mDescriptors, mBowVec, mFeatVec, 4)
+        if (argc > 6) {
+            ORBVocabulary voc;
+            const bool loaded = voc.loadFromBinaryFile(argv[6]);
+            void* ov = oracle_vocab_load(argv[6]);
+            report("vocabulary_load", loaded && ov != nullptr);
+            if (loaded && ov) {
+                for (int levelsup = 1; levelsup <= 4; levelsup += 3) {
+                    BowVector bow;
+                    BowFeatureVector fvec;
+                    voc.transform(d1, bow, fvec, levelsup);
+                    const int n = d1.rows;
+                    std::vector<int> bw(n + 1), off(n + 2), idx(n + 1);
+                    std::vector<double> bv(n + 1);
+                    std::vector<uint32_t> fn(n + 1);
+                    int nb = 0, nfv = 0;
+                    oracle_vocab_transform(ov, d1.buf.data(), n, levelsup, bw.data(), bv.data(), &nb, fn.data(),
+                                           off.data(), idx.data(), &nfv);
+                    bool ok = (int)bow.size() == nb && (int)fvec.size() == nfv;
+                    int b = 0;
+                    for (BowVector::const_iterator it = bow.begin(); ok && it != bow.end(); ++it, ++b)
+                        ok = (int)it->first == bw[b] && it->second == bv[b];
+                    int j = 0;
+                    for (BowFeatureVector::const_iterator it = fvec.begin(); ok && it != fvec.end(); ++it, ++j) {
+                        ok = it->first == fn[j] && (int)it->second.size() == off[j + 1] - off[j];
+                        for (size_t q = 0; ok && q < it->second.size(); q++) ok = (int)it->second[q] == idx[off[j] + q];
+                    }
+                    report("ComputeBoW_levelsup" + std::to_string(levelsup), ok,
+                           "words=" + std::to_string(bow.size()) + " nodes=" + std::to_string(fvec.size()));
+                }
+            }
+            if (ov) oracle_vocab_destroy(ov);
         }
     } catch (const std::exception& e) {
         report("exception", false, e.what());

@@ -23,12 +23,12 @@ def mirror_bin():
     return BIN
 
 
-def _run(bin_path, frames, nf, tmp_path):
+def _run(bin_path, frames, nf, tmp_path, vocab=None):
     n, h, w = frames.shape
     raw = tmp_path / f"frames_{w}x{h}.raw"
     raw.write_bytes(np.ascontiguousarray(frames, np.uint8).tobytes())
-    p = subprocess.run([bin_path, str(raw), str(w), str(h), str(n), str(nf)], capture_output=True, text=True,
-                       timeout=300)
+    argv = [bin_path, str(raw), str(w), str(h), str(n), str(nf)] + ([vocab] if vocab else [])
+    p = subprocess.run(argv, capture_output=True, text=True, timeout=300)
     return p.returncode, p.stdout, p.stderr
 
 
@@ -47,7 +47,8 @@ def test_mirror_library_exports_reference_api(mirror_bin):
                 "ORB_SLAM2::ORBmatcher::SearchForInitialization(",
                 "ORB_SLAM2::ORBmatcher::BirdviewMatch(",
                 "ORB_SLAM2::FrameGrid::GetFeaturesInArea(",
-                "ORB_SLAM2::ComputeStereoMatches("]:
+                "ORB_SLAM2::ComputeStereoMatches(",
+                "ORB_SLAM2::ORBVocabulary::transform("]:
         assert sym in out, sym
     del lib
 
@@ -69,7 +70,10 @@ def test_mirror_parity_on_gpu(mirror_bin, tmp_path, w, h, nf):
     a = synth_frame(w, h, 21)
     # frame 1: a rectified right view of frame 0 (matchers and ComputeStereoMatches use the pair)
     frames = np.stack([a, synth_stereo_right(a, 21), synth_frame(w, h, 5, "noise")])
-    rc, out, err = _run(mirror_bin, frames, nf, tmp_path)
+    from orbgpu.synth import write_synth_vocab
+    voc = str(tmp_path / "voc.bin")
+    write_synth_vocab(voc, 10, 4, seed=2)
+    rc, out, err = _run(mirror_bin, frames, nf, tmp_path, voc)
     fails = [l for l in out.splitlines() if " FAIL" in l]
     assert rc == 0 and not fails, "\n".join(fails) + "\n" + err[-2000:]
     summary = [l for l in out.splitlines() if l.startswith("SUMMARY")][0].split()

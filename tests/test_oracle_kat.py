@@ -269,3 +269,31 @@ def test_oracle_stereo_kat(oracle_mod):
     disp = kl["x"][ok] - u[ok]
     assert np.all(disp >= 0) and np.all(disp < 500.0)
     assert np.array_equal(d[ok], (np.float32(50.0) / disp.astype(np.float32)).astype(np.float32))
+
+
+def test_oracle_vocab_loader_and_descent_kat(oracle_mod, tmp_path):
+    """TemplatedVocabulary::loadFromBinaryFile (TemplatedVocabulary.h:1466-1510): nb_nodes - 1
+    records plus the while(!eof) duplicate of the last one (one extra node and word); a feature equal
+    to a leaf's stored descriptor whose path is unambiguous descends to that leaf; the L1-normalised
+    TF-IDF BowVector sums to 1."""
+    import struct
+    from orbgpu.synth import write_synth_vocab
+    path = str(tmp_path / "v.bin")
+    nb, nw = write_synth_vocab(path, 4, 3, seed=7, stop_frac=0.0)
+    v = oracle_mod.OracleVocabulary(path)
+    assert (v.k, v.L) == (4, 3) and v.nnodes == nb + 1 and v.nwords == nw + 1
+    raw = open(path, "rb").read()
+    recs = [raw[24 + 41 * i:24 + 41 * (i + 1)] for i in range(nb - 1)]
+    leaves = [(i + 1, np.frombuffer(r[4:36], np.uint8)) for i, r in enumerate(recs) if r[40]]
+    wid, wt, nid = v.transform_each(np.stack([d for _, d in leaves]), 0)
+    # leaves are numbered breadth-first after the internal nodes: word id = leaf order
+    ok = wid == np.arange(len(leaves))
+    assert ok.mean() > 0.9
+    # levelsup 0 -> nid_level = L: the FeatureVector node is the leaf itself
+    assert np.array_equal(nid[ok], np.array([i for i, _ in leaves])[ok])
+    _, _, nid_root = v.transform_each(np.stack([d for _, d in leaves]), 3)   # nid_level <= 0 -> root
+    assert (nid_root == 0).all()
+    bow, fv = v.transform(np.stack([d for _, d in leaves]), 1)
+    assert abs(sum(bow.values()) - 1.0) < 1e-12
+    assert sum(len(x) for x in fv.values()) == len(leaves)
+    assert struct.unpack("<6i", raw[:24])[1] == 41
