@@ -248,6 +248,15 @@ int orb_vocab_bow(const orb_vocab* v, int n, const int* word_id, const float* we
                   int* bow_words, double* bow_values, int* nbow, uint32_t* fv_nodes, int* fv_off, int* fv_idx,
                   int* nfv);
 
+/* ============ MapPoint::ComputeDistinctiveDescriptors, batched ============ */
+
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:242-307; MapPointBird.cc:87-152): for each
+ * of nmp map points, the descriptors of its observations from non-bad keyframes (observation order)
+ * are desc[offsets[m] .. offsets[m+1]) (32 B each); best_idx[m] receives the index (within the point's
+ * list) of the descriptor with the least median distance to the others — first on ties — or -1 for
+ * an empty list (the reference returns without touching mDescriptor).  Host pointers, synchronous. */
+int orb_distinctive_descriptors(orb_ctx* ctx, int nmp, const int* offsets, const uint8_t* desc, int* best_idx);
+
 #ifdef __cplusplus
 }
 #endif

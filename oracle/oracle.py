@@ -67,6 +67,7 @@ def lib():
         L.oracle_window_match.argtypes = [cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp]
         L.oracle_features_in_area.argtypes = [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]
         L.oracle_stereo_matches.argtypes = [vp, vp, ci, vp, vp, ci, vp, vp, cf, cf, vp, vp]
+        L.oracle_distinctive_descriptor.argtypes = [vp, ci]
         L.oracle_vocab_load.restype = vp
         L.oracle_vocab_load.argtypes = [ctypes.c_char_p]
         L.oracle_vocab_destroy.argtypes = [vp]
@@ -326,3 +327,9 @@ class OracleVocabulary:
         bow = {int(bw[i]): float(bv[i]) for i in range(nb.value)}
         fv = {int(fn[j]): fi[fo[j]:fo[j + 1]].tolist() for j in range(nf.value)}
         return bow, fv
+
+
+def distinctive_descriptor(desc):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): index of the chosen descriptor."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    return lib().oracle_distinctive_descriptor(_p(d) if len(d) else None, len(d))

@@ -1359,4 +1359,30 @@ int oracle_vocab_transform(void* h, const uint8_t* desc, int n, int levelsup, in
     return 0;
 }
 
+/* MapPoint::ComputeDistinctiveDescriptors  MapPoint.cc:242-307 (the distance / median part). */
+int oracle_distinctive_descriptor(const uint8_t* desc, int N) {
+    if (N <= 0) return -1;
+    std::vector<float> Distances((size_t)N * N);
+    for (int i = 0; i < N; i++) {
+        Distances[(size_t)i * N + i] = 0;
+        for (int j = i + 1; j < N; j++) {
+            const int distij = DescriptorDistance(desc + (size_t)i * 32, desc + (size_t)j * 32);
+            Distances[(size_t)i * N + j] = distij;
+            Distances[(size_t)j * N + i] = distij;
+        }
+    }
+    int BestMedian = INT_MAX;
+    int BestIdx = 0;
+    for (int i = 0; i < N; i++) {
+        std::vector<int> vDists(Distances.begin() + (size_t)i * N, Distances.begin() + (size_t)(i + 1) * N);
+        std::sort(vDists.begin(), vDists.end());
+        const int median = vDists[(size_t)(0.5 * (N - 1))];
+        if (median < BestMedian) {
+            BestMedian = median;
+            BestIdx = i;
+        }
+    }
+    return BestIdx;
+}
+
 }  // extern "C"

@@ -140,6 +140,9 @@ void  oracle_vocab_transform_each(void* h, const uint8_t* desc, int n, int level
 int   oracle_vocab_transform(void* h, const uint8_t* desc, int n, int levelsup, int* bow_words, double* bow_values,
                              int* nbow, uint32_t* fv_nodes, int* fv_off, int* fv_idx, int* nfv);
 
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): index of the chosen descriptor of N. */
+int oracle_distinctive_descriptor(const uint8_t* desc, int N);
+
 #ifdef __cplusplus
 }
 #endif

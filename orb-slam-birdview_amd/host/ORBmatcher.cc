@@ -283,4 +283,18 @@ int ORBmatcher::BirdviewMatch(const FrameData& F1, const FrameData& F2, std::vec
     return window_match(false, F1, F2, nullptr, windowSize, vnMatches12);
 }
 
+std::vector<int> ComputeDistinctiveDescriptors(const std::vector<std::vector<const uint8_t*> >& observations) {
+    const int nmp = (int)observations.size();
+    std::vector<int> off(nmp + 1, 0), best(std::max(nmp, 1), -1);
+    for (int m = 0; m < nmp; m++) off[m + 1] = off[m] + (int)observations[m].size();
+    std::vector<uint8_t> flat((size_t)std::max(off[nmp], 1) * 32);
+    for (int m = 0; m < nmp; m++)
+        for (size_t j = 0; j < observations[m].size(); j++)
+            memcpy(&flat[((size_t)off[m] + j) * 32], observations[m][j], 32);
+    check(orb_distinctive_descriptors(matcher_ctx(), nmp, off.data(), flat.data(), best.data()),
+          "ComputeDistinctiveDescriptors");
+    best.resize(nmp);
+    return best;
+}
+
 }  // namespace ORBGPU_MATCHER_NAMESPACE

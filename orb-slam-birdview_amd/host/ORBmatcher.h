@@ -121,6 +121,12 @@ protected:
     bool mbCheckOrientation;
 };
 
+// MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307), batched over map points:
+// observations[m] = the descriptors (32 B each, observation order, bad keyframes skipped) of map
+// point m.  Returns per point the index of the descriptor the reference copies into mDescriptor, or
+// -1 for an empty list (the reference then leaves mDescriptor untouched).
+std::vector<int> ComputeDistinctiveDescriptors(const std::vector<std::vector<const uint8_t*> >& observations);
+
 }  // namespace ORBGPU_MATCHER_NAMESPACE
 
 #endif

@@ -366,6 +366,19 @@ class ORBmatcher:
         Returns (nmatches, vnMatches12)."""
         return self._window(True, desc1, kps1, desc2, kps2, cand_off, cand_idx)
 
+    def ComputeDistinctiveDescriptors(self, descriptor_sets):
+        """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of map points:
+        descriptor_sets[m] = (n_m, 32) descriptors of point m's observations.  Returns the index of the
+        chosen descriptor per point (-1 for an empty set)."""
+        sets = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in descriptor_sets]
+        off = np.zeros(len(sets) + 1, np.int32)
+        off[1:] = np.cumsum([len(d) for d in sets])
+        allv = np.ascontiguousarray(np.concatenate(sets) if off[-1] else np.zeros((1, 32), np.uint8))
+        out = np.zeros(max(len(sets), 1), np.int32)
+        check(lib().orb_distinctive_descriptors(self._ctx.h, len(sets), _p(off), _p(allv), _p(out)),
+              "orb_distinctive_descriptors")
+        return out[:len(sets)]
+
     def BirdviewMatch(self, desc1, kps1, desc2, kps2, cand_off, cand_idx):
         """BirdviewMatch(const Frame&, const Frame&, vector<int>&, int) (ORBmatcher.cc:1790-1899)."""
         return self._window(False, desc1, kps1, desc2, kps2, cand_off, cand_idx)

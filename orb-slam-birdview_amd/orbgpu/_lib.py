@@ -71,6 +71,7 @@ SIGNATURES = {
     "orb_vocab_transform": (ci, [vp, vp, vp, ci, ci, vp, vp, vp]),
     "orb_vocab_transform_batch_device": (ci, [vp, vp, ci, ci, vp, vp, vp]),
     "orb_vocab_bow": (ci, [vp, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "orb_distinctive_descriptors": (ci, [vp, ci, vp, vp, vp]),
 }
 
 STATUS = {0: "ORB_OK", -1: "ORB_ERR_ARG", -2: "ORB_ERR_HIP", -3: "ORB_ERR_CAPACITY",

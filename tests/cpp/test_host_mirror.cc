@@ -341,6 +341,24 @@ int main(int argc, char** argv) {
                             memcmp(mvDepth.data(), od.data(), od.size() * 4) == 0;
             report("ComputeStereoMatches", ok, "n=" + std::to_string(n) + " oracle=" + std::to_string(on));
         }
+        // ---- MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): point m observed by
+        // descriptors m .. m+span of frame 0 (overlapping windows of 1..12 observations)
+        {
+            std::vector<std::vector<const uint8_t*> > obs;
+            for (int m = 0; m + 12 < d1.rows && m < 200; m++) {
+                std::vector<const uint8_t*> o;
+                for (int j = 0; j <= m % 12; j++) o.push_back(d1.ptr(m + j));
+                obs.push_back(o);
+            }
+            const std::vector<int> best = ComputeDistinctiveDescriptors(obs);
+            bool ok = best.size() == obs.size();
+            for (size_t m = 0; ok && m < obs.size(); m++) {
+                std::vector<uint8_t> flat(obs[m].size() * 32);
+                for (size_t j = 0; j < obs[m].size(); j++) memcpy(&flat[j * 32], obs[m][j], 32);
+                ok = best[m] == oracle_distinctive_descriptor(flat.data(), (int)obs[m].size());
+            }
+            report("ComputeDistinctiveDescriptors", ok, "points=" + std::to_string(obs.size()));
+        }
         // ---- Frame::ComputeBoW (Frame.cc:562-569): ORBVocabulary::transform(mDescriptors, mBowVec, mFeatVec, 4)
         if (argc > 6) {
             ORBVocabulary voc;

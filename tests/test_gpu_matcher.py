@@ -276,3 +276,18 @@ def test_top2_frames_batch_vs_numpy(orbgpu_mod):
     for d in out:
         L.orb_device_free(bx.h, d)
     bx.close()
+
+
+def test_distinctive_descriptors_vs_oracle(orbgpu_mod, oracle_mod):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307), batched over map points with
+    1..300 observations (noisy copies of a prototype: realistic ties in the medians), plus empty."""
+    rng = np.random.default_rng(11)
+    sets = [np.zeros((0, 32), np.uint8)]
+    for n in [1, 2, 3, 4, 7, 31, 64, 65, 130, 300] + list(rng.integers(1, 40, 40)):
+        proto = rng.integers(0, 256, 32, dtype=np.uint8)
+        flips = rng.random((n, 256)) < rng.uniform(0.02, 0.3)
+        sets.append(np.packbits(np.unpackbits(proto)[None, :] ^ flips.astype(np.uint8), axis=1))
+    m = orbgpu_mod.ORBmatcher()
+    got = m.ComputeDistinctiveDescriptors(sets)
+    exp = [oracle_mod.distinctive_descriptor(s) for s in sets]
+    assert got.tolist() == exp

@@ -297,3 +297,17 @@ def test_oracle_vocab_loader_and_descent_kat(oracle_mod, tmp_path):
     assert abs(sum(bow.values()) - 1.0) < 1e-12
     assert sum(len(x) for x in fv.values()) == len(leaves)
     assert struct.unpack("<6i", raw[:24])[1] == 41
+
+
+def test_oracle_distinctive_descriptor_kat(oracle_mod):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): median index (int)(0.5*(N-1));
+    N = 1, 2 -> 0 (median 0 for every row); three descriptors a, a', b with a' one bit from a -> a."""
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, 32, dtype=np.uint8)
+    b = ~a
+    a2 = a.copy()
+    a2[0] ^= 1
+    assert oracle_mod.distinctive_descriptor(np.zeros((0, 32), np.uint8)) == -1
+    assert oracle_mod.distinctive_descriptor(a[None]) == 0
+    assert oracle_mod.distinctive_descriptor(np.stack([b, a])) == 0
+    assert oracle_mod.distinctive_descriptor(np.stack([b, a2, a])) == 1   # rows: b->[0,255,256] a2->[0,1,255] a->[0,1,256]
