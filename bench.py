@@ -164,6 +164,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hamming", action="store_true")
     ap.add_argument("--no-stereo", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -324,6 +325,25 @@ def main():
             orbgpu._lib.lib().orb_device_free(sx.h, ptr)
         sx.close()
 
+    # ---- the reference's own boundary: ORBextractor::operator() on a HOST image (orb_extract: H2D
+    # of the frame, the same kernels, D2H of keypoints + descriptors, synchronous per frame, one
+    # context) — the PCIe-inclusive per-frame rate a drop-in caller sees.  Never the headline value.
+    host_path = None
+    if not args.no_host_path:
+        hx = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=local)
+        nh = min(16, len(frames))
+        hx(frames[0])
+        t0h = time.perf_counter()
+        nkp = 0
+        for i in range(nh):
+            k_, d_ = hx(frames[i])
+            nkp += len(k_)
+        t1h = time.perf_counter()
+        host_path = {"frames_per_s": round(nh / (t1h - t0h), 1), "features_per_s": round(nkp / (t1h - t0h), 1),
+                     "ms_per_frame": round((t1h - t0h) / nh * 1e3, 3),
+                     "note": "orb_extract per host frame: upload + 10 launches + download, one frame in flight"}
+        hx.close()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cfg, frames[:32])
@@ -339,7 +359,8 @@ def main():
                "frames_per_s": round(total_frames / tmax, 1),
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
-               "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo}
+               "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo,
+               "host_path": host_path}
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)
