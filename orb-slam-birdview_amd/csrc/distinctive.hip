@@ -13,7 +13,7 @@ namespace orbgpu {
 __global__ __launch_bounds__(256) void k_distinctive(const int* __restrict__ off, const uint8_t* __restrict__ desc,
                                                      int nmp, int* __restrict__ best_out) {
     __shared__ int s_hist[4][260];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int m = blockIdx.x * 4 + wv;
     if (m >= nmp) return;   // whole wave
     const int b = off[m], N = off[m + 1] - b;

@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
                                                    int remap) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (4 cells each)
     int blk = blockIdx.x;
     if (remap) {
@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kDescWin * kDescWinPitch + 16];
     __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][40 * kRtPitch];
     const int f = blockIdx.y;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int nl = g->nlevels;
     const int* cnts = lvlCount + f * nl;
     if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_stereo(const Geom* __restrict__ g, Ster
                                                 const int* __restrict__ rows, const int* __restrict__ sorted,
                                                 long long row_stride) {
     __shared__ int s_part[4][64];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int p = blockIdx.y;
     const int iL = blockIdx.x * 4 + wv;
     const int fL = L.frame0 + p * L.frame_step, fR = R.frame0 + p * R.frame_step;
