@@ -115,6 +115,9 @@ int orb_debug_candidates(orb_ctx* ctx, int frame, int level, int* out, int cap);
 /* Octree output of `level` (DistributeOctTree list order): 3 ints (x, y, score), level coords. */
 int orb_debug_level_keypoints(orb_ctx* ctx, int frame, int level, int* out, int cap);
 int orb_debug_level_image(orb_ctx* ctx, int frame, int level, uint8_t* out, int* w, int* h);
+/* Phase timestamps of the last FAST launch (diagnostic; only with ORBGPU_FAST_STAMPS=1 in the
+ * environment at orb_create): 8 s_memtime values per (frame, cell) item.  Returns the count copied. */
+int orb_debug_fast_stamps(orb_ctx* ctx, uint64_t* out, int cap);
 
 /* =========================== ORBmatcher =========================== */
 

@@ -325,6 +325,65 @@ __device__ __forceinline__ FastCell fast_cell(const Geom* __restrict__ g, int it
     return c;
 }
 
+// Host table of the cells (ComputeKeyPointsOctTree's grid, ORBextractor.cc:781-806), frame independent.
+void build_cells(const Geom& g, std::vector<CellDesc>& cells) {
+    cells.assign(g.ncells, CellDesc{});
+    for (int l = 0; l < g.nlevels; l++) {
+        const LevelGeom& L = g.L[l];
+        for (int ci = 0; ci < L.nRows; ci++)
+            for (int cj = 0; cj < L.nCols; cj++) {
+                const int cc = ci * L.nCols + cj;
+                CellDesc& d = cells[L.cell_base + cc];
+                const int iniY = kMinBorder + ci * L.hCell, iniX = kMinBorder + cj * L.wCell;
+                bool valid = !(iniY >= L.maxBY - 3 || iniX >= L.maxBX - 6);   // :794-806
+                const int maxY = std::min(iniY + L.hCell + 6, L.maxBY), maxX = std::min(iniX + L.wCell + 6, L.maxBX);
+                const int rw = maxX - iniX, rh = maxY - iniY;
+                valid = valid && rw - 6 > 0 && rh - 6 > 0;
+                d.lv = l | (valid ? 1 << 8 : 0);
+                d.iniX = iniX;
+                d.iniY = iniY;
+                d.rwrh = (rw & 0xFFFF) | (rh << 16);
+                d.out_off = L.cand_base + cc * L.cell_cap;
+                d.xoyo = (3 + cj * L.wCell) | ((3 + ci * L.hCell) << 16);
+                d.pitch = L.pitch;
+                d.pyr_off = (int)L.pyr_off;
+            }
+    }
+}
+
+struct FastCellT {
+    int f, cell, iniX, rw, rh, dw, dh, x0w, nw, out_off, xo, yo;
+    bool valid, aligned;
+    const uint8_t* base;   // ROI row 0, column 0
+    int stride;
+};
+
+__device__ __forceinline__ FastCellT fast_cell_t(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
+                                                 int item, const uint8_t* frames, long long framePitch, int rowStride,
+                                                 const uint8_t* pyr) {
+    FastCellT c;
+    c.f = item / g->ncells;
+    c.cell = item - c.f * g->ncells;
+    const CellDesc d = cells[c.cell];   // one scalar load
+    const int l = d.lv & 0xFF;
+    c.valid = (d.lv >> 8) & 1;
+    c.iniX = d.iniX;
+    c.rw = d.rwrh & 0xFFFF;
+    c.rh = d.rwrh >> 16;
+    c.dw = c.rw - 6;
+    c.dh = c.rh - 6;
+    c.out_off = d.out_off;
+    c.xo = d.xoyo & 0xFFFF;
+    c.yo = d.xoyo >> 16;
+    const uint8_t* lp = l == 0 ? frames + (long long)c.f * framePitch : pyr + (long long)c.f * g->pyr_bytes + d.pyr_off;
+    c.stride = l == 0 ? rowStride : d.pitch;
+    c.base = lp + (long long)d.iniY * c.stride;
+    c.aligned = ((reinterpret_cast<uintptr_t>(lp) | (uintptr_t)c.stride) & 3) == 0;
+    c.x0w = c.iniX >> 2;
+    c.nw = ((c.iniX + c.rw + 3) >> 2) - c.x0w;
+    return c;
+}
+
 __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                               long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                               uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
@@ -516,68 +575,64 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
     return ((b0 | b8) & (b4 | b12)) | ((d0 | d8) & (d4 | d12));
 }
 
-template <int TP, int SP>
-__global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
-                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
-                                                   uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
-                                                   int remap) {
-    extern __shared__ __attribute__((aligned(16))) int smem_fast[];
-    uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
-    // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (4 cells each)
-    int blk = blockIdx.x;
-    if (remap) {
-        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-        blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+// optional phase timestamps (ORBGPU_FAST_STAMPS=1): s_memtime at the phase boundaries, lane 0
+#define ORBGPU_STAMP(k) \
+    if (stamps && lane == 0) stamps[(long long)item * 8 + (k)] = __builtin_amdgcn_s_memtime();
+
+// ROI dwords 0..511 of a cell (aligned levels) issued into registers: the loads of the next cell
+// of a wavefront are in flight while the current one is processed.
+__device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uint32_t (&v)[8]) {
+    const int n = c.rh * c.nw;
+    const uint32_t mnw = recip20(c.nw);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int idx = k * 64 + lane;
+        const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
+        v[k] = idx < n ? *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4) : 0u;
     }
-    const int item = blk * 4 + wv;
-    if (item >= total) return;   // whole wave; nothing below uses a block barrier
-    const int wb = g->fast_wave_bytes;
-    uint8_t* tile = smem + (size_t)wv * wb;
-    // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*SP + dx+1]
-    uint8_t* sM = tile + ((g->fast_rows * TP + 16 + 15) & ~15);
-    uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * SP + 15) & ~15));
-    unsigned long long* keepb =
-        reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(sList) + ((g->fast_list * 2 + 15) & ~15));
-    const int tmin = min(g->iniTh, g->minTh);
-    const FastCell c = fast_cell(g, item, frames, framePitch, rowStride, pyr);
-    int* cntOut = cellCount + (long long)c.f * g->ncells + c.cell;
-    if (!c.valid) {
-        if (lane == 0) *cntOut = 0;
-        return;
-    }
-    const int dw = c.dw, dh = c.dh;
-    // ---- ROI -> LDS (rows TP apart), eight dword loads in flight per lane; zero the score map
-    int xoff = 0;
+}
+
+// ROI -> LDS tile (rows TP apart): the prefetched dwords, the remainder of a tall ROI, or bytes
+// for a level whose base / stride is not dword aligned.  Returns the tile column of ROI x = 0.
+template <int TP>
+__device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, const uint32_t (&v)[8], uint8_t* tile) {
     if (c.aligned) {
         const int n = c.rh * c.nw;
         const uint32_t mnw = recip20(c.nw);
-        for (int b0 = 0; b0 < n; b0 += 8 * 64) {
-            uint32_t v[8];
-            int dsto[8];
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int idx = b0 + k * 64 + lane;
-                const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
-                dsto[k] = idx < n ? yy * TP + ww * 4 : -1;
-                v[k] = idx < n ? *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4)
-                               : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (dsto[k] >= 0) *reinterpret_cast<uint32_t*>(&tile[dsto[k]]) = v[k];
+        for (int k = 0; k < 8; k++) {
+            const int idx = k * 64 + lane;
+            const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
+            if (idx < n) *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) = v[k];
         }
-        xoff = c.iniX & 3;
-    } else {
-        const uint32_t mrw = recip20(c.rw);
-        for (int idx = lane; idx < c.rh * c.rw; idx += 64) {
-            const int yy = (int)div20(idx, mrw), xx = idx - yy * c.rw;
-            tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
+        for (int idx = 512 + lane; idx < n; idx += 64) {
+            const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
+            *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) =
+                *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4);
         }
+        return c.iniX & 3;
     }
+    const uint32_t mrw = recip20(c.rw);
+    for (int idx = lane; idx < c.rh * c.rw; idx += 64) {
+        const int yy = (int)div20(idx, mrw), xx = idx - yy * c.rw;
+        tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
+    }
+    return 0;
+}
+
+// One cell after its ROI is in the tile: prefilter, exact arc strength, cell-local NMS with the
+// minThFAST fallback, raster-order emission (see k_fast above for the semantics).
+template <int TP, int SP>
+__device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane, int xoff,
+                                               uint8_t* tile, uint8_t* sM, uint16_t* sList,
+                                               unsigned long long* keepb, uint32_t* __restrict__ cands,
+                                               int* cntOut, unsigned long long* __restrict__ stamps, int item) {
+    const int tmin = min(g->iniTh, g->minTh);
+    const int dw = c.dw, dh = c.dh;
     for (int i = lane; i < (dh + 2) * (SP / 4); i += 64) reinterpret_cast<uint32_t*>(sM)[i] = 0u;
     if (lane < dh) keepb[lane] = 0ull;
     wave_lds_sync();
+    ORBGPU_STAMP(1);
     // ---- stage 1: compass prefilter, 4 pixels per lane in packed 16-bit lanes; lane -> (run, row)
     // fixed for the cell (rows advance by 64 / nruns per iteration), per-bit ballot compaction
     const int nruns = (dw + 3) >> 2;
@@ -621,6 +676,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         }
     }
     wave_lds_sync();
+    ORBGPU_STAMP(2);
     // ---- stage 2: exact arc strength for the survivors; corners at tmin are compacted in place
     // (each chunk is read into registers before any lane writes, and writes land at or before it)
     const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
@@ -639,6 +695,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         ncorner += __popcll(cm);
     }
     wave_lds_sync();
+    ORBGPU_STAMP(3);
     // ---- cell-local NMS at iniThFAST, then the minThFAST fallback if nothing survived (:812-816).
     // Neighbours outside the domain read the zero border; non-corners at th count 0.
     int th = g->iniTh;
@@ -672,19 +729,74 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         th = g->minTh;
     }
     wave_lds_sync();
+    ORBGPU_STAMP(4);
     // ---- emission in raster order: lane = domain row
-    const LevelGeom& L = g->L[c.l];
-    uint32_t* out = cands + (long long)c.f * g->ncand + L.cand_base + (long long)(c.cell - L.cell_base) * L.cell_cap;
+    uint32_t* out = cands + (long long)c.f * g->ncand + c.out_off;
     unsigned long long bits = lane < dh ? keepb[lane] : 0ull;
     int pos = wave_excl_scan(__popcll(bits));
-    const uint32_t yr = (uint32_t)(lane + 3 + c.ci * L.hCell);
+    const uint32_t yr = (uint32_t)(lane + c.yo);
     while (bits) {
         const int dx = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
-        const uint32_t xr = (uint32_t)(dx + 3 + c.cj * L.wCell);
+        const uint32_t xr = (uint32_t)(dx + c.xo);
         out[pos++] = xr | (yr << 12) | ((uint32_t)(sM[(lane + 1) * SP + dx + 1] - 1) << 24);
     }
     if (lane == 0) *cntOut = kept;
+    ORBGPU_STAMP(5);
+}
+
+/* Wave-per-cell form of the same algorithm: a wavefront owns two consecutive (frame, cell) items
+ * (four waves, eight cells per block), so every synchronisation is a wave barrier; the second
+ * cell's ROI loads are issued before the first cell is processed, hiding their latency.  The
+ * per-wave LDS carve is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors
+ * are compacted with per-bit ballots (list order is irrelevant: emission order comes from the keep
+ * bitmap, one 64-bit row mask per domain row, emitted in raster order by one lane per row). */
+template <int TP, int SP>
+__global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
+                                                   const uint8_t* __restrict__ frames,
+                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
+                                                   uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
+                                                   int remap, unsigned long long* __restrict__ stamps) {
+    extern __shared__ __attribute__((aligned(16))) int smem_fast[];
+    uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
+    // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (8 cells each)
+    int blk = blockIdx.x;
+    if (remap) {
+        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int item0 = (blk * 4 + wv) * 2;
+    if (item0 >= total) return;   // whole wave; nothing below uses a block barrier
+    const int wb = g->fast_wave_bytes;
+    uint8_t* tile = smem + (size_t)wv * wb;
+    // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*SP + dx+1]
+    uint8_t* sM = tile + ((g->fast_rows * TP + 16 + 15) & ~15);
+    uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * SP + 15) & ~15));
+    unsigned long long* keepb =
+        reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(sList) + ((g->fast_list * 2 + 15) & ~15));
+    const bool has1 = item0 + 1 < total;
+    const FastCellT c0 = fast_cell_t(g, cells, item0, frames, framePitch, rowStride, pyr);
+    const FastCellT c1 = fast_cell_t(g, cells, has1 ? item0 + 1 : item0, frames, framePitch, rowStride, pyr);
+    uint32_t v0[8], v1[8];
+    if (c0.valid && c0.aligned) fast_roi_issue(c0, lane, v0);
+    if (has1 && c1.valid && c1.aligned) fast_roi_issue(c1, lane, v1);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (k == 1 && !has1) break;
+        const FastCellT& c = k == 0 ? c0 : c1;
+        const int item = item0 + k;
+        int* cntOut = cellCount + (long long)c.f * g->ncells + c.cell;
+        if (!c.valid) {
+            if (lane == 0) *cntOut = 0;
+            continue;
+        }
+        ORBGPU_STAMP(0);
+        wave_lds_sync();   // the previous cell's last LDS reads happen before this one's writes
+        const int xoff = fast_roi_store<TP>(c, lane, k == 0 ? v0 : v1, tile);
+        ORBGPU_STAMP(6);
+        fast_cell_body<TP, SP>(g, c, lane, xoff, tile, sM, sList, keepb, cands, cntOut, stamps, item);
+    }
 }
 
 // Per-wave LDS carve of k_fast_wave.  Cells at most 36 px wide (every BASELINE config) use the
@@ -1357,13 +1469,13 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         hipLaunchKernelGGL(k_fast, dim3(fast_items), dim3(256), 0, stream, b.d_geom, d_frames,
                            frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
     else if (g.fast_compact)
-        hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(fast_items, 4)), dim3(256), (size_t)g.fast_wave_bytes * 4,
-                           stream, b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount,
-                           fast_items, b.fast_remap);
+        hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(fast_items, 8)), dim3(256), (size_t)g.fast_wave_bytes * 4,
+                           stream, b.d_geom, b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands,
+                           b.d_cellCount, fast_items, b.fast_remap, b.d_stamps);
     else
-        hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(fast_items, 4)), dim3(256),
-                           (size_t)g.fast_wave_bytes * 4, stream, b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr,
-                           b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
+        hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(fast_items, 8)), dim3(256),
+                           (size_t)g.fast_wave_bytes * 4, stream, b.d_geom, b.d_cells, d_frames, frame_pitch,
+                           row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap, b.d_stamps);
     if (marker) marker(user, ORB_K_FAST, 0, stream);
     if (marker) marker(user, ORB_K_OCTREE, 1, stream);
     {

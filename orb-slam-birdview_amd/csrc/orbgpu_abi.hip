@@ -208,6 +208,12 @@ int Ctx::ensure_geometry(int W, int H) {
     hipError_t e;
     if ((e = grow(d_geom, geom_cap, 1)) != hipSuccess) return set_error("hipMalloc geom", e), ORB_ERR_NOMEM;
     if ((e = grow(d_rcoef, rcoef_cap, coefs.size())) != hipSuccess) return set_error("hipMalloc coef", e), ORB_ERR_NOMEM;
+    std::vector<CellDesc> cells;
+    build_cells(g, cells);
+    if ((e = grow(d_cells, cells_cap, cells.size())) != hipSuccess) return set_error("hipMalloc cells", e), ORB_ERR_NOMEM;
+    if ((e = hipMemcpyAsync(d_cells, cells.data(), cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice, stream)) !=
+        hipSuccess)
+        return set_error("upload cells", e), ORB_ERR_HIP;
     if ((e = hipMemcpyAsync(d_geom, &g, sizeof g, hipMemcpyHostToDevice, stream)) != hipSuccess)
         return set_error("upload geom", e), ORB_ERR_HIP;
     if ((e = hipMemcpyAsync(d_rcoef, coefs.data(), coefs.size() * sizeof(ResizeCoef), hipMemcpyHostToDevice,
@@ -235,6 +241,8 @@ int Ctx::ensure_frames(int nframes) {
         set_error("device allocation for the extractor", e);
         return ORB_ERR_NOMEM;
     }
+    if (fast_stamps && (e = grow(d_stamps, stamps_cap, (size_t)nframes * g.ncells * 8)) != hipSuccess)
+        return set_error("stamps", e), ORB_ERR_NOMEM;
     // the overflow flag is read by orb_sync even before the first extraction
     if ((e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
     return ORB_OK;
@@ -244,6 +252,7 @@ ExtractBuffers Ctx::buffers() const {
     ExtractBuffers b;
     b.d_geom = d_geom;
     b.d_rcoef = d_rcoef;
+    b.d_cells = d_cells;
     std::memcpy(b.rcoef_off, rcoef_off, sizeof rcoef_off);
     b.d_pyr = d_pyr;
     b.d_cands = d_cands;
@@ -257,6 +266,7 @@ ExtractBuffers Ctx::buffers() const {
     b.resize_direct = resize_direct ? 1 : 0;
     b.resize_th = resize_th;
     b.fast_block = fast_block ? 1 : 0;
+    b.d_stamps = fast_stamps ? d_stamps : nullptr;
     return b;
 }
 
@@ -368,6 +378,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (const char* e = std::getenv("ORBGPU_RESIZE_DIRECT")) c->resize_direct = e[0] == '1';
     if (const char* e = std::getenv("ORBGPU_RESIZE_TH")) c->resize_th = std::atoi(e);
     if (const char* e = std::getenv("ORBGPU_FAST_BLOCK")) c->fast_block = e[0] == '1';
+    if (const char* e = std::getenv("ORBGPU_FAST_STAMPS")) c->fast_stamps = e[0] == '1';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);
@@ -410,7 +421,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.b);
         (void)hipEventDestroy(pr.e);
     }
-    void* bufs[] = {c->d_geom, c->d_rcoef, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
+    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_kps, c->d_desc, c->d_counts,
                     c->d_scratch};
     for (void* b : bufs)
@@ -560,6 +571,15 @@ int orb_get_level(orb_ctx* h, int level, const uint8_t** data, int* w, int* hgt,
     *hgt = lh;
     if (stride) *stride = (size_t)lw;
     return ORB_OK;
+}
+
+int orb_debug_fast_stamps(orb_ctx* h, uint64_t* out, int cap) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (!c->fast_stamps || !c->d_stamps) return 0;
+    const int n = std::min((int)c->stamps_cap, cap);
+    hipError_t e = hipMemcpy(out, c->d_stamps, (size_t)n * 8, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? n : ORB_ERR_HIP;
 }
 
 int orb_debug_level_image(orb_ctx* h, int frame, int level, uint8_t* out, int* w, int* hgt) {

@@ -22,6 +22,9 @@ struct Ctx {
     bool resize_direct = false;   // ORBGPU_RESIZE_DIRECT=1 forces the untiled resize kernel (A/B switch)
     int resize_th = 16;           // rows per resize tile (ORBGPU_RESIZE_TH = 16 | 32 | 64; 16 measured fastest)
     bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
+    bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: k_fast_wave records phase timestamps (diagnostic)
+    unsigned long long* d_stamps = nullptr;
+    size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
     // a batch of frames is split over `nsub` streams so that one sub-batch's low-occupancy phases
     // (short pyramid levels, the per-level octree) overlap another's kernels (ORBGPU_STREAMS, 1..4)
@@ -45,6 +48,8 @@ struct Ctx {
     size_t geom_cap = 0;
     ResizeCoef* d_rcoef = nullptr;
     size_t rcoef_cap = 0;
+    CellDesc* d_cells = nullptr;
+    size_t cells_cap = 0;
 
     // extractor work buffers (capacities in elements)
     uint8_t* d_pyr = nullptr;

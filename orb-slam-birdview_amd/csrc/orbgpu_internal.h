@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/orbgpu.h"
 
 namespace orbgpu {
@@ -64,6 +66,18 @@ struct Geom {
     LevelGeom L[ORBGPU_MAX_LEVELS];
 };
 
+// Per-cell descriptor of the FAST grid (host-built once per image size; k_fast_wave reads one per
+// wavefront with a single scalar load instead of decoding the cell from the level tables).
+struct CellDesc {
+    int lv;        // level | valid << 8
+    int iniX, iniY;
+    int rwrh;      // ROI width | height << 16 (clipped, ORBextractor.cc:791-806)
+    int out_off;   // first candidate slot of the cell within a frame
+    int xoyo;      // output coordinate offsets (3 + cj*wCell) | (3 + ci*hCell) << 16 (:822-823)
+    int pitch;     // level row pitch (levels >= 1)
+    int pyr_off;   // level offset in a frame's pyramid slot (levels >= 1)
+};
+
 // cv::resize INTER_LINEAR coefficient tables (OpenCV 3.2 imgwarp.cpp), one entry per dst column/row.
 struct ResizeCoef {
     int s0, s1;          // source column/row indices (clamped)
@@ -74,6 +88,7 @@ struct ResizeCoef {
 struct ExtractBuffers {
     const Geom* d_geom;
     const ResizeCoef* d_rcoef;     // per level: w_l x-coefs then h_l y-coefs, at rcoef_off[l]
+    const CellDesc* d_cells;       // ncells FAST cell descriptors
     int rcoef_off[ORBGPU_MAX_LEVELS];
     uint8_t* d_pyr;                // nframes * pyr_bytes
     uint32_t* d_cands;             // nframes * ncand
@@ -87,6 +102,7 @@ struct ExtractBuffers {
     int resize_direct;             // force the untiled k_resize (A/B switch, ORBGPU_RESIZE_DIRECT=1)
     int resize_th;                 // output rows per k_resize_tiled tile: 16, 32 or 64 (ORBGPU_RESIZE_TH)
     int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
+    unsigned long long* d_stamps;  // k_fast_wave phase timestamps, 8 per (frame, cell) (ORBGPU_FAST_STAMPS=1)
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin, hipStream_t stream);
@@ -153,5 +169,6 @@ hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L,
 
 size_t octree_lds_bytes(int node_cap);
 void fast_wave_layout(Geom& g);   // fills fast_rows/drows/list/wave_bytes from the level grids
+void build_cells(const Geom& g, std::vector<CellDesc>& cells);
 
 }  // namespace orbgpu
