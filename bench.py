@@ -169,6 +169,8 @@ def main():
 
     rank, world, local = dist_env()
     dist = dist_init(world)
+    if os.environ.get("ORBGPU_BENCH_ONE_DEVICE") == "1":   # rehearsal of the N-rank path on a 1-GPU box
+        local = 0
     import numpy as np
     import orbgpu
     from orbgpu.synth import synth_batch
