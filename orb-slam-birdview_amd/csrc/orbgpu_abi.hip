@@ -514,22 +514,41 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, c->d_kps, c->d_desc, c->d_counts,
                              kcap)) != ORB_OK)
         return st;
-    int nk = 0;
-    if ((e = hipMemcpyAsync(&nk, c->d_counts, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+    // one download into pinned staging: count, overflow flag, and every keypoint / descriptor slot
+    // (at most kcap * 60 bytes), then a single synchronisation
+    const size_t need = 16 + (size_t)kcap * (sizeof(orb_keypoint) + 32);
+    if (need > c->pinned_cap) {
+        if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+        c->h_pinned = nullptr;
+        c->pinned_cap = 0;
+        if ((e = hipHostMalloc(&c->h_pinned, need, hipHostMallocDefault)) != hipSuccess)
+            return set_error("pinned staging", e), ORB_ERR_NOMEM;
+        c->pinned_cap = need;
+    }
+    uint8_t* hp = static_cast<uint8_t*>(c->h_pinned);
+    int* hcnt = reinterpret_cast<int*>(hp);
+    orb_keypoint* hk = reinterpret_cast<orb_keypoint*>(hp + 16);
+    uint8_t* hd = hp + 16 + (size_t)kcap * sizeof(orb_keypoint);
+    if ((e = hipMemcpyAsync(hcnt, c->d_counts, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(hcnt + 1, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(hk, c->d_kps, (size_t)kcap * sizeof(orb_keypoint), hipMemcpyDeviceToHost, c->stream)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(hd, c->d_desc, (size_t)kcap * 32, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return set_error("download count", e), ORB_ERR_HIP;
-    if ((st = orb_sync(h)) != ORB_OK) return st;
+        return set_error("download keypoints", e), ORB_ERR_HIP;
+    if (hcnt[1]) {
+        set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
+        return ORB_ERR_INTERNAL;
+    }
+    const int nk = hcnt[0];
     if (nk > cap || !kps || !desc) {
         *n = nk;
         set_error("orb_extract: output capacity too small", hipSuccess);
         return ORB_ERR_CAPACITY;
     }
     if (nk > 0) {
-        if ((e = hipMemcpyAsync(kps, c->d_kps, (size_t)nk * sizeof(orb_keypoint), hipMemcpyDeviceToHost, c->stream)) !=
-                hipSuccess ||
-            (e = hipMemcpyAsync(desc, c->d_desc, (size_t)nk * 32, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-            return set_error("download keypoints", e), ORB_ERR_HIP;
+        std::memcpy(kps, hk, (size_t)nk * sizeof(orb_keypoint));
+        std::memcpy(desc, hd, (size_t)nk * 32);
     }
     *n = nk;
     return ORB_OK;

@@ -78,7 +78,8 @@ struct Ctx {
     size_t desc_cap = 0;
     int* d_counts = nullptr;
     size_t counts_cap = 0;
-    void* h_pinned = nullptr;
+    void* h_pinned = nullptr;     // pinned staging for orb_extract's single download (count, flag, keypoints, descriptors)
+    size_t pinned_cap = 0;
 
     std::vector<int2> frames_host;   // staging for orb_hamming_top2_frames_device pair lists
     // matcher scratch arena (bytes)
