@@ -86,7 +86,7 @@ int orb_get_level(orb_ctx* ctx, int level, const uint8_t** data, int* w, int* h,
 
 /* ---- device-resident batched path (bench, multi-camera streams). Asynchronous on the context
  * stream; call orb_sync before reading outputs. d_frames: nframes gray frames, frame f at
- * d_frames + f*frame_pitch, rows `row_stride` apart.  Outputs: frame f's keypoints at
+ * d_frames + f*frame_pitch, rows `row_stride` apart (w <= row_stride < 16 MiB).  Outputs: frame f's keypoints at
  * d_kps + f*kp_cap, descriptors at d_desc + f*kp_cap*32, count in d_counts[f].
  * kp_cap must be >= orb_batch_kp_cap(ctx, w, h). ---- */
 int orb_batch_kp_cap(orb_ctx* ctx, int w, int h);

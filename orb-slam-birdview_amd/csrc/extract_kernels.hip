@@ -107,9 +107,9 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
     for (int i = 0; i < 4; i++) {
         const int x = min(x0 + i, dw - 1);
         const ResizeCoef cx = coef[x];
-        const int h0 = r0[cx.s0] * cx.c0 + r0[cx.s1] * cx.c1;
-        const int h1 = r1[cx.s0] * cx.c0 + r1[cx.s1] * cx.c1;
-        const int v = (((cy.c0 * (h0 >> 4)) >> 16) + ((cy.c1 * (h1 >> 4)) >> 16) + 2) >> 2;
+        const unsigned h0 = __umul24(r0[cx.s0], (unsigned)cx.c0) + __umul24(r0[cx.s1], (unsigned)cx.c1);
+        const unsigned h1 = __umul24(r1[cx.s0], (unsigned)cx.c0) + __umul24(r1[cx.s1], (unsigned)cx.c1);
+        const unsigned v = ((__umul24((unsigned)cy.c0, h0 >> 4) >> 16) + (__umul24((unsigned)cy.c1, h1 >> 4) >> 16) + 2) >> 2;
         packed |= (uint32_t)v << (8 * i);
     }
     // the pitch is a multiple of 64, so the dword never leaves the row (pad bytes are never read)
@@ -117,17 +117,21 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
     *reinterpret_cast<uint32_t*>(dst + (long long)y * g->L[level].pitch + x0) = packed;
 }
 
-/* Same arithmetic, LDS-tiled: a block produces a 128 x 16 output tile.  The tile's source span
- * (<= 268 x 40 bytes, checked on the host: LevelGeom::rs_tiled) is staged with coalesced dword loads
- * (byte loads if the level base/stride is not dword aligned), the coefficients of the tile's
- * columns/rows are staged once, and each thread then produces 4 output pixels per row pass
- * (one dword store) from LDS byte reads. */
+/* Same arithmetic, LDS-tiled: a block produces a 128 x TH output tile.  The tile's source span
+ * (<= 272 x (2*TH+8) bytes from a 16-byte aligned column, checked on the host: LevelGeom::rs_tiled)
+ * is staged with 16-byte loads, all issued before the first wait (dword / byte loads if the level
+ * base or stride is not 16-byte aligned), the coefficients of the tile's columns/rows are staged
+ * once, and each thread then produces 4 output pixels per row pass (one dword store) from LDS byte
+ * reads. */
 template <int kRsTileH>
 __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
                                                       const ResizeCoef* __restrict__ coef, int level,
                                                       const uint8_t* __restrict__ frames, long long framePitch,
                                                       int rowStride, uint8_t* __restrict__ pyr) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[rs_rows(kRsTileH) * kRsPitch];
+    constexpr int kRows = rs_rows(kRsTileH);
+    constexpr int kQ = kRsPitch / 16;                                  // 16-byte chunks per LDS row
+    constexpr int kPer = (kRows * kQ + 255) / 256;                     // chunks per thread (upper bound)
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[kRows * kRsPitch];
     __shared__ int4 s_cx[kRsTileW];
     __shared__ int4 s_cy[kRsTileH];
     const int f = blockIdx.z;
@@ -136,53 +140,98 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
     const int tid = threadIdx.x;
     const LevelPtr src = level_ptr(g, level - 1, frames, framePitch, rowStride, pyr, f);
     const int nx = min(kRsTileW, dw - x0), ny = min(kRsTileH, dh - y0);
-    if (tid < kRsTileW) {
-        const ResizeCoef c = coef[x0 + min(tid, nx - 1)];
-        s_cx[tid] = make_int4(c.s0, c.s1, c.c0, c.c1);
-    }
-    for (int i = tid; i < kRsTileH; i += 256) {
-        const ResizeCoef c = coef[dw + y0 + min(i, ny - 1)];
-        s_cy[i] = make_int4(c.s0, c.s1, c.c0, c.c1);
-    }
-    // source span (the coefficient tables are monotone)
-    const int sx0 = coef[x0].s0 & ~3, sx1 = coef[x0 + nx - 1].s1;
+    // source span (the coefficient tables are monotone); wave-uniform, so these are scalar loads
+    const bool vec16 = ((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 15) == 0;
+    const int sx0 = coef[x0].s0 & (vec16 ? ~15 : ~3), sx1 = coef[x0 + nx - 1].s1;
     const int sy0 = coef[dw + y0].s0, sy1 = coef[dw + y0 + ny - 1].s1;
-    const int nw = (sx1 - sx0 + 4) >> 2, nr = sy1 - sy0 + 1;
+    const int nr = sy1 - sy0 + 1;
     const uint8_t* base = src.p + (long long)sy0 * src.stride + sx0;
-    if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
-        for (int i = tid; i < nr * 68; i += 256) {   // 68 dwords per LDS row
-            const int r = i / 68, wd = i - r * 68;
-            if (wd < nw)
-                *reinterpret_cast<uint32_t*>(&s_src[r * kRsPitch + 4 * wd]) =
-                    *reinterpret_cast<const uint32_t*>(base + (long long)r * src.stride + 4 * wd);
+    int4 cxv = make_int4(0, 0, 0, 0), cyv = make_int4(0, 0, 0, 0);
+    if (vec16) {
+        const int nq = ((sx1 - sx0) >> 4) + 1;
+        const unsigned magic = (65536u + nq - 1) / nq;                  // i / nq for i < 4096, nq <= 17
+        const int total = nr * nq;
+        uint4 v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {   // unconditional (clamped) loads: all in flight before the first wait
+            const int i = min(tid + 256 * k, total - 1);
+            const int r = (int)(((unsigned)i * magic) >> 16), q = i - r * nq;
+            v[k] = reinterpret_cast<const uint4*>(base + (long long)r * src.stride)[q];
+        }
+        if (tid < kRsTileW) {
+            const ResizeCoef c = coef[x0 + min(tid, nx - 1)];
+            cxv = make_int4(c.s0, c.s1, c.c0, c.c1);
+        }
+        if (tid < kRsTileH) {
+            const ResizeCoef c = coef[dw + y0 + min(tid, ny - 1)];
+            cyv = make_int4(c.s0, c.s1, c.c0, c.c1);
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {   // clamped duplicates store the same bytes to the same place
+            const int i = min(tid + 256 * k, total - 1);
+            const int r = (int)(((unsigned)i * magic) >> 16), q = i - r * nq;
+            *reinterpret_cast<uint4*>(&s_src[r * kRsPitch + 16 * q]) = v[k];
         }
     } else {
-        const int nb = sx1 - sx0 + 1;
-        for (int i = tid; i < nr * kRsPitch; i += 256) {
-            const int r = i / kRsPitch, b = i - r * kRsPitch;
-            if (b < nb) s_src[r * kRsPitch + b] = base[(long long)r * src.stride + b];
+        if (tid < kRsTileW) {
+            const ResizeCoef c = coef[x0 + min(tid, nx - 1)];
+            cxv = make_int4(c.s0, c.s1, c.c0, c.c1);
+        }
+        if (tid < kRsTileH) {
+            const ResizeCoef c = coef[dw + y0 + min(tid, ny - 1)];
+            cyv = make_int4(c.s0, c.s1, c.c0, c.c1);
+        }
+        if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
+            const int nw = (sx1 - sx0 + 4) >> 2;
+            for (int i = tid; i < nr * 68; i += 256) {   // 68 dwords per LDS row
+                const int r = i / 68, wd = i - r * 68;
+                if (wd < nw)
+                    *reinterpret_cast<uint32_t*>(&s_src[r * kRsPitch + 4 * wd]) =
+                        *reinterpret_cast<const uint32_t*>(base + (long long)r * src.stride + 4 * wd);
+            }
+        } else {
+            const int nb = sx1 - sx0 + 1;
+            for (int i = tid; i < nr * kRsPitch; i += 256) {
+                const int r = i / kRsPitch, b = i - r * kRsPitch;
+                if (b < nb) s_src[r * kRsPitch + b] = base[(long long)r * src.stride + b];
+            }
         }
     }
+    if (tid < kRsTileW) s_cx[tid] = cxv;
+    if (tid < kRsTileH) s_cy[tid] = cyv;
     __syncthreads();
+    // Weights are <= 2048 and pixels <= 255, so every product fits 24-bit multiplies (full rate;
+    // a 32-bit v_mul_lo is quarter rate).  s_cx / s_cy hold clamped entries for the whole tile.
     const int tx = (tid & 31) * 4;
-    uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off;
+    int o0[4], o1[4];
+    unsigned c0[4], c1[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int4 cx = s_cx[tx + i];
+        o0[i] = cx.x - sx0;
+        o1[i] = cx.y - sx0;
+        c0[i] = cx.z;
+        c1[i] = cx.w;
+    }
+    uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off + x0 + tx;
+    const int pitch = g->L[level].pitch;
+    if (tx >= nx) return;
 #pragma unroll
     for (int pass = 0; pass < kRsTileH / 8; pass++) {
         const int ty = pass * 8 + (tid >> 5);
-        if (ty >= ny || tx >= nx) continue;
+        if (ty >= ny) break;
         const int4 cy = s_cy[ty];
-        const uint8_t* r0 = &s_src[(cy.x - sy0) * kRsPitch - sx0];
-        const uint8_t* r1 = &s_src[(cy.y - sy0) * kRsPitch - sx0];
+        const uint8_t* r0 = &s_src[(cy.x - sy0) * kRsPitch];
+        const uint8_t* r1 = &s_src[(cy.y - sy0) * kRsPitch];
         uint32_t packed = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int4 cx = s_cx[min(tx + i, nx - 1)];
-            const int h0 = r0[cx.x] * cx.z + r0[cx.y] * cx.w;
-            const int h1 = r1[cx.x] * cx.z + r1[cx.y] * cx.w;
-            const int v = (((cy.z * (h0 >> 4)) >> 16) + ((cy.w * (h1 >> 4)) >> 16) + 2) >> 2;
-            packed |= (uint32_t)v << (8 * i);
+            const unsigned h0 = __umul24(r0[o0[i]], c0[i]) + __umul24(r0[o1[i]], c1[i]);
+            const unsigned h1 = __umul24(r1[o0[i]], c0[i]) + __umul24(r1[o1[i]], c1[i]);
+            const unsigned v = ((__umul24((unsigned)cy.z, h0 >> 4) >> 16) + (__umul24((unsigned)cy.w, h1 >> 4) >> 16) + 2) >> 2;
+            packed |= v << (8 * i);
         }
-        *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + ty) * g->L[level].pitch + x0 + tx) = packed;
+        *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + ty) * pitch) = packed;
     }
 }
 
@@ -351,6 +400,12 @@ void build_cells(const Geom& g, std::vector<CellDesc>& cells) {
     }
 }
 
+// Byte offset of row yy at column byte cb (yy, stride < 2^24, yy * stride < 2^32): one 24-bit multiply
+// (full rate) instead of 64-bit address arithmetic (quarter-rate v_mul_lo_u32 / v_mad_u64_u32).
+__device__ __forceinline__ unsigned roi_off(int yy, int stride, int cb) {
+    return __umul24((unsigned)yy, (unsigned)stride) + (unsigned)cb;
+}
+
 struct FastCellT {
     int f, cell, iniX, rw, rh, dw, dh, x0w, nw, out_off, xo, yo;
     bool valid, aligned;
@@ -417,13 +472,13 @@ __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const 
         for (int idx = tid; idx < c.rh * c.nw; idx += 256) {
             const int yy = idx / c.nw, ww = idx - yy * c.nw;
             *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) =
-                *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4);
+                *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + ww) * 4));
         }
         xoff = c.iniX & 3;
     } else {
         for (int idx = tid; idx < c.rh * c.rw; idx += 256) {
             const int yy = idx / c.rw, xx = idx - yy * c.rw;
-            tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
+            tile[yy * TP + xx] = c.base[roi_off(yy, c.stride, c.iniX + xx)];
         }
     }
     if (tid == 0) s_cnt = 0;
@@ -587,8 +642,8 @@ __device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uin
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         const int idx = k * 64 + lane;
-        const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
-        v[k] = idx < n ? *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4) : 0u;
+        const int yy = (int)div20(idx, mnw), ww = idx - (int)__umul24((unsigned)yy, (unsigned)c.nw);
+        v[k] = idx < n ? *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + ww) * 4)) : 0u;
     }
 }
 
@@ -602,20 +657,20 @@ __device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, cons
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const int idx = k * 64 + lane;
-            const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
+            const int yy = (int)div20(idx, mnw), ww = idx - (int)__umul24((unsigned)yy, (unsigned)c.nw);
             if (idx < n) *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) = v[k];
         }
         for (int idx = 512 + lane; idx < n; idx += 64) {
-            const int yy = (int)div20(idx, mnw), ww = idx - yy * c.nw;
+            const int yy = (int)div20(idx, mnw), ww = idx - (int)__umul24((unsigned)yy, (unsigned)c.nw);
             *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) =
-                *reinterpret_cast<const uint32_t*>(c.base + (long long)yy * c.stride + (c.x0w + ww) * 4);
+                *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + ww) * 4));
         }
         return c.iniX & 3;
     }
     const uint32_t mrw = recip20(c.rw);
     for (int idx = lane; idx < c.rh * c.rw; idx += 64) {
-        const int yy = (int)div20(idx, mrw), xx = idx - yy * c.rw;
-        tile[yy * TP + xx] = c.base[(long long)yy * c.stride + c.iniX + xx];
+        const int yy = (int)div20(idx, mrw), xx = idx - (int)__umul24((unsigned)yy, (unsigned)c.rw);
+        tile[yy * TP + xx] = c.base[roi_off(yy, c.stride, c.iniX + xx)];
     }
     return 0;
 }
@@ -1229,8 +1284,8 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
 #pragma unroll
         for (int r = 0; r < 9; r++) {   // 43 rows x 12 dwords = 516 <= 9 x 64, all loads in flight
             const int idx = lane + 64 * r;
-            const int wy = idx / 12, ww = idx - wy * 12;
-            v[r] = idx < kDescWin * 12 ? *reinterpret_cast<const uint32_t*>(row0 + (long long)wy * src.stride + 4 * ww)
+            const int wy = (int)(__umul24((unsigned)idx, 2731u) >> 15), ww = idx - wy * 12;   // idx / 12, idx < 576
+            v[r] = idx < kDescWin * 12 ? *reinterpret_cast<const uint32_t*>(row0 + roi_off(wy, src.stride, 4 * ww))
                                       : 0u;
         }
 #pragma unroll
@@ -1244,16 +1299,16 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
 #pragma unroll
         for (int r = 0; r < 29; r++) {   // 43*43 = 1849 <= 29 x 64
             const int idx = lane + 64 * r;
-            const int wy = idx / kDescWin, wx = idx - wy * kDescWin;
+            const int wy = (int)(__umul24((unsigned)idx, 24386u) >> 20), wx = idx - wy * kDescWin;   // idx / 43
             int sy = y - 21 + wy, sx = x - 21 + wx;
             sy = sy < 0 ? -sy : (sy >= L.h ? 2 * L.h - 2 - sy : sy);
             sx = sx < 0 ? -sx : (sx >= L.w ? 2 * L.w - 2 - sx : sx);
-            v[r] = idx < kDescWin * kDescWin ? src.p[(long long)sy * src.stride + sx] : (uint8_t)0;
+            v[r] = idx < kDescWin * kDescWin ? src.p[roi_off(sy, src.stride, sx)] : (uint8_t)0;
         }
 #pragma unroll
         for (int r = 0; r < 29; r++) {
             const int idx = lane + 64 * r;
-            const int wy = idx / kDescWin, wx = idx - wy * kDescWin;
+            const int wy = (int)(__umul24((unsigned)idx, 24386u) >> 20), wx = idx - wy * kDescWin;
             if (idx < kDescWin * kDescWin) wbase[wy * kDescWinPitch + wx] = v[r];
         }
         sh = 0;
@@ -1324,11 +1379,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                 r01 = P[j] * K[j] + r01;
                 r23 = P[j + 2] * K[j] + r23;
             }
-            const int rx = 4 * gq;
-            rt[(rx + 0) * kRtPitch + wy] = r01.x;
-            rt[(rx + 1) * kRtPitch + wy] = r01.y;
-            rt[(rx + 2) * kRtPitch + wy] = r23.x;
-            rt[(rx + 3) * kRtPitch + wy] = r23.y;
+            uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy;   // RT[4gq + j][wy]
+            rq[0 * kRtPitch] = r01.x;
+            rq[1 * kRtPitch] = r01.y;
+            rq[2 * kRtPitch] = r23.x;
+            rq[3 * kRtPitch] = r23.y;
         }
     }
     wave_lds_sync();
@@ -1350,7 +1405,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         outa[r] = -1;
         if (it < kDescBlur * 10) {
             const int bx = it / 10, gq = it - bx * 10;
-            const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + bx * kRtPitch + 4 * gq);
+            const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + __umul24((unsigned)bx, (unsigned)kRtPitch) + 4 * gq);
             ushort2_t D[5];
 #pragma unroll
             for (int i = 0; i < 5; i++) D[i] = __builtin_bit_cast(ushort2_t, rp[i]);
@@ -1373,7 +1428,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                 packed |= v << (8 * o);
             }
             outw[r] = packed;
-            outa[r] = (bx * kDescBlurPitch + 4 * gq) >> 2;
+            outa[r] = (int)(__umul24((unsigned)bx, (unsigned)kDescBlurPitch) + 4 * gq) >> 2;
         }
     }
     wave_lds_sync();   // every lane has finished reading the window before it is overwritten
@@ -1398,8 +1453,8 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         const float px1 = (float)pp.z, py1 = (float)pp.w;
         const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
         const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
-        const int t0 = ctr[__float2int_rn(u2 - u3) * kDescBlurPitch + __float2int_rn(u0 + u1)];
-        const int t1 = ctr[__float2int_rn(w2 - w3) * kDescBlurPitch + __float2int_rn(w0 + w1)];
+        const int t0 = ctr[__mul24(__float2int_rn(u2 - u3), kDescBlurPitch) + __float2int_rn(u0 + u1)];
+        const int t1 = ctr[__mul24(__float2int_rn(w2 - w3), kDescBlurPitch) + __float2int_rn(w0 + w1)];
         const unsigned long long m = __ballot(t0 < t1);
         if (lane == 0) dst[gq] = m;
     }

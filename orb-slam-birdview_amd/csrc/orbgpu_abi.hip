@@ -128,7 +128,7 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
             bool xfits = true;
             for (int x0 = 0; x0 < L.w && xfits; x0 += kRsTileW) {
                 const int x1 = std::min(x0 + kRsTileW, L.w) - 1;
-                xfits = cx[x1].s1 - (cx[x0].s0 & ~3) + 1 <= kRsPitch - 4;
+                xfits = cx[x1].s1 - (cx[x0].s0 & ~15) + 1 <= kRsPitch;   // 16-byte aligned span start
             }
             L.rs_tiled = 0;
             for (int i = 0; i < 3 && xfits; i++) {
@@ -465,7 +465,8 @@ int orb_extract_batch_device(orb_ctx* h, const uint8_t* d_frames, int nframes, i
                              size_t row_stride, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int kp_cap) {
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
-    if (!d_frames || nframes <= 0 || !d_kps || !d_desc || !d_counts || row_stride < (size_t)w)
+    if (!d_frames || nframes <= 0 || !d_kps || !d_desc || !d_counts || row_stride < (size_t)w ||
+        row_stride >= (size_t)1 << 24)   // kernels form row offsets with 24-bit multiplies
         return set_error("orb_extract_batch_device: bad arguments", hipSuccess), ORB_ERR_ARG;
     int st = c->ensure_geometry(w, hgt);
     if (st != ORB_OK) return st;

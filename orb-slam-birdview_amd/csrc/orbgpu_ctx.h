@@ -20,7 +20,7 @@ struct Ctx {
     int num_cu = 256;
     bool fast_remap = true;   // ORBGPU_FAST_REMAP=0 disables the XCD-contiguous cell remap (A/B switch)
     bool resize_direct = false;   // ORBGPU_RESIZE_DIRECT=1 forces the untiled resize kernel (A/B switch)
-    int resize_th = 16;           // rows per resize tile (ORBGPU_RESIZE_TH = 16 | 32 | 64; 16 measured fastest)
+    int resize_th = 32;           // rows per resize tile (ORBGPU_RESIZE_TH = 16 | 32 | 64; 32 measured fastest)
     bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
     bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: k_fast_wave records phase timestamps (diagnostic)
     unsigned long long* d_stamps = nullptr;

@@ -23,7 +23,7 @@ constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
 constexpr int kRtPitch = 50;          // k_describe row-pass sums, u16 per transposed row
 constexpr int kRsTileW = 128;         // k_resize_tiled<TH>: output tile 128 x TH, 4 px per thread
-constexpr int kRsPitch = 272;         // LDS source tile: up to 268 bytes x (2*TH + 8) rows (scale factors <= 2)
+constexpr int kRsPitch = 272;         // LDS source tile: up to 272 bytes (from a 16-B aligned column) x (2*TH + 8) rows
 constexpr int rs_rows(int th) { return 2 * th + 8; }
 
 // Per-level geometry (host-computed once per image size; lives in device memory).
