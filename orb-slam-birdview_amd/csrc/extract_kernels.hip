@@ -37,51 +37,6 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
 }
 
-// Exclusive block scan of one int per thread; sc needs (waves+1) ints. Ends with a barrier.
-__device__ int block_excl_scan(int v, int* sc, int& total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) sc[wave] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int i = 0; i < nw; i++) {
-            int t = sc[i];
-            sc[i] = acc;
-            acc += t;
-        }
-        sc[nw] = acc;
-    }
-    __syncthreads();
-    const int r = x - v + sc[wave];
-    total = sc[nw];
-    __syncthreads();
-    return r;
-}
-
-// In-place exclusive scan of arr[0..n) by the whole block (contiguous chunk per thread).
-__device__ int block_scan_array(int* arr, int n, int* sc) {
-    const int nt = blockDim.x;
-    const int chunk = (n + nt - 1) / nt;
-    const int s0 = threadIdx.x * chunk, s1 = min(s0 + chunk, n);
-    int local = 0;
-    for (int i = s0; i < s1; i++) local += arr[i];
-    int total;
-    int run = block_excl_scan(local, sc, total);
-    for (int i = s0; i < s1; i++) {
-        int t = arr[i];
-        arr[i] = run;
-        run += t;
-    }
-    __syncthreads();
-    return total;
-}
-
 }  // namespace
 
 /* ------------------------------------------------------------------------------------------------
@@ -415,10 +370,10 @@ struct FastCellT {
 
 __device__ __forceinline__ FastCellT fast_cell_t(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                  int item, const uint8_t* frames, long long framePitch, int rowStride,
-                                                 const uint8_t* pyr) {
-    FastCellT c;
-    c.f = item / g->ncells;
-    c.cell = item - c.f * g->ncells;
+                                                 const uint8_t* pyr, int cbeg, int cnum) {
+    FastCellT c;   // items cover cells [cbeg, cbeg + cnum) of every frame
+    c.f = item / cnum;
+    c.cell = cbeg + item - c.f * cnum;
     const CellDesc d = cells[c.cell];   // one scalar load
     const int l = d.lv & 0xFF;
     c.valid = (d.lv >> 8) & 1;
@@ -601,11 +556,19 @@ __device__ __forceinline__ int wave_excl_scan(int v) {
     return x - v;
 }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+// Wavefront inclusive scan with DPP: row_shr 1/2/4/8 inside each 16-lane row (zero fill at the row
+// start), then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the row totals.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    return x;
 }
+
+__device__ __forceinline__ int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
 
 // q = x / n for x < 2^20 / n via a 20-bit reciprocal (wave-uniform n <= 64): two VALU ops, exact.
 __device__ __forceinline__ uint32_t recip20(uint32_t n) { return ((1u << 20) + n - 1) / n; }
@@ -811,7 +774,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
-                                                   int remap, unsigned long long* __restrict__ stamps) {
+                                                   int cbeg, int cnum, int remap, unsigned long long* __restrict__ stamps) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
@@ -831,8 +794,8 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     unsigned long long* keepb =
         reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(sList) + ((g->fast_list * 2 + 15) & ~15));
     const bool has1 = item0 + 1 < total;
-    const FastCellT c0 = fast_cell_t(g, cells, item0, frames, framePitch, rowStride, pyr);
-    const FastCellT c1 = fast_cell_t(g, cells, has1 ? item0 + 1 : item0, frames, framePitch, rowStride, pyr);
+    const FastCellT c0 = fast_cell_t(g, cells, item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
+    const FastCellT c1 = fast_cell_t(g, cells, has1 ? item0 + 1 : item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
     uint32_t v0[8], v1[8];
     if (c0.valid && c0.aligned) fast_roi_issue(c0, lane, v0);
     if (has1 && c1.valid && c1.aligned) fast_roi_issue(c1, lane, v1);
@@ -906,21 +869,61 @@ __device__ __forceinline__ void child_rect(uint32_t rx, uint32_t ry, int q, uint
     cry = (uint32_t)cy0 | ((uint32_t)cy1 << 16);
 }
 
-__global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restrict__ g,
-                                                           const uint32_t* __restrict__ cands,
-                                                           const int* __restrict__ cellCount,
-                                                           uint32_t* __restrict__ keysAll,
-                                                           uint16_t* __restrict__ knodeAll,
-                                                           uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
-                                                           int* __restrict__ err, int lds_keys) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
+// Exclusive scan over the k_octree block with one barrier: wave totals go to one of two 16-int
+// buffers (`par` flips on every call, which every thread makes in the same order), and every thread
+// adds the totals of the waves before its own.  The buffer written by call k+2 was last read in
+// call k, before every thread reached call k+1's barrier, so no trailing barrier is needed.
+__device__ __forceinline__ int oct_scan(int v, int* sc, int& par, int& total) {
+    constexpr int NW = kOctreeThreads / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = wave_incl_scan(v);
+    int* buf = sc + 16 * par;
+    par ^= 1;
+    if (lane == 63) buf[wave] = x;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        const int t = buf[i];
+        pre += i < wave ? t : 0;
+        tot += t;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
+// Wave-aggregated LDS counter add: one atomic per distinct target in the wave (LDS atomics from many
+// lanes to one address serialise at ~2 cycles per lane).  Uniform control flow required.
+__device__ __forceinline__ void wave_agg_add(int* ctr, bool ok, int tgt) {
+    unsigned long long pending = __ballot(ok);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int tl = __builtin_amdgcn_readlane(tgt, leader);
+        const unsigned long long m = __ballot(ok && tgt == tl);
+        if ((int)(threadIdx.x & 63) == leader) atomicAdd(&ctr[tl], __popcll(m));
+        pending &= ~m;
+    }
+}
+
+__device__ __forceinline__ int quad_mask(const int* qd) {
+    return (qd[0] > 0) | ((qd[1] > 0) << 1) | ((qd[2] > 0) << 2) | ((qd[3] > 0) << 3);
+}
+
+// One (frame, level) of DistributeOctTree once the candidate count C is known.  KeysInLds selects
+// whether keys / knode live in LDS (after the node tables) or in the per-level global scratch; the
+// two instantiations let the compiler use ds_* or global_* accesses instead of flat ones.
+template <bool KeysInLds>
+__device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const LevelGeom& L, int f, int l, int* smem,
+                                             int C, const int* __restrict__ cc, const uint32_t* __restrict__ cs,
+                                             uint32_t* keys, uint16_t* knode, uint32_t* __restrict__ lvlKps,
+                                             int* __restrict__ lvlCount, int* __restrict__ err, int par,
+                                             unsigned long long* __restrict__ ost) {
     const int NC = g->node_cap;
     const int tid = threadIdx.x;
     constexpr int NT = kOctreeThreads;
-    // frames along x so that every frame's level-0 block (the longest) is dispatched first
-    const int f = blockIdx.x, l = blockIdx.y;
-    const LevelGeom& L = g->L[l];
-    // LDS carve: A table, B table (also the sort buffer), quad, rank, info, ord, nchr, scalars.
+    // LDS carve: tables P and Q (ping-pong: A = current list, B = next), quad, rank, info, ord, nchr,
+    // scan buffers, scalars.  Phase 2's dense sort keys alias B's rx/ry, its per-rank d / prefix
+    // alias B's cnt/seq (all consumed before B is written).
     uint32_t* rxA = (uint32_t*)smem;
     uint32_t* ryA = rxA + NC;
     int* cntA = (int*)(ryA + NC);
@@ -929,52 +932,71 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
     uint32_t* ryB = rxB + NC;
     int* cntB = (int*)(ryB + NC);
     int* seqB = cntB + NC;
-    int* quad = seqB + NC;        // 4*NC
-    int* rank = quad + 4 * NC;
-    int* info = rank + NC;        // new position (| child mask << 16 for processed nodes)
+    int* quad = seqB + NC;        // 4*NC (the candidate gather's cell offsets before round 1)
+    int* rank = quad + 4 * NC;    // node -> processing rank, -1 = not divided this round
+    int* info = rank + NC;        // node -> new position (| child mask << 16 for divided nodes)
     int* ord = info + NC;         // rank -> node
-    int* nchr = ord + NC;         // per rank: #children, then its exclusive prefix
-    int* sc = nchr + NC;          // 32 ints of scan scratch
+    int* nchr = ord + NC;         // node -> children of the nodes divided before it
+    int* sc = nchr + NC;          // 2 x 16 ints of scan buffers
     int* sv = sc + 32;            // scalars
-    unsigned long long* skey = (unsigned long long*)rxB;   // phase-2 sort keys alias table B
-    int NC2 = 1;
-    while (NC2 < NC) NC2 <<= 1;
+#define OCT_STAMP(k) \
+    if (ost && tid == 0) ost[(k)] = __builtin_amdgcn_s_memtime();
 
-    uint32_t* outK = lvlKps + (long long)f * g->nkpcap + L.kp_base;
-
-    // 1. gather candidates in cell order (vToDistributeKeys, :818-825).  The keys and their node
-    // indices live in LDS after the node tables when they fit (every round re-reads them), else in
-    // the per-level global scratch.
+    // 1. gather candidates in cell order (vToDistributeKeys, :818-825)
     const int ncl = L.nCols * L.nRows;
-    const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
-    const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
-    int Ctot = 0;
-    {
-        int mine = 0;
-        for (int c = tid; c < ncl; c += NT) mine += cc[c];
-        (void)block_excl_scan(mine, sc, Ctot);
-    }
-    uint32_t* keys;
-    uint16_t* knode;
-    if (Ctot <= lds_keys) {
-        keys = reinterpret_cast<uint32_t*>(sv + 8);
-        knode = reinterpret_cast<uint16_t*>(keys + lds_keys);
+    if (ncl + 1 <= 8 * NC) {
+        // cell offsets in LDS, then a flat copy: key i lives in the last cell whose offset is <= i
+        // (binary search), so each lane's loads are independent and issued together
+        int* coff = quad;   // holds the cell counts (staged by k_octree), scanned in place
+        int base = 0;
+        for (int c0 = 0; c0 < ncl; c0 += NT) {
+            const int c = c0 + tid;
+            const int n = c < ncl ? coff[c] : 0;
+            int tot;
+            const int off = oct_scan(n, sc, par, tot);
+            if (c < ncl) coff[c] = base + off;
+            base += tot;
+        }
+        if (tid == 0) coff[ncl] = base;
+        __syncthreads();
+        constexpr int U = 4;
+        for (int i0 = 0; i0 < C; i0 += U * NT) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = i0 + u * NT + tid;
+                v[u] = 0;
+                if (i < C) {
+                    int lo = 0, hi = ncl;   // coff[lo] <= i < coff[hi]
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (coff[mid] <= i) lo = mid; else hi = mid;
+                    }
+                    v[u] = cs[__umul24((unsigned)lo, (unsigned)L.cell_cap) + (unsigned)(i - coff[lo])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = i0 + u * NT + tid;
+                if (i < C) keys[i] = v[u];
+            }
+        }
     } else {
-        keys = keysAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
-        knode = knodeAll + ((long long)f * g->nlevels + l) * g->max_level_cand;
-    }
-    int C = 0;
-    for (int c0 = 0; c0 < ncl; c0 += NT) {
-        const int c = c0 + tid;
-        const int n = c < ncl ? cc[c] : 0;
-        int tot;
-        const int off = block_excl_scan(n, sc, tot);
-        for (int k = 0; k < n; k++) keys[C + off + k] = cs[(long long)c * L.cell_cap + k];
-        C += tot;
+        int base = 0;
+        for (int c0 = 0; c0 < ncl; c0 += NT) {
+            const int c = c0 + tid;
+            const int n = c < ncl ? cc[c] : 0;
+            int tot;
+            const int off = oct_scan(n, sc, par, tot);
+            for (int k = 0; k < n; k++) keys[base + off + k] = cs[(long long)c * L.cell_cap + k];
+            base += tot;
+        }
     }
     __syncthreads();
+    OCT_STAMP(1);
+    if (ost && tid == 0) ost[29] = (unsigned long long)C;
 
-    // 2. root nodes (:543-585)
+    // 2. root nodes (:543-585): nIni columns of the level's border-trimmed area; empty ones erased
     const int N = L.nfeat;
     const int nIni = L.nIni;
     const float hX = L.hX;
@@ -983,144 +1005,212 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
         if (tid == 0) { atomicOr(err, 1); lvlCount[f * g->nlevels + l] = 0; }
         return;
     }
-    for (int t = tid; t < nIni; t += NT) {
-        const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
-        rxB[t] = (uint32_t)x0 | ((uint32_t)x1 << 16);
-        ryB[t] = (uint32_t)Hn << 16;
-        cntB[t] = 0;
-    }
+    for (int t = tid; t < nIni; t += NT) cntB[t] = 0;
     __syncthreads();
-    for (int i = tid; i < C; i += NT) {
-        const int x = keys[i] & 0xFFF;
-        int r = (int)((float)x / hX);
-        r = min(r, nIni - 1);
-        knode[i] = (uint16_t)r;
-        atomicAdd(&cntB[r], 1);
-    }
-    __syncthreads();
-    if (tid == 0) {   // erase empty roots, keep list order
-        int s = 0;
-        for (int t = 0; t < nIni; t++) {
-            if (cntB[t] > 0) {
-                rxA[s] = rxB[t];
-                ryA[s] = ryB[t];
-                cntA[s] = cntB[t];
-                seqA[s] = -1 - t;
-                info[t] = s++;
-            }
+    for (int i0 = 0; i0 < C; i0 += NT) {   // uniform trip count: the ballots need the whole wave
+        const int i = i0 + tid;
+        const bool ok = i < C;
+        int r = 0;
+        if (ok) {
+            const int x = keys[i] & 0xFFF;
+            r = min((int)((float)x / hX), nIni - 1);
+            knode[i] = (uint16_t)r;
         }
-        sv[0] = s;
+        wave_agg_add(cntB, ok, r);   // the roots are few: a wave's keys usually share one or two
+    }
+    __syncthreads();
+    int S = 0;
+    for (int t0 = 0; t0 < nIni; t0 += NT) {   // keep the non-empty roots in order
+        const int t = t0 + tid;
+        const int n = t < nIni ? cntB[t] : 0;
+        int tot;
+        const int pos = S + oct_scan(n > 0 ? 1 : 0, sc, par, tot);
+        if (n > 0) {
+            const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
+            rxA[pos] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+            ryA[pos] = (uint32_t)Hn << 16;
+            cntA[pos] = n;
+            seqA[pos] = -1 - t;
+        }
+        if (t < nIni) info[t] = pos;
+        S += tot;
     }
     __syncthreads();
     for (int i = tid; i < C; i += NT) knode[i] = (uint16_t)info[knode[i]];
-    int S = sv[0];
+    if (tid == 0) sv[3] = 0;
     int nextSeq = 0;
     int phase = 1;
     __syncthreads();
+    OCT_STAMP(2);
 
+    int p2seen = 0;
     for (int round = 0; round < 4 * NC + 64; round++) {
         const int prevSize = S;
+        // sub-step stamps of round 0 (slots 12..16) and of the first phase-2 round (20..28)
+        const int subBase = round == 0 ? 12 : (phase == 2 && !p2seen) ? 20 : -1;
+        if (phase == 2) p2seen = 1;
+#define OCT_SUB(k) \
+    if (ost && tid == 0 && subBase >= 0 && subBase + (k) < 29) ost[subBase + (k)] = __builtin_amdgcn_s_memtime();
         for (int t = tid; t < 4 * S; t += NT) quad[t] = 0;
         for (int t = tid; t < S; t += NT) rank[t] = -1;
         __syncthreads();
-        for (int i = tid; i < C; i += NT) {
-            const int t = knode[i];
-            if (cntA[t] > 1) atomicAdd(&quad[4 * t + quadrant_of(keys[i], rxA[t], ryA[t])], 1);
+        OCT_SUB(0);
+        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread in flight
+            int tt[4];
+            uint32_t kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * NT + tid;
+                tt[u] = i < C ? knode[i] : -1;
+                kk[u] = i < C ? keys[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = tt[u];
+                if (t >= 0 && cntA[t] > 1) atomicAdd(&quad[4 * t + quadrant_of(kk[u], rxA[t], ryA[t])], 1);
+            }
         }
         __syncthreads();
-        int nproc;
+        OCT_SUB(1);
+        int CH = 0, ndiv = 0;   // children created / nodes divided this round
         if (phase == 1) {
-            // every node with > 1 key, in list order
-            for (int t = tid; t < S; t += NT) nchr[t] = cntA[t] > 1 ? 1 : 0;
-            __syncthreads();
-            block_scan_array(nchr, S, sc);
-            if (tid == 0) sv[1] = 0;
-            __syncthreads();
-            for (int t = tid; t < S; t += NT) {
-                if (cntA[t] > 1) {
-                    const int r = nchr[t];
-                    rank[t] = r;
-                    ord[r] = t;
-                    atomicAdd(&sv[1], 1);
+            // every node with > 1 key, in list order: one scan of (divided, #children) packed 16:16;
+            // rank / children-before are written for the node's own thread (same mapping below)
+            int nproc = 0;
+            for (int t0 = 0; t0 < S; t0 += NT) {
+                const int t = t0 + tid;
+                int val = 0, mask = 0;
+                if (t < S && cntA[t] > 1) {
+                    mask = quad_mask(&quad[4 * t]);
+                    val = 1 | (__popc(mask) << 16);
                 }
-            }
-            __syncthreads();
-            nproc = sv[1];
-        } else {
-            // sort > 1-key nodes by (size, seq) descending (:684-685), then cut at N (:730)
-            for (int j = tid; j < NC2; j += NT) {
-                unsigned long long key = 0;
-                if (j < S && cntA[j] > 1)
-                    key = ((unsigned long long)cntA[j] << 40) | ((unsigned long long)seqA[j] << 16) |
-                          (unsigned long long)j;
-                skey[j] = key;
-            }
-            __syncthreads();
-            for (int k = 2; k <= NC2; k <<= 1) {
-                for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                    for (int i = tid; i < NC2; i += NT) {
-                        const int ixj = i ^ jj;
-                        if (ixj > i) {
-                            const unsigned long long a = skey[i], b = skey[ixj];
-                            const bool desc = (i & k) == 0;
-                            if (desc ? (a < b) : (a > b)) {
-                                skey[i] = b;
-                                skey[ixj] = a;
-                            }
-                        }
+                int tot;
+                const int pre = oct_scan(val, sc, par, tot);
+                if (t < S) {
+                    if (val) {
+                        rank[t] = nproc + (pre & 0xFFFF);
+                        nchr[t] = CH + (pre >> 16);
+                        info[t] = mask << 16;
+                    } else {
+                        info[t] = t - nproc - (pre & 0xFFFF);   // index among the undivided nodes
                     }
-                    __syncthreads();
                 }
+                nproc += tot & 0xFFFF;
+                CH += tot >> 16;
             }
-            if (tid == 0) sv[1] = 0;
+            ndiv = nproc;
+            OCT_SUB(2);
+        } else {
+            // sort the > 1-key nodes by (size, seq) descending (:684-685): dense keys, then each
+            // node's rank = number of larger keys (keys are unique)
+            unsigned long long* skey = reinterpret_cast<unsigned long long*>(rxB);
+            int* dd = cntB;     // rank -> #children - 1
+            int* dpre = seqB;   // rank -> exclusive prefix of dd
+            int nsort = 0;
+            for (int t0 = 0; t0 < S; t0 += NT) {
+                const int t = t0 + tid;
+                const bool big = t < S && cntA[t] > 1;
+                int tot;
+                const int pos = nsort + oct_scan(big ? 1 : 0, sc, par, tot);
+                if (big)
+                    skey[pos] = ((unsigned long long)cntA[t] << 40) | ((unsigned long long)seqA[t] << 16) |
+                                (unsigned long long)t;
+                nsort += tot;
+            }
+            if (tid == 0) sv[2] = nsort;
             __syncthreads();
-            for (int j = tid; j < NC2; j += NT) {
-                const unsigned long long key = skey[j];
-                if (key) {
+            OCT_SUB(2);
+            // G lanes per key (G = 8, 4, 2 or 1 so that the keys fill the block), each comparing a
+            // strided 8-key slice, summed with xor shuffles inside the lane group
+            const int G = nsort <= NT / 8 ? 8 : nsort <= NT / 4 ? 4 : nsort <= NT / 2 ? 2 : 1;
+            const int lg = tid & (G - 1);
+            for (int j0 = 0; j0 < nsort * G; j0 += NT) {   // uniform trip count (shuffles below)
+                const int j = (j0 + tid) / G;
+                const bool ok = j < nsort;
+                const unsigned long long key = ok ? skey[j] : ~0ull;
+                int r = 0;
+                for (int i = 8 * lg; i + 8 <= nsort; i += 8 * G) {
+                    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(skey + i);
+                    const ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
+                    r += (a.x > key) + (a.y > key) + (b.x > key) + (b.y > key) + (c.x > key) + (c.y > key) +
+                         (d.x > key) + (d.y > key);
+                }
+                if (lg == 0)
+                    for (int i = nsort & ~7; i < nsort; i++) r += skey[i] > key;
+                for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o);
+                if (ok && lg == 0) {
                     const int t = (int)(key & 0xFFFF);
-                    ord[j] = t;
-                    const int* qd = &quad[4 * t];
-                    nchr[j] = (qd[0] > 0) + (qd[1] > 0) + (qd[2] > 0) + (qd[3] > 0) - 1;
-                    atomicAdd(&sv[1], 1);
+                    ord[r] = t;
+                    dd[r] = __popc(quad_mask(&quad[4 * t])) - 1;
                 }
             }
             __syncthreads();
-            const int nsort = sv[1];
-            block_scan_array(nchr, nsort, sc);
-            if (tid == 0) sv[2] = 0;
-            __syncthreads();
-            for (int j = tid; j < nsort; j += NT) {
-                const int t = ord[j];
-                const int* qd = &quad[4 * t];
-                const int d = (qd[0] > 0) + (qd[1] > 0) + (qd[2] > 0) + (qd[3] > 0) - 1;
-                if (S + nchr[j] + d < N) atomicAdd(&sv[2], 1);   // still below N after dividing j
+            OCT_SUB(3);
+            // cut at N (:730): divide ranks 0..j while the list stays below N, plus the one reaching it
+            int run = 0;
+            for (int r0 = 0; r0 < nsort; r0 += NT) {
+                const int r = r0 + tid;
+                const int d = r < nsort ? dd[r] : 0;
+                int tot;
+                const int pre = run + oct_scan(d, sc, par, tot);
+                if (r < nsort) dpre[r] = pre;
+                const unsigned long long fail = __ballot(r < nsort && S + pre + d >= N);
+                if (fail && (threadIdx.x & 63) == 0) atomicMin(&sv[2], r0 + (tid & ~63) + __ffsll((long long)fail) - 1);
+                run += tot;
             }
             __syncthreads();
-            const int below = sv[2];
-            nproc = below < nsort ? below + 1 : nsort;
-            for (int j = tid; j < nproc; j += NT) rank[ord[j]] = j;
+            OCT_SUB(4);
+            const int first_stop = sv[2];
+            const int nproc = first_stop < nsort ? first_stop + 1 : nsort;
+            ndiv = nproc;
+            CH = nproc > 0 ? dpre[nproc - 1] + dd[nproc - 1] + nproc : 0;
+            for (int r = tid; r < nproc; r += NT) {
+                const int t = ord[r];
+                rank[t] = r;
+                nchr[t] = dpre[r] + r;
+                info[t] = quad_mask(&quad[4 * t]) << 16;
+            }
             __syncthreads();
+            OCT_SUB(5);
+            int und = 0;
+            for (int t0 = 0; t0 < S; t0 += NT) {   // index among the undivided nodes, list order
+                const int t = t0 + tid;
+                const bool keep = t < S && rank[t] < 0;
+                int tot;
+                const int pre = und + oct_scan(keep ? 1 : 0, sc, par, tot);
+                if (keep) info[t] = pre;
+                und += tot;
+            }
+            OCT_SUB(6);
         }
-        // children counts by rank, positions, sequence numbers
-        for (int r = tid; r < nproc; r += NT) {
-            const int* qd = &quad[4 * ord[r]];
-            nchr[r] = (qd[0] > 0) + (qd[1] > 0) + (qd[2] > 0) + (qd[3] > 0);
-        }
-        __syncthreads();
-        const int CH = block_scan_array(nchr, nproc, sc);
-        // non-processed nodes keep their relative order after the children block
-        for (int t = tid; t < S; t += NT) info[t] = rank[t] < 0 ? 1 : 0;
-        __syncthreads();
-        const int nrest = block_scan_array(info, S, sc);
-        const int Snew = CH + nrest;
+        // new list: [children of the last-divided node (n4..n1)] ... [of the first] [undivided nodes]
+        const int Snew = CH + S - ndiv;
         if (Snew > NC) {
             if (tid == 0) { atomicOr(err, 2); lvlCount[f * g->nlevels + l] = 0; }
             return;
         }
-        if (tid == 0) sv[3] = 0;
-        for (int t = tid; t < S; t += NT) {
-            const int r = rank[t];
-            if (r < 0) {
+        int big = 0;
+        for (int t0 = 0; t0 < S; t0 += NT) {   // same node -> thread mapping as the scans above
+            const int t = t0 + tid;
+            if (t >= S) break;
+            if (rank[t] >= 0) {
+                const int mask = info[t] >> 16;
+                const int P = nchr[t];
+                const int start = CH - P - __popc(mask);   // later-divided nodes end up nearer the front
+                const int* qd = &quad[4 * t];
+                for (int q = 0; q < 4; q++) {
+                    if (!(mask & (1 << q))) continue;
+                    const int pos = start + __popc(mask >> (q + 1));          // n4 first .. n1 last
+                    uint32_t crx, cry;
+                    child_rect(rxA[t], ryA[t], q, crx, cry);
+                    rxB[pos] = crx;
+                    ryB[pos] = cry;
+                    cntB[pos] = qd[q];
+                    seqB[pos] = nextSeq + P + __popc(mask & ((1 << q) - 1));  // creation order n1..n4
+                    big += qd[q] > 1;
+                }
+                info[t] = start | (mask << 16);
+            } else {
                 const int pos = CH + info[t];
                 rxB[pos] = rxA[t];
                 ryB[pos] = ryA[t];
@@ -1129,58 +1219,50 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
                 info[t] = pos;
             }
         }
+        big = wave_sum(big);
+        if ((threadIdx.x & 63) == 0 && big) atomicAdd(&sv[3], big);
         __syncthreads();
-        for (int r = tid; r < nproc; r += NT) {
-            const int t = ord[r];
-            const int* qd = &quad[4 * t];
-            const int mask = (qd[0] > 0) | ((qd[1] > 0) << 1) | ((qd[2] > 0) << 2) | ((qd[3] > 0) << 3);
-            const int nch = __popc(mask);
-            const int P = nchr[r];
-            const int start = CH - P - nch;          // later-processed nodes end up nearer the front
-            int big = 0;
-            for (int q = 0; q < 4; q++) {
-                if (!(mask & (1 << q))) continue;
-                const int pos = start + __popc(mask >> (q + 1));              // n4 first .. n1 last
-                uint32_t crx, cry;
-                child_rect(rxA[t], ryA[t], q, crx, cry);
-                rxB[pos] = crx;
-                ryB[pos] = cry;
-                cntB[pos] = qd[q];
-                seqB[pos] = nextSeq + P + __popc(mask & ((1 << q) - 1));      // creation order n1..n4
-                big += qd[q] > 1;
+        OCT_SUB(phase == 1 ? 3 : 7);
+        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread in flight
+            int tt[4];
+            uint32_t kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * NT + tid;
+                tt[u] = i < C ? knode[i] : -1;
+                kk[u] = i < C ? keys[i] : 0u;
             }
-            info[t] = start | (mask << 16);
-            if (big) atomicAdd(&sv[3], big);
-        }
-        __syncthreads();
-        for (int i = tid; i < C; i += NT) {
-            const int t = knode[i];
-            int nt;
-            if (rank[t] >= 0) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = tt[u];
+                if (t < 0) continue;
                 const int inf = info[t];
-                const int q = quadrant_of(keys[i], rxA[t], ryA[t]);
-                nt = (inf & 0xFFFF) + __popc((inf >> 16) >> (q + 1));
-            } else {
-                nt = info[t];
+                int nt = inf;
+                if (rank[t] >= 0) nt = (inf & 0xFFFF) + __popc((inf >> 16) >> (quadrant_of(kk[u], rxA[t], ryA[t]) + 1));
+                knode[i0 + u * NT + tid] = (uint16_t)nt;
             }
-            knode[i] = (uint16_t)nt;
         }
         const int nToExpand = sv[3];
         __syncthreads();
-        // swap tables
-        for (int t = tid; t < Snew; t += NT) {
-            rxA[t] = rxB[t];
-            ryA[t] = ryB[t];
-            cntA[t] = cntB[t];
-            seqA[t] = seqB[t];
+        OCT_SUB(phase == 1 ? 4 : 8);
+        if (tid == 0) sv[3] = 0;
+        {   // B becomes the current list
+            uint32_t* p = rxA; rxA = rxB; rxB = p;
+            p = ryA; ryA = ryB; ryB = p;
+            int* q = cntA; cntA = cntB; cntB = q;
+            q = seqA; seqA = seqB; seqB = q;
         }
         nextSeq += CH;
         S = Snew;
-        __syncthreads();
+        if (round < 9) OCT_STAMP(3 + round);
         if (S >= N || S == prevSize) break;                       // :669-672 / :734-735
-        if (phase == 1 && S + nToExpand * 3 > N) phase = 2;       // :673
+        if (phase == 1 && S + nToExpand * 3 > N) {                // :673
+            phase = 2;
+            if (ost && tid == 0) ost[30] = (unsigned long long)(round + 1);
+        }
     }
 
+#undef OCT_SUB
     // 3. retain the best key per node (:741-762): max response, first in key order on ties
     uint32_t* best = (uint32_t*)quad;
     for (int t = tid; t < S; t += NT) best[t] = 0;
@@ -1190,6 +1272,7 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
         atomicMax(&best[knode[i]], v);
     }
     __syncthreads();
+    uint32_t* outK = lvlKps + (long long)f * g->nkpcap + L.kp_base;
     for (int t = tid; t < S; t += NT) {
         const int i = 0xFFFFFF - (int)(best[t] & 0xFFFFFF);
         const uint32_t k = keys[i];
@@ -1197,6 +1280,55 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
         outK[t] = x | (y << 12) | (k & 0xFF000000u);
     }
     if (tid == 0) lvlCount[f * g->nlevels + l] = S;
+    OCT_STAMP(31);
+#undef OCT_STAMP
+}
+
+__global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restrict__ g,
+                                                           const uint32_t* __restrict__ cands,
+                                                           const int* __restrict__ cellCount,
+                                                           uint32_t* __restrict__ keysAll,
+                                                           uint16_t* __restrict__ knodeAll,
+                                                           uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
+                                                           int* __restrict__ err, int lds_keys,
+                                                           unsigned long long* __restrict__ ostamps) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int NC = g->node_cap;
+    const int tid = threadIdx.x;
+    constexpr int NT = kOctreeThreads;
+    // frames along x so that every frame's level-0 block (the longest) is dispatched first
+    const int f = blockIdx.x, l = blockIdx.y;
+    const LevelGeom& L = g->L[l];
+    int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
+    int* sv = sc + 32;
+    // optional timestamps (ORBGPU_FAST_STAMPS=1): 32 per (frame, level): 0 start, 1 gathered, 2 roots,
+    // 3.. end of round r (up to 9), 12.. / 20.. sub-steps of round 0 / the first phase-2 round,
+    // 29 = C, 30 = phase-2 start round, 31 done
+    unsigned long long* ost = ostamps ? ostamps + ((long long)f * g->nlevels + l) * 32 : nullptr;
+    if (ost && tid == 0) ost[0] = __builtin_amdgcn_s_memtime();
+    const int ncl = L.nCols * L.nRows;
+    const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
+    const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
+    int mine = 0;
+    int* cstage = smem + 8 * NC;   // octree_level's quad area: cell counts for its gather
+    const bool stage = ncl + 1 <= 8 * NC;
+    for (int c = tid; c < ncl; c += NT) {
+        const int n = cc[c];
+        mine += n;
+        if (stage) cstage[c] = n;
+    }
+    int par = 0, C = 0;
+    (void)oct_scan(mine, sc, par, C);
+    // keys and their node indices live in LDS after the node tables when they fit (every round
+    // re-reads them), else in the per-level global scratch
+    if (C <= lds_keys) {
+        uint32_t* keys = reinterpret_cast<uint32_t*>(sv + 8);
+        octree_level<true>(g, L, f, l, smem, C, cc, cs, keys, reinterpret_cast<uint16_t*>(keys + lds_keys), lvlKps,
+                           lvlCount, err, par, ost);
+    } else {
+        const long long o = ((long long)f * g->nlevels + l) * g->max_level_cand;
+        octree_level<false>(g, L, f, l, smem, C, cc, cs, keysAll + o, knodeAll + o, lvlKps, lvlCount, err, par, ost);
+    }
 }
 
 /* ------------------------------------------------------------------------------------------------
@@ -1491,6 +1623,34 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                           int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
     if (nframes <= 0) return hipSuccess;
+    const bool wave_fast = !(b.fast_block || (size_t)g.fast_wave_bytes * 4 > 65536);
+    auto launch_fast = [&](int cbeg, int cnum, hipStream_t s) {
+        const int items = cnum * nframes;
+        if (!wave_fast)   // very large cells: block-per-cell kernel (all cells)
+            hipLaunchKernelGGL(k_fast, dim3(items), dim3(256), 0, s, b.d_geom, d_frames, frame_pitch, row_stride,
+                               b.d_pyr, b.d_cands, b.d_cellCount, items, b.fast_remap);
+        else if (g.fast_compact)
+            hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(items, 8)), dim3(256), (size_t)g.fast_wave_bytes * 4, s,
+                               b.d_geom, b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands,
+                               b.d_cellCount, items, cbeg, cnum, b.fast_remap, b.d_stamps);
+        else
+            hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(items, 8)), dim3(256),
+                               (size_t)g.fast_wave_bytes * 4, s, b.d_geom, b.d_cells, d_frames, frame_pitch,
+                               row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum, b.fast_remap,
+                               b.d_stamps);
+    };
+    // level-0 cells are [0, L[1].cell_base): they read the frames only, so they can overlap the pyramid
+    const int nc0 = g.nlevels > 1 ? g.L[1].cell_base : g.ncells;
+    const bool split = b.side && wave_fast && g.nlevels > 1 && nc0 > 0;
+    hipError_t e;
+    if (split) {
+        if ((e = hipEventRecord(b.side_fork, stream)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(b.side, b.side_fork, 0)) != hipSuccess) return e;
+        if (marker) marker(user, ORB_K_FAST, 1, b.side);
+        launch_fast(0, nc0, b.side);
+        if (marker) marker(user, ORB_K_FAST, 0, b.side);
+        if ((e = hipEventRecord(b.side_join, b.side)) != hipSuccess) return e;
+    }
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);
     for (int l = 1; l < g.nlevels; l++) {
         const int t = g.L[l].rs_tiled;
@@ -1519,25 +1679,19 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     }
     if (marker) marker(user, ORB_K_RESIZE, 0, stream);
     if (marker) marker(user, ORB_K_FAST, 1, stream);
-    const int fast_items = g.ncells * nframes;
-    if (b.fast_block || (size_t)g.fast_wave_bytes * 4 > 65536)   // very large cells: block-per-cell kernel
-        hipLaunchKernelGGL(k_fast, dim3(fast_items), dim3(256), 0, stream, b.d_geom, d_frames,
-                           frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap);
-    else if (g.fast_compact)
-        hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(fast_items, 8)), dim3(256), (size_t)g.fast_wave_bytes * 4,
-                           stream, b.d_geom, b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands,
-                           b.d_cellCount, fast_items, b.fast_remap, b.d_stamps);
+    if (split)
+        launch_fast(nc0, g.ncells - nc0, stream);
     else
-        hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(fast_items, 8)), dim3(256),
-                           (size_t)g.fast_wave_bytes * 4, stream, b.d_geom, b.d_cells, d_frames, frame_pitch,
-                           row_stride, b.d_pyr, b.d_cands, b.d_cellCount, fast_items, b.fast_remap, b.d_stamps);
+        launch_fast(0, g.ncells, stream);
     if (marker) marker(user, ORB_K_FAST, 0, stream);
+    if (split && (e = hipStreamWaitEvent(stream, b.side_join, 0)) != hipSuccess) return e;
     if (marker) marker(user, ORB_K_OCTREE, 1, stream);
     {
         const int lk = octree_lds_keys(g.node_cap);
         hipLaunchKernelGGL(k_octree, dim3(nframes, g.nlevels), dim3(kOctreeThreads),
                            octree_lds_bytes(g.node_cap) + (size_t)lk * 6, stream, b.d_geom, b.d_cands, b.d_cellCount,
-                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk);
+                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
+                           b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr);
     }
     if (marker) marker(user, ORB_K_OCTREE, 0, stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);

@@ -241,7 +241,7 @@ int Ctx::ensure_frames(int nframes) {
         set_error("device allocation for the extractor", e);
         return ORB_ERR_NOMEM;
     }
-    if (fast_stamps && (e = grow(d_stamps, stamps_cap, (size_t)nframes * g.ncells * 8)) != hipSuccess)
+    if (fast_stamps && (e = grow(d_stamps, stamps_cap, (size_t)nframes * (g.ncells * 8 + g.nlevels * 32))) != hipSuccess)
         return set_error("stamps", e), ORB_ERR_NOMEM;
     // the overflow flag is read by orb_sync even before the first extraction
     if ((e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
@@ -267,6 +267,9 @@ ExtractBuffers Ctx::buffers() const {
     b.resize_th = resize_th;
     b.fast_block = fast_block ? 1 : 0;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
+    b.side = fast_split && !fast_stamps ? side_stream : nullptr;
+    b.side_fork = ev_side_fork;
+    b.side_join = ev_side_join;
     return b;
 }
 
@@ -298,6 +301,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             const int f0 = (int)((long long)nframes * si / ns), f1 = (int)((long long)nframes * (si + 1) / ns);
             if ((e = hipStreamWaitEvent(sub[si], ev_fork, 0)) != hipSuccess) return set_error("wait", e), ORB_ERR_HIP;
             ExtractBuffers b = buffers();
+            b.side = nullptr;
             b.d_pyr += (size_t)f0 * g.pyr_bytes;
             b.d_cands += (size_t)f0 * g.ncand;
             b.d_cellCount += (size_t)f0 * g.ncells;
@@ -389,6 +393,10 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     for (int i = 0; i < kMaxSubStreams && sub_ok; i++)
         sub_ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) == hipSuccess;
+    if (const char* ev = std::getenv("ORBGPU_FAST_SPLIT")) c->fast_split = ev[0] == '1';
+    sub_ok = sub_ok && hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_side_fork, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_side_join, hipEventDisableTiming) == hipSuccess;
     if (!sub_ok) {
         orb_destroy(reinterpret_cast<orb_ctx*>(c));
         set_error("hipStreamCreate (sub-batch streams)", hipErrorOutOfMemory);
@@ -432,6 +440,9 @@ void orb_destroy(orb_ctx* h) {
         if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
+    if (c->ev_side_fork) (void)hipEventDestroy(c->ev_side_fork);
+    if (c->ev_side_join) (void)hipEventDestroy(c->ev_side_join);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -31,6 +31,9 @@ struct Ctx {
     int nsub = 1;   // measured: 2 and 4 are slower at B = 64 (every phase already fills the GPU)
     hipStream_t sub[kMaxSubStreams]{};
     hipEvent_t ev_fork = nullptr, ev_join[kMaxSubStreams]{};
+    bool fast_split = false;       // level-0 FAST on side_stream, overlapping the resize chain (ORBGPU_FAST_SPLIT=1; measured 2 % slower: FAST starves the resize chain)
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_side_fork = nullptr, ev_side_join = nullptr;
 
     // ORBextractor tables (ORBextractor.cc:410-470)
     float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},
