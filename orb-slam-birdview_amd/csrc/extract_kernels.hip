@@ -1055,20 +1055,25 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         for (int t = tid; t < S; t += NT) rank[t] = -1;
         __syncthreads();
         OCT_SUB(0);
-        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread in flight
-            int tt[4];
+        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread, branch-free reads (clamped)
+            int tt[4], tg[4];
             uint32_t kk[4];
+            bool inc[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const int i = i0 + u * NT + tid;
-                tt[u] = i < C ? knode[i] : -1;
-                kk[u] = i < C ? keys[i] : 0u;
+                const int ic = min(i0 + u * NT + tid, C - 1);
+                tt[u] = knode[ic];
+                kk[u] = keys[ic];
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int t = tt[u];
-                if (t >= 0 && cntA[t] > 1) atomicAdd(&quad[4 * t + quadrant_of(kk[u], rxA[t], ryA[t])], 1);
+                inc[u] = i0 + u * NT + tid < C && cntA[t] > 1;
+                tg[u] = 4 * t + quadrant_of(kk[u], rxA[t], ryA[t]);
             }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (inc[u]) atomicAdd(&quad[tg[u]], 1);
         }
         __syncthreads();
         OCT_SUB(1);
@@ -1193,29 +1198,33 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         for (int t0 = 0; t0 < S; t0 += NT) {   // same node -> thread mapping as the scans above
             const int t = t0 + tid;
             if (t >= S) break;
-            if (rank[t] >= 0) {
-                const int mask = info[t] >> 16;
-                const int P = nchr[t];
+            // every read first (one LDS wait), then the writes of whichever case applies
+            const int rk = rank[t], inf = info[t], P = nchr[t], cnt = cntA[t], sq = seqA[t];
+            const uint32_t rx = rxA[t], ry = ryA[t];
+            const int4 qd = *reinterpret_cast<const int4*>(&quad[4 * t]);
+            if (rk >= 0) {
+                const int qc[4] = {qd.x, qd.y, qd.z, qd.w};
+                const int mask = inf >> 16;
                 const int start = CH - P - __popc(mask);   // later-divided nodes end up nearer the front
-                const int* qd = &quad[4 * t];
+#pragma unroll
                 for (int q = 0; q < 4; q++) {
                     if (!(mask & (1 << q))) continue;
                     const int pos = start + __popc(mask >> (q + 1));          // n4 first .. n1 last
                     uint32_t crx, cry;
-                    child_rect(rxA[t], ryA[t], q, crx, cry);
+                    child_rect(rx, ry, q, crx, cry);
                     rxB[pos] = crx;
                     ryB[pos] = cry;
-                    cntB[pos] = qd[q];
+                    cntB[pos] = qc[q];
                     seqB[pos] = nextSeq + P + __popc(mask & ((1 << q) - 1));  // creation order n1..n4
-                    big += qd[q] > 1;
+                    big += qc[q] > 1;
                 }
                 info[t] = start | (mask << 16);
             } else {
-                const int pos = CH + info[t];
-                rxB[pos] = rxA[t];
-                ryB[pos] = ryA[t];
-                cntB[pos] = cntA[t];
-                seqB[pos] = seqA[t];
+                const int pos = CH + inf;
+                rxB[pos] = rx;
+                ryB[pos] = ry;
+                cntB[pos] = cnt;
+                seqB[pos] = sq;
                 info[t] = pos;
             }
         }
@@ -1223,24 +1232,25 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         if ((threadIdx.x & 63) == 0 && big) atomicAdd(&sv[3], big);
         __syncthreads();
         OCT_SUB(phase == 1 ? 3 : 7);
-        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread in flight
-            int tt[4];
+        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread, branch-free reads (clamped)
+            int tt[4], nt[4];
             uint32_t kk[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const int i = i0 + u * NT + tid;
-                tt[u] = i < C ? knode[i] : -1;
-                kk[u] = i < C ? keys[i] : 0u;
+                const int ic = min(i0 + u * NT + tid, C - 1);
+                tt[u] = knode[ic];
+                kk[u] = keys[ic];
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int t = tt[u];
-                if (t < 0) continue;
-                const int inf = info[t];
-                int nt = inf;
-                if (rank[t] >= 0) nt = (inf & 0xFFFF) + __popc((inf >> 16) >> (quadrant_of(kk[u], rxA[t], ryA[t]) + 1));
-                knode[i0 + u * NT + tid] = (uint16_t)nt;
+                const int inf = info[t], rk = rank[t];
+                const int q = quadrant_of(kk[u], rxA[t], ryA[t]);
+                nt[u] = rk >= 0 ? (inf & 0xFFFF) + __popc((inf >> 16) >> (q + 1)) : inf;
             }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (i0 + u * NT + tid < C) knode[i0 + u * NT + tid] = (uint16_t)nt[u];
         }
         const int nToExpand = sv[3];
         __syncthreads();
