@@ -1385,7 +1385,8 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
-                                                  uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap) {
+                                                  uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
+                                                  unsigned long long* __restrict__ dstamps) {
     // per wave: 43x48 window (+16 B pad; reused for the transposed 37x40 blurred patch) and the
     // transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch; pitch 50 spreads the transposed
     // stores of the 10 column groups over distinct banks)
@@ -1411,10 +1412,21 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     for (int i = 0; i < l; i++) outIdx += cnts[i];
     const uint32_t kp = lvlKps[(long long)f * g->nkpcap + s];
     const int x = kp & 0xFFF, y = (kp >> 12) & 0xFFF, score = kp >> 24;
+    // optional phase timestamps (ORBGPU_FAST_STAMPS=1), 8 per keypoint slot: start, window, angle,
+    // row pass, column pass, sin/cos, done
+    unsigned long long* dst_st = dstamps ? dstamps + ((long long)f * g->nkpcap + s) * 8 : nullptr;
+#define DESC_STAMP(k) \
+    if (dst_st && lane == 0) dst_st[(k)] = __builtin_amdgcn_s_memtime();
+    DESC_STAMP(0);
     const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
     uint8_t* wbase = s_win[wv];
     uint32_t* w32 = reinterpret_cast<uint32_t*>(wbase);
     uint16_t* rt = s_rt[wv];
+
+    // BRIEF test pairs of this lane (lane + 64 gq), fetched now so their latency hides under the window's
+    char4 pat[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) pat[gq] = reinterpret_cast<const char4*>(c_pattern)[lane + 64 * gq];
 
     // ---- 43x43 window of the unblurred level, pixel (wy, wx) at byte wy*48 + sh + wx
     int sh;
@@ -1436,26 +1448,31 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
             if (idx < kDescWin * 12) w32[idx] = v[r];
         }
         sh = (x - 21) & 3;
-    } else {   // near the level border: REFLECT_101 gather (as the blur's border mode), byte loads in flight
-        uint8_t v[29];
+    } else {   // near the level border: REFLECT_101 gather (as the blur's border mode), byte loads in
+               // flight in two batches of 15 (fewer live registers than one batch of 29)
 #pragma unroll
-        for (int r = 0; r < 29; r++) {   // 43*43 = 1849 <= 29 x 64
-            const int idx = lane + 64 * r;
-            const int wy = (int)(__umul24((unsigned)idx, 24386u) >> 20), wx = idx - wy * kDescWin;   // idx / 43
-            int sy = y - 21 + wy, sx = x - 21 + wx;
-            sy = sy < 0 ? -sy : (sy >= L.h ? 2 * L.h - 2 - sy : sy);
-            sx = sx < 0 ? -sx : (sx >= L.w ? 2 * L.w - 2 - sx : sx);
-            v[r] = idx < kDescWin * kDescWin ? src.p[roi_off(sy, src.stride, sx)] : (uint8_t)0;
-        }
+        for (int hb = 0; hb < 2; hb++) {
+            uint8_t v[15];
 #pragma unroll
-        for (int r = 0; r < 29; r++) {
-            const int idx = lane + 64 * r;
-            const int wy = (int)(__umul24((unsigned)idx, 24386u) >> 20), wx = idx - wy * kDescWin;
-            if (idx < kDescWin * kDescWin) wbase[wy * kDescWinPitch + wx] = v[r];
+            for (int r = 0; r < 15; r++) {   // 43*43 = 1849 <= 30 x 64
+                const int idx = lane + 64 * (15 * hb + r);
+                const int wy = (int)(__umul24((unsigned)idx, 24386u) >> 20), wx = idx - wy * kDescWin;   // idx / 43
+                int sy = y - 21 + wy, sx = x - 21 + wx;
+                sy = sy < 0 ? -sy : (sy >= L.h ? 2 * L.h - 2 - sy : sy);
+                sx = sx < 0 ? -sx : (sx >= L.w ? 2 * L.w - 2 - sx : sx);
+                v[r] = idx < kDescWin * kDescWin ? src.p[roi_off(sy, src.stride, sx)] : (uint8_t)0;
+            }
+#pragma unroll
+            for (int r = 0; r < 15; r++) {
+                const int idx = lane + 64 * (15 * hb + r);
+                const int wy = (int)(__umul24((unsigned)idx, 24386u) >> 20), wx = idx - wy * kDescWin;
+                if (idx < kDescWin * kDescWin) wbase[wy * kDescWinPitch + wx] = v[r];
+            }
         }
         sh = 0;
     }
     wave_lds_sync();
+    DESC_STAMP(1);
 
     // ---- IC_Angle (:77-104) on the unblurred window: lane r < 31 sums row v = r - 15 over the
     // circular patch |u| <= umax[|v|] with v_dot4_u32_u8 (u*I = (u+16)*I - 16*I).
@@ -1483,12 +1500,10 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         m10 = (int)sW - 16 * (int)sI;
         m01 = v * (int)sI;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        m10 += __shfl_xor(m10, o);
-        m01 += __shfl_xor(m01, o);
-    }
+    m10 = wave_sum(m10);   // DPP reductions: no LDS round trips
+    m01 = wave_sum(m01);
     const float angle = fast_atan2((float)m01, (float)m10);
+    DESC_STAMP(2);
 
     // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass: item = (row wy, 4 outputs
     // rx = 4g..4g+3) over window bytes 4g..4g+9; packed u16 MACs on byte pairs (b_j, b_j+1).
@@ -1529,6 +1544,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         }
     }
     wave_lds_sync();
+    DESC_STAMP(3);
 
     // ---- column pass: item = (column bx, 4 outputs by = 4g..4g+3) over RT[bx][4g .. 4g+9],
     // v_dot2_u32_u16 on row pairs; rounding as the pinned OpenCV 3.2 8U path: half-to-even where the
@@ -1578,6 +1594,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     for (int r = 0; r < 6; r++)
         if (outa[r] >= 0) w32[outa[r]] = outw[r];
     wave_lds_sync();
+    DESC_STAMP(4);
 
     // ---- rBRIEF (:108-147): pinned correctly-rounded cos/sin; 256 tests as
     // four 64-lane ballots; sample (ix, iy) of the blurred patch at blurT[(18+ix)*40 + 18+iy]
@@ -1585,12 +1602,12 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     double sd, cd;
     sincos((double)ang, &sd, &cd);
     const float a = (float)cd, b = (float)sd;
+    DESC_STAMP(5);
     const uint8_t* ctr = wbase + 18 * kDescBlurPitch + 18;
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(outD + ((long long)f * kpCap + outIdx) * 32);
 #pragma unroll
     for (int gq = 0; gq < 4; gq++) {
-        const int p = lane + 64 * gq;
-        const char4 pp = reinterpret_cast<const char4*>(c_pattern)[p];   // (x0, y0, x1, y1) of test pair p
+        const char4 pp = pat[gq];   // (x0, y0, x1, y1) of test pair lane + 64 gq
         const float px0 = (float)pp.x, py0 = (float)pp.y;
         const float px1 = (float)pp.z, py1 = (float)pp.w;
         const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
@@ -1615,6 +1632,8 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         o.class_id = -1;
         outK[(long long)f * kpCap + outIdx] = o;
     }
+    DESC_STAMP(6);
+#undef DESC_STAMP
 }
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -1706,7 +1725,8 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     if (marker) marker(user, ORB_K_OCTREE, 0, stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
     hipLaunchKernelGGL(k_describe, dim3(cdiv(g.nkpcap, 4), nframes), dim3(256), 0, stream, b.d_geom, d_frames,
-                       frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap);
+                       frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
+                       b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr);
     if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);
     return hipGetLastError();
 }

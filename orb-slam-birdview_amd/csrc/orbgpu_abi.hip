@@ -241,7 +241,7 @@ int Ctx::ensure_frames(int nframes) {
         set_error("device allocation for the extractor", e);
         return ORB_ERR_NOMEM;
     }
-    if (fast_stamps && (e = grow(d_stamps, stamps_cap, (size_t)nframes * (g.ncells * 8 + g.nlevels * 32))) != hipSuccess)
+    if (fast_stamps && (e = grow(d_stamps, stamps_cap, (size_t)nframes * (g.ncells * 8 + g.nlevels * 32 + g.nkpcap * 8))) != hipSuccess)
         return set_error("stamps", e), ORB_ERR_NOMEM;
     // the overflow flag is read by orb_sync even before the first extraction
     if ((e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
