@@ -2,7 +2,7 @@
 # SQ counter passes (issue/stall breakdown per kernel) over a short bench run; --kernel-trace only.
 # Results under gpurun_out/pmc_sq/; summarised by tools/pmc_sq_report.py.
 OUT=gpurun_out/pmc_sq; mkdir -p $OUT; export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu --no-hamming ${BENCH_ARGS}"
+ARGS="--steps 2 --warmup 1 --no-cpu --no-hamming --no-host-path --no-stereo ${BENCH_ARGS}"
 timeout -k 10 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
