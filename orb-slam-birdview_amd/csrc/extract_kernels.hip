@@ -1506,13 +1506,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     DESC_STAMP(2);
 
     // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass: item = (row wy, 4 outputs
-    // rx = 4g..4g+3) over window bytes 4g..4g+9; packed u16 MACs on byte pairs (b_j, b_j+1).
-    const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4], k5 = g->gk[5],
-              k6 = g->gk[6];
-    const ushort2_t K[7] = {ushort2_t{(unsigned short)k0, (unsigned short)k0}, ushort2_t{(unsigned short)k1, (unsigned short)k1},
-                            ushort2_t{(unsigned short)k2, (unsigned short)k2}, ushort2_t{(unsigned short)k3, (unsigned short)k3},
-                            ushort2_t{(unsigned short)k4, (unsigned short)k4}, ushort2_t{(unsigned short)k5, (unsigned short)k5},
-                            ushort2_t{(unsigned short)k6, (unsigned short)k6}};
+    // rx = 4g..4g+3) over window bytes 4g..4g+9; output o = v_dot4(bytes o..o+3, k0..k3) +
+    // v_dot4(bytes o+4..o+7, k4 k5 k6 0) (the 8-bit taps sum to 257, so every sum fits 16 bits).
+    const uint32_t K0123 = (uint32_t)g->gk[0] | ((uint32_t)g->gk[1] << 8) | ((uint32_t)g->gk[2] << 16) |
+                           ((uint32_t)g->gk[3] << 24);
+    const uint32_t K456 = (uint32_t)g->gk[4] | ((uint32_t)g->gk[5] << 8) | ((uint32_t)g->gk[6] << 16);
 #pragma unroll
     for (int r = 0; r < 7; r++) {   // 43 rows x 10 groups = 430 <= 7 x 64
         const int it = lane + 64 * r;
@@ -1520,27 +1518,21 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
             const int wy = it / 10, gq = it - wy * 10;
             const int d0 = wy * 12 + gq;
             const uint32_t w0 = w32[d0], w1 = w32[d0 + 1], w2 = w32[d0 + 2], w3 = w32[d0 + 3];
-            const uint32_t a[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                   __builtin_amdgcn_alignbyte(w3, w2, sh)};
-            ushort2_t P[9];
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh), a1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+                           a2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+            uint32_t rv[4];
+            rv[0] = __builtin_amdgcn_udot4(a1, K456, __builtin_amdgcn_udot4(a0, K0123, 0u, false), false);
 #pragma unroll
-            for (int j = 0; j < 9; j++) {
-                const int q = j & 3;
-                const uint32_t sel = 0x0c000c00u | ((uint32_t)(q + 1) << 16) | (uint32_t)q;
-                P[j] = __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(a[(j >> 2) + 1 < 3 ? (j >> 2) + 1 : 2],
-                                                                              a[j >> 2], sel));
-            }
-            ushort2_t r01 = P[0] * K[0], r23 = P[2] * K[0];
-#pragma unroll
-            for (int j = 1; j < 7; j++) {
-                r01 = P[j] * K[j] + r01;
-                r23 = P[j + 2] * K[j] + r23;
-            }
+            for (int o = 1; o < 4; o++)
+                rv[o] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a2, a1, o), K456,
+                                               __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a1, a0, o), K0123, 0u,
+                                                                      false),
+                                               false);
             uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy;   // RT[4gq + j][wy]
-            rq[0 * kRtPitch] = r01.x;
-            rq[1 * kRtPitch] = r01.y;
-            rq[2 * kRtPitch] = r23.x;
-            rq[3 * kRtPitch] = r23.y;
+            rq[0 * kRtPitch] = (uint16_t)rv[0];
+            rq[1 * kRtPitch] = (uint16_t)rv[1];
+            rq[2 * kRtPitch] = (uint16_t)rv[2];
+            rq[3 * kRtPitch] = (uint16_t)rv[3];
         }
     }
     wave_lds_sync();
@@ -1551,6 +1543,8 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     // SSE2 body runs (x < W & ~3), half-up in the scalar tail.  Result stored transposed,
     // blurT[bx][by] at bx*40 + by, over the (now dead) window buffer.
     const int xsimd = L.w & ~3;
+    const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4], k5 = g->gk[5],
+              k6 = g->gk[6];
     const ushort2_t K01 = {(unsigned short)k0, (unsigned short)k1}, K23 = {(unsigned short)k2, (unsigned short)k3},
                     K45 = {(unsigned short)k4, (unsigned short)k5}, K60 = {(unsigned short)k6, 0},
                     K0s = {0, (unsigned short)k0}, K12 = {(unsigned short)k1, (unsigned short)k2},
