@@ -1662,52 +1662,62 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                                row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum, b.fast_remap,
                                b.d_stamps);
     };
-    // level-0 cells are [0, L[1].cell_base): they read the frames only, so they can overlap the pyramid
-    const int nc0 = g.nlevels > 1 ? g.L[1].cell_base : g.ncells;
-    const bool split = b.side && wave_fast && g.nlevels > 1 && nc0 > 0;
+    auto resize_levels = [&](int l0, int l1, hipStream_t s) {
+        for (int l = l0; l < l1; l++) {
+            const int t = g.L[l].rs_tiled;
+            const int want = b.resize_th >= 64 ? 2 : b.resize_th >= 32 ? 1 : 0;
+            int sel = -1;
+            for (int i = want; i >= 0 && sel < 0; i--)
+                if (t & (1 << i)) sel = i;
+            if (sel >= 0 && !b.resize_direct) {
+                const int th = 16 << sel;
+                dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
+                const ResizeCoef* cf = b.d_rcoef + b.rcoef_off[l];
+                if (sel == 2)
+                    hipLaunchKernelGGL(k_resize_tiled<64>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames,
+                                       frame_pitch, row_stride, b.d_pyr);
+                else if (sel == 1)
+                    hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames,
+                                       frame_pitch, row_stride, b.d_pyr);
+                else
+                    hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames,
+                                       frame_pitch, row_stride, b.d_pyr);
+            } else {
+                dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
+                hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,
+                                   d_frames, frame_pitch, row_stride, b.d_pyr);
+            }
+        }
+    };
+    // Pyramid tail split (ORBGPU_RESIZE_SPLIT = s): the small levels s+1.. are latency-bound launches,
+    // so they run on the side stream while FAST processes the cells of levels 0..s; FAST of the
+    // remaining levels waits for them.
+    const int sp = b.resize_split;
+    const bool split = b.side && wave_fast && sp >= 1 && sp + 1 < g.nlevels;
     hipError_t e;
+    if (marker) marker(user, ORB_K_RESIZE, 1, stream);
+    resize_levels(1, split ? sp + 1 : g.nlevels, stream);
+    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
     if (split) {
         if ((e = hipEventRecord(b.side_fork, stream)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(b.side, b.side_fork, 0)) != hipSuccess) return e;
-        if (marker) marker(user, ORB_K_FAST, 1, b.side);
-        launch_fast(0, nc0, b.side);
-        if (marker) marker(user, ORB_K_FAST, 0, b.side);
+        if (marker) marker(user, ORB_K_RESIZE, 1, b.side);
+        resize_levels(sp + 1, g.nlevels, b.side);
+        if (marker) marker(user, ORB_K_RESIZE, 0, b.side);
         if ((e = hipEventRecord(b.side_join, b.side)) != hipSuccess) return e;
-    }
-    if (marker) marker(user, ORB_K_RESIZE, 1, stream);
-    for (int l = 1; l < g.nlevels; l++) {
-        const int t = g.L[l].rs_tiled;
-        const int want = b.resize_th >= 64 ? 2 : b.resize_th >= 32 ? 1 : 0;
-        int sel = -1;
-        for (int i = want; i >= 0 && sel < 0; i--)
-            if (t & (1 << i)) sel = i;
-        if (sel >= 0 && !b.resize_direct) {
-            const int th = 16 << sel;
-            dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
-            const ResizeCoef* cf = b.d_rcoef + b.rcoef_off[l];
-            if (sel == 2)
-                hipLaunchKernelGGL(k_resize_tiled<64>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames,
-                                   frame_pitch, row_stride, b.d_pyr);
-            else if (sel == 1)
-                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames,
-                                   frame_pitch, row_stride, b.d_pyr);
-            else
-                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames,
-                                   frame_pitch, row_stride, b.d_pyr);
-        } else {
-            dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
-            hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, stream, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,
-                               d_frames, frame_pitch, row_stride, b.d_pyr);
-        }
-    }
-    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
-    if (marker) marker(user, ORB_K_FAST, 1, stream);
-    if (split)
-        launch_fast(nc0, g.ncells - nc0, stream);
-    else
+        const int ncs = g.L[sp + 1].cell_base;   // cells of levels 0..sp
+        if (marker) marker(user, ORB_K_FAST, 1, stream);
+        launch_fast(0, ncs, stream);
+        if (marker) marker(user, ORB_K_FAST, 0, stream);
+        if ((e = hipStreamWaitEvent(stream, b.side_join, 0)) != hipSuccess) return e;
+        if (marker) marker(user, ORB_K_FAST, 1, stream);
+        launch_fast(ncs, g.ncells - ncs, stream);
+        if (marker) marker(user, ORB_K_FAST, 0, stream);
+    } else {
+        if (marker) marker(user, ORB_K_FAST, 1, stream);
         launch_fast(0, g.ncells, stream);
-    if (marker) marker(user, ORB_K_FAST, 0, stream);
-    if (split && (e = hipStreamWaitEvent(stream, b.side_join, 0)) != hipSuccess) return e;
+        if (marker) marker(user, ORB_K_FAST, 0, stream);
+    }
     if (marker) marker(user, ORB_K_OCTREE, 1, stream);
     {
         const int lk = octree_lds_keys(g.node_cap);

@@ -267,7 +267,8 @@ ExtractBuffers Ctx::buffers() const {
     b.resize_th = resize_th;
     b.fast_block = fast_block ? 1 : 0;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
-    b.side = fast_split && !fast_stamps ? side_stream : nullptr;
+    b.side = side_stream;
+    b.resize_split = resize_split;
     b.side_fork = ev_side_fork;
     b.side_join = ev_side_join;
     return b;
@@ -393,7 +394,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     for (int i = 0; i < kMaxSubStreams && sub_ok; i++)
         sub_ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) == hipSuccess;
-    if (const char* ev = std::getenv("ORBGPU_FAST_SPLIT")) c->fast_split = ev[0] == '1';
+    if (const char* ev = std::getenv("ORBGPU_RESIZE_SPLIT")) c->resize_split = std::atoi(ev);
     sub_ok = sub_ok && hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_side_fork, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_side_join, hipEventDisableTiming) == hipSuccess;

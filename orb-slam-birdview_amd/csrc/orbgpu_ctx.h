@@ -31,7 +31,7 @@ struct Ctx {
     int nsub = 1;   // measured: 2 and 4 are slower at B = 64 (every phase already fills the GPU)
     hipStream_t sub[kMaxSubStreams]{};
     hipEvent_t ev_fork = nullptr, ev_join[kMaxSubStreams]{};
-    bool fast_split = false;       // level-0 FAST on side_stream, overlapping the resize chain (ORBGPU_FAST_SPLIT=1; measured 2 % slower: FAST starves the resize chain)
+    int resize_split = 0;          // ORBGPU_RESIZE_SPLIT=s: levels s+1.. resized on side_stream during FAST of levels 0..s
     hipStream_t side_stream = nullptr;
     hipEvent_t ev_side_fork = nullptr, ev_side_join = nullptr;
 

@@ -103,10 +103,11 @@ struct ExtractBuffers {
     int resize_th;                 // output rows per k_resize_tiled tile: 16, 32 or 64 (ORBGPU_RESIZE_TH)
     int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
     unsigned long long* d_stamps;  // k_fast_wave phase timestamps, 8 per (frame, cell) (ORBGPU_FAST_STAMPS=1)
-    // Level-0 FAST does not depend on the pyramid: when `side` is set it runs there, forked from the
-    // main stream before the resize chain and joined before k_octree (ORBGPU_FAST_SPLIT).
+    // Side stream for the pyramid tail split: levels resize_split+1.. are resized there while FAST runs
+    // on the cells of levels 0..resize_split (0 = no split; ORBGPU_RESIZE_SPLIT)
     hipStream_t side;
     hipEvent_t side_fork, side_join;
+    int resize_split;
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin, hipStream_t stream);
