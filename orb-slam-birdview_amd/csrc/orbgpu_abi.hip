@@ -223,6 +223,7 @@ int Ctx::ensure_geometry(int W, int H) {
     geom = g;
     std::memcpy(rcoef_off, off, sizeof off);
     have_geom = true;
+    ++geom_serial;
     return ORB_OK;
 }
 
@@ -286,9 +287,46 @@ void Ctx::marker(void* user, int id, int begin, hipStream_t s) {
 
 int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
                      uint8_t* d_desc, int* d_counts, int kp_cap) {
-    hipError_t e = hipMemsetAsync(d_err, 0, sizeof(int), stream);
-    if (e != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
+    hipError_t e;
     const int ns = std::min(std::min(nsub, kMaxSubStreams), nframes);
+    if (ns <= 1 && use_graph && !prof_on && !fast_stamps && resize_split == 0) {
+        // HIP graph replay: one submission per batch instead of 11
+        const std::array<uintptr_t, 32> key = {
+            (uintptr_t)d_frames, (uintptr_t)nframes, (uintptr_t)frame_pitch, (uintptr_t)row_stride, (uintptr_t)d_kps,
+            (uintptr_t)d_desc, (uintptr_t)d_counts, (uintptr_t)kp_cap, (uintptr_t)geom.W, (uintptr_t)geom.H,
+            (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
+            (uintptr_t)d_cands, (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
+            (uintptr_t)d_lvlCount, (uintptr_t)d_err, (uintptr_t)resize_th, (uintptr_t)resize_direct,
+            (uintptr_t)fast_block, (uintptr_t)fast_remap, (uintptr_t)stream};
+        if (!gexec || key != gkey) {
+            if (gexec) (void)hipGraphExecDestroy(gexec);
+            if (graph) (void)hipGraphDestroy(graph);
+            gexec = nullptr;
+            graph = nullptr;
+            if ((e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal)) != hipSuccess)
+                return set_error("graph capture", e), ORB_ERR_HIP;
+            hipError_t le = hipMemsetAsync(d_err, 0, sizeof(int), stream);
+            if (le == hipSuccess)
+                le = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc,
+                                    d_counts, kp_cap, stream, nullptr, nullptr);
+            hipGraph_t gr = nullptr;
+            e = hipStreamEndCapture(stream, &gr);
+            if (le != hipSuccess || e != hipSuccess) {
+                if (gr) (void)hipGraphDestroy(gr);
+                return set_error("graph capture", le != hipSuccess ? le : e), ORB_ERR_HIP;
+            }
+            if ((e = hipGraphInstantiate(&gexec, gr, nullptr, nullptr, 0)) != hipSuccess) {
+                (void)hipGraphDestroy(gr);
+                gexec = nullptr;
+                return set_error("graph instantiate", e), ORB_ERR_HIP;
+            }
+            graph = gr;
+            gkey = key;
+        }
+        if ((e = hipGraphLaunch(gexec, stream)) != hipSuccess) return set_error("graph launch", e), ORB_ERR_HIP;
+    } else {
+    e = hipMemsetAsync(d_err, 0, sizeof(int), stream);
+    if (e != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
     if (ns <= 1) {
         e = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
                            stream, &Ctx::marker, this);
@@ -318,6 +356,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
                 (e = hipStreamWaitEvent(stream, ev_join[si], 0)) != hipSuccess)
                 return set_error("join", e), ORB_ERR_HIP;
         }
+    }
     }
     last_frames = d_frames;
     last_frame_pitch = frame_pitch;
@@ -395,6 +434,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         sub_ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) == hipSuccess;
     if (const char* ev = std::getenv("ORBGPU_RESIZE_SPLIT")) c->resize_split = std::atoi(ev);
+    if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
     sub_ok = sub_ok && hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_side_fork, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_side_join, hipEventDisableTiming) == hipSuccess;
@@ -440,6 +480,8 @@ void orb_destroy(orb_ctx* h) {
         if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
         if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
     }
+    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
     if (c->ev_side_fork) (void)hipEventDestroy(c->ev_side_fork);

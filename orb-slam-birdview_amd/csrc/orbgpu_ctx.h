@@ -1,6 +1,7 @@
 // liborbgpu context (the object behind the opaque orb_ctx*).
 #pragma once
 #include <string>
+#include <array>
 #include <vector>
 
 #include "orbgpu_internal.h"
@@ -103,6 +104,13 @@ struct Ctx {
 
     // profiling
     bool prof_on = false;
+    // Replay of the per-batch launch sequence as a HIP graph (ORBGPU_GRAPH=0 disables): captured on the
+    // first batch with a given set of buffers / arguments and re-instantiated when any of them changes
+    bool use_graph = true;
+    unsigned geom_serial = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    std::array<uintptr_t, 32> gkey{};
     hipEvent_t prof_open[ORB_K_COUNT]{};
     std::vector<ProfPair> prof_pairs;
 
