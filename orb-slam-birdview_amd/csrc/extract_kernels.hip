@@ -774,8 +774,10 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
-                                                   int cbeg, int cnum, int remap, unsigned long long* __restrict__ stamps) {
+                                                   int cbeg, int cnum, int remap, unsigned long long* __restrict__ stamps,
+                                                   int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
+    if (err && blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // k_octree's overflow flag (set after this kernel)
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (8 cells each)
@@ -1649,18 +1651,20 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     const bool wave_fast = !(b.fast_block || (size_t)g.fast_wave_bytes * 4 > 65536);
     auto launch_fast = [&](int cbeg, int cnum, hipStream_t s) {
         const int items = cnum * nframes;
-        if (!wave_fast)   // very large cells: block-per-cell kernel (all cells)
+        if (!wave_fast) {   // very large cells: block-per-cell kernel (all cells)
+            if (b.zero_err) (void)hipMemsetAsync(b.d_err, 0, sizeof(int), s);
             hipLaunchKernelGGL(k_fast, dim3(items), dim3(256), 0, s, b.d_geom, d_frames, frame_pitch, row_stride,
                                b.d_pyr, b.d_cands, b.d_cellCount, items, b.fast_remap);
+        }
         else if (g.fast_compact)
             hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(items, 8)), dim3(256), (size_t)g.fast_wave_bytes * 4, s,
                                b.d_geom, b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands,
-                               b.d_cellCount, items, cbeg, cnum, b.fast_remap, b.d_stamps);
+                               b.d_cellCount, items, cbeg, cnum, b.fast_remap, b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
         else
             hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(items, 8)), dim3(256),
                                (size_t)g.fast_wave_bytes * 4, s, b.d_geom, b.d_cells, d_frames, frame_pitch,
                                row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum, b.fast_remap,
-                               b.d_stamps);
+                               b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
     };
     auto resize_levels = [&](int l0, int l1, hipStream_t s) {
         for (int l = l0; l < l1; l++) {

@@ -263,6 +263,7 @@ ExtractBuffers Ctx::buffers() const {
     b.d_lvlKps = d_lvlKps;
     b.d_lvlCount = d_lvlCount;
     b.d_err = d_err;
+    b.zero_err = 1;
     b.fast_remap = fast_remap ? 1 : 0;
     b.resize_direct = resize_direct ? 1 : 0;
     b.resize_th = resize_th;
@@ -305,10 +306,9 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             graph = nullptr;
             if ((e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal)) != hipSuccess)
                 return set_error("graph capture", e), ORB_ERR_HIP;
-            hipError_t le = hipMemsetAsync(d_err, 0, sizeof(int), stream);
-            if (le == hipSuccess)
-                le = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc,
-                                    d_counts, kp_cap, stream, nullptr, nullptr);
+            // the overflow flag is zeroed by the FAST kernel (no separate memset node)
+            const hipError_t le = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps,
+                                                 d_desc, d_counts, kp_cap, stream, nullptr, nullptr);
             hipGraph_t gr = nullptr;
             e = hipStreamEndCapture(stream, &gr);
             if (le != hipSuccess || e != hipSuccess) {
@@ -325,14 +325,13 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
         }
         if ((e = hipGraphLaunch(gexec, stream)) != hipSuccess) return set_error("graph launch", e), ORB_ERR_HIP;
     } else {
-    e = hipMemsetAsync(d_err, 0, sizeof(int), stream);
-    if (e != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
     if (ns <= 1) {
         e = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
                            stream, &Ctx::marker, this);
         if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
     } else {
         // fork: sub-batch s (frames [f0, f0+nf)) runs on sub[s] with its own frame slots; join on `stream`
+        if ((e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
         if ((e = hipEventRecord(ev_fork, stream)) != hipSuccess) return set_error("event record", e), ORB_ERR_HIP;
         const Geom& g = geom;
         const size_t nl = g.nlevels;
@@ -341,6 +340,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             if ((e = hipStreamWaitEvent(sub[si], ev_fork, 0)) != hipSuccess) return set_error("wait", e), ORB_ERR_HIP;
             ExtractBuffers b = buffers();
             b.side = nullptr;
+            b.zero_err = 0;
             b.d_pyr += (size_t)f0 * g.pyr_bytes;
             b.d_cands += (size_t)f0 * g.ncand;
             b.d_cellCount += (size_t)f0 * g.ncells;

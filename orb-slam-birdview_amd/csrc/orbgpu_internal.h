@@ -98,6 +98,7 @@ struct ExtractBuffers {
     uint32_t* d_lvlKps;            // nframes * nkpcap
     int* d_lvlCount;               // nframes * nlevels
     int* d_err;                    // 1 int: internal overflow flag
+    int zero_err;                  // FAST zeroes d_err (0: the caller did, e.g. before a sub-batch fork)
     int fast_remap;                // XCD-contiguous block->cell remap in k_fast (speed only)
     int resize_direct;             // force the untiled k_resize (A/B switch, ORBGPU_RESIZE_DIRECT=1)
     int resize_th;                 // output rows per k_resize_tiled tile: 16, 32 or 64 (ORBGPU_RESIZE_TH)
