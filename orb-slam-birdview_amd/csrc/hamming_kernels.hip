@@ -3,6 +3,7 @@
 // on the order of earlier accepted matches (SearchByBoW's taken set, SearchForInitialization's
 // vMatchedDistance) is replayed on the host from these exact top-k lists (matcher.cpp).
 #include <algorithm>
+#include <cstdlib>
 
 #include "orbgpu_internal.h"
 
@@ -156,6 +157,130 @@ __global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, c
     second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
 }
 
+/* The same all-pairs top-2 on the matrix cores.  With descriptor bits as +-1 int8 values,
+ * q . t = 256 - 2 popcount(q ^ t), so a tile of Hamming distances is one 32x32 i8 GEMM over K = 256:
+ * eight v_mfma_i32_32x32x32_i8.  A workgroup owns 128 queries (4 waves x 32, the B operand, expanded
+ * once into registers) and walks its train slice in tiles of 32 (the A operand, expanded into LDS,
+ * double-buffered; rows padded to 272 bytes so the 16-byte fragment reads are conflict-free).  The
+ * accumulator puts trains on the registers and queries on the lanes (row = (r&3) + 8(r>>2) + 4(lane>>5),
+ * column = lane & 31), so the top-2 update is lane-local; the two lane halves are merged at the end.
+ * Keys, tie order and outputs are those of k_top2_batch. */
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+constexpr int kMfTr = 32;      // trains per tile (MFMA rows)
+constexpr int kMfPitch = 272;  // LDS bytes per expanded train (256 + 16)
+constexpr int kMfQ = 128;      // queries per workgroup
+
+__device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {   // v_med3_u32
+    unsigned r;
+    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// 4 descriptor bits -> 4 bytes: +1 where the bit is set, -1 (0xFF) where it is clear
+__device__ __forceinline__ int pm1x4(uint32_t n) {
+    const uint32_t s = __umul24(n & 15u, 0x00204081u) & 0x01010101u;   // bit i -> byte i (no carries)
+    const uint32_t m = (s << 8) - s;                                    // 0xFF in the set bytes
+    return (int)((m & s) | ~m);
+}
+__device__ __forceinline__ v4i_t pm1x16(uint32_t w) {   // bits 0..15 of w -> 16 int8
+    v4i_t r;
+    r.x = pm1x4(w);
+    r.y = pm1x4(w >> 4);
+    r.z = pm1x4(w >> 8);
+    r.w = pm1x4(w >> 12);
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
+                                                   int* __restrict__ idx_o, int* __restrict__ second_o) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_t[2][kMfTr * kMfPitch];
+    const int p = blockIdx.z, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
+    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
+    const int qblk = blockIdx.x * kMfQ;
+    if (qblk >= nq) return;   // whole workgroup
+    const int t0 = blockIdx.y * a.slice, t1 = min(nt, t0 + a.slice);
+    const int h = lane >> 5, c = lane & 31;
+    const int qi = qblk + wv * 32 + c;
+    // B operand: K-step s = descriptor dword s, lane half h = its bits 16h .. 16h+15
+    v4i_t qf[8];
+    {
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+        if (qi < nq) {
+            const uint4* qp = reinterpret_cast<const uint4*>(a.q + ((long long)fr.x * a.q_stride + qi) * 32);
+            q0 = qp[0];
+            q1 = qp[1];
+        }
+        const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int s = 0; s < 8; s++) qf[s] = pm1x16(qd[s] >> (16 * h));
+    }
+    const uint32_t* __restrict__ T = reinterpret_cast<const uint32_t*>(a.t + (long long)fr.y * a.t_stride * 32);
+    const int er = tid >> 3, es = tid & 7;   // staging: thread -> (train row, descriptor dword)
+    auto stage = [&](int buf, uint32_t w) {
+        v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * kMfPitch + es * 32]);
+        d[0] = pm1x16(w);
+        d[1] = pm1x16(w >> 16);
+    };
+    unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
+    const int ntile = t1 > t0 ? (t1 - t0 + kMfTr - 1) / kMfTr : 0;   // uniform
+    if (ntile > 0) {
+        stage(0, t0 + er < t1 ? T[(long long)(t0 + er) * 8 + es] : 0u);
+        __syncthreads();
+        for (int j = 0; j < ntile; j++) {
+            const int tb = t0 + kMfTr * j;
+            const bool more = j + 1 < ntile;
+            uint32_t wn = 0;
+            if (more && tb + kMfTr + er < t1) wn = T[(long long)(tb + kMfTr + er) * 8 + es];
+            const uint8_t* A = &s_t[j & 1][c * kMfPitch + 16 * h];
+            v16i_t acc0 = {}, acc1 = {};
+#pragma unroll
+            for (int s = 0; s < 8; s += 2) {   // two accumulators: independent MFMA chains
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s], acc0, 0,
+                                                             0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s + 32),
+                                                             qf[s + 1], acc1, 0, 0, 0);
+            }
+            // key = dist << 16 | train = (256 - dot) * 2^15 + train (256 - dot is even); with b <= s2,
+            // min(s2, max(b, key)) is med3(b, key, s2)
+            const int kb = (256 << 15) + tb + 4 * h;
+            if (tb + kMfTr <= t1) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const unsigned key = (unsigned)(__mul24(acc0[r] + acc1[r], -32768) + kb + (r & 3) + 8 * (r >> 2));
+                    s2 = umed3(b, key, s2);
+                    b = min(b, key);
+                }
+            } else {   // the slice's last, partial tile
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int tr = tb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const unsigned key = tr < t1
+                        ? (unsigned)(__mul24(acc0[r] + acc1[r], -32768) + kb + (r & 3) + 8 * (r >> 2)) : 0xFFFFFFFFu;
+                    s2 = umed3(b, key, s2);
+                    b = min(b, key);
+                }
+            }
+            if (more) stage((j + 1) & 1, wn);
+            __syncthreads();
+        }
+    }
+    // the two lane halves hold different train rows of the same query
+    const unsigned ob = __shfl_xor(b, 32), os = __shfl_xor(s2, 32);
+    s2 = min(min(s2, os), max(b, ob));
+    b = min(b, ob);
+    if (h != 0 || qi >= nq) return;
+    const long long o = (long long)p * a.out_stride + qi;
+    if (gridDim.y == 1) {
+        best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
+        idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
+        second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
+    } else {
+        part[((long long)p * gridDim.y + blockIdx.y) * a.out_stride + qi] = make_uint2(b, s2);
+    }
+}
+
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     const int qwaves = std::max(1, (max_nq + 63) / 64);
     int ns = (8192 + npairs * qwaves - 1) / (npairs * qwaves);   // aim for >= 8192 wavefronts
@@ -168,11 +293,26 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (npairs <= 0 || max_nq <= 0) return hipSuccess;
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
-    const int ns = top2_batch_slices(npairs, max_nq, max_nt);
-    a.slice = std::max(1, (max_nt + ns - 1) / ns);
-    const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
-    hipLaunchKernelGGL(k_top2_batch, dim3((max_nq + 255) / 256, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best,
-                       d_best_idx, d_second);
+    const int ns = top2_batch_slices(npairs, max_nq, max_nt);   // the partial buffer is sized for this many
+    static const bool mfma = [] {
+        const char* e = std::getenv("ORBGPU_TOP2_MFMA");
+        return !(e && e[0] == '0');
+    }();
+    int nsu;
+    if (mfma) {   // matrix-core form: >= 2048 workgroups, slices of whole 32-train tiles
+        const int qb = (max_nq + kMfQ - 1) / kMfQ;
+        int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
+        want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
+        a.slice = ((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr;
+        nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
+        hipLaunchKernelGGL(k_top2_mfma, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
+                           d_second);
+    } else {
+        a.slice = std::max(1, (max_nt + ns - 1) / ns);
+        nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
+        hipLaunchKernelGGL(k_top2_batch, dim3((max_nq + 255) / 256, nsu, npairs), dim3(256), 0, stream, a, d_part,
+                           d_best, d_best_idx, d_second);
+    }
     if (nsu > 1)
         hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,
                            d_best, d_best_idx, d_second);
