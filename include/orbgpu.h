@@ -119,6 +119,52 @@ int orb_debug_level_image(orb_ctx* ctx, int frame, int level, uint8_t* out, int*
  * environment at orb_create): 8 s_memtime values per (frame, cell) item.  Returns the count copied. */
 int orb_debug_fast_stamps(orb_ctx* ctx, uint64_t* out, int cap);
 
+/* =========================== Birdview stream (Frame.cc:318-342) ===========================
+ * The reference runs OpenCV's cv::ORB (HARRIS_SCORE, not ORBextractor) plus cv::cornerSubPix on the
+ * birdview image.  orb_bird mirrors cv::ORB::create(nfeatures, scaleFactor, nlevels, edgeThreshold,
+ * firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31, fastThreshold) — Frame.cc:329 uses
+ * ORB::create(2000): {2000, 1.2f, 8, 31, 20}.  One HIP stream per object; one host thread at a time. */
+typedef struct {
+    int nfeatures;
+    float scaleFactor;
+    int nlevels;
+    int edgeThreshold;
+    int fastThreshold;
+    int device;
+} orb_bird_params;
+
+typedef struct orb_bird orb_bird;
+
+orb_bird* orb_bird_create(const orb_bird_params* p, int* status);
+void      orb_bird_destroy(orb_bird* b);
+
+/* cv::ORB::detect(image, keypoints, mask) — Frame.cc:330 (OpenCV 3.2 ORB_Impl::detectAndCompute,
+ * computeKeyPoints).  mask may be NULL (no mask).  Keypoints in level-0 coordinates, reference order.
+ * Empty image: *n = 0.  cap too small: ORB_ERR_CAPACITY with *n set. */
+int orb_bird_detect(orb_bird* b, const uint8_t* img, int w, int h, size_t stride, const uint8_t* mask,
+                    size_t mask_stride, orb_keypoint* kps, int cap, int* n);
+/* cv::ORB::compute(image, keypoints, descriptors) — Frame.cc:342.  kps in/out: border-culled
+ * (runByImageBorder, edgeThreshold) and level-sorted in place, *n updated; desc receives *n x 32. */
+int orb_bird_compute(orb_bird* b, const uint8_t* img, int w, int h, size_t stride, orb_keypoint* kps, int* n,
+                     uint8_t* desc);
+/* cv::cornerSubPix(image, pts (n x float2, in/out), Size(win_w, win_h), Size(-1,-1),
+ * TermCriteria(EPS+MAX_ITER, max_iter, eps)) — Frame.cc:336-337.  Only Size(5,5) is built. */
+int orb_corner_subpix(orb_bird* b, const uint8_t* img, int w, int h, size_t stride, float* pts, int n, int win_w,
+                      int win_h, int max_iter, double eps);
+/* Frame.cc:320-342 fused: footprint-masked detect, cornerSubPix(5x5, 40, 0.001), compute — one upload,
+ * one pyramid.  mask (birdviewMask) is not modified: the footprint is zeroed in the device copy. */
+int orb_bird_extract(orb_bird* b, const uint8_t* img, int w, int h, size_t stride, const uint8_t* mask,
+                     size_t mask_stride, orb_keypoint* kps, int cap, int* n, uint8_t* desc);
+/* Same, image and mask already in device memory (bench / multi-stream callers). */
+int orb_bird_extract_device(orb_bird* b, const uint8_t* d_img, int w, int h, size_t stride, const uint8_t* d_mask,
+                            size_t mask_stride, orb_keypoint* kps, int cap, int* n, uint8_t* desc);
+/* Frame.cc:320-327: zero the vehicle footprint (+15 px boundary) of a birdview mask in place (host). */
+int orb_bird_footprint_mask(uint8_t* mask, int w, int h, size_t stride);
+/* debug: last detect's level-l candidates after mask / border / NMS, raster order, level coordinates;
+ * response = Harris response, class_id = FAST score.  Returns the count (or -count-1 if cap is too small). */
+int orb_bird_debug_candidates(orb_bird* b, int level, orb_keypoint* out, int cap);
+int orb_bird_debug_level(orb_bird* b, int level, uint8_t* out, int* w, int* h);
+
 /* =========================== ORBmatcher =========================== */
 
 /* static int ORBmatcher::DescriptorDistance(const cv::Mat&, const cv::Mat&)  ORBmatcher.cc:1647-1663

@@ -74,6 +74,16 @@ def lib():
         L.oracle_vocab_info.argtypes = [vp] * 7
         L.oracle_vocab_transform_each.argtypes = [vp, vp, ci, ci, vp, vp, vp]
         L.oracle_vocab_transform.argtypes = [vp, vp, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_cvorb_create.restype = vp
+        L.oracle_cvorb_create.argtypes = [ci, cf, ci, ci, ci]
+        L.oracle_cvorb_destroy.argtypes = [vp]
+        L.oracle_cvorb_detect.argtypes = [vp, vp, ci, ci, ci, vp, ci, vp, ci]
+        L.oracle_cvorb_candidates.argtypes = [vp, ci, vp, ci]
+        L.oracle_cvorb_level.argtypes = [vp, ci, vp, vp, vp]
+        L.oracle_cvorb_compute.argtypes = [vp, vp, ci, ci, ci, vp, ci, vp]
+        L.oracle_corner_subpix.argtypes = [vp, ci, ci, ci, vp, ci, ci, ci, ci, ctypes.c_double]
+        L.oracle_bird_footprint_mask.argtypes = [vp, ci, ci, ci]
+        L.oracle_bird_extract.argtypes = [vp, vp, ci, ci, ci, vp, ci, vp, ci, vp]
         _LIB = L
     return _LIB
 
@@ -333,3 +343,84 @@ def distinctive_descriptor(desc):
     """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): index of the chosen descriptor."""
     d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
     return lib().oracle_distinctive_descriptor(_p(d) if len(d) else None, len(d))
+
+
+class OracleCvORB:
+    """Restated OpenCV 3.2 cv::ORB (HARRIS_SCORE) + cornerSubPix of the birdview stream
+    (Frame.cc:318-342; oracle/cvorb_oracle.inc).  Parity unpinned against OpenCV itself."""
+
+    def __init__(self, nfeatures=2000, scale_factor=1.2, nlevels=8, edge_threshold=31, fast_threshold=20):
+        self.nlevels = nlevels
+        self.h = lib().oracle_cvorb_create(nfeatures, scale_factor, nlevels, edge_threshold, fast_threshold)
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_cvorb_destroy(self.h)
+            self.h = None
+
+    def detect(self, img, mask=None):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        cap = 1 << 13
+        while True:
+            out = np.zeros(cap, KP_DTYPE)
+            n = lib().oracle_cvorb_detect(self.h, _p(img), w, h, w, None if m is None else _p(m), w, _p(out), cap)
+            if n >= 0:
+                return out[:n]
+            cap = -n
+
+    def candidates(self, l):
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, KP_DTYPE)
+            n = lib().oracle_cvorb_candidates(self.h, l, _p(out), cap)
+            if n >= 0:
+                return out[:n]
+            cap = -n
+
+    def level(self, l):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        assert lib().oracle_cvorb_level(self.h, l, None, ctypes.byref(w), ctypes.byref(h)) == 0
+        out = np.zeros((h.value, w.value), np.uint8)
+        lib().oracle_cvorb_level(self.h, l, _p(out), ctypes.byref(w), ctypes.byref(h))
+        return out
+
+    def compute(self, img, kps):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        k = np.ascontiguousarray(kps, KP_DTYPE).copy()
+        desc = np.zeros((max(len(k), 1), 32), np.uint8)
+        n = lib().oracle_cvorb_compute(self.h, _p(img), w, h, w, _p(k), len(k), _p(desc))
+        return k[:n], desc[:n]
+
+    def extract(self, img, mask=None):
+        """Frame.cc:320-342: footprint-masked detect, cornerSubPix(5x5, 40, 0.001), compute."""
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        cap = 1 << 13
+        while True:
+            out = np.zeros(cap, KP_DTYPE)
+            desc = np.zeros((cap, 32), np.uint8)
+            n = lib().oracle_bird_extract(self.h, _p(img), w, h, w, None if m is None else _p(m), w, _p(out), cap,
+                                          _p(desc))
+            if n >= 0:
+                return out[:n], desc[:n]
+            cap = -n
+
+
+def corner_subpix(img, pts, win=(5, 5), max_iter=40, eps=0.001):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2).copy()
+    lib().oracle_corner_subpix(_p(img), w, h, w, _p(p), len(p), win[0], win[1], max_iter, eps)
+    return p
+
+
+def bird_footprint_mask(mask):
+    m = np.ascontiguousarray(mask, np.uint8).copy()
+    h, w = m.shape
+    lib().oracle_bird_footprint_mask(_p(m), w, h, w)
+    return m

@@ -1386,3 +1386,5 @@ int oracle_distinctive_descriptor(const uint8_t* desc, int N) {
 }
 
 }  // extern "C"
+
+#include "cvorb_oracle.inc"

@@ -143,6 +143,27 @@ int   oracle_vocab_transform(void* h, const uint8_t* desc, int n, int levelsup, 
 /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): index of the chosen descriptor of N. */
 int oracle_distinctive_descriptor(const uint8_t* desc, int N);
 
+/* ---- Birdview stream (Frame.cc:318-342): OpenCV 3.2 cv::ORB(HARRIS) detect/compute + cornerSubPix,
+ * restated in cvorb_oracle.inc.  PARITY UNPINNED (OpenCV absent, no reference fixture). ---- */
+void* oracle_cvorb_create(int nfeatures, float scaleFactor, int nlevels, int edgeThreshold, int fastThreshold);
+void  oracle_cvorb_destroy(void* h);
+/* cv::ORB::detect(img, kps, mask); mask may be NULL.  Returns n (or -n-1 if cap too small). */
+int   oracle_cvorb_detect(void* h, const uint8_t* img, int w, int hgt, int stride, const uint8_t* mask, int mstride,
+                          OracleKeyPoint* out, int cap);
+/* last detect(): level-l FAST candidates after the mask and border filters, raster order, Harris response */
+int   oracle_cvorb_candidates(void* h, int level, OracleKeyPoint* out, int cap);
+int   oracle_cvorb_level(void* h, int level, uint8_t* out, int* w, int* hgt);
+/* cv::ORB::compute(img, kps, desc): kps in/out (border-culled, level-sorted); returns the new n */
+int   oracle_cvorb_compute(void* h, const uint8_t* img, int w, int hgt, int stride, OracleKeyPoint* kps, int n,
+                           uint8_t* desc);
+/* cv::cornerSubPix(img, pts(2n floats, in/out), Size(winW,winH), Size(-1,-1), EPS|ITER(maxIter, eps)) */
+void  oracle_corner_subpix(const uint8_t* img, int w, int hgt, int stride, float* pts, int n, int winW, int winH,
+                           int maxIter, double eps);
+void  oracle_bird_footprint_mask(uint8_t* mask, int w, int hgt, int stride);   /* Frame.cc:320-327 */
+/* Frame.cc:320-342 end to end (mask gets the footprint applied to a copy; NULL = no mask) */
+int   oracle_bird_extract(void* h, const uint8_t* img, int w, int hgt, int stride, const uint8_t* mask, int mstride,
+                          OracleKeyPoint* out, int cap, uint8_t* desc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,7 +77,7 @@ void compute_tables(Ctx* c) {
 }
 
 /* ---------------- per-image-size geometry ---------------- */
-static void resize_coefs(int sw, int dw, std::vector<ResizeCoef>& out, bool vertical) {
+void resize_coefs(int sw, int dw, std::vector<ResizeCoef>& out, bool vertical) {
     // OpenCV 3.2 resize INTER_LINEAR coefficient setup (imgwarp.cpp)
     const double scale = 1. / ((double)dw / sw);
     for (int d = 0; d < dw; d++) {

@@ -173,6 +173,8 @@ hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L,
                          float mb, float mbf, float* d_uright, float* d_depth, int* d_scratch, long long out_stride,
                          int* d_nmatched, hipStream_t stream);
 
+// OpenCV 3.2 resize INTER_LINEAR coefficients for sw -> dw (orbgpu_abi.hip), appended to `out`
+void resize_coefs(int sw, int dw, std::vector<ResizeCoef>& out, bool vertical);
 size_t octree_lds_bytes(int node_cap);
 void fast_wave_layout(Geom& g);   // fills fast_rows/drows/list/wave_bytes from the level grids
 void build_cells(const Geom& g, std::vector<CellDesc>& cells);

@@ -10,10 +10,11 @@ import ctypes
 
 import numpy as np
 
-from ._lib import OrbError, OrbFeatVec, OrbParams, check, lib
+from ._lib import OrbBirdParams, OrbError, OrbFeatVec, OrbParams, check, lib
 
 __all__ = ["ORBextractor", "ORBmatcher", "BatchExtractor", "KP_DTYPE", "OrbError", "device_count",
-           "features_in_area", "compute_stereo_matches", "ORBVocabulary"]
+           "features_in_area", "compute_stereo_matches", "ORBVocabulary", "BirdORB", "cornerSubPix",
+           "bird_footprint_mask"]
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -443,3 +444,139 @@ class ORBVocabulary:
 
     def __del__(self):
         self.close()
+
+
+class BirdORB:
+    """cv::ORB as the birdview stream uses it (Frame.cc:329: ORB::create(2000) -> nfeatures 2000,
+    scaleFactor 1.2, nlevels 8, edgeThreshold 31, HARRIS_SCORE, patchSize 31, fastThreshold 20),
+    plus cornerSubPix and the fused Frame.cc:320-342 sequence, on one MI355X (orb_bird_* C-ABI)."""
+
+    def __init__(self, nfeatures=2000, scaleFactor=1.2, nlevels=8, edgeThreshold=31, fastThreshold=20, device=0):
+        self.params = OrbBirdParams(nfeatures, scaleFactor, nlevels, edgeThreshold, fastThreshold, device)
+        st = ctypes.c_int()
+        self.h = lib().orb_bird_create(ctypes.byref(self.params), ctypes.byref(st))
+        if not self.h:
+            raise OrbError(st.value, "orb_bird_create")
+        self.nlevels = nlevels
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().orb_bird_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def _img(image):
+        img = np.asarray(image)
+        assert img.dtype == np.uint8 and img.ndim == 2, "CV_8UC1 expected"
+        return np.ascontiguousarray(img)
+
+    def detect(self, image, mask=None):
+        """cv::ORB::detect(image, keypoints, mask) -> keypoints (KP_DTYPE)."""
+        img = self._img(image)
+        if img.size == 0:
+            return np.zeros(0, KP_DTYPE)
+        h, w = img.shape
+        m = None if mask is None else self._img(mask)
+        cap = 2 * max(self.params.nfeatures, 1) + 256
+        while True:
+            kps = np.zeros(cap, KP_DTYPE)
+            n = ctypes.c_int(0)
+            st = lib().orb_bird_detect(self.h, _p(img), w, h, img.strides[0], _p(m), w if m is None else m.strides[0],
+                                       _p(kps), cap, ctypes.byref(n))
+            if st == -3:
+                cap = n.value
+                continue
+            check(st, "orb_bird_detect")
+            return kps[:n.value].copy()
+
+    def compute(self, image, keypoints):
+        """cv::ORB::compute(image, keypoints, descriptors) -> (keypoints, descriptors); keypoints are
+        border-culled and level-sorted as the reference does in place."""
+        img = self._img(image)
+        k = np.ascontiguousarray(keypoints, KP_DTYPE).copy()
+        if img.size == 0:
+            return k, np.zeros((0, 32), np.uint8)
+        h, w = img.shape
+        desc = np.zeros((max(len(k), 1), 32), np.uint8)
+        n = ctypes.c_int(len(k))
+        check(lib().orb_bird_compute(self.h, _p(img), w, h, img.strides[0], _p(k) if len(k) else None,
+                                     ctypes.byref(n), _p(desc)), "orb_bird_compute")
+        return k[:n.value].copy(), desc[:n.value].copy()
+
+    def cornerSubPix(self, image, corners, winSize=(5, 5), maxCount=40, epsilon=0.001):
+        img = self._img(image)
+        h, w = img.shape
+        p = np.ascontiguousarray(corners, np.float32).reshape(-1, 2).copy()
+        check(lib().orb_corner_subpix(self.h, _p(img), w, h, img.strides[0], _p(p), len(p), winSize[0], winSize[1],
+                                      maxCount, epsilon), "orb_corner_subpix")
+        return p
+
+    def extract(self, image, mask=None):
+        """Frame.cc:320-342 fused: footprint-masked detect, cornerSubPix(5x5, 40, 0.001), compute."""
+        img = self._img(image)
+        if img.size == 0:
+            return np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8)
+        h, w = img.shape
+        m = None if mask is None else self._img(mask)
+        cap = 2 * max(self.params.nfeatures, 1) + 256
+        while True:
+            kps = np.zeros(cap, KP_DTYPE)
+            desc = np.zeros((cap, 32), np.uint8)
+            n = ctypes.c_int(0)
+            st = lib().orb_bird_extract(self.h, _p(img), w, h, img.strides[0], _p(m), w if m is None else m.strides[0],
+                                        _p(kps), cap, ctypes.byref(n), _p(desc))
+            if st == -3:
+                cap = n.value
+                continue
+            check(st, "orb_bird_extract")
+            return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_device(self, d_img, w, h, d_mask=None, cap=None):
+        """Fused extract on a device-resident image (and mask) — device pointers as ints."""
+        cap = cap or 2 * max(self.params.nfeatures, 1) + 256
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int(0)
+        check(lib().orb_bird_extract_device(self.h, ctypes.c_void_p(d_img), w, h, w,
+                                            None if d_mask is None else ctypes.c_void_p(d_mask), w, _p(kps), cap,
+                                            ctypes.byref(n), _p(desc)), "orb_bird_extract_device")
+        return kps[:n.value], desc[:n.value]
+
+    def debug_candidates(self, level):
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, KP_DTYPE)
+            n = lib().orb_bird_debug_candidates(self.h, level, _p(out), cap)
+            if n >= 0:
+                return out[:n]
+            if n < -1:
+                cap = -n - 1
+                continue
+            check(n, "orb_bird_debug_candidates")
+
+    def debug_level(self, level):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check(lib().orb_bird_debug_level(self.h, level, None, ctypes.byref(w), ctypes.byref(h)), "debug_level")
+        out = np.zeros((h.value, w.value), np.uint8)
+        check(lib().orb_bird_debug_level(self.h, level, _p(out), ctypes.byref(w), ctypes.byref(h)), "debug_level")
+        return out
+
+
+def cornerSubPix(image, corners, winSize=(5, 5), maxCount=40, epsilon=0.001, device=0):
+    """cv::cornerSubPix(image, corners, winSize, Size(-1,-1), TermCriteria(EPS+MAX_ITER, maxCount, epsilon))."""
+    b = BirdORB(device=device)
+    try:
+        return b.cornerSubPix(image, corners, winSize, maxCount, epsilon)
+    finally:
+        b.close()
+
+
+def bird_footprint_mask(mask):
+    """Frame.cc:320-327: copy of `mask` with the vehicle footprint (+15 px) zeroed (host helper)."""
+    m = np.ascontiguousarray(mask, np.uint8).copy()
+    h, w = m.shape
+    check(lib().orb_bird_footprint_mask(_p(m), w, h, m.strides[0]), "orb_bird_footprint_mask")
+    return m

@@ -23,6 +23,11 @@ class OrbParams(ctypes.Structure):
                 ("max_batch", ci)]
 
 
+class OrbBirdParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ci), ("scaleFactor", cf), ("nlevels", ci), ("edgeThreshold", ci),
+                ("fastThreshold", ci), ("device", ci)]
+
+
 class OrbFeatVec(ctypes.Structure):
     _fields_ = [("nnodes", ci), ("node_ids", vp), ("offsets", vp), ("indices", vp)]
 
@@ -73,6 +78,16 @@ SIGNATURES = {
     "orb_vocab_transform_batch_device": (ci, [vp, vp, ci, ci, vp, vp, vp]),
     "orb_vocab_bow": (ci, [vp, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "orb_distinctive_descriptors": (ci, [vp, ci, vp, vp, vp]),
+    "orb_bird_create": (vp, [ctypes.POINTER(OrbBirdParams), ctypes.POINTER(ci)]),
+    "orb_bird_destroy": (None, [vp]),
+    "orb_bird_detect": (ci, [vp, vp, ci, ci, csz, vp, csz, vp, ci, ctypes.POINTER(ci)]),
+    "orb_bird_compute": (ci, [vp, vp, ci, ci, csz, vp, ctypes.POINTER(ci), vp]),
+    "orb_corner_subpix": (ci, [vp, vp, ci, ci, csz, vp, ci, ci, ci, ci, ctypes.c_double]),
+    "orb_bird_extract": (ci, [vp, vp, ci, ci, csz, vp, csz, vp, ci, ctypes.POINTER(ci), vp]),
+    "orb_bird_extract_device": (ci, [vp, vp, ci, ci, csz, vp, csz, vp, ci, ctypes.POINTER(ci), vp]),
+    "orb_bird_footprint_mask": (ci, [vp, ci, ci, csz]),
+    "orb_bird_debug_candidates": (ci, [vp, ci, vp, ci]),
+    "orb_bird_debug_level": (ci, [vp, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci)]),
 }
 
 STATUS = {0: "ORB_OK", -1: "ORB_ERR_ARG", -2: "ORB_ERR_HIP", -3: "ORB_ERR_CAPACITY",

@@ -99,6 +99,21 @@ def synth_stereo_right(left, idx=0, max_disp=64):
     return right
 
 
+def synth_bird_mask(w, h, idx=0):
+    """Birdview validity mask (0 / 255), like mono_fisheye.cc's ConvertMaskBirdview output: the
+    four corners outside the fisheye coverage are zero (quarter ellipses), plus a seeded zero band."""
+    rng = SplitMix64(0xB1D00000 + idx)
+    yy, xx = np.mgrid[0:h, 0:w]
+    m = np.full((h, w), 255, np.uint8)
+    rx, ry = w * 0.22, h * 0.22
+    for cx, cy in ((0, 0), (w - 1, 0), (0, h - 1), (w - 1, h - 1)):
+        m[((xx - cx) / rx) ** 2 + ((yy - cy) / ry) ** 2 < 1.0] = 0
+    r = rng.draw(2)
+    y0 = int(r[0] % np.uint64(max(h - 8, 1)))
+    m[y0:y0 + 2 + int(r[1] % np.uint64(6)), :] = 0
+    return m
+
+
 def synth_batch(w, h, n, first=0, kind="scene"):
     return np.stack([synth_frame(w, h, first + i, kind) for i in range(n)])
 
