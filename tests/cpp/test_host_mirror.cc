@@ -12,7 +12,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -21,6 +23,7 @@
 #include "../../orb-slam-birdview_amd/host/ORBmatcher.h"
 #include "../../orb-slam-birdview_amd/host/Stereo.h"
 #include "../../orb-slam-birdview_amd/host/ORBVocabulary.h"
+#include "../../orb-slam-birdview_amd/host/BirdviewORB.h"
 
 using namespace ORB_SLAM2;
 
@@ -162,6 +165,66 @@ int main(int argc, char** argv) {
             d.create(3);
             extractor(ImageView(flat.data(), w, h), ImageView(), k, d);
             report("flat_image_released", k.empty() && d.empty());
+        }
+
+        // ---- birdview stream, written as Frame.cc:318-342 writes it
+        {
+            const uint8_t* img = frames.data();
+            std::vector<uint8_t> mask((size_t)w * h, 255);
+            for (int y = 0; y < h; y++)      // a birdview-style mask: the four corners are invalid
+                for (int x = 0; x < w; x++) {
+                    const int dx = std::min(x, w - 1 - x), dy = std::min(y, h - 1 - y);
+                    if (dx * h + dy * w < (w * h) / 5) mask[(size_t)y * w + x] = 0;
+                }
+            std::vector<uint8_t> bmask = mask;
+            BirdviewFootprintMask(bmask.data(), w, h, w);                // cv::rectangle(mask, footprint, 0, -1)
+            std::vector<uint8_t> omask = mask;
+            oracle_bird_footprint_mask(omask.data(), w, h, w);
+            report("bird_footprint", bmask == omask);
+
+            std::shared_ptr<BirdviewORB> extractorBird = BirdviewORB::create(2000);
+            std::vector<KeyPoint> mvKeysBird;
+            extractorBird->detect(ImageView(img, w, h), mvKeysBird, ImageView(bmask.data(), w, h));
+            void* oh = oracle_cvorb_create(2000, 1.2f, 8, 31, 20);
+            std::vector<OracleKeyPoint> ok(8192);
+            const int on = oracle_cvorb_detect(oh, img, w, h, w, bmask.data(), w, ok.data(), (int)ok.size());
+            ok.resize(std::max(on, 0));
+            report("bird_detect", on >= 0 && mvKeysBird.size() == ok.size() &&
+                                      (ok.empty() || memcmp(mvKeysBird.data(), ok.data(), ok.size() * sizeof(KeyPoint)) == 0),
+                   "n=" + std::to_string(mvKeysBird.size()));
+            std::vector<Point2f> vKeysBird(mvKeysBird.size());
+            for (size_t k = 0; k < mvKeysBird.size(); k++) vKeysBird[k] = {mvKeysBird[k].x, mvKeysBird[k].y};
+            TermCriteria criteria(TermCriteria::EPS + TermCriteria::MAX_ITER, 40, 0.001);
+            cornerSubPix(ImageView(img, w, h), vKeysBird, Size{5, 5}, Size{-1, -1}, criteria);
+            std::vector<float> opts(2 * ok.size());
+            for (size_t k = 0; k < ok.size(); k++) {
+                opts[2 * k] = ok[k].x;
+                opts[2 * k + 1] = ok[k].y;
+            }
+            oracle_corner_subpix(img, w, h, w, opts.data(), (int)ok.size(), 5, 5, 40, 0.001);
+            report("bird_cornerSubPix", memcmp(vKeysBird.data(), opts.data(), opts.size() * sizeof(float)) == 0);
+            for (size_t k = 0; k < mvKeysBird.size(); k++) {
+                mvKeysBird[k].x = vKeysBird[k].x;
+                mvKeysBird[k].y = vKeysBird[k].y;
+                ok[k].x = opts[2 * k];
+                ok[k].y = opts[2 * k + 1];
+            }
+            DescriptorMat mDescriptorsBird;
+            extractorBird->compute(ImageView(img, w, h), mvKeysBird, mDescriptorsBird);
+            std::vector<uint8_t> od(ok.size() * 32 + 32);
+            const int oc = oracle_cvorb_compute(oh, img, w, h, w, ok.data(), (int)ok.size(), od.data());
+            report("bird_compute", (int)mvKeysBird.size() == oc && mDescriptorsBird.rows == oc &&
+                                       memcmp(mvKeysBird.data(), ok.data(), oc * sizeof(KeyPoint)) == 0 &&
+                                       memcmp(mDescriptorsBird.buf.data(), od.data(), (size_t)oc * 32) == 0,
+                   "Nbird=" + std::to_string(mvKeysBird.size()));
+            // the fused call gives the same Nbird keypoints and descriptors
+            std::vector<KeyPoint> fk;
+            DescriptorMat fd;
+            extractorBird->extractBirdview(ImageView(img, w, h), ImageView(mask.data(), w, h), fk, fd);
+            report("bird_extract_fused", fk.size() == mvKeysBird.size() && fd.rows == mDescriptorsBird.rows &&
+                                             memcmp(fk.data(), mvKeysBird.data(), fk.size() * sizeof(KeyPoint)) == 0 &&
+                                             fd.buf == mDescriptorsBird.buf);
+            oracle_cvorb_destroy(oh);
         }
 
         if (nframes < 2) {
