@@ -645,86 +645,89 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                                                uint8_t* tile, uint8_t* sM, uint16_t* sList,
                                                unsigned long long* keepb, uint32_t* __restrict__ cands,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
-    const int tmin = min(g->iniTh, g->minTh);
     const int dw = c.dw, dh = c.dh;
     for (int i = lane; i < (dh + 2) * (SP / 4); i += 64) reinterpret_cast<uint32_t*>(sM)[i] = 0u;
     if (lane < dh) keepb[lane] = 0ull;
     wave_lds_sync();
     ORBGPU_STAMP(1);
-    // ---- stage 1: compass prefilter, 4 pixels per lane in packed 16-bit lanes; lane -> (run, row)
-    // fixed for the cell (rows advance by 64 / nruns per iteration), per-bit ballot compaction
+    // lane -> (run of 4 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
     const int nruns = (dw + 3) >> 2;
     const int rpi = 64 / nruns;                          // rows per iteration
     const int lrow = (int)div20(lane, recip20(nruns));
     const int x0 = 4 * (lane - lrow * nruns);
     const bool lane_on = lrow < rpi;
-    const uint32_t tt = (uint32_t)tmin | ((uint32_t)tmin << 16);
     const uint32_t xvalid = x0 + 4 <= dw ? 0xFu : (1u << max(dw - x0, 0)) - 1u;
     const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
-    int nlist = 0;
-    for (int r0 = 0; r0 < dh; r0 += rpi) {
-        const int dy = r0 + lrow;
-        int pm = 0;
-        if (lane_on && dy < dh) {
-            const int sc = (dy + 3) * TP + x0 + xoff;       // centre row, from pixel x0-3
-            const int s0 = (dy + 6) * TP + x0 + 3 + xoff;   // row +3
-            const int s8 = dy * TP + x0 + 3 + xoff;         // row -3
-            const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
-            const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3];
-            const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);   // pixels x0-3 .. x0
-            const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);   // x0+1 .. x0+4
-            const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);   // x0+5 .. x0+8
-            const uint32_t P0 = __builtin_amdgcn_alignbyte(t32[d0 + 1], t32[d0], s0 & 3);
-            const uint32_t P8 = __builtin_amdgcn_alignbyte(t32[d8 + 1], t32[d8], s8 & 3);
-            const uint32_t V = __builtin_amdgcn_alignbyte(A1, A0, 3);     // centres x0 .. x0+3
-            const uint32_t P4 = __builtin_amdgcn_alignbyte(A2, A1, 2);    // x0+3 .. x0+6
-            const uint32_t P12 = A0;                                      // x0-3 .. x0
-            constexpr uint32_t LO = 0x00FF00FFu;
-            const uint32_t re = compass2(V & LO, P0 & LO, P4 & LO, P8 & LO, P12 & LO, tt);                 // px 0, 2
-            const uint32_t ro = compass2((V >> 8) & LO, (P0 >> 8) & LO, (P4 >> 8) & LO, (P8 >> 8) & LO,
-                                         (P12 >> 8) & LO, tt);                                          // px 1, 3
-            pm = (int)((((re >> 15) & 1u) | ((ro >> 14) & 2u) | ((re >> 29) & 4u) | ((ro >> 28) & 8u)) & xvalid);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const bool bit = (pm >> i) & 1;
-            const unsigned long long m = __ballot(bit);
-            if (bit) sList[nlist + lanes_below(m)] = (uint16_t)(dy * 64 + x0 + i);
-            nlist += __popcll(m);
-        }
-    }
-    wave_lds_sync();
-    ORBGPU_STAMP(2);
-    // ---- stage 2: exact arc strength for the survivors; corners at tmin are compacted in place
-    // (each chunk is read into registers before any lane writes, and writes land at or before it)
     const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
-    int ncorner = 0;
-    for (int b0 = 0; b0 < nlist; b0 += 64) {
-        const int i = b0 + lane;
-        int p = 0, m = 0;
-        if (i < nlist) {
-            p = sList[i];
-            m = fast_arc_strength<TP>(t0 + (p >> 6) * TP + (p & 63));
-            sM[(p >> 6) * SP + (p & 63) + SP + 1] = (uint8_t)m;
-        }
-        const bool corner = m > tmin;
-        const unsigned long long cm = __ballot(corner);
-        if (corner) sList[ncorner + lanes_below(cm)] = (uint16_t)p;
-        ncorner += __popcll(cm);
-    }
-    wave_lds_sync();
-    ORBGPU_STAMP(3);
-    // ---- cell-local NMS at iniThFAST, then the minThFAST fallback if nothing survived (:812-816).
-    // Neighbours outside the domain read the zero border; non-corners at th count 0.
+    // Pass 0 runs the whole cell at iniThFAST; only a cell left with no keypoint (:812-816) runs pass 1
+    // at minThFAST.  The prefilter is a necessary condition for M > th at the pass threshold, so a
+    // pass only scores the pixels that can matter at its threshold: everything else reads 0 in the map
+    // (M <= th counts 0 in the NMS), and pass 1's survivors are a superset that overwrites pass 0's.
     int th = g->iniTh;
     int kept = 0;
     for (int pass = 0; pass < 2; pass++) {
+        // ---- stage 1: compass prefilter at th, 4 pixels per lane in packed 16-bit lanes, per-bit
+        // ballot compaction into sList
+        const uint32_t tt = (uint32_t)th | ((uint32_t)th << 16);
+        int nlist = 0;
+        for (int r0 = 0; r0 < dh; r0 += rpi) {
+            const int dy = r0 + lrow;
+            int pm = 0;
+            if (lane_on && dy < dh) {
+                const int sc = (dy + 3) * TP + x0 + xoff;       // centre row, from pixel x0-3
+                const int s0 = (dy + 6) * TP + x0 + 3 + xoff;   // row +3
+                const int s8 = dy * TP + x0 + 3 + xoff;         // row -3
+                const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
+                const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3];
+                const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);   // pixels x0-3 .. x0
+                const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);   // x0+1 .. x0+4
+                const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);   // x0+5 .. x0+8
+                const uint32_t P0 = __builtin_amdgcn_alignbyte(t32[d0 + 1], t32[d0], s0 & 3);
+                const uint32_t P8 = __builtin_amdgcn_alignbyte(t32[d8 + 1], t32[d8], s8 & 3);
+                const uint32_t V = __builtin_amdgcn_alignbyte(A1, A0, 3);     // centres x0 .. x0+3
+                const uint32_t P4 = __builtin_amdgcn_alignbyte(A2, A1, 2);    // x0+3 .. x0+6
+                const uint32_t P12 = A0;                                      // x0-3 .. x0
+                constexpr uint32_t LO = 0x00FF00FFu;
+                const uint32_t re = compass2(V & LO, P0 & LO, P4 & LO, P8 & LO, P12 & LO, tt);                 // px 0, 2
+                const uint32_t ro = compass2((V >> 8) & LO, (P0 >> 8) & LO, (P4 >> 8) & LO, (P8 >> 8) & LO,
+                                             (P12 >> 8) & LO, tt);                                          // px 1, 3
+                pm = (int)((((re >> 15) & 1u) | ((ro >> 14) & 2u) | ((re >> 29) & 4u) | ((ro >> 28) & 8u)) & xvalid);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const bool bit = (pm >> i) & 1;
+                const unsigned long long m = __ballot(bit);
+                if (bit) sList[nlist + lanes_below(m)] = (uint16_t)(dy * 64 + x0 + i);
+                nlist += __popcll(m);
+            }
+        }
+        wave_lds_sync();
+        ORBGPU_STAMP(2);
+        // ---- stage 2: exact arc strength for the survivors; corners at th are compacted in place
+        // (each chunk is read into registers before any lane writes, and writes land at or before it)
+        int ncorner = 0;
+        for (int b0 = 0; b0 < nlist; b0 += 64) {
+            const int i = b0 + lane;
+            int p = 0, m = 0;
+            if (i < nlist) {
+                p = sList[i];
+                m = fast_arc_strength<TP>(t0 + (p >> 6) * TP + (p & 63));
+                sM[(p >> 6) * SP + (p & 63) + SP + 1] = (uint8_t)m;
+            }
+            const bool corner = m > th;
+            const unsigned long long cm = __ballot(corner);
+            if (corner) sList[ncorner + lanes_below(cm)] = (uint16_t)p;
+            ncorner += __popcll(cm);
+        }
+        wave_lds_sync();
+        ORBGPU_STAMP(3);
+        // ---- cell-local NMS at th.  Neighbours outside the domain read the zero border; M <= th
+        // counts 0.
         int mine = 0;
         for (int i = lane; i < ncorner; i += 64) {
             const int p = sList[i];
             const uint8_t* q = sM + (p >> 6) * SP + (p & 63) + SP + 1;
             const int m = q[0];
-            if (m <= th) continue;
             const int s = m - 1;
             bool k = true;
 #pragma unroll
@@ -744,7 +747,8 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         }
         kept = wave_sum(mine);
         if (kept > 0 || th == g->minTh) break;
-        th = g->minTh;
+        th = g->minTh;   // nothing kept: keepb is still all zero
+        wave_lds_sync();
     }
     wave_lds_sync();
     ORBGPU_STAMP(4);
