@@ -56,6 +56,12 @@ struct BirdCand {
     float harris;    // HarrisResponses(blockSize 7, k 0.04)
 };
 
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int reflect101_d(int p, int len) {
     if (len == 1) return 0;
     while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
@@ -317,13 +323,17 @@ __global__ __launch_bounds__(256) void k_bird_angle(const BirdGeom* __restrict__
 }
 
 /* ---------------- cv::cornerSubPix(win (5,5), zeroZone (-1,-1)) --------------------------------------
- * One thread per point; the five accumulators are summed in the reference's (i, j) order in double, so
- * the iteration is bit-identical to the sequential code.  The 13 x 13 patch (getRectSubPix_8u32f) is
- * generated row by row into a 3-row register window. */
+ * One wavefront per point.  Per iteration: lanes 0..12 generate the 13 rows of the getRectSubPix_8u32f
+ * patch (each row is a 13-step float recurrence) into LDS; lanes then compute the 121 per-pixel terms
+ * (gxx, gxy, gyy, gxx*px + gxy*py, gxy*px + gyy*py, in double) into LDS; lanes 0..4 each run ONE of the
+ * five accumulations sequentially in the reference's (i, j) order, so every double sum is bit-identical
+ * to the sequential code; the sums are broadcast and every lane updates the point identically. */
 struct SubpixSrc {
     const uint8_t* img;
     int pitch, W, H;
 };
+
+constexpr int kSubE = kSubW * kSubW;   // 121 window pixels
 
 // one patch row r of getRectSubPix(img, (13, 13), (cx, cy)) into out[13]
 __device__ __forceinline__ void subpix_row(const SubpixSrc& s, bool inside, int ipx, int ipy, float a, float b,
@@ -352,18 +362,22 @@ __device__ __forceinline__ void subpix_row(const SubpixSrc& s, bool inside, int 
     }
 }
 
-__global__ __launch_bounds__(64) void k_bird_subpix(SubpixSrc s, const float* __restrict__ wmask, float* pts,
-                                                    int stride, int n, int max_iters, double eps2, int edge,
-                                                    int* __restrict__ keep) {
-    const int k = blockIdx.x * 64 + threadIdx.x;
+__global__ __launch_bounds__(256) void k_bird_subpix(SubpixSrc s, const float* __restrict__ wmask, float* pts,
+                                                     int stride, int n, int max_iters, double eps2, int edge,
+                                                     int* __restrict__ keep) {
+    __shared__ float s_patch[4][kSubP * kSubP + 3];
+    __shared__ double s_terms[4][5 * kSubE + 1];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int k = blockIdx.x * 4 + wv;
     if (k >= n) return;
+    float* patch = s_patch[wv];
+    double* terms = s_terms[wv];
     float* pt = pts + (long long)k * stride;
     const float cTx = pt[0], cTy = pt[1];
     float cIx = cTx, cIy = cTy;
     int iter = 0;
     double err = 0;
     do {
-        double a = 0, b = 0, c = 0, bb1 = 0, bb2 = 0;
         const float centx = cIx - (kSubP - 1) * 0.5f, centy = cIy - (kSubP - 1) * 0.5f;
         const int ipx = (int)floorf(centx), ipy = (int)floorf(centy);
         const bool inside = 0 <= ipx && ipx + kSubP < s.W && 0 <= ipy && ipy + kSubP < s.H;
@@ -373,31 +387,36 @@ __global__ __launch_bounds__(64) void k_bird_subpix(SubpixSrc s, const float* __
             fa = fmaxf(fa, 0.0001f);
             sd = (1. - fa) / fa;
         }
-        float R0[kSubP], R1[kSubP], R2[kSubP];
-        subpix_row(s, inside, ipx, ipy, fa, fb, sd, 0, R0);
-        subpix_row(s, inside, ipx, ipy, fa, fb, sd, 1, R1);
-        for (int i = 0; i < kSubW; i++) {
-            subpix_row(s, inside, ipx, ipy, fa, fb, sd, i + 2, R2);
-            const double py = i - kSubWin;
+        if (lane < kSubP) {
+            float row[kSubP];
+            subpix_row(s, inside, ipx, ipy, fa, fb, sd, lane, row);
 #pragma unroll
-            for (int j = 0; j < kSubW; j++) {
-                const double m = wmask[i * kSubW + j];
-                const double tgx = R1[j + 2] - R1[j];
-                const double tgy = R2[j + 1] - R0[j + 1];
-                const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
-                const double px = j - kSubWin;
-                a += gxx;
-                b += gxy;
-                c += gyy;
-                bb1 += gxx * px + gxy * py;
-                bb2 += gxy * px + gyy * py;
-            }
-#pragma unroll
-            for (int j = 0; j < kSubP; j++) {
-                R0[j] = R1[j];
-                R1[j] = R2[j];
-            }
+            for (int j = 0; j < kSubP; j++) patch[lane * kSubP + j] = row[j];
         }
+        wave_lds_sync();
+        for (int e = lane; e < kSubE; e += 64) {
+            const int i = e / kSubW, j = e - i * kSubW;
+            const float* sp = patch + (i + 1) * kSubP + (j + 1);
+            const double m = wmask[e];
+            const double tgx = sp[1] - sp[-1];
+            const double tgy = sp[kSubP] - sp[-kSubP];
+            const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+            const double px = j - kSubWin, py = i - kSubWin;
+            terms[e] = gxx;
+            terms[kSubE + e] = gxy;
+            terms[2 * kSubE + e] = gyy;
+            terms[3 * kSubE + e] = gxx * px + gxy * py;
+            terms[4 * kSubE + e] = gxy * px + gyy * py;
+        }
+        wave_lds_sync();
+        double acc = 0;
+        if (lane < 5) {
+            const double* t = terms + lane * kSubE;
+            for (int e = 0; e < kSubE; e++) acc += t[e];
+        }
+        const double a = __shfl(acc, 0), b = __shfl(acc, 1), c = __shfl(acc, 2), bb1 = __shfl(acc, 3),
+                     bb2 = __shfl(acc, 4);
+        wave_lds_sync();   // this iteration's LDS reads precede the next iteration's patch stores
         const double det = a * c - b * b;
         if (fabs(det) <= DBL_EPSILON * DBL_EPSILON) break;
         const double sc = 1.0 / det;
@@ -412,12 +431,14 @@ __global__ __launch_bounds__(64) void k_bird_subpix(SubpixSrc s, const float* __
         cIx = cTx;
         cIy = cTy;
     }
-    pt[0] = cIx;
-    pt[1] = cIy;
-    if (keep) {   // ORB::compute -> runByImageBorder(image.size(), edgeThreshold): Rect::contains(cvRound(pt))
-        const int px = (int)rintf(cIx), py = (int)rintf(cIy);
-        keep[k] = s.W > 2 * edge && s.H > 2 * edge && edge <= px && px < s.W - edge && edge <= py &&
-                  py < s.H - edge;
+    if (lane == 0) {
+        pt[0] = cIx;
+        pt[1] = cIy;
+        if (keep) {   // ORB::compute -> runByImageBorder(image.size(), edgeThreshold): Rect::contains(cvRound(pt))
+            const int px = (int)rintf(cIx), py = (int)rintf(cIy);
+            keep[k] = s.W > 2 * edge && s.H > 2 * edge && edge <= px && px < s.W - edge && edge <= py &&
+                      py < s.H - edge;
+        }
     }
 }
 
@@ -852,7 +873,7 @@ int Bird::launch_angle(int n) {
 int Bird::launch_subpix(int n, bool keep) {
     SubpixSrc s{d_pyr + g.L[0].off, g.L[0].pitch, g.L[0].w, g.L[0].h};
     if (n)
-        hipLaunchKernelGGL(k_bird_subpix, dim3((n + 63) / 64), dim3(64), 0, stream, s, d_wmask,
+        hipLaunchKernelGGL(k_bird_subpix, dim3((n + 3) / 4), dim3(256), 0, stream, s, d_wmask,
                            reinterpret_cast<float*>(d_kps), 7, n, 40, 0.001 * 0.001, edge, keep ? d_keep : nullptr);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? ORB_OK : (set_error("k_bird_subpix", e), ORB_ERR_HIP);
@@ -1131,7 +1152,7 @@ extern "C" int orb_corner_subpix(orb_bird* b, const uint8_t* img, int w, int h, 
     SubpixSrc s{b->d_pyr + b->g.L[0].off, b->g.L[0].pitch, w, h};
     if ((e = hipMemcpyAsync(b->d_pts, pts, (size_t)n * 8, hipMemcpyHostToDevice, b->stream)) != hipSuccess)
         return set_error("subpix upload", e), ORB_ERR_HIP;
-    hipLaunchKernelGGL(k_bird_subpix, dim3((n + 63) / 64), dim3(64), 0, b->stream, s, b->d_wmask, b->d_pts, 2, n, iters,
+    hipLaunchKernelGGL(k_bird_subpix, dim3((n + 3) / 4), dim3(256), 0, b->stream, s, b->d_wmask, b->d_pts, 2, n, iters,
                        ep * ep, b->edge, (int*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess ||
         (e = hipMemcpyAsync(pts, b->d_pts, (size_t)n * 8, hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
