@@ -17,6 +17,9 @@
 // with the same library call the OpenCV build makes.
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -135,29 +138,20 @@ __global__ __launch_bounds__(256) void k_bird_fast(const BirdGeom* __restrict__ 
     const int x = g->edge - 1 + blockIdx.x * 256 + threadIdx.x;
     if (x > L.w - g->edge) return;
     const long long o = L.off + (long long)r.y * L.pitch + x;
-    score[o] = (uint8_t)fast_score_at(pyr + o, L.pitch, g->fastTh);
+    const uint8_t* c = pyr + o;
+    const int P = L.pitch, t = g->fastTh, v = c[0];
+    // compass prefilter (a 9-arc holds two cyclically adjacent compass points): necessary for a corner
+    const int p0 = c[3 * P], p4 = c[3], p8 = c[-3 * P], p12 = c[-3];
+    const int hi = v + t, lo = v - t;
+    const int bm = (p0 > hi) | ((p4 > hi) << 1) | ((p8 > hi) << 2) | ((p12 > hi) << 3);
+    const int dm = (p0 < lo) | ((p4 < lo) << 1) | ((p8 < lo) << 2) | ((p12 < lo) << 3);
+    score[o] = ((0xFAC8 >> bm) | (0xFAC8 >> dm)) & 1 ? (uint8_t)fast_score_at(c, P, t) : (uint8_t)0;
 }
 
 /* ---------------- candidates: NMS + runByPixelsMask + runByImageBorder, raster order ------------
  * One wave per (level, y) row of [edge, h-edge); mode 0 counts, mode 1 writes at the scanned
- * offsets with the Harris response (orb.cpp HarrisResponses, blockSize 7, HARRIS_K 0.04f). */
-__device__ __forceinline__ float harris_at(const uint8_t* c, int P, float scale4) {
-    const uint8_t* p0 = c - 3 * P - 3;
-    int a = 0, b = 0, cc = 0;
-    for (int i = 0; i < 7; i++)
-#pragma unroll
-        for (int j = 0; j < 7; j++) {
-            const uint8_t* p = p0 + i * P + j;
-            const int Ix = (p[1] - p[-1]) * 2 + (p[-P + 1] - p[-P - 1]) + (p[P + 1] - p[P - 1]);
-            const int Iy = (p[P] - p[-P]) * 2 + (p[P - 1] - p[-P - 1]) + (p[P + 1] - p[-P + 1]);
-            a += Ix * Ix;
-            b += Iy * Iy;
-            cc += Ix * Iy;
-        }
-    const float fa = (float)a, fb = (float)b, fc = (float)cc;
-    return (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * scale4;
-}
-
+ * offsets with the Harris response (orb.cpp HarrisResponses, blockSize 7, HARRIS_K 0.04f: integer
+ * gradient sums, then the float formula in the reference's evaluation order). */
 template <int kMode>
 __global__ __launch_bounds__(256) void k_bird_cands(const BirdGeom* __restrict__ g, const int2* __restrict__ rows,
                                                     int nrows, const uint8_t* __restrict__ pyr,
@@ -185,14 +179,44 @@ __global__ __launch_bounds__(256) void k_bird_cands(const BirdGeom* __restrict__
             }
         }
         const unsigned long long m = __ballot(keep);
-        if (kMode && keep) {
-            const int rank = __popcll(m & ((1ull << lane) - 1));
-            BirdCand c;
-            c.xy = x | (r.y << 16);
-            c.level = r.x;
-            c.score = s;
-            c.harris = harris_at(pyr + o, P, g->harris_scale4);
-            out[pos + rank] = c;
+        if (kMode) {
+            // Harris responses, one candidate at a time over the whole wave: lane q < 49 takes pixel
+            // (q / 7, q % 7) of the 7x7 block, the integer sums are wave reductions (order-free)
+            float hr = 0.f;
+            unsigned long long mm = m;
+            while (mm) {
+                const int src = __ffsll((long long)mm) - 1;
+                mm &= mm - 1;
+                const long long oc = o - lane + src;   // the candidate's pixel (same row, x0 + src)
+                int ixx = 0, iyy = 0, ixy = 0;
+                if (lane < 49) {
+                    const int i = lane / 7, j = lane - 7 * (lane / 7);
+                    const uint8_t* q = pyr + oc + (long long)(i - 3) * P + (j - 3);
+                    const int Ix = (q[1] - q[-1]) * 2 + (q[-P + 1] - q[-P - 1]) + (q[P + 1] - q[P - 1]);
+                    const int Iy = (q[P] - q[-P]) * 2 + (q[P - 1] - q[-P - 1]) + (q[P + 1] - q[-P + 1]);
+                    ixx = Ix * Ix;
+                    iyy = Iy * Iy;
+                    ixy = Ix * Iy;
+                }
+#pragma unroll
+                for (int sft = 32; sft > 0; sft >>= 1) {
+                    ixx += __shfl_xor(ixx, sft);
+                    iyy += __shfl_xor(iyy, sft);
+                    ixy += __shfl_xor(ixy, sft);
+                }
+                const float fa = (float)ixx, fb = (float)iyy, fc = (float)ixy;
+                const float h = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * g->harris_scale4;
+                if (lane == src) hr = h;
+            }
+            if (keep) {
+                const int rank = __popcll(m & ((1ull << lane) - 1));
+                BirdCand c;
+                c.xy = x | (r.y << 16);
+                c.level = r.x;
+                c.score = s;
+                c.harris = hr;
+                out[pos + rank] = c;
+            }
         }
         pos += __popcll(m);
     }
@@ -335,13 +359,19 @@ struct SubpixSrc {
 
 constexpr int kSubE = kSubW * kSubW;   // 121 window pixels
 
-// one patch row r of getRectSubPix(img, (13, 13), (cx, cy)) into out[13]
+// one patch row r of getRectSubPix(img, (13, 13), (cx, cy)) into out[13]; interior windows read the
+// point's cached neighbourhood (`cache`, pitch kSubC, origin (cx0, cy0)) when they lie inside it
+constexpr int kSubC = 32;
 __device__ __forceinline__ void subpix_row(const SubpixSrc& s, bool inside, int ipx, int ipy, float a, float b,
-                                           double sd, int r, float (&out)[kSubP]) {
+                                           double sd, int r, float (&out)[kSubP], const uint8_t* cache, int cx0,
+                                           int cy0) {
     if (inside) {
         const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
-        const uint8_t* s0 = s.img + (long long)(ipy + r) * s.pitch + ipx;
-        const uint8_t* s1 = s0 + s.pitch;
+        const bool cached = cache && ipx >= cx0 && ipx + kSubP < cx0 + kSubC && ipy >= cy0 &&
+                            ipy + kSubP < cy0 + kSubC;
+        const uint8_t* s0 = cached ? cache + (ipy + r - cy0) * kSubC + (ipx - cx0)
+                                   : s.img + (long long)(ipy + r) * s.pitch + ipx;
+        const uint8_t* s1 = s0 + (cached ? kSubC : s.pitch);
         float prev = (1 - a) * (b1 * s0[0] + b2 * s1[0]);
 #pragma unroll
         for (int j = 0; j < kSubP; j++) {
@@ -367,6 +397,7 @@ __global__ __launch_bounds__(256) void k_bird_subpix(SubpixSrc s, const float* _
                                                      int* __restrict__ keep) {
     __shared__ float s_patch[4][kSubP * kSubP + 3];
     __shared__ double s_terms[4][5 * kSubE + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cache[4][kSubC * kSubC];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int k = blockIdx.x * 4 + wv;
     if (k >= n) return;
@@ -374,6 +405,23 @@ __global__ __launch_bounds__(256) void k_bird_subpix(SubpixSrc s, const float* _
     double* terms = s_terms[wv];
     float* pt = pts + (long long)k * stride;
     const float cTx = pt[0], cTy = pt[1];
+    // the 32 x 32 neighbourhood of the start point, staged once (windows within +-9 px of it read LDS)
+    const int cx0 = (int)floorf(cTx) - 15, cy0 = (int)floorf(cTy) - 15;
+    const uint8_t* cache = nullptr;
+    if (cx0 >= 0 && cy0 >= 0 && cx0 + kSubC <= s.W && cy0 + kSubC <= s.H && (cTx == cTx) && (cTy == cTy)) {
+        uint8_t* c = s_cache[wv];
+#pragma unroll
+        for (int q = 0; q < kSubC * kSubC / 64 / 4; q++) {   // 4 bytes per lane per step
+            const int i = (q * 64 + lane) * 4, yy = i / kSubC, xx = i - yy * kSubC;
+            const uint8_t* src = s.img + (long long)(cy0 + yy) * s.pitch + cx0 + xx;
+            c[i] = src[0];
+            c[i + 1] = src[1];
+            c[i + 2] = src[2];
+            c[i + 3] = src[3];
+        }
+        cache = c;
+        wave_lds_sync();
+    }
     float cIx = cTx, cIy = cTy;
     int iter = 0;
     double err = 0;
@@ -389,7 +437,7 @@ __global__ __launch_bounds__(256) void k_bird_subpix(SubpixSrc s, const float* _
         }
         if (lane < kSubP) {
             float row[kSubP];
-            subpix_row(s, inside, ipx, ipy, fa, fb, sd, lane, row);
+            subpix_row(s, inside, ipx, ipy, fa, fb, sd, lane, row, cache, cx0, cy0);
 #pragma unroll
             for (int j = 0; j < kSubP; j++) patch[lane * kSubP + j] = row[j];
         }
@@ -410,9 +458,22 @@ __global__ __launch_bounds__(256) void k_bird_subpix(SubpixSrc s, const float* _
         }
         wave_lds_sync();
         double acc = 0;
-        if (lane < 5) {
+        if (lane < 5) {   // in order; row g+1's loads are in flight while row g is added
             const double* t = terms + lane * kSubE;
-            for (int e = 0; e < kSubE; e++) acc += t[e];
+            double v[kSubW], w[kSubW];
+#pragma unroll
+            for (int j = 0; j < kSubW; j++) v[j] = t[j];
+#pragma unroll
+            for (int g = 0; g < kSubW; g++) {
+                if (g + 1 < kSubW) {
+#pragma unroll
+                    for (int j = 0; j < kSubW; j++) w[j] = t[(g + 1) * kSubW + j];
+                }
+#pragma unroll
+                for (int j = 0; j < kSubW; j++) acc += v[j];
+#pragma unroll
+                for (int j = 0; j < kSubW; j++) v[j] = w[j];
+            }
         }
         const double a = __shfl(acc, 0), b = __shfl(acc, 1), c = __shfl(acc, 2), bb1 = __shfl(acc, 3),
                      bb2 = __shfl(acc, 4);
@@ -495,18 +556,23 @@ struct HostKP {   // cv::KeyPoint + the candidate it came from (payload only: th
     int cand;
 };
 
+struct SelKey {   // (KeyPoint::response, candidate index)
+    float response;
+    int cand;
+};
+
 // KeyPointsFilter::retainBest (keypoint.cpp): nth_element + partition of the boundary ties
-void retain_best(std::vector<HostKP>& kps, int n_points) {
+void retain_best(std::vector<SelKey>& kps, int n_points) {
     if (n_points >= 0 && kps.size() > (size_t)n_points) {
         if (n_points == 0) {
             kps.clear();
             return;
         }
         std::nth_element(kps.begin(), kps.begin() + n_points, kps.end(),
-                         [](const HostKP& a, const HostKP& b) { return a.response > b.response; });
+                         [](const SelKey& a, const SelKey& b) { return a.response > b.response; });
         const float amb = kps[n_points - 1].response;
         auto e = std::partition(kps.begin() + n_points, kps.end(),
-                                [amb](const HostKP& k) { return k.response >= amb; });
+                                [amb](const SelKey& k) { return k.response >= amb; });
         kps.resize(e - kps.begin());
     }
 }
@@ -540,6 +606,17 @@ struct Bird {
     int *d_rowcnt = nullptr, *d_rowoff = nullptr, *d_lvlcnt = nullptr;
     BirdCand* d_cand = nullptr;
     size_t cand_cap = 0;
+    size_t cand_guess = 16384;      // candidates downloaded with the counts (next frame: this one's + 1/8)
+    // host phase timing (ORBGPU_BIRD_TIMING=1: mean microseconds per call printed every 100 calls)
+    bool timing = std::getenv("ORBGPU_BIRD_TIMING") != nullptr;
+    double tacc[8]{};
+    int tcalls = 0;
+    std::chrono::steady_clock::time_point t0;
+    void tstamp(int k) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        tacc[k] += std::chrono::duration<double, std::micro>(now - t0).count();
+    }
     orb_keypoint* d_kps = nullptr;
     int* d_keep = nullptr;
     uint8_t* d_desc = nullptr;
@@ -560,10 +637,11 @@ struct Bird {
     int ensure_pin(size_t bytes);
     int upload(const uint8_t* img, size_t stride, const uint8_t* mask, size_t mstride, bool footprint, bool device_src);
     int build_pyramid(int nl, bool with_mask);
-    int detect_select(bool with_mask, std::vector<HostKP>& sel);
+    int detect_select(bool with_mask, std::vector<HostKP>& sel, int blur_levels);
     int launch_angle(int n);
     int launch_subpix(int n, bool keep);
-    int launch_blur_desc(int nl, int n, bool keep);
+    int launch_blur(int nl);
+    int launch_desc(int n, bool keep);
 };
 
 void Bird::free_geom() {
@@ -796,7 +874,7 @@ int Bird::build_pyramid(int nl, bool with_mask) {
 
 // computeKeyPoints up to the final per-level selection; sel receives the kept keypoints (level coords,
 // octave, size, Harris response) in the reference's order.
-int Bird::detect_select(bool with_mask, std::vector<HostKP>& sel) {
+int Bird::detect_select(bool with_mask, std::vector<HostKP>& sel, int blur_levels) {
     sel.clear();
     const int nl = g.nlevels;
     const int nf = (int)frows.size(), nc = (int)crows.size();
@@ -818,40 +896,50 @@ int Bird::detect_select(bool with_mask, std::vector<HostKP>& sel) {
                            d_score, (int*)nullptr, d_rowoff, d_cand);
         if ((e = hipGetLastError()) != hipSuccess) return set_error("birdview FAST", e), ORB_ERR_HIP;
         int r;
-        if ((r = ensure_pin(kBirdMaxLevels * sizeof(int))) != ORB_OK) return r;
-        if ((e = hipMemcpyAsync(h_pin, d_lvlcnt, nl * sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        // the blurred pyramid only needs the pyramid: it runs while the host selects
+        if (blur_levels > 0 && (r = launch_blur(blur_levels)) != ORB_OK) return r;
+        // one download of the level counts and a speculative prefix of the candidates (sized from the
+        // previous frame); a second only if this frame has more
+        const size_t hdr = 64, guess = std::min(cand_guess, cand_cap);
+        if ((r = ensure_pin(hdr + guess * sizeof(BirdCand))) != ORB_OK) return r;
+        uint8_t* hp = (uint8_t*)h_pin;
+        if ((e = hipMemcpyAsync(hp, d_lvlcnt, nl * sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (guess && (e = hipMemcpyAsync(hp + hdr, d_cand, guess * sizeof(BirdCand), hipMemcpyDeviceToHost, stream)) !=
+                          hipSuccess) ||
             (e = hipStreamSynchronize(stream)) != hipSuccess)
-            return set_error("birdview candidate counts", e), ORB_ERR_HIP;
-        std::memcpy(last_lvlcnt.data(), h_pin, nl * sizeof(int));
+            return set_error("birdview candidate download", e), ORB_ERR_HIP;
+        tstamp(1);
+        std::memcpy(last_lvlcnt.data(), hp, nl * sizeof(int));
         size_t total = 0;
         for (int l = 0; l < nl; l++) total += last_lvlcnt[l];
         if (total > cand_cap) return set_error("birdview candidate overflow", hipSuccess), ORB_ERR_INTERNAL;
         last_cands.resize(total);
-        if (total) {
-            if ((r = ensure_pin(total * sizeof(BirdCand))) != ORB_OK) return r;
-            if ((e = hipMemcpyAsync(h_pin, d_cand, total * sizeof(BirdCand), hipMemcpyDeviceToHost, stream)) !=
+        std::memcpy(last_cands.data(), hp + hdr, std::min(total, guess) * sizeof(BirdCand));
+        if (total > guess) {
+            const size_t rest = total - guess;
+            if ((r = ensure_pin(rest * sizeof(BirdCand))) != ORB_OK) return r;
+            if ((e = hipMemcpyAsync(h_pin, d_cand + guess, rest * sizeof(BirdCand), hipMemcpyDeviceToHost, stream)) !=
                     hipSuccess ||
                 (e = hipStreamSynchronize(stream)) != hipSuccess)
                 return set_error("birdview candidates download", e), ORB_ERR_HIP;
-            std::memcpy(last_cands.data(), h_pin, total * sizeof(BirdCand));
+            std::memcpy(last_cands.data() + guess, h_pin, rest * sizeof(BirdCand));
         }
+        cand_guess = total + total / 8 + 256;
+    } else if (blur_levels > 0) {
+        int r;
+        if ((r = launch_blur(blur_levels)) != ORB_OK) return r;
     }
-    // KeyPointsFilter::retainBest(2 N) on the FAST response, per level; then Harris, retainBest(N)
-    std::vector<std::vector<HostKP>> lv(nl);
+    // KeyPointsFilter::retainBest(2 N) on the FAST response, per level; then Harris, retainBest(N).
+    // nth_element / partition see only the responses, so they run on 8-byte (response, candidate)
+    // keys: the resulting arrangement is the one a vector<cv::KeyPoint> gets.
+    std::vector<std::vector<SelKey>> lv(nl);
     size_t off = 0;
     for (int l = 0; l < nl; l++) {
         auto& k = lv[l];
-        k.reserve(last_lvlcnt[l]);
-        for (int i = 0; i < last_lvlcnt[l]; i++) {
-            const BirdCand& c = last_cands[off + i];
-            k.push_back({(float)(c.xy & 0xFFFF), (float)(c.xy >> 16), 7.f, -1.f, (float)c.score, 0, -1, (int)(off + i)});
-        }
+        k.resize(last_lvlcnt[l]);
+        for (int i = 0; i < last_lvlcnt[l]; i++) k[i] = {(float)last_cands[off + i].score, (int)(off + i)};
         off += last_lvlcnt[l];
         retain_best(k, 2 * g.L[l].nfeat);
-        for (auto& kp : k) {
-            kp.octave = l;
-            kp.size = 31 * g.L[l].scale;
-        }
     }
     size_t any = 0;
     for (int l = 0; l < nl; l++) any += lv[l].size();
@@ -859,7 +947,11 @@ int Bird::detect_select(bool with_mask, std::vector<HostKP>& sel) {
     for (int l = 0; l < nl; l++) {
         for (auto& kp : lv[l]) kp.response = last_cands[kp.cand].harris;
         retain_best(lv[l], g.L[l].nfeat);
-        sel.insert(sel.end(), lv[l].begin(), lv[l].end());
+        const float size = 31 * g.L[l].scale;
+        for (const auto& kp : lv[l]) {
+            const BirdCand& c = last_cands[kp.cand];
+            sel.push_back({(float)(c.xy & 0xFFFF), (float)(c.xy >> 16), size, -1.f, kp.response, l, -1, kp.cand});
+        }
     }
     return ORB_OK;
 }
@@ -879,10 +971,15 @@ int Bird::launch_subpix(int n, bool keep) {
     return e == hipSuccess ? ORB_OK : (set_error("k_bird_subpix", e), ORB_ERR_HIP);
 }
 
-int Bird::launch_blur_desc(int nl, int n, bool keep) {
+int Bird::launch_blur(int nl) {
     const int2* d_brows = d_rows + frows.size() + crows.size();
     const int nb = brow0[nl];
     if (nb) hipLaunchKernelGGL(k_bird_blur, dim3((max_w + 255) / 256, nb), dim3(256), 0, stream, d_geom, d_brows, d_pyr, d_blur);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ORB_OK : (set_error("k_bird_blur", e), ORB_ERR_HIP);
+}
+
+int Bird::launch_desc(int n, bool keep) {
     if (n)
         hipLaunchKernelGGL(k_bird_desc, dim3((n + 3) / 4), dim3(256), 0, stream, d_geom, d_pyr, d_blur, d_pattern, d_kps,
                            keep ? d_keep : nullptr, n, d_desc);
@@ -979,8 +1076,12 @@ static int bird_run(orb_bird* b, bool with_mask, bool subpix_compute, orb_keypoi
                     uint8_t* desc) {
     int r;
     std::vector<HostKP> sel;
+    if (b->timing) b->t0 = std::chrono::steady_clock::now();
     if ((r = b->build_pyramid(b->g.nlevels, with_mask)) != ORB_OK) return r;
-    if ((r = b->detect_select(with_mask, sel)) != ORB_OK) return r;
+    // the fused call blurs every level while the host selects (compute() would blur max octave + 1 of
+    // them; the extra levels are never read)
+    if ((r = b->detect_select(with_mask, sel, subpix_compute ? b->g.nlevels : 0)) != ORB_OK) return r;
+    b->tstamp(2);
     const int ns = (int)sel.size();
     if (!subpix_compute && ns > cap) {
         *n = ns;
@@ -1002,11 +1103,9 @@ static int bird_run(orb_bird* b, bool with_mask, bool subpix_compute, orb_keypoi
         *n = ns;
         return ORB_OK;
     }
-    // cornerSubPix on the level-0 image, border flag, blurred pyramid, descriptors
-    int nl = 0;
-    for (const auto& k : sel) nl = std::max(nl, k.octave + 1);
+    // cornerSubPix on the level-0 image, border flag, descriptors on the blurred pyramid
     if ((r = b->launch_subpix(ns, true)) != ORB_OK) return r;
-    if ((r = b->launch_blur_desc(std::max(nl, 1), ns, true)) != ORB_OK) return r;
+    if ((r = b->launch_desc(ns, true)) != ORB_OK) return r;
     const size_t kb = (size_t)ns * sizeof(orb_keypoint), fb = (size_t)ns * sizeof(int), db = (size_t)ns * 32;
     if ((r = b->ensure_pin(kb + fb + db + 64)) != ORB_OK) return r;
     uint8_t* hp = (uint8_t*)b->h_pin;
@@ -1014,7 +1113,15 @@ static int bird_run(orb_bird* b, bool with_mask, bool subpix_compute, orb_keypoi
                (e = hipMemcpyAsync(hp + kb, b->d_keep, fb, hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
                (e = hipMemcpyAsync(hp + kb + fb, b->d_desc, db, hipMemcpyDeviceToHost, b->stream)) != hipSuccess))
         return set_error("birdview result download", e), ORB_ERR_HIP;
+    b->tstamp(3);
     if ((e = hipStreamSynchronize(b->stream)) != hipSuccess) return set_error("birdview sync", e), ORB_ERR_HIP;
+    b->tstamp(4);
+    if (b->timing && ++b->tcalls % 100 == 0) {
+        std::fprintf(stderr, "bird timing (us, cumulative from call start): counts+cands sync %.1f  selection done %.1f  "
+                             "phase-2 issued %.1f  final sync %.1f\n", b->tacc[1] / 100, b->tacc[2] / 100,
+                     b->tacc[3] / 100, b->tacc[4] / 100);
+        for (double& t : b->tacc) t = 0;
+    }
     const orb_keypoint* rk = (const orb_keypoint*)hp;
     const int* keep = (const int*)(hp + kb);
     const uint8_t* rd = hp + kb + fb;
@@ -1119,7 +1226,7 @@ extern "C" int orb_bird_compute(orb_bird* b, const uint8_t* img, int w, int h, s
     if ((he = hipMemcpyAsync(b->d_kps, v.data(), m * sizeof(orb_keypoint), hipMemcpyHostToDevice, b->stream)) !=
         hipSuccess)
         return set_error("birdview keypoint upload", he), ORB_ERR_HIP;
-    if ((r = b->launch_blur_desc(nl, m, false)) != ORB_OK) return r;
+    if ((r = b->launch_blur(nl)) != ORB_OK || (r = b->launch_desc(m, false)) != ORB_OK) return r;
     if ((he = hipMemcpyAsync(desc, b->d_desc, (size_t)m * 32, hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
         (he = hipStreamSynchronize(b->stream)) != hipSuccess)
         return set_error("birdview descriptor download", he), ORB_ERR_HIP;
