@@ -166,6 +166,7 @@ def main():
     ap.add_argument("--no-stereo", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-bird", action="store_true")
+    ap.add_argument("--no-c4", action="store_true")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -395,6 +396,49 @@ def main():
         for ptr in (di, dm):
             L.orb_device_free(ex.h, ptr)
 
+    # ---- C4 end to end through the reference's own host-image boundary, one GPU: per tracking frame,
+    # ORBextractor on the rectified left and right images (Frame.cc:124-127), ComputeStereoMatches
+    # (:662-836), the birdview cv::ORB stream (:320-342) and the bird(t) x bird(t-1) all-pairs Hamming
+    # top-2 — synchronous per frame, uploads and downloads included (latency a drop-in caller sees)
+    c4 = None
+    if not args.no_c4:
+        from orbgpu.synth import synth_bird_mask, synth_stereo_right
+        exl = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=local)
+        exr = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=local)
+        bo = orbgpu.BirdORB(2000, device=local)
+        mt = orbgpu.ORBmatcher(0.7, True, device=local)
+        nc4 = min(16, len(frames) - 1)
+        lefts = [np.ascontiguousarray(frames[i]) for i in range(nc4 + 1)]
+        rights = [synth_stereo_right(lefts[i], first + i) for i in range(nc4 + 1)]
+        bmask = synth_bird_mask(w, h, first)
+        birds = [np.ascontiguousarray(frames[(i + nc4 // 2) % len(frames)]) for i in range(nc4 + 1)]
+
+        def c4_frame(i, prev_desc):
+            kl, dl = exl(lefts[i])
+            kr, dr = exr(rights[i])
+            _u, _d, nst = orbgpu.compute_stereo_matches(exl, exr, kl, dl, kr, dr, 0.54, 0.54 * 721.5)
+            kb, db = bo.extract(birds[i], bmask)
+            nm = 0
+            if prev_desc is not None and len(db) and len(prev_desc):
+                dist, _idx, _nv = mt.hamming_topk(db, prev_desc, 2)
+                nm = int((dist[:, 0] <= 50).sum())
+            return db, len(kl) + len(kr), nst, len(kb), nm
+        prev, _, _, _, _ = c4_frame(0, None)
+        barrier(dist)
+        tc0 = time.perf_counter()
+        tot = [0, 0, 0, 0]
+        for i in range(1, nc4 + 1):
+            prev, a, b_, c_, d_ = c4_frame(i, prev)
+            tot = [tot[0] + a, tot[1] + b_, tot[2] + c_, tot[3] + d_]
+        tc1 = time.perf_counter()
+        c4 = {"ms_per_frame": round((tc1 - tc0) / nc4 * 1e3, 3), "frames_per_s": round(nc4 / (tc1 - tc0), 1),
+              "stereo_keypoints_per_frame": tot[0] // nc4, "left_with_depth_per_frame": tot[1] // nc4,
+              "bird_keypoints_per_frame": tot[2] // nc4, "bird_matches_le_th_low_per_frame": tot[3] // nc4,
+              "note": "host images: left + right ORBextractor, ComputeStereoMatches, birdview cv::ORB + cornerSubPix, "
+                      "bird(t) x bird(t-1) Hamming top-2; synchronous per frame on one GPU"}
+        for o in (exl, exr, bo):
+            o.close()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cfg, frames[:32])
@@ -411,7 +455,7 @@ def main():
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
                "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo,
-               "bird": bird, "host_path": host_path}
+               "bird": bird, "c4_frame": c4, "host_path": host_path}
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)
