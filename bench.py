@@ -167,6 +167,9 @@ def main():
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-bird", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("ORBGPU_BENCH_PIPELINES", "3")),
+                    help="batches in flight: consecutive steps alternate over this many extractor contexts "
+                         "(own stream and buffers each), so one batch's latency-bound phases overlap another's")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -190,22 +193,32 @@ def main():
     except Exception:
         torch, has_torch_cuda = None, False
 
+    exs = [ex]
+    for _ in range(1, max(1, args.pipelines)):
+        e2 = orbgpu.BatchExtractor(nf, w, h, B, device=local)
+        e2.upload(frames)
+        exs.append(e2)
+
     def sync():
-        ex.sync()
+        for e in exs:
+            e.sync()
         if has_torch_cuda:
             torch.cuda.synchronize(local)
 
     for _ in range(args.warmup):
-        ex.launch()
+        for e in exs:
+            e.launch()
     sync()
     kps_per_step = int(ex.counts().sum())
+    assert all(int(e.counts().sum()) == kps_per_step for e in exs)
 
-    # timed region: no per-kernel events (they add a marker packet per kernel boundary)
+    # timed region: no per-kernel events (they add a marker packet per kernel boundary); step s runs
+    # on context s mod pipelines
     barrier(dist)
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ex.launch()
+    for st in range(args.steps):
+        exs[st % len(exs)].launch()
     sync()
     t1 = time.perf_counter()
     barrier(dist)
@@ -450,7 +463,8 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": cfg["name"], "width": w, "height": h, "nfeatures": nf, "nlevels": 8,
                           "scale_factor": 1.2, "ini_th_fast": 20, "min_th_fast": 7, "batch_per_gpu": B,
-                          "global_batch": B * world, "parallelism": f"frame-sharded x{world} (no collective)"},
+                          "global_batch": B * world, "parallelism": f"frame-sharded x{world} (no collective)",
+                          "batches_in_flight": len(exs)},
                "frames_per_s": round(total_frames / tmax, 1),
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
@@ -459,7 +473,8 @@ def main():
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)
-    ex.close()
+    for e in exs:
+        e.close()
     if dist is not None:
         dist.destroy_process_group()
 
