@@ -687,19 +687,23 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const uint32_t V = __builtin_amdgcn_alignbyte(A1, A0, 3);     // centres x0 .. x0+3
                 const uint32_t P4 = __builtin_amdgcn_alignbyte(A2, A1, 2);    // x0+3 .. x0+6
                 const uint32_t P12 = A0;                                      // x0-3 .. x0
-                constexpr uint32_t LO = 0x00FF00FFu;
-                const uint32_t re = compass2(V & LO, P0 & LO, P4 & LO, P8 & LO, P12 & LO, tt);                 // px 0, 2
-                const uint32_t ro = compass2((V >> 8) & LO, (P0 >> 8) & LO, (P4 >> 8) & LO, (P8 >> 8) & LO,
-                                             (P12 >> 8) & LO, tt);                                          // px 1, 3
+                // bytes 0, 2 / 1, 3 into 16-bit lanes: one v_perm_b32 each (0x0c selects a zero byte)
+                auto ev = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c00u); };
+                auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
+                const uint32_t re = compass2(ev(V), ev(P0), ev(P4), ev(P8), ev(P12), tt);   // px 0, 2
+                const uint32_t ro = compass2(od(V), od(P0), od(P4), od(P8), od(P12), tt);   // px 1, 3
                 pm = (int)((((re >> 15) & 1u) | ((ro >> 14) & 2u) | ((re >> 29) & 4u) | ((ro >> 28) & 8u)) & xvalid);
             }
+            // compaction: one wave prefix sum of the per-lane survivor counts, then each lane writes
+            // its (<= 4) entries at its offset
+            const int cnt = __popc(pm);
+            const int incl = wave_incl_scan(cnt);
+            int pos = nlist + incl - cnt;
+            const int base = dy * 64 + x0;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const bool bit = (pm >> i) & 1;
-                const unsigned long long m = __ballot(bit);
-                if (bit) sList[nlist + lanes_below(m)] = (uint16_t)(dy * 64 + x0 + i);
-                nlist += __popcll(m);
-            }
+            for (int i = 0; i < 4; i++)
+                if ((pm >> i) & 1) sList[pos++] = (uint16_t)(base + i);
+            nlist += __builtin_amdgcn_readlane(incl, 63);
         }
         wave_lds_sync();
         ORBGPU_STAMP(2);
@@ -790,7 +794,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
         blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
-    const int item0 = (blk * 4 + wv) * 2;
+    const int item0 = (blk * (int)(blockDim.x >> 6) + wv) * 2;
     if (item0 >= total) return;   // whole wave; nothing below uses a block barrier
     const int wb = g->fast_wave_bytes;
     uint8_t* tile = smem + (size_t)wv * wb;
@@ -1387,6 +1391,7 @@ __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
     return lb & ~la;
 }
 
+template <int WPB>
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
@@ -1396,8 +1401,8 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     // per wave: 43x48 window (+16 B pad; reused for the transposed 37x40 blurred patch) and the
     // transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch; pitch 50 spreads the transposed
     // stores of the 10 column groups over distinct banks)
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kDescWin * kDescWinPitch + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][40 * kRtPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[WPB][kDescWin * kDescWinPitch + 16];
+    __shared__ __attribute__((aligned(16))) uint16_t s_rt[WPB][40 * kRtPitch];
     const int f = blockIdx.y;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int nl = g->nlevels;
@@ -1407,7 +1412,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         for (int i = 0; i < nl; i++) tot += cnts[i];
         outN[f] = tot;
     }
-    const int s = blockIdx.x * 4 + wv;
+    const int s = blockIdx.x * WPB + wv;
     if (s >= g->nkpcap) return;
     int l = 0;
     while (l + 1 < nl && s >= g->L[l + 1].kp_base) ++l;
@@ -1660,15 +1665,22 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
             hipLaunchKernelGGL(k_fast, dim3(items), dim3(256), 0, s, b.d_geom, d_frames, frame_pitch, row_stride,
                                b.d_pyr, b.d_cands, b.d_cellCount, items, b.fast_remap);
         }
-        else if (g.fast_compact)
-            hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(cdiv(items, 8)), dim3(256), (size_t)g.fast_wave_bytes * 4, s,
-                               b.d_geom, b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands,
-                               b.d_cellCount, items, cbeg, cnum, b.fast_remap, b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
-        else
-            hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(cdiv(items, 8)), dim3(256),
-                               (size_t)g.fast_wave_bytes * 4, s, b.d_geom, b.d_cells, d_frames, frame_pitch,
-                               row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum, b.fast_remap,
-                               b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
+        else {
+            // b.fast_wpb waves per workgroup: a workgroup's LDS is released only when its slowest wave
+            // ends, so fewer waves per workgroup waste less of the CU on uneven cells
+            const int wpb = b.fast_wpb;
+            const unsigned nblk = cdiv(items, 2 * wpb);
+            const size_t lds = (size_t)g.fast_wave_bytes * wpb;
+            if (g.fast_compact)
+                hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(nblk), dim3(64 * wpb), lds, s, b.d_geom, b.d_cells,
+                                   d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg,
+                                   cnum, b.fast_remap, b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
+            else
+                hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(nblk), dim3(64 * wpb), lds, s, b.d_geom,
+                                   b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount,
+                                   items, cbeg, cnum, b.fast_remap, b.d_stamps,
+                                   cbeg == 0 && b.zero_err ? b.d_err : nullptr);
+        }
     };
     auto resize_levels = [&](int l0, int l1, hipStream_t s) {
         for (int l = l0; l < l1; l++) {
@@ -1736,9 +1748,14 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     }
     if (marker) marker(user, ORB_K_OCTREE, 0, stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
-    hipLaunchKernelGGL(k_describe, dim3(cdiv(g.nkpcap, 4), nframes), dim3(256), 0, stream, b.d_geom, d_frames,
-                       frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
-                       b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr);
+    {   // b.desc_wpb keypoint wavefronts per workgroup
+        unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
+        const int wpb = b.desc_wpb;
+        auto kern = wpb == 1 ? k_describe<1> : wpb == 2 ? k_describe<2> : k_describe<4>;
+        hipLaunchKernelGGL(kern, dim3(cdiv(g.nkpcap, wpb), nframes), dim3(64 * wpb), 0, stream, b.d_geom, d_frames,
+                           frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
+                           dst);
+    }
     if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);
     return hipGetLastError();
 }
