@@ -119,3 +119,32 @@ def test_bird_empty_and_capacity(orbgpu_mod, bird):
     assert len(k) == 0
     kk, d = bird.extract(np.full((300, 400), 77, np.uint8))
     assert len(kk) == 0 and d.shape == (0, 32)
+
+
+def test_bird_stream_into_birdview_match(orbgpu_mod, oracle_mod, bird):
+    """Birdview chain of Tracking (Tracking.cc:744 BirdviewMatch(LastFrame, CurrentFrame, ..., 15)): both
+    frames' birdview features from the GPU stream, candidates from the birdview grid, the windowed
+    matcher on the GPU — equal to the oracle chain."""
+    w, h = 640, 480
+    a = _frame(w, h, 20)
+    rng = np.random.default_rng(20)
+    b = np.clip(np.roll(a, (2, 3), axis=(0, 1)).astype(np.int16) + rng.integers(-2, 3, a.shape), 0, 255).astype(np.uint8)
+    mask = _mask(w, h, 20)
+    ka, da = bird.extract(a, mask)
+    kb, db = bird.extract(b, mask)
+    oka, oda = oracle_mod.OracleCvORB(2000).extract(a, mask)
+    okb, odb = oracle_mod.OracleCvORB(2000).extract(b, mask)
+    assert ka.tobytes() == oka.tobytes() and kb.tobytes() == okb.tobytes()
+    assert np.array_equal(da, oda) and np.array_equal(db, odb)
+    offs, idxs = [0], []
+    for k in ka:   # Frame::GetFeaturesInAreaBirdview over the birdview grid (the whole image)
+        c = orbgpu_mod.features_in_area(kb, 0, w, 0, h, float(k["x"]), float(k["y"]), 15, -1, -1)
+        idxs.extend(c.tolist())
+        offs.append(len(idxs))
+    off = np.array(offs, np.int32)
+    cand = np.array(idxs, np.int32)
+    m = orbgpu_mod.ORBmatcher(0.9, True)
+    n, mm = m.BirdviewMatch(da, ka, db, kb, off, cand)
+    on, om = oracle_mod.window_match(0.9, True, False, da, ka, db, kb, off, cand)
+    assert n == on and np.array_equal(mm, om)
+    assert n > 200
