@@ -34,7 +34,7 @@ def main():
     if os.path.exists(rep):
         d = json.load(open(rep))
         d["commit"] = commit
-        d["batch_frames_per_launch"] = 64
+        d["batch_frames_per_launch"] = json.loads(lines[-1])["config"]["batch_per_gpu"]
         d["config"] = "C3 1280x720, 2000 features, bench.py --steps 3 --warmup 1 --no-cpu"
         d["method"] = ("tools/pmc.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_* --kernel-trace (separate "
                        "passes); tools/pmc_calib.hip known-byte streams give the per-width factor")
