@@ -4,9 +4,9 @@
 #   WRITE_SIZE.  Results under gpurun_out/pmc/<pass>/; tools/pmc_report.py turns them into
 #   profiles/pmc_traffic.json.  Every GPU step has its own time limit; the script stops at the first failure.
 OUT=gpurun_out/pmc; mkdir -p $OUT; export TMPDIR=/tmp
-# only the 64-frame batch launches: the host-path and stereo legs would mix 1- and 32-frame dispatches
+# only the batch launches: the host-path, stereo and C4 legs would mix 1- and 2-frame dispatches
 # into the per-launch means
-ARGS="--steps 3 --warmup 1 --no-cpu --no-host-path --no-stereo ${BENCH_ARGS}"
+ARGS="--steps 3 --warmup 1 --no-cpu --no-host-path --no-stereo --no-c4 ${BENCH_ARGS}"
 timeout -k 10 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/pmc_calib tools/pmc_calib.hip || { echo "calib build failed"; exit 1; }
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/calib_$ctr -o run -- /tmp/pmc_calib > $OUT/calib_$ctr.log 2>&1 || { echo "calib $ctr failed"; tail -20 $OUT/calib_$ctr.log; exit 1; }
