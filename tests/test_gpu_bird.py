@@ -47,6 +47,7 @@ def test_bird_pyramid_and_candidates(orbgpu_mod, oracle_mod, bird, w, h, idx, ma
     (1280, 720, 3, "noise", 2000),      # maximum candidate count: large nth_element inputs
     (640, 480, 5, "scene", 500),
     (200, 150, 6, "scene", 300),         # small: the top levels fall under 2*edgeThreshold
+    (641, 479, 14, "scene", 1000),       # odd sizes: unaligned rows, blur tail columns
     (1280, 720, 7, "flat", 2000),        # no corners at all
 ])
 def test_bird_detect_bit_exact(orbgpu_mod, oracle_mod, w, h, idx, kind, nf):
@@ -88,7 +89,8 @@ def test_bird_compute_bit_exact(orbgpu_mod, oracle_mod, bird):
     assert np.array_equal(dg, do)
 
 
-@pytest.mark.parametrize("w,h,idx,masked", [(1280, 720, 10, True), (1280, 720, 11, False), (640, 480, 12, True)])
+@pytest.mark.parametrize("w,h,idx,masked", [(1280, 720, 10, True), (1280, 720, 11, False), (640, 480, 12, True),
+                                             (643, 477, 15, True)])
 def test_bird_extract_fused_bit_exact(orbgpu_mod, oracle_mod, bird, w, h, idx, masked):
     """Frame.cc:320-342 end to end: footprint, masked detect, cornerSubPix, border cull, descriptors."""
     img = _frame(w, h, idx)
