@@ -18,6 +18,7 @@ Also reported on the same line:
 Usage: python bench.py [--gpus N --steps K --warmup W --batch B --config c3|c2|c5 --no-cpu]
 """
 import argparse
+import resource
 import json
 import os
 import platform
@@ -224,11 +225,15 @@ def main():
     # on context s mod pipelines
     barrier(dist)
     sync()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     for st in range(args.steps):
         exs[st % len(exs)].launch()
     sync()
     t1 = time.perf_counter()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    # host cores this rank kept busy during the timed steps (host utilisation beside the 1->N curve)
+    host_busy = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / max(t1 - t0, 1e-9)
     barrier(dist)
     # per-kernel breakdown (HIP events on the library's stream) from a separate pass of the same steps
     ex.profile(True)
@@ -238,6 +243,7 @@ def main():
     kms, klaunch = ex.profile_read()
     ex.profile(False)
     local_time = t1 - t0
+    _, host_busy_sum = reduce_max_sum(dist, 0.0, host_busy)
     local_kps = kps_per_step * args.steps
     tmax, total_kps = reduce_max_sum(dist, local_time, local_kps)
     _, total_frames = reduce_max_sum(dist, 0.0, float(B * args.steps))
@@ -474,6 +480,7 @@ def main():
                           "global_batch": B * world, "parallelism": f"frame-sharded x{world} (no collective)",
                           "batches_in_flight": len(exs)},
                "frames_per_s": round(total_frames / tmax, 1),
+               "host_cores_busy": round(host_busy_sum, 3),   # all ranks' processes, timed region
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
                "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo,
