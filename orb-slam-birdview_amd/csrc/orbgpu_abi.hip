@@ -481,7 +481,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.e);
     }
     void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
-                    c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_kps, c->d_desc, c->d_counts,
+                    c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_hout,
                     c->d_scratch};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -569,39 +569,37 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     hipError_t e;
     const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
     const int kcap = c->geom.nkpcap;
-    if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess ||
-        (e = grow(c->d_kps, c->kps_cap, (size_t)kcap)) != hipSuccess ||
-        (e = grow(c->d_desc, c->desc_cap, (size_t)kcap * 32)) != hipSuccess ||
-        (e = grow(c->d_counts, c->counts_cap, 1)) != hipSuccess)
+    const size_t kbytes = ((size_t)kcap * sizeof(orb_keypoint) + 63) & ~(size_t)63;   // descriptors 64-B aligned
+    const size_t need = 16 + kbytes + (size_t)kcap * 32;
+    if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess || (e = grow(c->d_hout, c->hout_cap, need)) != hipSuccess)
         return set_error("device allocation", e), ORB_ERR_NOMEM;
+    int* d_cnt = reinterpret_cast<int*>(c->d_hout);
+    orb_keypoint* d_k = reinterpret_cast<orb_keypoint*>(c->d_hout + 16);
+    uint8_t* d_d = c->d_hout + 16 + kbytes;
     if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return set_error("upload image", e), ORB_ERR_HIP;
-    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, c->d_kps, c->d_desc, c->d_counts,
-                             kcap)) != ORB_OK)
+    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, d_k, d_d, d_cnt, kcap)) != ORB_OK)
         return st;
-    // one download into pinned staging: count, overflow flag, and every keypoint / descriptor slot
-    // (at most kcap * 60 bytes), then a single synchronisation
-    const size_t need = 16 + (size_t)kcap * (sizeof(orb_keypoint) + 32);
-    if (need > c->pinned_cap) {
+    // two downloads into pinned staging (the output block: count, every keypoint / descriptor slot; and
+    // the overflow flag), then a single synchronisation
+    if (need + 16 > c->pinned_cap) {
         if (c->h_pinned) (void)hipHostFree(c->h_pinned);
         c->h_pinned = nullptr;
         c->pinned_cap = 0;
-        if ((e = hipHostMalloc(&c->h_pinned, need, hipHostMallocDefault)) != hipSuccess)
+        if ((e = hipHostMalloc(&c->h_pinned, need + 16, hipHostMallocDefault)) != hipSuccess)
             return set_error("pinned staging", e), ORB_ERR_NOMEM;
-        c->pinned_cap = need;
+        c->pinned_cap = need + 16;
     }
     uint8_t* hp = static_cast<uint8_t*>(c->h_pinned);
     int* hcnt = reinterpret_cast<int*>(hp);
-    orb_keypoint* hk = reinterpret_cast<orb_keypoint*>(hp + 16);
-    uint8_t* hd = hp + 16 + (size_t)kcap * sizeof(orb_keypoint);
-    if ((e = hipMemcpyAsync(hcnt, c->d_counts, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(hcnt + 1, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(hk, c->d_kps, (size_t)kcap * sizeof(orb_keypoint), hipMemcpyDeviceToHost, c->stream)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(hd, c->d_desc, (size_t)kcap * 32, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+    int* herr = reinterpret_cast<int*>(hp + need);
+    const orb_keypoint* hk = reinterpret_cast<const orb_keypoint*>(hp + 16);
+    const uint8_t* hd = hp + 16 + kbytes;
+    if ((e = hipMemcpyAsync(hp, c->d_hout, need, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return set_error("download keypoints", e), ORB_ERR_HIP;
-    if (hcnt[1]) {
+    if (*herr) {
         set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
         return ORB_ERR_INTERNAL;
     }

@@ -78,12 +78,10 @@ struct Ctx {
     // host-image path (orb_extract)
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
-    orb_keypoint* d_kps = nullptr;
-    size_t kps_cap = 0;
-    uint8_t* d_desc = nullptr;
-    size_t desc_cap = 0;
-    int* d_counts = nullptr;
-    size_t counts_cap = 0;
+    // host-path outputs in one allocation, [count | 12 B pad | keypoints | descriptors], so that one
+    // download brings all of them back
+    uint8_t* d_hout = nullptr;
+    size_t hout_cap = 0;
     void* h_pinned = nullptr;     // pinned staging for orb_extract's single download (count, flag, keypoints, descriptors)
     size_t pinned_cap = 0;
 
