@@ -640,7 +640,7 @@ __device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, cons
 
 // One cell after its ROI is in the tile: prefilter, exact arc strength, cell-local NMS with the
 // minThFAST fallback, raster-order emission (see k_fast above for the semantics).
-template <int TP, int SP>
+template <int TP, int SP, int PX>
 __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane, int xoff,
                                                uint8_t* tile, uint8_t* sM, uint16_t* sList,
                                                unsigned long long* keepb, uint32_t* __restrict__ cands,
@@ -650,13 +650,13 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
     if (lane < dh) keepb[lane] = 0ull;
     wave_lds_sync();
     ORBGPU_STAMP(1);
-    // lane -> (run of 4 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
-    const int nruns = (dw + 3) >> 2;
+    // lane -> (run of PX pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
+    const int nruns = (dw + PX - 1) / PX;
     const int rpi = 64 / nruns;                          // rows per iteration
     const int lrow = (int)div20(lane, recip20(nruns));
-    const int x0 = 4 * (lane - lrow * nruns);
+    const int x0 = PX * (lane - lrow * nruns);
     const bool lane_on = lrow < rpi;
-    const uint32_t xvalid = x0 + 4 <= dw ? 0xFu : (1u << max(dw - x0, 0)) - 1u;
+    const uint32_t xvalid = x0 + PX <= dw ? (1u << PX) - 1u : (1u << max(dw - x0, 0)) - 1u;
     const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
     const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
     // Pass 0 runs the whole cell at iniThFAST; only a cell left with no keypoint (:812-816) runs pass 1
@@ -673,7 +673,35 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         for (int r0 = 0; r0 < dh; r0 += rpi) {
             const int dy = r0 + lrow;
             int pm = 0;
-            if (lane_on && dy < dh) {
+            if (PX == 8 && lane_on && dy < dh) {
+                // 8 pixels: centre bytes x0-3 .. x0+12 (5 dwords), rows +-3 bytes x0 .. x0+7 (3 dwords each)
+                const int sc = (dy + 3) * TP + x0 + xoff;
+                const int s0 = (dy + 6) * TP + x0 + 3 + xoff;
+                const int s8 = dy * TP + x0 + 3 + xoff;
+                const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
+                const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3], w4 = t32[dc + 4];
+                const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);   // x0-3 .. x0
+                const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);   // x0+1 .. x0+4
+                const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);   // x0+5 .. x0+8
+                const uint32_t A3 = __builtin_amdgcn_alignbyte(w4, w3, sc & 3);   // x0+9 .. x0+12
+                const uint32_t q0 = t32[d0], q1 = t32[d0 + 1], q2 = t32[d0 + 2];
+                const uint32_t r0 = t32[d8], r1 = t32[d8 + 1], r2 = t32[d8 + 2];
+                const uint32_t P0a = __builtin_amdgcn_alignbyte(q1, q0, s0 & 3), P0b = __builtin_amdgcn_alignbyte(q2, q1, s0 & 3);
+                const uint32_t P8a = __builtin_amdgcn_alignbyte(r1, r0, s8 & 3), P8b = __builtin_amdgcn_alignbyte(r2, r1, s8 & 3);
+                const uint32_t Va = __builtin_amdgcn_alignbyte(A1, A0, 3), Vb = __builtin_amdgcn_alignbyte(A2, A1, 3);
+                const uint32_t P4a = __builtin_amdgcn_alignbyte(A2, A1, 2), P4b = __builtin_amdgcn_alignbyte(A3, A2, 2);
+                const uint32_t P12a = A0, P12b = A1;
+                auto ev = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c00u); };
+                auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
+                const uint32_t rea = compass2(ev(Va), ev(P0a), ev(P4a), ev(P8a), ev(P12a), tt);
+                const uint32_t roa = compass2(od(Va), od(P0a), od(P4a), od(P8a), od(P12a), tt);
+                const uint32_t reb = compass2(ev(Vb), ev(P0b), ev(P4b), ev(P8b), ev(P12b), tt);
+                const uint32_t rob = compass2(od(Vb), od(P0b), od(P4b), od(P8b), od(P12b), tt);
+                const uint32_t lo4 = ((rea >> 15) & 1u) | ((roa >> 14) & 2u) | ((rea >> 29) & 4u) | ((roa >> 28) & 8u);
+                const uint32_t hi4 = ((reb >> 15) & 1u) | ((rob >> 14) & 2u) | ((reb >> 29) & 4u) | ((rob >> 28) & 8u);
+                pm = (int)((lo4 | (hi4 << 4)) & xvalid);
+            }
+            if (PX == 4 && lane_on && dy < dh) {
                 const int sc = (dy + 3) * TP + x0 + xoff;       // centre row, from pixel x0-3
                 const int s0 = (dy + 6) * TP + x0 + 3 + xoff;   // row +3
                 const int s8 = dy * TP + x0 + 3 + xoff;         // row -3
@@ -701,7 +729,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             int pos = nlist + incl - cnt;
             const int base = dy * 64 + x0;
 #pragma unroll
-            for (int i = 0; i < 4; i++)
+            for (int i = 0; i < PX; i++)
                 if ((pm >> i) & 1) sList[pos++] = (uint16_t)(base + i);
             nlist += __builtin_amdgcn_readlane(incl, 63);
         }
@@ -777,7 +805,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
  * per-wave LDS carve is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors
  * are compacted with per-bit ballots (list order is irrelevant: emission order comes from the keep
  * bitmap, one 64-bit row mask per domain row, emitted in raster order by one lane per row). */
-template <int TP, int SP>
+template <int TP, int SP, int PX>
 __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
@@ -823,7 +851,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         wave_lds_sync();   // the previous cell's last LDS reads happen before this one's writes
         const int xoff = fast_roi_store<TP>(c, lane, k == 0 ? v0 : v1, tile);
         ORBGPU_STAMP(6);
-        fast_cell_body<TP, SP>(g, c, lane, xoff, tile, sM, sList, keepb, cands, cntOut, stamps, item);
+        fast_cell_body<TP, SP, PX>(g, c, lane, xoff, tile, sM, sList, keepb, cands, cntOut, stamps, item);
     }
 }
 
@@ -1671,15 +1699,12 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
             const int wpb = b.fast_wpb;
             const unsigned nblk = cdiv(items, 2 * wpb);
             const size_t lds = (size_t)g.fast_wave_bytes * wpb;
-            if (g.fast_compact)
-                hipLaunchKernelGGL((k_fast_wave<56, 40>), dim3(nblk), dim3(64 * wpb), lds, s, b.d_geom, b.d_cells,
-                                   d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg,
-                                   cnum, b.fast_remap, b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
-            else
-                hipLaunchKernelGGL((k_fast_wave<kFastTilePitch, 64>), dim3(nblk), dim3(64 * wpb), lds, s, b.d_geom,
-                                   b.d_cells, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount,
-                                   items, cbeg, cnum, b.fast_remap, b.d_stamps,
-                                   cbeg == 0 && b.zero_err ? b.d_err : nullptr);
+            auto kern = g.fast_compact ? (b.fast_px == 8 ? k_fast_wave<56, 40, 8> : k_fast_wave<56, 40, 4>)
+                                       : (b.fast_px == 8 ? k_fast_wave<kFastTilePitch, 64, 8>
+                                                         : k_fast_wave<kFastTilePitch, 64, 4>);
+            hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * wpb), lds, s, b.d_geom, b.d_cells, d_frames, frame_pitch,
+                               row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum, b.fast_remap,
+                               b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
         }
     };
     auto resize_levels = [&](int l0, int l1, hipStream_t s) {

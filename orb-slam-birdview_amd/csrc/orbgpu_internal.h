@@ -104,7 +104,8 @@ struct ExtractBuffers {
     int resize_th;                 // output rows per k_resize_tiled tile: 16, 32 or 64 (ORBGPU_RESIZE_TH)
     int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
     int fast_wpb;                  // k_fast_wave wavefronts per workgroup (ORBGPU_FAST_WPB = 1 | 2 | 4)
-    int desc_wpb;                  // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
+    int desc_wpb;
+    int fast_px;                   // k_fast_wave prefilter pixels per lane (ORBGPU_FAST_PX = 4 | 8)                  // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
     unsigned long long* d_stamps;  // k_fast_wave phase timestamps, 8 per (frame, cell) (ORBGPU_FAST_STAMPS=1)
     // Side stream for the pyramid tail split: levels resize_split+1.. are resized there while FAST runs
     // on the cells of levels 0..resize_split (0 = no split; ORBGPU_RESIZE_SPLIT)
