@@ -1419,7 +1419,7 @@ __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
     return lb & ~la;
 }
 
-template <int WPB>
+template <int WPB, bool SMP>
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
@@ -1588,6 +1588,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                     K45 = {(unsigned short)k4, (unsigned short)k5}, K60 = {(unsigned short)k6, 0},
                     K0s = {0, (unsigned short)k0}, K12 = {(unsigned short)k1, (unsigned short)k2},
                     K34 = {(unsigned short)k3, (unsigned short)k4}, K56 = {(unsigned short)k5, (unsigned short)k6};
+    if constexpr (!SMP) {
     uint32_t outw[6];
     int outa[6];
 #pragma unroll
@@ -1627,6 +1628,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     for (int r = 0; r < 6; r++)
         if (outa[r] >= 0) w32[outa[r]] = outw[r];
     wave_lds_sync();
+    }
     DESC_STAMP(4);
 
     // ---- rBRIEF (:108-147): pinned correctly-rounded cos/sin; 256 tests as
@@ -1645,8 +1647,28 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         const float px1 = (float)pp.z, py1 = (float)pp.w;
         const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
         const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
-        const int t0 = ctr[__mul24(__float2int_rn(u2 - u3), kDescBlurPitch) + __float2int_rn(u0 + u1)];
-        const int t1 = ctr[__mul24(__float2int_rn(w2 - w3), kDescBlurPitch) + __float2int_rn(w0 + w1)];
+        int t0, t1;
+        if constexpr (SMP) {
+            // the column pass only at the two sampled pixels: blurred (bx, by) from RT[bx][by .. by+6]
+            auto blur_at = [&](int bx, int by) -> int {
+                const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + __umul24((unsigned)bx, (unsigned)kRtPitch) +
+                                                                       (by & ~1));
+                const bool odd = by & 1;
+                const uint32_t S = __builtin_amdgcn_udot2(odd ? K56 : K60, __builtin_bit_cast(ushort2_t, rp[3]),
+                                   __builtin_amdgcn_udot2(odd ? K34 : K45, __builtin_bit_cast(ushort2_t, rp[2]),
+                                   __builtin_amdgcn_udot2(odd ? K12 : K23, __builtin_bit_cast(ushort2_t, rp[1]),
+                                   __builtin_amdgcn_udot2(odd ? K0s : K01, __builtin_bit_cast(ushort2_t, rp[0]), 0u,
+                                                          false), false), false), false);
+                const bool even = x - 18 + bx < xsimd;
+                const uint32_t bias = even ? 32767u + ((S >> 16) & 1u) : 32768u;
+                return (int)min((S + bias) >> 16, 255u);
+            };
+            t0 = blur_at(18 + __float2int_rn(u2 - u3), 18 + __float2int_rn(u0 + u1));
+            t1 = blur_at(18 + __float2int_rn(w2 - w3), 18 + __float2int_rn(w0 + w1));
+        } else {
+            t0 = ctr[__mul24(__float2int_rn(u2 - u3), kDescBlurPitch) + __float2int_rn(u0 + u1)];
+            t1 = ctr[__mul24(__float2int_rn(w2 - w3), kDescBlurPitch) + __float2int_rn(w0 + w1)];
+        }
         const unsigned long long m = __ballot(t0 < t1);
         if (lane == 0) dst[gq] = m;
     }
@@ -1776,7 +1798,8 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     {   // b.desc_wpb keypoint wavefronts per workgroup
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
         const int wpb = b.desc_wpb;
-        auto kern = wpb == 1 ? k_describe<1> : wpb == 2 ? k_describe<2> : k_describe<4>;
+        auto kern = b.desc_sampled ? (wpb == 1 ? k_describe<1, true> : wpb == 2 ? k_describe<2, true> : k_describe<4, true>)
+                                   : (wpb == 1 ? k_describe<1, false> : wpb == 2 ? k_describe<2, false> : k_describe<4, false>);
         hipLaunchKernelGGL(kern, dim3(cdiv(g.nkpcap, wpb), nframes), dim3(64 * wpb), 0, stream, b.d_geom, d_frames,
                            frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
                            dst);
