@@ -1419,75 +1419,76 @@ __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
     return lb & ~la;
 }
 
-template <int WPB, bool SMP>
-__global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
-                                                  long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
-                                                  const uint32_t* __restrict__ lvlKps,
-                                                  const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
-                                                  uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
-                                                  unsigned long long* __restrict__ dstamps) {
-    // per wave: 43x48 window (+16 B pad; reused for the transposed 37x40 blurred patch) and the
-    // transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch; pitch 50 spreads the transposed
-    // stores of the 10 column groups over distinct banks)
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[WPB][kDescWin * kDescWinPitch + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t s_rt[WPB][40 * kRtPitch];
-    const int f = blockIdx.y;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
+// One keypoint slot of k_describe: decoded from the octree output (level, coordinates, output index).
+struct DescSlot {
+    bool ok, interior;   // a keypoint; its 48-byte aligned window rows stay inside the level (dword loads)
+    int s, l, x, y, score, outIdx;
+    LevelPtr src;
+};
+
+__device__ __forceinline__ DescSlot desc_slot(const Geom* __restrict__ g, int f, int s, const int* cnts,
+                                              const uint32_t* __restrict__ lvlKps, const uint8_t* frames,
+                                              long long framePitch, int rowStride, const uint8_t* pyr) {
+    DescSlot d;
+    d.s = s;
+    d.ok = false;
+    d.interior = false;
+    if (s >= g->nkpcap) return d;
     const int nl = g->nlevels;
-    const int* cnts = lvlCount + f * nl;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        int tot = 0;
-        for (int i = 0; i < nl; i++) tot += cnts[i];
-        outN[f] = tot;
-    }
-    const int s = blockIdx.x * WPB + wv;
-    if (s >= g->nkpcap) return;
     int l = 0;
     while (l + 1 < nl && s >= g->L[l + 1].kp_base) ++l;
     const LevelGeom& L = g->L[l];
     const int k = s - L.kp_base;
-    if (k >= cnts[l]) return;
+    if (k >= cnts[l]) return d;
     int outIdx = k;
     for (int i = 0; i < l; i++) outIdx += cnts[i];
     const uint32_t kp = lvlKps[(long long)f * g->nkpcap + s];
-    const int x = kp & 0xFFF, y = (kp >> 12) & 0xFFF, score = kp >> 24;
-    // optional phase timestamps (ORBGPU_FAST_STAMPS=1), 8 per keypoint slot: start, window, angle,
-    // row pass, column pass, sin/cos, done
-    unsigned long long* dst_st = dstamps ? dstamps + ((long long)f * g->nkpcap + s) * 8 : nullptr;
+    d.ok = true;
+    d.l = l;
+    d.x = kp & 0xFFF;
+    d.y = (kp >> 12) & 0xFFF;
+    d.score = kp >> 24;
+    d.outIdx = outIdx;
+    d.src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(d.src.p) | (uintptr_t)d.src.stride) & 3) == 0;
+    d.interior = aligned && d.x >= 21 && d.x + 27 <= L.w && d.y >= 21 && d.y + 21 < L.h;
+    return d;
+}
+
+// 43 rows x 12 dwords of an interior window, issued into registers
+__device__ __forceinline__ void desc_issue(const DescSlot& d, int lane, uint32_t (&v)[9]) {
+    const int a0 = (d.x - 21) & ~3;
+    const uint8_t* row0 = d.src.p + (long long)(d.y - 21) * d.src.stride + a0;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {   // 43 rows x 12 dwords = 516 <= 9 x 64, all loads in flight
+        const int idx = lane + 64 * r;
+        const int wy = (int)(__umul24((unsigned)idx, 2731u) >> 15), ww = idx - wy * 12;   // idx / 12, idx < 576
+        v[r] = idx < kDescWin * 12 ? *reinterpret_cast<const uint32_t*>(row0 + roi_off(wy, d.src.stride, 4 * ww)) : 0u;
+    }
+}
+
+template <bool SMP>
+__device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
+                                          const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const char4 (&pat)[4],
+                                          orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
+                                          unsigned long long* __restrict__ dstamps) {
+    const int l = d.l, x = d.x, y = d.y, score = d.score, outIdx = d.outIdx;
+    const LevelGeom& L = g->L[l];
+    const LevelPtr src = d.src;
+    unsigned long long* dst_st = dstamps ? dstamps + ((long long)f * g->nkpcap + d.s) * 8 : nullptr;
 #define DESC_STAMP(k) \
     if (dst_st && lane == 0) dst_st[(k)] = __builtin_amdgcn_s_memtime();
     DESC_STAMP(0);
-    const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, f);
-    uint8_t* wbase = s_win[wv];
     uint32_t* w32 = reinterpret_cast<uint32_t*>(wbase);
-    uint16_t* rt = s_rt[wv];
-
-    // BRIEF test pairs of this lane (lane + 64 gq), fetched now so their latency hides under the window's
-    char4 pat[4];
-#pragma unroll
-    for (int gq = 0; gq < 4; gq++) pat[gq] = reinterpret_cast<const char4*>(c_pattern)[lane + 64 * gq];
-
-    // ---- 43x43 window of the unblurred level, pixel (wy, wx) at byte wy*48 + sh + wx
     int sh;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0;
-    if (aligned && x >= 21 && x + 27 <= L.w && y >= 21 && y + 21 < L.h) {   // 48 aligned bytes stay in the row
-        const int a0 = (x - 21) & ~3;
-        const uint8_t* row0 = src.p + (long long)(y - 21) * src.stride + a0;
-        uint32_t v[9];
-#pragma unroll
-        for (int r = 0; r < 9; r++) {   // 43 rows x 12 dwords = 516 <= 9 x 64, all loads in flight
-            const int idx = lane + 64 * r;
-            const int wy = (int)(__umul24((unsigned)idx, 2731u) >> 15), ww = idx - wy * 12;   // idx / 12, idx < 576
-            v[r] = idx < kDescWin * 12 ? *reinterpret_cast<const uint32_t*>(row0 + roi_off(wy, src.stride, 4 * ww))
-                                      : 0u;
-        }
+    if (d.interior) {
 #pragma unroll
         for (int r = 0; r < 9; r++) {
             const int idx = lane + 64 * r;
             if (idx < kDescWin * 12) w32[idx] = v[r];
         }
         sh = (x - 21) & 3;
-    } else {   // near the level border: REFLECT_101 gather (as the blur's border mode), byte loads in
+    } else {
                // flight in two batches of 15 (fewer live registers than one batch of 29)
 #pragma unroll
         for (int hb = 0; hb < 2; hb++) {
@@ -1691,6 +1692,48 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
 #undef DESC_STAMP
 }
 
+/* Fused IC angle + 7x7 blur + rBRIEF, one wavefront per keypoint slot; a wavefront owns NPW consecutive
+ * slots and issues the second interior window's loads before processing the first. */
+template <int WPB, bool SMP, int NPW>
+__global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
+                                                  long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
+                                                  const uint32_t* __restrict__ lvlKps,
+                                                  const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
+                                                  uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
+                                                  unsigned long long* __restrict__ dstamps) {
+    // per wave: 43x48 window (+16 B pad) and the transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch;
+    // pitch 50 spreads the transposed stores of the 10 column groups over distinct banks)
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[WPB][kDescWin * kDescWinPitch + 16];
+    __shared__ __attribute__((aligned(16))) uint16_t s_rt[WPB][40 * kRtPitch];
+    const int f = blockIdx.y;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
+    const int nl = g->nlevels;
+    const int* cnts = lvlCount + f * nl;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int tot = 0;
+        for (int i = 0; i < nl; i++) tot += cnts[i];
+        outN[f] = tot;
+    }
+    const int s0 = (blockIdx.x * WPB + wv) * NPW;
+    if (s0 >= g->nkpcap) return;
+    const DescSlot d0 = desc_slot(g, f, s0, cnts, lvlKps, frames, framePitch, rowStride, pyr);
+    const DescSlot d1 = NPW > 1 ? desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr) : DescSlot{};
+    if (!d0.ok && !(NPW > 1 && d1.ok)) return;   // (the two slots may straddle a level boundary)
+    uint32_t v0[9], v1[9];
+    if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
+    if (NPW > 1 && d1.ok && d1.interior) desc_issue(d1, lane, v1);
+    // BRIEF test pairs of this lane (lane + 64 gq), fetched now so their latency hides under the window's
+    char4 pat[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) pat[gq] = reinterpret_cast<const char4*>(c_pattern)[lane + 64 * gq];
+    if (d0.ok) desc_body<SMP>(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pat, outK, outD, kpCap, dstamps);
+    if (NPW > 1 && d1.ok) {
+        __builtin_amdgcn_sched_barrier(0);
+        wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
+        desc_body<SMP>(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pat, outK, outD, kpCap, dstamps);
+    }
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 static inline unsigned cdiv(unsigned a, unsigned b) { return (a + b - 1) / b; }
 
@@ -1798,9 +1841,11 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     {   // b.desc_wpb keypoint wavefronts per workgroup
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
         const int wpb = b.desc_wpb;
-        auto kern = b.desc_sampled ? (wpb == 1 ? k_describe<1, true> : wpb == 2 ? k_describe<2, true> : k_describe<4, true>)
-                                   : (wpb == 1 ? k_describe<1, false> : wpb == 2 ? k_describe<2, false> : k_describe<4, false>);
-        hipLaunchKernelGGL(kern, dim3(cdiv(g.nkpcap, wpb), nframes), dim3(64 * wpb), 0, stream, b.d_geom, d_frames,
+        auto kern = b.desc_npw >= 2 ? (b.desc_sampled ? k_describe<4, true, 2> : k_describe<4, false, 2>)
+                    : b.desc_sampled ? (wpb == 1 ? k_describe<1, true, 1> : wpb == 2 ? k_describe<2, true, 1> : k_describe<4, true, 1>)
+                                     : (wpb == 1 ? k_describe<1, false, 1> : wpb == 2 ? k_describe<2, false, 1> : k_describe<4, false, 1>);
+        const int per = (b.desc_npw >= 2 ? 4 : wpb) * (b.desc_npw >= 2 ? 2 : 1);
+        hipLaunchKernelGGL(kern, dim3(cdiv(g.nkpcap, per), nframes), dim3(64 * (b.desc_npw >= 2 ? 4 : wpb)), 0, stream, b.d_geom, d_frames,
                            frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
                            dst);
     }

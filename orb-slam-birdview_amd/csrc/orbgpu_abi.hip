@@ -270,6 +270,7 @@ ExtractBuffers Ctx::buffers() const {
     b.fast_block = fast_block ? 1 : 0;
     b.fast_wpb = fast_wpb;
     b.desc_wpb = desc_wpb;
+    b.desc_npw = desc_npw;
     b.desc_sampled = desc_sampled ? 1 : 0;
     b.fast_px = fast_px;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
@@ -302,7 +303,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
             (uintptr_t)d_lvlCount, (uintptr_t)d_err, (uintptr_t)resize_th, (uintptr_t)resize_direct,
-            (uintptr_t)fast_block, (uintptr_t)fast_wpb, (uintptr_t)desc_wpb, (uintptr_t)desc_sampled, (uintptr_t)fast_px, (uintptr_t)fast_remap, (uintptr_t)stream};
+            (uintptr_t)fast_block, (uintptr_t)fast_wpb, (uintptr_t)desc_wpb, (uintptr_t)desc_npw, (uintptr_t)desc_sampled, (uintptr_t)fast_px, (uintptr_t)fast_remap, (uintptr_t)stream};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -430,6 +431,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         const int v = std::atoi(e);
         c->fast_wpb = v <= 1 ? 1 : v <= 2 ? 2 : 4;
     }
+    if (const char* e = std::getenv("ORBGPU_DESC_NPW")) c->desc_npw = std::atoi(e) >= 2 ? 2 : 1;
     if (const char* e = std::getenv("ORBGPU_DESC_SAMPLED")) c->desc_sampled = e[0] == '1';
     if (const char* e = std::getenv("ORBGPU_FAST_PX")) c->fast_px = std::atoi(e) == 8 ? 8 : 4;
     if (const char* e = std::getenv("ORBGPU_DESC_WPB")) {

@@ -24,6 +24,7 @@ struct Ctx {
     int resize_th = 32;           // rows per resize tile (ORBGPU_RESIZE_TH = 16 | 32 | 64; 32 measured fastest)
     bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
     bool desc_sampled = true;     // blur column pass only at the 512 BRIEF samples (ORBGPU_DESC_SAMPLED=0: whole 37x37 patch)
+    int desc_npw = 2;             // keypoints per describe wave, second window prefetched (ORBGPU_DESC_NPW=1|2; 2: -2 %)
     int desc_wpb = 4;             // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
     int fast_px = 8;              // k_fast_wave prefilter pixels per lane (ORBGPU_FAST_PX = 4 | 8; 8: -2 % fast)
     int fast_wpb = 1;             // k_fast_wave wavefronts per workgroup (ORBGPU_FAST_WPB = 1 | 2 | 4; 1 measured fastest)
