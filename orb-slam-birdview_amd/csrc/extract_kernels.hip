@@ -1467,9 +1467,47 @@ __device__ __forceinline__ void desc_issue(const DescSlot& d, int lane, uint32_t
     }
 }
 
+// 256 rBRIEF tests of one keypoint, the blurred samples computed at the sample pixels only (the column
+// pass of the 7x7 blur over RT[bx][by .. by+6], rounded as the pinned OpenCV 3.2 8U path: half-to-even
+// where the SSE2 body runs (x < W & ~3), half-up in the scalar tail).  ALLEVEN: every sampled column
+// lies in the SSE2 body (x + 18 < W & ~3), so the per-sample column test drops out.
+template <bool ALLEVEN>
+__device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float b, const float (&pf)[4][4], int colBase,
+                                              int xsimd, ushort2_t K01, ushort2_t K23, ushort2_t K45, ushort2_t K60,
+                                              int lane, unsigned long long* __restrict__ dst) {
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(rt);
+    // S + rounding bias of the blurred pixel at offset (cvRound(fx), cvRound(fy)) from the centre;
+    // the blurred value is the high half
+    auto sample = [&](float fx, float fy) -> uint32_t {
+        // cvRound (half-to-even) as one add: v + 1.5*2^23 rounds to an integer for |v| < 2^22, and the
+        // +18 centre offset is folded into the constant (it is even, so ties still go to even)
+        const uint32_t xb = __builtin_bit_cast(uint32_t, fx + 12582930.0f) & 0xFFFFu;
+        const uint32_t yb = __builtin_bit_cast(uint32_t, fy + 12582930.0f);
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + __umul24(xb, 2u * kRtPitch) + ((yb & 0xFFFEu) << 1));
+        const uint32_t sh = yb << 4;   // v_alignbit reads bits 4:0: 16 for an odd row, realigning the u16 pairs
+        const uint32_t d0 = rp[0], d1 = rp[1], d2 = rp[2], d3 = rp[3], d4 = rp[4];
+        uint32_t S = __builtin_amdgcn_udot2(K01, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d1, d0, sh)), 0u, false);
+        S = __builtin_amdgcn_udot2(K23, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d2, d1, sh)), S, false);
+        S = __builtin_amdgcn_udot2(K45, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d3, d2, sh)), S, false);
+        S = __builtin_amdgcn_udot2(K60, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d4, d3, sh)), S, false);
+        // round(S / 65536): half-to-even = (S + 32767 + q&1) >> 16, half-up = (S + 32768) >> 16
+        if (ALLEVEN) return S + 32767u + ((S >> 16) & 1u);
+        return S + (colBase + (int)xb < xsimd ? 32767u + ((S >> 16) & 1u) : 32768u);
+    };
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {   // test pair lane + 64 gq: (x0, y0, x1, y1) = pf[gq]
+        const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
+        const uint32_t r0 = sample(px0 * a - py0 * b, px0 * b + py0 * a);
+        const uint32_t r1 = sample(px1 * a - py1 * b, px1 * b + py1 * a);
+        // saturate_cast<uchar>: only the right-hand side needs the clamp (t0 = 256 compares as 255 would)
+        const unsigned long long m = __ballot((r0 >> 16) < min(r1 >> 16, 255u));
+        if (lane == 0) dst[gq] = m;
+    }
+}
+
 template <bool SMP>
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
-                                          const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const char4 (&pat)[4],
+                                          const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const float (&pf)[4][4],
                                           orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
                                           unsigned long long* __restrict__ dstamps) {
     const int l = d.l, x = d.x, y = d.y, score = d.score, outIdx = d.outIdx;
@@ -1639,39 +1677,22 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     sincos((double)ang, &sd, &cd);
     const float a = (float)cd, b = (float)sd;
     DESC_STAMP(5);
-    const uint8_t* ctr = wbase + 18 * kDescBlurPitch + 18;
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(outD + ((long long)f * kpCap + outIdx) * 32);
+    if constexpr (SMP) {
+        if (x + 18 < xsimd) brief_sampled<true>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
+        else brief_sampled<false>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
+    } else {
+        const uint8_t* ctr = wbase + 18 * kDescBlurPitch + 18;
 #pragma unroll
-    for (int gq = 0; gq < 4; gq++) {
-        const char4 pp = pat[gq];   // (x0, y0, x1, y1) of test pair lane + 64 gq
-        const float px0 = (float)pp.x, py0 = (float)pp.y;
-        const float px1 = (float)pp.z, py1 = (float)pp.w;
-        const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
-        const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
-        int t0, t1;
-        if constexpr (SMP) {
-            // the column pass only at the two sampled pixels: blurred (bx, by) from RT[bx][by .. by+6]
-            auto blur_at = [&](int bx, int by) -> int {
-                const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + __umul24((unsigned)bx, (unsigned)kRtPitch) +
-                                                                       (by & ~1));
-                const bool odd = by & 1;
-                const uint32_t S = __builtin_amdgcn_udot2(odd ? K56 : K60, __builtin_bit_cast(ushort2_t, rp[3]),
-                                   __builtin_amdgcn_udot2(odd ? K34 : K45, __builtin_bit_cast(ushort2_t, rp[2]),
-                                   __builtin_amdgcn_udot2(odd ? K12 : K23, __builtin_bit_cast(ushort2_t, rp[1]),
-                                   __builtin_amdgcn_udot2(odd ? K0s : K01, __builtin_bit_cast(ushort2_t, rp[0]), 0u,
-                                                          false), false), false), false);
-                const bool even = x - 18 + bx < xsimd;
-                const uint32_t bias = even ? 32767u + ((S >> 16) & 1u) : 32768u;
-                return (int)min((S + bias) >> 16, 255u);
-            };
-            t0 = blur_at(18 + __float2int_rn(u2 - u3), 18 + __float2int_rn(u0 + u1));
-            t1 = blur_at(18 + __float2int_rn(w2 - w3), 18 + __float2int_rn(w0 + w1));
-        } else {
-            t0 = ctr[__mul24(__float2int_rn(u2 - u3), kDescBlurPitch) + __float2int_rn(u0 + u1)];
-            t1 = ctr[__mul24(__float2int_rn(w2 - w3), kDescBlurPitch) + __float2int_rn(w0 + w1)];
+        for (int gq = 0; gq < 4; gq++) {
+            const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
+            const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
+            const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
+            const int t0 = ctr[__mul24(__float2int_rn(u2 - u3), kDescBlurPitch) + __float2int_rn(u0 + u1)];
+            const int t1 = ctr[__mul24(__float2int_rn(w2 - w3), kDescBlurPitch) + __float2int_rn(w0 + w1)];
+            const unsigned long long m = __ballot(t0 < t1);
+            if (lane == 0) dst[gq] = m;
         }
-        const unsigned long long m = __ballot(t0 < t1);
-        if (lane == 0) dst[gq] = m;
     }
     if (lane == 0) {
         orb_keypoint o;
@@ -1700,21 +1721,28 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
-                                                  unsigned long long* __restrict__ dstamps) {
+                                                  int remap, unsigned long long* __restrict__ dstamps) {
     // per wave: 43x48 window (+16 B pad) and the transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch;
     // pitch 50 spreads the transposed stores of the 10 column groups over distinct banks)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[WPB][kDescWin * kDescWinPitch + 16];
     __shared__ __attribute__((aligned(16))) uint16_t s_rt[WPB][40 * kRtPitch];
-    const int f = blockIdx.y;
+    int f = blockIdx.y, bx = blockIdx.x;
+    if (remap) {   // workgroups are dealt round-robin over the 8 XCDs: give each XCD a contiguous range of frames
+        const int gx = gridDim.x, nb = gx * gridDim.y, q = nb >> 3, r = nb & 7;
+        const int hw = blockIdx.y * gx + blockIdx.x, xcd = hw & 7, j = hw >> 3;
+        const int lg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+        f = lg / gx;
+        bx = lg - f * gx;
+    }
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int nl = g->nlevels;
     const int* cnts = lvlCount + f * nl;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bx == 0 && threadIdx.x == 0) {
         int tot = 0;
         for (int i = 0; i < nl; i++) tot += cnts[i];
         outN[f] = tot;
     }
-    const int s0 = (blockIdx.x * WPB + wv) * NPW;
+    const int s0 = (bx * WPB + wv) * NPW;
     if (s0 >= g->nkpcap) return;
     const DescSlot d0 = desc_slot(g, f, s0, cnts, lvlKps, frames, framePitch, rowStride, pyr);
     const DescSlot d1 = NPW > 1 ? desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr) : DescSlot{};
@@ -1723,14 +1751,20 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
     if (NPW > 1 && d1.ok && d1.interior) desc_issue(d1, lane, v1);
     // BRIEF test pairs of this lane (lane + 64 gq), fetched now so their latency hides under the window's
-    char4 pat[4];
+    float pf[4][4];
 #pragma unroll
-    for (int gq = 0; gq < 4; gq++) pat[gq] = reinterpret_cast<const char4*>(c_pattern)[lane + 64 * gq];
-    if (d0.ok) desc_body<SMP>(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pat, outK, outD, kpCap, dstamps);
+    for (int gq = 0; gq < 4; gq++) {
+        const char4 pp = reinterpret_cast<const char4*>(c_pattern)[lane + 64 * gq];
+        pf[gq][0] = (float)pp.x;
+        pf[gq][1] = (float)pp.y;
+        pf[gq][2] = (float)pp.z;
+        pf[gq][3] = (float)pp.w;
+    }
+    if (d0.ok) desc_body<SMP>(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
     if (NPW > 1 && d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
-        desc_body<SMP>(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pat, outK, outD, kpCap, dstamps);
+        desc_body<SMP>(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
     }
 }
 
@@ -1847,7 +1881,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         const int per = (b.desc_npw >= 2 ? 4 : wpb) * (b.desc_npw >= 2 ? 2 : 1);
         hipLaunchKernelGGL(kern, dim3(cdiv(g.nkpcap, per), nframes), dim3(64 * (b.desc_npw >= 2 ? 4 : wpb)), 0, stream, b.d_geom, d_frames,
                            frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
-                           dst);
+                           b.desc_remap, dst);
     }
     if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);
     return hipGetLastError();

@@ -271,6 +271,7 @@ ExtractBuffers Ctx::buffers() const {
     b.fast_wpb = fast_wpb;
     b.desc_wpb = desc_wpb;
     b.desc_npw = desc_npw;
+    b.desc_remap = desc_remap ? 1 : 0;
     b.desc_sampled = desc_sampled ? 1 : 0;
     b.fast_px = fast_px;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
@@ -297,13 +298,14 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     const int ns = std::min(std::min(nsub, kMaxSubStreams), nframes);
     if (ns <= 1 && use_graph && !prof_on && !fast_stamps && resize_split == 0) {
         // HIP graph replay: one submission per batch instead of 11
-        const std::array<uintptr_t, 32> key = {
+        const std::array<uintptr_t, 40> key = {
             (uintptr_t)d_frames, (uintptr_t)nframes, (uintptr_t)frame_pitch, (uintptr_t)row_stride, (uintptr_t)d_kps,
             (uintptr_t)d_desc, (uintptr_t)d_counts, (uintptr_t)kp_cap, (uintptr_t)geom.W, (uintptr_t)geom.H,
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
             (uintptr_t)d_lvlCount, (uintptr_t)d_err, (uintptr_t)resize_th, (uintptr_t)resize_direct,
-            (uintptr_t)fast_block, (uintptr_t)fast_wpb, (uintptr_t)desc_wpb, (uintptr_t)desc_npw, (uintptr_t)desc_sampled, (uintptr_t)fast_px, (uintptr_t)fast_remap, (uintptr_t)stream};
+            (uintptr_t)fast_block, (uintptr_t)fast_wpb, (uintptr_t)desc_wpb, (uintptr_t)desc_npw, (uintptr_t)desc_sampled, (uintptr_t)fast_px, (uintptr_t)fast_remap, (uintptr_t)desc_remap,
+            (uintptr_t)stream};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -431,6 +433,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         const int v = std::atoi(e);
         c->fast_wpb = v <= 1 ? 1 : v <= 2 ? 2 : 4;
     }
+    if (const char* e = std::getenv("ORBGPU_DESC_REMAP")) c->desc_remap = e[0] == '1';
     if (const char* e = std::getenv("ORBGPU_DESC_NPW")) c->desc_npw = std::atoi(e) >= 2 ? 2 : 1;
     if (const char* e = std::getenv("ORBGPU_DESC_SAMPLED")) c->desc_sampled = e[0] == '1';
     if (const char* e = std::getenv("ORBGPU_FAST_PX")) c->fast_px = std::atoi(e) == 8 ? 8 : 4;

@@ -25,6 +25,7 @@ struct Ctx {
     bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
     bool desc_sampled = true;     // blur column pass only at the 512 BRIEF samples (ORBGPU_DESC_SAMPLED=0: whole 37x37 patch)
     int desc_npw = 2;             // keypoints per describe wave, second window prefetched (ORBGPU_DESC_NPW=1|2; 2: -2 %)
+    bool desc_remap = false;      // ORBGPU_DESC_REMAP=1: each XCD describes a contiguous range of frames (its L2 holds their pyramids)
     int desc_wpb = 4;             // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
     int fast_px = 8;              // k_fast_wave prefilter pixels per lane (ORBGPU_FAST_PX = 4 | 8; 8: -2 % fast)
     int fast_wpb = 1;             // k_fast_wave wavefronts per workgroup (ORBGPU_FAST_WPB = 1 | 2 | 4; 1 measured fastest)
@@ -113,7 +114,7 @@ struct Ctx {
     unsigned geom_serial = 0;
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    std::array<uintptr_t, 32> gkey{};
+    std::array<uintptr_t, 40> gkey{};
     hipEvent_t prof_open[ORB_K_COUNT]{};
     std::vector<ProfPair> prof_pairs;
 

@@ -106,6 +106,7 @@ struct ExtractBuffers {
     int fast_wpb;                  // k_fast_wave wavefronts per workgroup (ORBGPU_FAST_WPB = 1 | 2 | 4)
     int desc_wpb;
     int desc_npw;                  // keypoint slots per k_describe wavefront (ORBGPU_DESC_NPW = 1 | 2)
+    int desc_remap;                // k_describe workgroups dealt to XCDs as contiguous frame ranges (ORBGPU_DESC_REMAP)
     int desc_sampled;              // k_describe: column pass only at the BRIEF samples (ORBGPU_DESC_SAMPLED)
     int fast_px;                   // k_fast_wave prefilter pixels per lane (ORBGPU_FAST_PX = 4 | 8)                  // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
     unsigned long long* d_stamps;  // k_fast_wave phase timestamps, 8 per (frame, cell) (ORBGPU_FAST_STAMPS=1)

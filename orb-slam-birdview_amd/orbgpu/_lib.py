@@ -9,7 +9,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "liborbgpu.so")
+# ORBGPU_LIB_PATH: an alternative in-tree build of the same library (A/B of kernel variants)
+LIB_PATH = os.environ.get("ORBGPU_LIB_PATH") or os.path.join(PKG_ROOT, "liborbgpu.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "orbgpu.h")
 
 _LIB = None
