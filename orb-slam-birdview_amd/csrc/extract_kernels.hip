@@ -1505,6 +1505,28 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
     }
 }
 
+// k_describe row pass, 8 rounds of one lane: RT[4gq + o][wy] = sum_t k_t * window[wy][SH + 4gq + o + t]
+// (the window row starts SH bytes into its first dword)
+template <int SH>
+__device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, uint32_t K0123, uint32_t K456) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = rw[72 * r + i];
+        // bytes b .. b+3 of w[0..3]
+        auto run = [&](int b) -> uint32_t {
+            return (b & 3) == 0 ? w[b >> 2] : __builtin_amdgcn_alignbyte(w[(b >> 2) + 1], w[b >> 2], b & 3);
+        };
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const uint32_t v = __builtin_amdgcn_udot4(run(SH + o + 4), K456, __builtin_amdgcn_udot4(run(SH + o), K0123, 0u, false),
+                                                      false);
+            rq[o * kRtPitch + 6 * r] = (uint16_t)v;
+        }
+    }
+}
+
 template <bool SMP>
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
                                           const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const float (&pf)[4][4],
@@ -1589,28 +1611,20 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     const uint32_t K0123 = (uint32_t)g->gk[0] | ((uint32_t)g->gk[1] << 8) | ((uint32_t)g->gk[2] << 16) |
                            ((uint32_t)g->gk[3] << 24);
     const uint32_t K456 = (uint32_t)g->gk[4] | ((uint32_t)g->gk[5] << 8) | ((uint32_t)g->gk[6] << 16);
-#pragma unroll
-    for (int r = 0; r < 7; r++) {   // 43 rows x 10 groups = 430 <= 7 x 64
-        const int it = lane + 64 * r;
-        if (it < kDescWin * 10) {
-            const int wy = it / 10, gq = it - wy * 10;
-            const int d0 = wy * 12 + gq;
-            const uint32_t w0 = w32[d0], w1 = w32[d0 + 1], w2 = w32[d0 + 2], w3 = w32[d0 + 3];
-            const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh), a1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
-                           a2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-            uint32_t rv[4];
-            rv[0] = __builtin_amdgcn_udot4(a1, K456, __builtin_amdgcn_udot4(a0, K0123, 0u, false), false);
-#pragma unroll
-            for (int o = 1; o < 4; o++)
-                rv[o] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a2, a1, o), K456,
-                                               __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a1, a0, o), K0123, 0u,
-                                                                      false),
-                                               false);
-            uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy;   // RT[4gq + j][wy]
-            rq[0 * kRtPitch] = (uint16_t)rv[0];
-            rq[1 * kRtPitch] = (uint16_t)rv[1];
-            rq[2 * kRtPitch] = (uint16_t)rv[2];
-            rq[3 * kRtPitch] = (uint16_t)rv[3];
+    // lane = (row wy0 = lane / 10, group gq = lane % 10), round r takes row wy0 + 6r: the read and store
+    // addresses are the lane's base plus immediate offsets.  8 rounds cover rows 0..47; rows 43..47 are
+    // scratch (they read past the window, inside the workgroup's LDS, into RT rows no sample reads
+    // with a nonzero tap).  The window shift sh is wave-uniform: one instantiation per value, so output
+    // o's byte runs start at the compile-time offset sh + o (aligned runs need no v_alignbyte).
+    if (lane < 60) {
+        const int wy0 = (int)(__umul24((unsigned)lane, 205u) >> 11), gq = lane - wy0 * 10;   // lane / 10, lane < 60
+        const uint32_t* rw = w32 + wy0 * 12 + gq;
+        uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy0;   // RT[4gq + j][wy]
+        switch (sh) {
+            case 0: desc_row_pass<0>(rw, rq, K0123, K456); break;
+            case 1: desc_row_pass<1>(rw, rq, K0123, K456); break;
+            case 2: desc_row_pass<2>(rw, rq, K0123, K456); break;
+            default: desc_row_pass<3>(rw, rq, K0123, K456); break;
         }
     }
     wave_lds_sync();
