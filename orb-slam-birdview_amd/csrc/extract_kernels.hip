@@ -1455,16 +1455,28 @@ __device__ __forceinline__ DescSlot desc_slot(const Geom* __restrict__ g, int f,
     return d;
 }
 
-// 43 rows x 12 dwords of an interior window, issued into registers
+// 43 rows x 12 dwords of an interior window, issued into registers: lane = (row wy0 = lane / 12,
+// dword ww = lane % 12), round r loads row wy0 + 5r (9 rounds).  Lanes 60..63 duplicate lanes 0..3 of
+// the next round (same dword, same value); rows 43..47 of the last round are not read.  The per-lane
+// offset is computed once; each round adds a wave-uniform soffset.
 __device__ __forceinline__ void desc_issue(const DescSlot& d, int lane, uint32_t (&v)[9]) {
     const int a0 = (d.x - 21) & ~3;
-    const uint8_t* row0 = d.src.p + (long long)(d.y - 21) * d.src.stride + a0;
+    // the slot is wave-uniform: a buffer descriptor over the window rows (SGPRs), the lane's dword as
+    // voffset and the round's row step as soffset, so no per-round address arithmetic
+    const int stride = __builtin_amdgcn_readfirstlane(d.src.stride);
+    const uint64_t rb = reinterpret_cast<uint64_t>(d.src.p + (long long)(d.y - 21) * stride + a0);
+    // (readfirstlane returns int: zero-extend both halves)
+    const uint64_t rbu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(rb >> 32)) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)rb);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(rbu), 0, (kDescWin - 1) * stride + 48,
+                                                          0x00020000);
+    const int wy0 = (int)(__umul24((unsigned)lane, 2731u) >> 15), ww = lane - wy0 * 12;   // lane / 12
+    const int off = (int)roi_off(wy0, stride, 4 * ww);
 #pragma unroll
-    for (int r = 0; r < 9; r++) {   // 43 rows x 12 dwords = 516 <= 9 x 64, all loads in flight
-        const int idx = lane + 64 * r;
-        const int wy = (int)(__umul24((unsigned)idx, 2731u) >> 15), ww = idx - wy * 12;   // idx / 12, idx < 576
-        v[r] = idx < kDescWin * 12 ? *reinterpret_cast<const uint32_t*>(row0 + roi_off(wy, d.src.stride, 4 * ww)) : 0u;
-    }
+    for (int r = 0; r < 8; r++) v[r] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 5 * r * stride, 0);
+    // last round: rows 40..42 only (lane < 36); the others take a voffset past the range (reads 0 whether
+    // or not the range check counts soffset)
+    v[8] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane < 36 ? off : 0x40000000, 40 * stride, 0);
 }
 
 // 256 rBRIEF tests of one keypoint, the blurred samples computed at the sample pixels only (the column
@@ -1543,10 +1555,8 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     int sh;
     if (d.interior) {
 #pragma unroll
-        for (int r = 0; r < 9; r++) {
-            const int idx = lane + 64 * r;
-            if (idx < kDescWin * 12) w32[idx] = v[r];
-        }
+        for (int r = 0; r < 9; r++)   // window dword (wy0 + 5r) * 12 + ww = lane + 60 r; rows < 43 only
+            if (r < 8 || lane < 36) w32[lane + 60 * r] = v[r];
         sh = (x - 21) & 3;
     } else {
                // flight in two batches of 15 (fewer live registers than one batch of 29)
