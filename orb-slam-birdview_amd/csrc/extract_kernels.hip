@@ -597,37 +597,58 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
 #define ORBGPU_STAMP(k) \
     if (stamps && lane == 0) stamps[(long long)item * 8 + (k)] = __builtin_amdgcn_s_memtime();
 
-// ROI dwords 0..511 of a cell (aligned levels) issued into registers: the loads of the next cell
-// of a wavefront are in flight while the current one is processed.
-__device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uint32_t (&v)[8]) {
-    const int n = c.rh * c.nw;
-    const uint32_t mnw = recip20(c.nw);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const int idx = k * 64 + lane;
-        const int yy = (int)div20(idx, mnw), ww = idx - (int)__umul24((unsigned)yy, (unsigned)c.nw);
-        v[k] = idx < n ? *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + ww) * 4)) : 0u;
-    }
+// ROI dwords of a cell (aligned levels) issued into registers, so that the next cell's loads are in
+// flight while the current one is processed.  lane = (row yy0 = lane / nw, dword ww = lane % nw);
+// round k takes row yy0 + k * rpr (rpr = 64 / nw rows per round): the lane's offset is computed once
+// and each round adds a wave-uniform row step, the soffset of a buffer load whose descriptor (SGPRs)
+// starts at the ROI's first dword.  Rows past the ROI and lanes past rpr rows take an out-of-range
+// voffset (read 0).  Rows from 8 * rpr on (tall cells) are loaded by fast_roi_store.
+struct RoiLanes {
+    int yy0, ww, rpr, off;
+    __amdgpu_buffer_rsrc_t rsrc;
+};
+
+__device__ __forceinline__ RoiLanes roi_lanes(const FastCellT& c, int lane) {
+    RoiLanes r;
+    const int nw = __builtin_amdgcn_readfirstlane(c.nw), stride = __builtin_amdgcn_readfirstlane(c.stride);
+    const uint32_t m = recip20(nw);
+    r.rpr = (int)div20(64, m);
+    r.yy0 = (int)div20(lane, m);
+    r.ww = lane - r.yy0 * nw;
+    r.off = (int)roi_off(r.yy0, stride, 4 * r.ww);
+    // the cell is wave-uniform (readfirstlane returns int: zero-extend both halves)
+    const uint64_t pb = reinterpret_cast<uint64_t>(c.base + 4 * c.x0w);
+    const uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(pb >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)pb);
+    r.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pu), 0, (c.rh - 1) * stride + 4 * nw, 0x00020000);
+    return r;
 }
 
-// ROI -> LDS tile (rows TP apart): the prefetched dwords, the remainder of a tall ROI, or bytes
+__device__ __forceinline__ bool roi_row_ok(const FastCellT& c, const RoiLanes& r, int k) {
+    return r.yy0 < r.rpr && r.yy0 + k * r.rpr < c.rh;
+}
+
+__device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uint32_t (&v)[8]) {
+    const RoiLanes r = roi_lanes(c, lane);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        v[k] = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, roi_row_ok(c, r, k) ? r.off : 0x40000000, k * r.rpr * c.stride, 0);
+}
+
+// ROI -> LDS tile (rows TP apart): the prefetched dwords, the rows of a tall ROI past them, or bytes
 // for a level whose base / stride is not dword aligned.  Returns the tile column of ROI x = 0.
 template <int TP>
 __device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, const uint32_t (&v)[8], uint8_t* tile) {
     if (c.aligned) {
-        const int n = c.rh * c.nw;
-        const uint32_t mnw = recip20(c.nw);
+        const RoiLanes r = roi_lanes(c, lane);
+        uint32_t* t = reinterpret_cast<uint32_t*>(&tile[r.yy0 * TP + 4 * r.ww]);
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int idx = k * 64 + lane;
-            const int yy = (int)div20(idx, mnw), ww = idx - (int)__umul24((unsigned)yy, (unsigned)c.nw);
-            if (idx < n) *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) = v[k];
-        }
-        for (int idx = 512 + lane; idx < n; idx += 64) {
-            const int yy = (int)div20(idx, mnw), ww = idx - (int)__umul24((unsigned)yy, (unsigned)c.nw);
-            *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) =
-                *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + ww) * 4));
-        }
+        for (int k = 0; k < 8; k++)
+            if (roi_row_ok(c, r, k)) t[k * r.rpr * (TP / 4)] = v[k];
+        if (r.yy0 < r.rpr)
+            for (int yy = r.yy0 + 8 * r.rpr; yy < c.rh; yy += r.rpr)
+                *reinterpret_cast<uint32_t*>(&tile[yy * TP + 4 * r.ww]) =
+                    *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + r.ww) * 4));
         return c.iniX & 3;
     }
     const uint32_t mrw = recip20(c.rw);
