@@ -39,6 +39,8 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 
 }  // namespace
 
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
 /* ------------------------------------------------------------------------------------------------
  * Pyramid: cv::resize(level l-1 -> level l, INTER_LINEAR) for every frame of the batch
  * (ComputePyramid, ORBextractor.cc:1118-1120).  OpenCV-3.x 8U fixed point: 11-bit horizontal
@@ -171,6 +173,44 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
     uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off + x0 + tx;
     const int pitch = g->L[level].pitch;
     if (tx >= nx) return;
+    // The 4 pixels' source bytes lie within 8 bytes from o0[0] (scale factor <= ~1.6; otherwise the
+    // byte path below): a row's 3 dwords from LDS, realigned to o0[0], give each pixel's byte pair as
+    // 16-bit lanes through one v_perm, and the horizontal sum is one v_dot2 with (c0, c1).
+    const int bo = o0[0];
+    const bool packed_ok = o1[3] - bo <= 7;
+    if (__builtin_amdgcn_ballot_w64(!packed_ok) == 0) {
+        unsigned sel[4];
+        uint32_t cc[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            sel[i] = (unsigned)(o0[i] - bo) | 0x0C00u | ((unsigned)(o1[i] - bo) << 16) | 0x0C000000u;
+            cc[i] = c0[i] | (c1[i] << 16);
+        }
+        const int bw = bo >> 2, bsh = bo & 3;
+#pragma unroll
+        for (int pass = 0; pass < kRsTileH / 8; pass++) {
+            const int ty = pass * 8 + (tid >> 5);
+            if (ty >= ny) break;
+            const int4 cy = s_cy[ty];
+            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(&s_src[(cy.x - sy0) * kRsPitch]) + bw;
+            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(&s_src[(cy.y - sy0) * kRsPitch]) + bw;
+            const uint32_t u0 = q0[0], u1 = q0[1], u2 = q0[2], w0 = q1[0], w1 = q1[1], w2 = q1[2];
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(u1, u0, bsh), a1 = __builtin_amdgcn_alignbyte(u2, u1, bsh);
+            const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, bsh), b1 = __builtin_amdgcn_alignbyte(w2, w1, bsh);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const unsigned h0 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cc[i]),
+                                                           __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(a1, a0, sel[i])), 0u, false);
+                const unsigned h1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cc[i]),
+                                                           __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(b1, b0, sel[i])), 0u, false);
+                const unsigned v = ((__umul24((unsigned)cy.z, h0 >> 4) >> 16) + (__umul24((unsigned)cy.w, h1 >> 4) >> 16) + 2) >> 2;
+                packed |= v << (8 * i);
+            }
+            *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + ty) * pitch) = packed;
+        }
+        return;
+    }
 #pragma unroll
     for (int pass = 0; pass < kRsTileH / 8; pass++) {
         const int ty = pass * 8 + (tid >> 5);
@@ -1431,7 +1471,6 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {   // cv::fastAta
     return a;
 }
 
-typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
 // IC_Angle row sums: bytes of the aligned 32-byte row slice that lie in [lo, hi] (inclusive)
 __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
