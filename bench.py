@@ -111,7 +111,9 @@ def read_pmc(kernel, batch):
     """(HBM bytes per launch, VALU instructions per launch, source commit) of `kernel` from the
     committed rocprofv3 PMC summary (tools/pmc.sh -> profiles/pmc_traffic.json), scaled from the
     summary's frames per launch to `batch` (both are per-frame linear), or Nones."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    # ORBGPU_PMC_JSON: a summary measured in the same GPU session (tools/gpu_round.sh runs the PMC passes
+    # before the bench and points here at their report)
+    path = os.environ.get("ORBGPU_PMC_JSON") or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -120,7 +122,7 @@ def read_pmc(kernel, batch):
     k = batch / float(d.get("batch_frames_per_launch", batch) or batch)
     sq = d.get("sq_per_launch", {}).get(kernel, {})
     tb, vi = d.get("per_launch_bytes", {}).get(kernel), sq.get("SQ_INSTS_VALU")
-    return (tb * k if tb is not None else None), (vi * k if vi is not None else None), d.get("commit")
+    return (tb * k if tb is not None else None), (vi * k if vi is not None else None), d.get("commit", "this session")
 
 
 # ---------------------------------------------------------------- CPU baseline (oracle, rank 0, N=1)
