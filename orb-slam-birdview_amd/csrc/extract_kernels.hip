@@ -625,12 +625,19 @@ __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {   // per 
 // Compass prefilter (see fast_maybe) for two pixels held as 16-bit lanes: returns sign bits 15/31
 // set where the pixel may be a corner at threshold t.  Bright: (v+t) - p < 0, dark: p - (v-t) < 0;
 // the four cyclically adjacent compass pairs reduce to (b0|b8) & (b4|b12).
+// As min/max: bright needs min(max(p0, p8), max(p4, p12)) > v + t, dark max(min(p0, p8), min(p4, p12))
+// < v - t (v_pk_max_u16 / v_pk_min_u16: 11 packed ops for the two pixels instead of 16).
+typedef unsigned short ushort2_pk __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p4, uint32_t p8, uint32_t p12,
                                              uint32_t tt) {
+    const ushort2_pk a0 = __builtin_bit_cast(ushort2_pk, p0), a4 = __builtin_bit_cast(ushort2_pk, p4),
+                     a8 = __builtin_bit_cast(ushort2_pk, p8), a12 = __builtin_bit_cast(ushort2_pk, p12);
+    const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                                               __builtin_elementwise_max(a4, a12)));
+    const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                                               __builtin_elementwise_min(a4, a12)));
     const uint32_t vt = pk_add16(v, tt), vmt = pk_sub16(v, tt);   // v + t, v - t (per lane)
-    const uint32_t b0 = pk_sub16(vt, p0), b4 = pk_sub16(vt, p4), b8 = pk_sub16(vt, p8), b12 = pk_sub16(vt, p12);
-    const uint32_t d0 = pk_sub16(p0, vmt), d4 = pk_sub16(p4, vmt), d8 = pk_sub16(p8, vmt), d12 = pk_sub16(p12, vmt);
-    return ((b0 | b8) & (b4 | b12)) | ((d0 | d8) & (d4 | d12));
+    return pk_sub16(vt, hi) | pk_sub16(lo, vmt);
 }
 
 // optional phase timestamps (ORBGPU_FAST_STAMPS=1): s_memtime at the phase boundaries, lane 0
