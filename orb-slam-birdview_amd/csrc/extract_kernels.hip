@@ -765,9 +765,13 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const uint32_t roa = compass2(od(Va), od(P0a), od(P4a), od(P8a), od(P12a), tt);
                 const uint32_t reb = compass2(ev(Vb), ev(P0b), ev(P4b), ev(P8b), ev(P12b), tt);
                 const uint32_t rob = compass2(od(Vb), od(P0b), od(P4b), od(P8b), od(P12b), tt);
-                const uint32_t lo4 = ((rea >> 15) & 1u) | ((roa >> 14) & 2u) | ((rea >> 29) & 4u) | ((roa >> 28) & 8u);
-                const uint32_t hi4 = ((reb >> 15) & 1u) | ((rob >> 14) & 2u) | ((reb >> 29) & 4u) | ((rob >> 28) & 8u);
-                pm = (int)((lo4 | (hi4 << 4)) & xvalid);
+                // sign bits 15 / 31 of the four results -> pixel bits 0..7: gather the high bytes (one
+                // v_perm per pair), put pixel i and i+4 in byte i's bits 0 and 4, and fold the four bytes
+                // into the top byte with one multiply
+                const uint32_t X = __builtin_amdgcn_perm(roa, rea, 0x07030501u);   // rea.b1 roa.b1 rea.b3 roa.b3
+                const uint32_t Y = __builtin_amdgcn_perm(rob, reb, 0x07030501u);
+                const uint32_t Z = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
+                pm = (int)(((Z * 0x01020408u) >> 24) & xvalid);
             }
             if (PX == 4 && lane_on && dy < dh) {
                 const int sc = (dy + 3) * TP + x0 + xoff;       // centre row, from pixel x0-3
@@ -796,9 +800,8 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             const int incl = wave_incl_scan(cnt);
             int pos = nlist + incl - cnt;
             const int base = dy * 64 + x0;
-#pragma unroll
-            for (int i = 0; i < PX; i++)
-                if ((pm >> i) & 1) sList[pos++] = (uint16_t)(base + i);
+            // one iteration per set bit (survivors are sparse: the wave runs max-popcount iterations)
+            for (uint32_t b = (uint32_t)pm; b; b &= b - 1) sList[pos++] = (uint16_t)(base + __builtin_ctz(b));
             nlist += __builtin_amdgcn_readlane(incl, 63);
         }
         wave_lds_sync();
