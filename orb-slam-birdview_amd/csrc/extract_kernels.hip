@@ -714,7 +714,8 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                                                unsigned long long* keepb, uint32_t* __restrict__ cands,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
     const int dw = c.dw, dh = c.dh;
-    for (int i = lane; i < (dh + 2) * (SP / 4); i += 64) reinterpret_cast<uint32_t*>(sM)[i] = 0u;
+    // (16-byte stores; the map's LDS carve is rounded up to 16 bytes)
+    for (int i = lane; i < ((dh + 2) * SP + 15) / 16; i += 64) reinterpret_cast<uint4*>(sM)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (lane < dh) keepb[lane] = 0ull;
     wave_lds_sync();
     ORBGPU_STAMP(1);
