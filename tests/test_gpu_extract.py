@@ -71,7 +71,9 @@ def test_other_parameters(orbgpu_mod, oracle_mod):
     # fisheye.yaml (2000 / 1.2 / 8 / 15 / 5) and KITTI04-12 stereo (iniTh 12)
     from orbgpu.synth import synth_frame
     img = synth_frame(640, 480, 21)
-    for params in [(2000, 1.2, 8, 15, 5), (1000, 1.2, 8, 12, 7), (1500, 1.3, 6, 20, 7)]:
+    # large scale factors: longer 4-pixel source spans in the tiled resize (1.6), the untiled resize (2.3)
+    for params in [(2000, 1.2, 8, 15, 5), (1000, 1.2, 8, 12, 7), (1500, 1.3, 6, 20, 7), (1000, 1.6, 5, 20, 7),
+                   (800, 2.3, 3, 20, 7)]:
         o = oracle_mod.OracleExtractor(params[0], params[1], params[2], params[3], params[4])
         ok, od = o(img)
         gk, gd = orbgpu_mod.ORBextractor(*params)(img)
