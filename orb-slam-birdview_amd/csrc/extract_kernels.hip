@@ -716,7 +716,6 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
     const int dw = c.dw, dh = c.dh;
     // (16-byte stores; the map's LDS carve is rounded up to 16 bytes)
     for (int i = lane; i < ((dh + 2) * SP + 15) / 16; i += 64) reinterpret_cast<uint4*>(sM)[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < dh) keepb[lane] = 0ull;
     wave_lds_sync();
     ORBGPU_STAMP(1);
     // lane -> (run of PX pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
@@ -826,47 +825,41 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         wave_lds_sync();
         ORBGPU_STAMP(3);
         // ---- cell-local NMS at th.  Neighbours outside the domain read the zero border; M <= th
-        // counts 0.
-        int mine = 0;
-        for (int i = lane; i < ncorner; i += 64) {
-            const int p = sList[i];
-            const uint8_t* q = sM + (p >> 6) * SP + (p & 63) + SP + 1;
-            const int m = q[0];
-            const int s = m - 1;
-            bool k = true;
+        // counts 0.  The corner list is in raster order (the prefilter compacts rows in order, pixels
+        // ascending within a lane's run, runs in lane order), so the kept corners are emitted as they
+        // are found: one ballot compaction per chunk of 64, FAST emission order.
+        kept = 0;
+        for (int b0 = 0; b0 < ncorner; b0 += 64) {
+            const int i = b0 + lane;
+            bool k = false;
+            uint32_t packed = 0;
+            if (i < ncorner) {
+                const int p = sList[i];
+                const uint8_t* q = sM + (p >> 6) * SP + (p & 63) + SP + 1;
+                const int m = q[0];
+                const int s = m - 1;
+                k = true;
 #pragma unroll
-            for (int oy = -1; oy <= 1; oy++) {
+                for (int oy = -1; oy <= 1; oy++) {
 #pragma unroll
-                for (int ox = -1; ox <= 1; ox++) {
-                    if (ox == 0 && oy == 0) continue;
-                    const int mn = q[oy * SP + ox];
-                    const int sn = mn > th ? mn - 1 : 0;
-                    k = k && (s > sn);
+                    for (int ox = -1; ox <= 1; ox++) {
+                        if (ox == 0 && oy == 0) continue;
+                        const int mn = q[oy * SP + ox];
+                        const int sn = mn > th ? mn - 1 : 0;
+                        k = k && (s > sn);
+                    }
                 }
+                packed = (uint32_t)((p & 63) + c.xo) | ((uint32_t)((p >> 6) + c.yo) << 12) | ((uint32_t)s << 24);
             }
-            if (k) {
-                atomicOr(&keepb[p >> 6], 1ull << (p & 63));
-                mine++;
-            }
+            const unsigned long long km = __ballot(k);
+            if (k) cands[(long long)c.f * g->ncand + c.out_off + kept + lanes_below(km)] = packed;
+            kept += __popcll(km);
         }
-        kept = wave_sum(mine);
         if (kept > 0 || th == g->minTh) break;
-        th = g->minTh;   // nothing kept: keepb is still all zero
+        th = g->minTh;   // nothing kept: nothing was emitted
         wave_lds_sync();
     }
-    wave_lds_sync();
     ORBGPU_STAMP(4);
-    // ---- emission in raster order: lane = domain row
-    uint32_t* out = cands + (long long)c.f * g->ncand + c.out_off;
-    unsigned long long bits = lane < dh ? keepb[lane] : 0ull;
-    int pos = wave_excl_scan(__popcll(bits));
-    const uint32_t yr = (uint32_t)(lane + c.yo);
-    while (bits) {
-        const int dx = __ffsll((long long)bits) - 1;
-        bits &= bits - 1;
-        const uint32_t xr = (uint32_t)(dx + c.xo);
-        out[pos++] = xr | (yr << 12) | ((uint32_t)(sM[(lane + 1) * SP + dx + 1] - 1) << 24);
-    }
     if (lane == 0) *cntOut = kept;
     ORBGPU_STAMP(5);
 }
