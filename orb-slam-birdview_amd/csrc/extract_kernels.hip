@@ -580,11 +580,7 @@ __global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const 
     }
 }
 
-/* Wave-per-cell form of the same algorithm: four (frame, cell) items per 256-thread block, one per
- * wavefront, so every synchronisation is a wave barrier (no block barriers).  The per-wave LDS carve
- * is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors are compacted with
- * per-bit ballots (list order is irrelevant: emission order comes from the keep bitmap, one 64-bit
- * row mask per domain row, emitted in raster order by one lane per row). */
+// wave-level scans (DPP) for the wave-per-cell FAST kernel below
 __device__ __forceinline__ int wave_excl_scan(int v) {
     const int lane = threadIdx.x & 63;
     int x = v;
@@ -868,8 +864,8 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
  * (four waves, eight cells per block), so every synchronisation is a wave barrier; the second
  * cell's ROI loads are issued before the first cell is processed, hiding their latency.  The
  * per-wave LDS carve is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors
- * are compacted with per-bit ballots (list order is irrelevant: emission order comes from the keep
- * bitmap, one 64-bit row mask per domain row, emitted in raster order by one lane per row). */
+ * are compacted by one wave scan into a raster-ordered list, so corners keep that order and the NMS
+ * pass emits the kept ones directly (FAST emission order) by ballot compaction. */
 template <int TP, int SP, int PX>
 __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                    const uint8_t* __restrict__ frames,
