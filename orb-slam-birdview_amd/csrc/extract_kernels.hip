@@ -707,7 +707,7 @@ __device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, cons
 template <int TP, int SP, int PX>
 __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane, int xoff,
                                                uint8_t* tile, uint8_t* sM, uint16_t* sList,
-                                               unsigned long long* keepb, uint32_t* __restrict__ cands,
+                                               uint32_t* __restrict__ cands,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
     const int dw = c.dw, dh = c.dh;
     // (16-byte stores; the map's LDS carve is rounded up to 16 bytes)
@@ -890,8 +890,6 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*SP + dx+1]
     uint8_t* sM = tile + ((g->fast_rows * TP + 16 + 15) & ~15);
     uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * SP + 15) & ~15));
-    unsigned long long* keepb =
-        reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(sList) + ((g->fast_list * 2 + 15) & ~15));
     const bool has1 = item0 + 1 < total;
     const FastCellT c0 = fast_cell_t(g, cells, item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
     const FastCellT c1 = fast_cell_t(g, cells, has1 ? item0 + 1 : item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
@@ -912,7 +910,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         wave_lds_sync();   // the previous cell's last LDS reads happen before this one's writes
         const int xoff = fast_roi_store<TP>(c, lane, k == 0 ? v0 : v1, tile);
         ORBGPU_STAMP(6);
-        fast_cell_body<TP, SP, PX>(g, c, lane, xoff, tile, sM, sList, keepb, cands, cntOut, stamps, item);
+        fast_cell_body<TP, SP, PX>(g, c, lane, xoff, tile, sM, sList, cands, cntOut, stamps, item);
     }
 }
 
@@ -933,8 +931,7 @@ void fast_wave_layout(Geom& g) {
     g.fast_list = list;
     g.fast_compact = maxw <= 36 ? 1 : 0;
     const int tp = g.fast_compact ? 56 : kFastTilePitch, sp = g.fast_compact ? 40 : 64;
-    g.fast_wave_bytes = ((rows * tp + 16 + 15) & ~15) + (((drows + 2) * sp + 15) & ~15) + ((list * 2 + 15) & ~15) +
-                        drows * 8;
+    g.fast_wave_bytes = ((rows * tp + 16 + 15) & ~15) + (((drows + 2) * sp + 15) & ~15) + ((list * 2 + 15) & ~15);
     g.fast_wave_bytes = (g.fast_wave_bytes + 15) & ~15;
 }
 
