@@ -118,6 +118,9 @@ int orb_debug_level_image(orb_ctx* ctx, int frame, int level, uint8_t* out, int*
 /* Phase timestamps of the last FAST launch (diagnostic; only with ORBGPU_FAST_STAMPS=1 in the
  * environment at orb_create): 8 s_memtime values per (frame, cell) item.  Returns the count copied. */
 int orb_debug_fast_stamps(orb_ctx* ctx, uint64_t* out, int cap);
+/* The BRIEF rotation's sin/cos as the kernels compute them (glibc sinf/cosf restated, ORBextractor.cc:113)
+ * for n host angles (radians, 0 <= x < 120): s[i] = sinf(x[i]), c[i] = cosf(x[i]).  Pin test only. */
+int orb_debug_sincosf(orb_ctx* ctx, const float* x, int n, float* s, float* c);
 
 /* =========================== Birdview stream (Frame.cc:318-342) ===========================
  * The reference runs OpenCV's cv::ORB (HARRIS_SCORE, not ORBextractor) plus cv::cornerSubPix on the

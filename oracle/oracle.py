@@ -18,6 +18,9 @@ KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4
 TIE_REVERSE_SEQ = 1
 RESIZE_GENERIC = 2
 BLUR_ALL_HALFUP = 4
+NO_FMA = 8
+TRIG_CR = 16
+TIE_LITERAL = 32
 
 
 class FeatVec(ctypes.Structure):
@@ -58,6 +61,7 @@ def lib():
         L.oracle_resize.argtypes = [vp, ci, ci, vp, ci, ci, ci]
         L.oracle_blur.argtypes = [vp, ci, ci, vp, ci]
         L.oracle_pattern.argtypes = [vp]
+        L.oracle_sincosf.argtypes = [vp, ci, vp, vp]
         L.oracle_time_extract.restype = ctypes.c_double
         L.oracle_time_extract.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ci, vp]
         L.oracle_search_by_bow_kf_f.argtypes = [cf, ci, ci, vp, vp, vp, FeatVec, ci, vp, vp, FeatVec, vp]
@@ -213,6 +217,14 @@ def pattern():
     out = np.zeros(1024, np.int32)
     lib().oracle_pattern(_p(out))
     return out
+
+
+def sincosf(x):
+    """glibc sinf/cosf restated (glibc_sincosf.inc): (sin, cos) of a float32 array."""
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.zeros_like(x), np.zeros_like(x)
+    lib().oracle_sincosf(_p(x), len(x), _p(s), _p(c))
+    return s, c
 
 
 def time_extract(frames, nfeatures, nthreads=1, iters=1, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):

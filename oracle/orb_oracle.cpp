@@ -6,6 +6,7 @@
  * Every function cites the reference file:line it restates.
  */
 #include "orb_oracle.h"
+#include "glibc_sincosf.inc"
 
 #include <algorithm>
 #include <atomic>
@@ -212,10 +213,25 @@ void fast9_roi(const uint8_t* base, int step, int rows, int cols, int threshold,
     uint8_t tab[512];
     for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
     if (cols <= 0 || rows <= 0) return;
-    std::vector<uint8_t> bufv((size_t)cols * 3, 0);
-    std::vector<int> cpv((size_t)(cols + 1) * 3, 0);
-    uint8_t* buf[3] = {bufv.data(), bufv.data() + cols, bufv.data() + 2 * cols};
-    int* cpbuf[3] = {cpv.data() + 1, cpv.data() + (cols + 1) + 1, cpv.data() + 2 * (cols + 1) + 1};
+    // row buffers on the stack for cell-sized ROIs, as OpenCV's AutoBuffer does (no heap traffic per
+    // cell: ORACLE_TIE_LITERAL's heap then sees only the allocations the reference makes)
+    uint8_t sbuf[3 * 128];
+    int scp[3 * 129];
+    std::vector<uint8_t> bufv;
+    std::vector<int> cpv;
+    uint8_t* b0 = sbuf;
+    int* c0 = scp;
+    if (cols > 128) {
+        bufv.assign((size_t)cols * 3, 0);
+        cpv.assign((size_t)(cols + 1) * 3, 0);
+        b0 = bufv.data();
+        c0 = cpv.data();
+    } else {
+        std::memset(sbuf, 0, (size_t)cols * 3);
+        std::memset(scp, 0, sizeof(int) * (size_t)(cols + 1) * 3);
+    }
+    uint8_t* buf[3] = {b0, b0 + cols, b0 + 2 * cols};
+    int* cpbuf[3] = {c0 + 1, c0 + (cols + 1) + 1, c0 + 2 * (cols + 1) + 1};
     for (int i = 3; i < rows - 2; i++) {
         const uint8_t* ptr = base + (size_t)i * step + 3;
         uint8_t* curr = buf[(i - 3) % 3];
@@ -322,24 +338,37 @@ float IC_Angle(const Img& image, float px, float py, const std::vector<int>& u_m
     return fastAtan2((float)m_01, (float)m_10);
 }
 
-/* Pinned trig: the reference calls glibc cosf/sinf (:113), whose
- * last-bit behaviour differs across glibc ifunc variants; the restatement and the HIP path both
- * use the correctly-rounded value, computed in double and rounded once. */
-inline float cos_cr(float a) { return (float)std::cos((double)a); }
-inline float sin_cr(float a) { return (float)std::sin((double)a); }
+/* BRIEF rotation trig (ORBextractor.cc:113, std::cos/std::sin of a float = glibc cosf/sinf, merged by
+ * GCC -O3 into one sincosf): glibc 2.35's algorithm restated in glibc_sincosf.inc, FMA ifunc variant,
+ * pinned bit for bit against libm over every float in [0, 2*pi] (tools/trig_pin.cpp).
+ * ORACLE_TRIG_CR gives round 1's correctly rounded pin instead (sensitivity only). */
+inline float orb_cos(float a, int flags) {
+    return (flags & ORACLE_TRIG_CR) ? (float)std::cos((double)a) : glibc_sincosf::cosf_(a);
+}
+inline float orb_sin(float a, int flags) {
+    return (flags & ORACLE_TRIG_CR) ? (float)std::sin((double)a) : glibc_sincosf::sinf_(a);
+}
+/* OpenCV's own (uncontracted) build of the same call (cv::ORB, birdview stream): glibc trig too */
+inline float cv_cosf(float a) { return glibc_sincosf::cosf_(a); }
+inline float cv_sinf(float a) { return glibc_sincosf::sinf_(a); }
 
 const float factorPI = (float)(M_PI / 180.f);   // ORBextractor.cc:107
 
-/* computeOrbDescriptor  ORBextractor.cc:108-147 */
-void computeOrbDescriptor(const KP& kpt, const Img& img, const int* pattern, uint8_t* desc) {
+/* computeOrbDescriptor  ORBextractor.cc:108-147.  The reference is built -O3 -march=native
+ * (CMakeLists.txt:10-11), so on an FMA host GCC contracts the two sample-offset expressions of :119-120;
+ * tools/ref_flags_probe.cpp compiled with those flags fixes the forms: y = fma(x, b, y*a),
+ * x = fma(x, a, -(y*b)).  ORACLE_NO_FMA evaluates them uncontracted (sensitivity only). */
+void computeOrbDescriptor(const KP& kpt, const Img& img, const int* pattern, uint8_t* desc, int flags) {
     float angle = (float)kpt.angle * factorPI;
-    float a = cos_cr(angle), b = sin_cr(angle);
+    float a = orb_cos(angle, flags), b = orb_sin(angle, flags);
     const uint8_t* center = img.row(cvRound(kpt.y)) + cvRound(kpt.x);
     const int step = img.w;
+    const bool fused = !(flags & ORACLE_NO_FMA);
     auto GET = [&](const int* p, int idx) -> int {
         float px = (float)p[2 * idx], py = (float)p[2 * idx + 1];
-        float t1 = px * b, t2 = py * a, t3 = px * a, t4 = py * b;
-        return center[cvRound(t1 + t2) * step + cvRound(t3 - t4)];
+        const float oy = fused ? std::fmaf(px, b, py * a) : px * b + py * a;
+        const float ox = fused ? std::fmaf(px, a, -(py * b)) : px * a - py * b;
+        return center[cvRound(oy) * step + cvRound(ox)];
     };
     for (int i = 0; i < 32; ++i, pattern += 32) {
         int val = 0;
@@ -493,6 +522,135 @@ std::vector<KP> DistributeOctTree(const std::vector<KP>& vToDistributeKeys, int 
     return vResultKeys;
 }
 
+/* ---------------- DistributeOctTree as the reference RUNS it (ORACLE_TIE_LITERAL) ----------------
+ * ORBextractor.cc:481-763 with the reference's own data structures, so that the heap sees the same
+ * allocation sequence: nodes laid out like ExtractorNode (ORBextractor.h:32-43: vector<cv::KeyPoint>,
+ * four cv::Point2i, a list iterator, a bool) in a std::list, children created as locals with
+ * reserve(parent size) and copied in with push_front, parents erased, and the final phase sorting
+ * std::pair<int, node*> — equal sizes ordered by heap ADDRESS (:684), i.e. by whatever glibc malloc
+ * handed out in this process.  Used only to measure the tie-order sensitivity (tools/tie_study.py). */
+struct LPoint { int x, y; };
+struct LNode {
+    LNode() : bNoMore(false) {}
+    std::vector<KP> vKeys;
+    LPoint UL, UR, BL, BR;
+    std::list<LNode>::iterator lit;
+    bool bNoMore;
+
+    void DivideNode(LNode& n1, LNode& n2, LNode& n3, LNode& n4) {   // :481-537
+        const int halfX = (int)std::ceil(static_cast<float>(UR.x - UL.x) / 2);
+        const int halfY = (int)std::ceil(static_cast<float>(BR.y - UL.y) / 2);
+        n1.UL = UL;
+        n1.UR = {UL.x + halfX, UL.y};
+        n1.BL = {UL.x, UL.y + halfY};
+        n1.BR = {UL.x + halfX, UL.y + halfY};
+        n1.vKeys.reserve(vKeys.size());
+        n2.UL = n1.UR;
+        n2.UR = UR;
+        n2.BL = n1.BR;
+        n2.BR = {UR.x, UL.y + halfY};
+        n2.vKeys.reserve(vKeys.size());
+        n3.UL = n1.BL;
+        n3.UR = n1.BR;
+        n3.BL = BL;
+        n3.BR = {n1.BR.x, BL.y};
+        n3.vKeys.reserve(vKeys.size());
+        n4.UL = n3.UR;
+        n4.UR = n2.BR;
+        n4.BL = n3.BR;
+        n4.BR = BR;
+        n4.vKeys.reserve(vKeys.size());
+        for (const KP& kp : vKeys) {
+            if (kp.x < n1.UR.x) (kp.y < n1.BR.y ? n1 : n3).vKeys.push_back(kp);
+            else (kp.y < n1.BR.y ? n2 : n4).vKeys.push_back(kp);
+        }
+        for (LNode* n : {&n1, &n2, &n3, &n4})
+            if (n->vKeys.size() == 1) n->bNoMore = true;
+    }
+};
+
+std::vector<KP> DistributeOctTreeLiteral(const std::vector<KP>& vToDistributeKeys, int minX, int maxX, int minY,
+                                         int maxY, int N, int nfeatures) {
+    const int nIni = (int)std::round(static_cast<float>(maxX - minX) / (maxY - minY));   // :543
+    const float hX = static_cast<float>(maxX - minX) / nIni;
+    std::list<LNode> lNodes;
+    std::vector<LNode*> vpIniNodes;
+    vpIniNodes.resize(nIni);
+    for (int i = 0; i < nIni; i++) {                                                     // :552-563
+        LNode ni;
+        ni.UL = {(int)(hX * static_cast<float>(i)), 0};
+        ni.UR = {(int)(hX * static_cast<float>(i + 1)), 0};
+        ni.BL = {ni.UL.x, maxY - minY};
+        ni.BR = {ni.UR.x, maxY - minY};
+        ni.vKeys.reserve(vToDistributeKeys.size());
+        lNodes.push_back(ni);
+        vpIniNodes[i] = &lNodes.back();
+    }
+    for (const KP& kp : vToDistributeKeys) vpIniNodes[(size_t)(kp.x / hX)]->vKeys.push_back(kp);   // :566-570
+    for (auto lit = lNodes.begin(); lit != lNodes.end();) {                             // :574-585
+        if (lit->vKeys.size() == 1) { lit->bNoMore = true; ++lit; }
+        else if (lit->vKeys.empty()) lit = lNodes.erase(lit);
+        else ++lit;
+    }
+    bool bFinish = false;
+    std::vector<std::pair<int, LNode*>> vSizeAndPointerToNode;
+    vSizeAndPointerToNode.reserve(lNodes.size() * 4);
+    // children n1..n4 of `parent` into the list front (:621-660 / :691-726)
+    auto add_children = [&](LNode& n1, LNode& n2, LNode& n3, LNode& n4, int* nToExpand) {
+        for (LNode* c : {&n1, &n2, &n3, &n4}) {
+            if (c->vKeys.size() > 0) {
+                lNodes.push_front(*c);
+                if (c->vKeys.size() > 1) {
+                    if (nToExpand) (*nToExpand)++;
+                    vSizeAndPointerToNode.push_back(std::make_pair((int)c->vKeys.size(), &lNodes.front()));
+                    lNodes.front().lit = lNodes.begin();
+                }
+            }
+        }
+    };
+    while (!bFinish) {                                                                   // :594-739
+        int prevSize = (int)lNodes.size();
+        auto lit = lNodes.begin();
+        int nToExpand = 0;
+        vSizeAndPointerToNode.clear();
+        while (lit != lNodes.end()) {
+            if (lit->bNoMore) { ++lit; continue; }
+            LNode n1, n2, n3, n4;
+            lit->DivideNode(n1, n2, n3, n4);
+            add_children(n1, n2, n3, n4, &nToExpand);
+            lit = lNodes.erase(lit);
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+            bFinish = true;
+        } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+            while (!bFinish) {
+                prevSize = (int)lNodes.size();
+                std::vector<std::pair<int, LNode*>> vPrevSizeAndPointerToNode = vSizeAndPointerToNode;
+                vSizeAndPointerToNode.clear();
+                std::sort(vPrevSizeAndPointerToNode.begin(), vPrevSizeAndPointerToNode.end());   // :684
+                for (int j = (int)vPrevSizeAndPointerToNode.size() - 1; j >= 0; j--) {
+                    LNode n1, n2, n3, n4;
+                    vPrevSizeAndPointerToNode[j].second->DivideNode(n1, n2, n3, n4);
+                    add_children(n1, n2, n3, n4, nullptr);
+                    lNodes.erase(vPrevSizeAndPointerToNode[j].second->lit);
+                    if ((int)lNodes.size() >= N) break;
+                }
+                if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
+            }
+        }
+    }
+    std::vector<KP> vResultKeys;                                                         // :741-762
+    vResultKeys.reserve(nfeatures);
+    for (auto& node : lNodes) {
+        const KP* pKP = &node.vKeys[0];
+        float maxResponse = pKP->response;
+        for (size_t k = 1; k < node.vKeys.size(); k++)
+            if (node.vKeys[k].response > maxResponse) { pKP = &node.vKeys[k]; maxResponse = node.vKeys[k].response; }
+        vResultKeys.push_back(*pKP);
+    }
+    return vResultKeys;
+}
+
 /* ---------------- the extractor object (ORBextractor.cc:410-470, 765-853, 1043-1132) ------- */
 struct Extractor {
     int nfeatures, nlevels, iniThFAST, minThFAST, flags;
@@ -558,15 +716,21 @@ struct Extractor {
     bool ComputeKeyPointsOctTree() {                                                // :765-853
         cand.assign(nlevels, {});
         lvlKps.assign(nlevels, {});
+        const bool literal = (flags & ORACLE_TIE_LITERAL) != 0;
         const float W = 30;
-        std::vector<Corner> vKeysCell;
+        std::vector<Corner> corners;
+        corners.reserve(4096);
         for (int level = 0; level < nlevels; ++level) {
             const Img& im = pyr[level];
             const int minBorderX = EDGE_THRESHOLD - 3;
             const int minBorderY = minBorderX;
             const int maxBorderX = im.w - EDGE_THRESHOLD + 3;
             const int maxBorderY = im.h - EDGE_THRESHOLD + 3;
-            std::vector<KP>& vToDistributeKeys = cand[level];
+            // literal mode: the reference's local vector and its reserve (:778-779), so the heap sees
+            // the reference's allocations; the pinned mode keeps the candidates for the debug view
+            std::vector<KP> local;
+            if (literal) local.reserve((size_t)nfeatures * 10);
+            std::vector<KP>& vToDistributeKeys = literal ? local : cand[level];
             const float width = (float)(maxBorderX - minBorderX);
             const float height = (float)(maxBorderY - minBorderY);
             const int nCols = (int)(width / W);
@@ -586,10 +750,11 @@ struct Extractor {
                     if (maxX > maxBorderX) maxX = (float)maxBorderX;
                     const int y0 = (int)iniY, y1 = (int)maxY, x0 = (int)iniX, x1 = (int)maxX;
                     const uint8_t* roi = im.row(y0) + x0;
-                    fast9_roi(roi, im.w, y1 - y0, x1 - x0, iniThFAST, vKeysCell);
-                    if (vKeysCell.empty()) fast9_roi(roi, im.w, y1 - y0, x1 - x0, minThFAST, vKeysCell);
-                    for (const Corner& c : vKeysCell) {
-                        KP kp{(float)c.x, (float)c.y, 7.f, -1.f, (float)c.score, 0, -1};
+                    fast9_roi(roi, im.w, y1 - y0, x1 - x0, iniThFAST, corners);
+                    if (corners.empty()) fast9_roi(roi, im.w, y1 - y0, x1 - x0, minThFAST, corners);
+                    std::vector<KP> vKeysCell;   // :808, grown by push_back as cv::FAST grows it
+                    for (const Corner& c : corners) vKeysCell.push_back(KP{(float)c.x, (float)c.y, 7.f, -1.f, (float)c.score, 0, -1});
+                    for (KP& kp : vKeysCell) {
                         kp.x += j * wCell;
                         kp.y += i * hCell;
                         vToDistributeKeys.push_back(kp);
@@ -598,8 +763,14 @@ struct Extractor {
             }
             if ((float)(maxBorderX - minBorderX) / (maxBorderY - minBorderY) < 0.5f) return false;  // nIni==0
             std::vector<KP>& keypoints = lvlKps[level];
-            keypoints = DistributeOctTree(vToDistributeKeys, minBorderX, maxBorderX, minBorderY, maxBorderY,
-                                          mnFeaturesPerLevel[level], (flags & ORACLE_TIE_REVERSE_SEQ) != 0);
+            if (literal) {
+                keypoints.reserve(nfeatures);   // :832
+                keypoints = DistributeOctTreeLiteral(vToDistributeKeys, minBorderX, maxBorderX, minBorderY, maxBorderY,
+                                                     mnFeaturesPerLevel[level], nfeatures);
+            } else {
+                keypoints = DistributeOctTree(vToDistributeKeys, minBorderX, maxBorderX, minBorderY, maxBorderY,
+                                              mnFeaturesPerLevel[level], (flags & ORACLE_TIE_REVERSE_SEQ) != 0);
+            }
             const int scaledPatchSize = (int)(PATCH_SIZE * mvScaleFactor[level]);
             for (KP& kp : keypoints) {
                 kp.x += minBorderX;
@@ -629,7 +800,7 @@ struct Extractor {
             if (nkl == 0) continue;
             gauss7_blur(pyr[level], blurred[level], flags);
             for (int i = 0; i < nkl; i++)
-                computeOrbDescriptor(keypoints[i], blurred[level], kPattern, &outDesc[(size_t)(offset + i) * 32]);
+                computeOrbDescriptor(keypoints[i], blurred[level], kPattern, &outDesc[(size_t)(offset + i) * 32], flags);
             offset += nkl;
             if (level != 0) {
                 float scale = mvScaleFactor[level];
@@ -705,11 +876,13 @@ void cull_rotation(std::vector<int>* rotHist, std::vector<int>& matches, int& nm
 const float* CheckF(const float* F, int r, int c) { return &F[r * 3 + c]; }
 
 bool CheckDistEpipolarLine(const KP& kp1, const KP& kp2, const float* F12, const float* sigma2) {  // :140-157
-    const float a = kp1.x * *CheckF(F12, 0, 0) + kp1.y * *CheckF(F12, 1, 0) + *CheckF(F12, 2, 0);
-    const float b = kp1.x * *CheckF(F12, 0, 1) + kp1.y * *CheckF(F12, 1, 1) + *CheckF(F12, 2, 1);
-    const float c = kp1.x * *CheckF(F12, 0, 2) + kp1.y * *CheckF(F12, 1, 2) + *CheckF(F12, 2, 2);
-    const float num = a * kp2.x + b * kp2.y + c;
-    const float den = a * a + b * b;
+    // the contraction GCC applies to these lines under the reference's -O3 -march=native on an FMA host,
+    // as tools/ref_flags_probe.cpp compiles them (the oracle itself is built -ffp-contract=off)
+    const float a = std::fmaf(kp1.x, *CheckF(F12, 0, 0), kp1.y * *CheckF(F12, 1, 0)) + *CheckF(F12, 2, 0);
+    const float b = std::fmaf(kp1.x, *CheckF(F12, 0, 1), kp1.y * *CheckF(F12, 1, 1)) + *CheckF(F12, 2, 1);
+    const float c = std::fmaf(kp1.y, *CheckF(F12, 1, 2), kp1.x * *CheckF(F12, 0, 2)) + *CheckF(F12, 2, 2);
+    const float num = std::fmaf(b, kp2.y, a * kp2.x) + c;
+    const float den = std::fmaf(a, a, b * b);
     if (den == 0) return false;
     const float dsqr = num * num / den;
     return dsqr < 3.84 * sigma2[kp2.octave];
@@ -832,6 +1005,12 @@ void oracle_blur(const uint8_t* src, int w, int h, uint8_t* dst, int flags) {
     std::memcpy(dst, d.d.data(), (size_t)w * h);
 }
 void oracle_pattern(int* out) { std::memcpy(out, kPattern, sizeof(kPattern)); }
+void oracle_sincosf(const float* x, int n, float* s, float* c) {
+    for (int i = 0; i < n; i++) {
+        s[i] = glibc_sincosf::sinf_(x[i]);
+        c[i] = glibc_sincosf::cosf_(x[i]);
+    }
+}
 
 double oracle_time_extract(const uint8_t* frames, int nframes, int w, int h, int nfeatures, float scaleFactor,
                            int nlevels, int iniTh, int minTh, int nthreads, int iters, long long* total_kps) {
@@ -966,7 +1145,7 @@ int oracle_search_for_triangulation(int checkOri, int onlyStereo, int n1, const 
                 if (!bStereo1 && !bStereo2) {
                     const float distex = ex - kp2.x;
                     const float distey = ey - kp2.y;
-                    if (distex * distex + distey * distey < 100 * scaleFactors2[kp2.octave]) continue;
+                    if (std::fmaf(distex, distex, distey * distey) < 100 * scaleFactors2[kp2.octave]) continue;   // contracted, as above
                 }
                 if (CheckDistEpipolarLine(kp1, kp2, F12, levelSigma2_2)) { bestIdx2 = idx2; bestDist = dist; }
             }

@@ -35,6 +35,10 @@ typedef struct {
 #define ORACLE_TIE_REVERSE_SEQ   1  /* octree sort tie: later-created = SMALLER "pointer"   */
 #define ORACLE_RESIZE_GENERIC    2  /* VResize uses generic FixedPtCast instead of 3.x >>4  */
 #define ORACLE_BLUR_ALL_HALFUP   4  /* column pass rounds half-up everywhere (no SSE body)  */
+#define ORACLE_NO_FMA            8  /* BRIEF offsets uncontracted (reference built without FMA) */
+#define ORACLE_TRIG_CR          16  /* BRIEF cos/sin correctly rounded instead of glibc cosf/sinf */
+#define ORACLE_TIE_LITERAL      32  /* DistributeOctTree as the reference runs it: std::list nodes,
+                                       pair<int, node*> sort by heap address (glibc malloc, this process) */
 
 void* oracle_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int flags);
 void  oracle_destroy(void* h);
@@ -62,6 +66,8 @@ int   oracle_fast_roi(const uint8_t* roi, int w, int h, int stride, int threshol
 void  oracle_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh, int flags);
 void  oracle_blur(const uint8_t* src, int w, int hgt, uint8_t* dst, int flags);
 void  oracle_pattern(int* out1024);
+/* glibc sinf/cosf as restated in glibc_sincosf.inc (ORBextractor.cc:113), n angles */
+void  oracle_sincosf(const float* x, int n, float* s, float* c);
 
 /* ---- CPU baseline timing: extract `nframes` frames (contiguous w*h each), round-robin over
  * `nthreads` threads (one frame per thread at a time), `iters` passes.  Returns wall seconds;

@@ -25,6 +25,7 @@
 #include <new>
 #include <vector>
 
+#include "glibc_trig.h"
 #include "orbgpu_ctx.h"
 
 namespace orbgpu {
@@ -522,9 +523,8 @@ __global__ __launch_bounds__(256) void k_bird_desc(const BirdGeom* __restrict__ 
     const float scale = 1.f / L.scale;
     const int cy = (int)rintf(kp.y * scale), cx = (int)rintf(kp.x * scale);
     const float angle = kp.angle * kFactorPI;
-    double sd, cd;
-    sincos((double)angle, &sd, &cd);
-    const float a = (float)cd, b = (float)sd;
+    float a, b;
+    glibc_sincosf(angle, &b, &a);   // cv::ORB's (float)cos / (float)sin of a float: glibc cosf / sinf
 #pragma unroll
     for (int rnd = 0; rnd < 4; rnd++) {
         const int p = rnd * 64 + lane;   // pair p: points 2p, 2p+1 -> byte p/8, bit p%8

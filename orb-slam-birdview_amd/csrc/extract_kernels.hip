@@ -2,9 +2,11 @@
 // IC-angle + 7x7 Gaussian + rBRIEF descriptor.  Integer/byte work: no MFMA anywhere; the bounds
 // are HBM bytes and VALU issue.
 //
-// Compiled with -ffp-contract=off and correctly-rounded fp32 divide: every float expression on the
-// path (root split hX, fastAtan2, BRIEF rotation, keypoint scaling) is evaluated exactly as the
-// reference's scalar C++ evaluates it.
+// Compiled with -ffp-contract=off and correctly-rounded fp32 divide, so every float expression on the
+// path (root split hX, fastAtan2, BRIEF rotation, keypoint scaling) is evaluated exactly as written; the
+// two the reference's -O3 -march=native build contracts into FMAs (the BRIEF sample offsets) are
+// written as explicit fmaf, and cos/sin follow glibc.
+#include "glibc_trig.h"
 #include "orbgpu_internal.h"
 #include "pattern31_data.inc"
 
@@ -277,98 +279,6 @@ __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
     return max(A, -Bn);
 }
 
-// Necessary condition for a FAST corner at any threshold >= t: a 9-arc always contains two
-// cyclically adjacent compass points (circle positions 0, 4, 8, 12), so two adjacent compass points
-// must both be brighter than v + t or both darker than v - t.  0xFAC8 marks the 4-bit patterns with
-// two cyclically adjacent set bits.
-__device__ __forceinline__ bool fast_maybe(int v, int p0, int p4, int p8, int p12, int t) {
-    const int hi = v + t, lo = v - t;
-    const int bm = (p0 > hi) | ((p4 > hi) << 1) | ((p8 > hi) << 2) | ((p12 > hi) << 3);
-    const int dm = (p0 < lo) | ((p4 < lo) << 1) | ((p8 < lo) << 2) | ((p12 < lo) << 3);
-    return ((0xFAC8 >> bm) | (0xFAC8 >> dm)) & 1;
-}
-
-__device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xFF; }
-
-// Exclusive scan of one int per thread over a 256-thread block (two barriers).
-__device__ __forceinline__ int block256_excl_scan(int v, int* s_wave, int& total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wave[wave] = x;
-    __syncthreads();
-    int before = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const int cw = s_wave[w];
-        before += w < wave ? cw : 0;
-        tot += cw;
-    }
-    __syncthreads();
-    total = tot;
-    return before + x - v;
-}
-
-// Raster-ordered append of one flag per thread (ballot form of the scan above).
-__device__ __forceinline__ int chunk_append(bool flag, int running, int* s_wave, int& pos) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long mask = __ballot(flag);
-    if (lane == 0) s_wave[wave] = __popcll(mask);
-    __syncthreads();
-    int before = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const int cw = s_wave[w];
-        before += w < wave ? cw : 0;
-        tot += cw;
-    }
-    pos = running + before + lanes_below(mask);
-    __syncthreads();
-    return running + tot;
-}
-
-struct FastCell {
-    int f, cell, l, ci, cj, iniX, iniY, rw, rh, dw, dh, x0w, nw;
-    bool valid, aligned;
-    const uint8_t* base;   // ROI row 0, column 0
-    int stride;
-};
-
-__device__ __forceinline__ FastCell fast_cell(const Geom* __restrict__ g, int item, const uint8_t* frames,
-                                              long long framePitch, int rowStride, const uint8_t* pyr) {
-    FastCell c;
-    c.f = item / g->ncells;
-    c.cell = item - c.f * g->ncells;
-    int l = 0;
-    while (l + 1 < g->nlevels && c.cell >= g->L[l + 1].cell_base) ++l;
-    c.l = l;
-    const LevelGeom& L = g->L[l];
-    const int cc = c.cell - L.cell_base;
-    c.ci = cc / L.nCols;
-    c.cj = cc - c.ci * L.nCols;
-    c.iniY = kMinBorder + c.ci * L.hCell;
-    c.iniX = kMinBorder + c.cj * L.wCell;
-    c.valid = !(c.iniY >= L.maxBY - 3 || c.iniX >= L.maxBX - 6);   // :794-806
-    const int maxY = min(c.iniY + L.hCell + 6, L.maxBY);
-    const int maxX = min(c.iniX + L.wCell + 6, L.maxBX);
-    c.rw = maxX - c.iniX;
-    c.rh = maxY - c.iniY;
-    c.dw = c.rw - 6;   // FAST detection domain: ROI rows/cols 3 .. n-4
-    c.dh = c.rh - 6;
-    c.valid = c.valid && c.dw > 0 && c.dh > 0;
-    const LevelPtr src = level_ptr(g, l, frames, framePitch, rowStride, pyr, c.f);
-    c.base = src.p + (long long)c.iniY * src.stride;
-    c.stride = src.stride;
-    c.aligned = ((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0;
-    c.x0w = c.iniX >> 2;
-    c.nw = ((c.iniX + c.rw + 3) >> 2) - c.x0w;
-    return c;
-}
-
 // Host table of the cells (ComputeKeyPointsOctTree's grid, ORBextractor.cc:781-806), frame independent.
 void build_cells(const Geom& g, std::vector<CellDesc>& cells) {
     cells.assign(g.ncells, CellDesc{});
@@ -432,152 +342,6 @@ __device__ __forceinline__ FastCellT fast_cell_t(const Geom* __restrict__ g, con
     c.x0w = c.iniX >> 2;
     c.nw = ((c.iniX + c.rw + 3) >> 2) - c.x0w;
     return c;
-}
-
-__global__ __launch_bounds__(256) void k_fast(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
-                                              long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
-                                              uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
-                                              int remap) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kFastMaxRoi * kFastTilePitch + 16];
-    // sized so that 8 blocks (32 waves) fit a CU's 160 KiB: domain <= 60 x 60 px (wCell, hCell <= 60)
-    __shared__ __attribute__((aligned(16))) uint8_t sM[60 * 64];   // arc strength, pitch 64 (0 = cannot be a corner)
-    __shared__ uint16_t sList[60 * 60];                            // prefilter survivors (dy*64+dx), raster order
-    __shared__ uint8_t sKeep[60 * 60];                             // NMS verdict per list entry
-    __shared__ int s_wave[4];
-    __shared__ int s_cnt;
-    const int tid = threadIdx.x;
-    // One (frame, cell) item per block.  Blocks are dealt round-robin over the 8 XCDs, so the
-    // bijective remap below gives each XCD a contiguous range of items: neighbouring cells (which
-    // share ROI rows) then hit the same L2 (speed only; any placement is correct).
-    int item = blockIdx.x;
-    if (remap) {
-        const int q = total >> 3, r = total & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-        item = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int tmin = min(g->iniTh, g->minTh);
-    constexpr int TP = kFastTilePitch;
-    const FastCell c = fast_cell(g, item, frames, framePitch, rowStride, pyr);
-    int* cntOut = cellCount + (long long)c.f * g->ncells + c.cell;
-    if (!c.valid) {
-        if (tid == 0) *cntOut = 0;
-        return;
-    }
-    int xoff = 0;
-    if (c.aligned) {
-        for (int idx = tid; idx < c.rh * c.nw; idx += 256) {
-            const int yy = idx / c.nw, ww = idx - yy * c.nw;
-            *reinterpret_cast<uint32_t*>(&tile[yy * TP + ww * 4]) =
-                *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + ww) * 4));
-        }
-        xoff = c.iniX & 3;
-    } else {
-        for (int idx = tid; idx < c.rh * c.rw; idx += 256) {
-            const int yy = idx / c.rw, xx = idx - yy * c.rw;
-            tile[yy * TP + xx] = c.base[roi_off(yy, c.stride, c.iniX + xx)];
-        }
-    }
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    {
-        const int dw = c.dw, dh = c.dh;
-        // stage 1: compass prefilter on runs of 4 pixels (dword LDS reads), compaction in raster order
-        const int nruns = (dw + 3) >> 2;
-        int nlist = 0;
-        for (int b0 = 0; b0 < dh * nruns; b0 += 256) {
-            const int it = b0 + tid;
-            int pm = 0, dy = 0, x0 = 0;
-            if (it < dh * nruns) {
-                dy = it / nruns;
-                x0 = 4 * (it - dy * nruns);
-                const int sc = (dy + 3) * TP + x0 + xoff;   // center row, from pixel x0-3
-                const int s0 = (dy + 6) * TP + x0 + 3 + xoff;
-                const int s8 = dy * TP + x0 + 3 + xoff;
-                const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
-                const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
-                const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3];
-                const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);
-                const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);
-                const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);
-                const uint32_t B = __builtin_amdgcn_alignbyte(t32[d0 + 1], t32[d0], s0 & 3);
-                const uint32_t C = __builtin_amdgcn_alignbyte(t32[d8 + 1], t32[d8], s8 & 3);
-                const unsigned long long c64 = (unsigned long long)A0 | ((unsigned long long)A1 << 32);
-                const uint32_t c8_11 = A2;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int v = (int)((c64 >> (8 * (3 + i))) & 0xFF);
-                    const int p12 = (int)((c64 >> (8 * i)) & 0xFF);
-                    const int p4 = i < 2 ? (int)((c64 >> (8 * (6 + i))) & 0xFF) : byte_of(c8_11, i - 2);
-                    const int p0 = byte_of(B, i), p8 = byte_of(C, i);
-                    if (x0 + i < dw && fast_maybe(v, p0, p4, p8, p12, tmin)) pm |= 1 << i;
-                }
-                *reinterpret_cast<uint32_t*>(&sM[dy * 64 + x0]) = 0u;
-            }
-            int tot;
-            int pos = nlist + block256_excl_scan(__popc(pm), s_wave, tot);
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if (pm & (1 << i)) sList[pos++] = (uint16_t)(dy * 64 + x0 + i);
-            nlist += tot;
-        }
-        __syncthreads();
-        // stage 2: exact arc strength for the survivors only
-        const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
-        for (int i = tid; i < nlist; i += 256) {
-            const int p = sList[i];
-            sM[p] = (uint8_t)fast_arc_strength(t0 + (p >> 6) * TP + (p & 63));
-        }
-        __syncthreads();
-        // NMS (cell-local): keep iff corner at th and score > every in-domain neighbour's score, where
-        // a neighbour that is not a corner at th counts 0 (cv::FAST row buffers)
-        auto keep = [&](int p, int th) -> bool {
-            const int m = sM[p];
-            if (m <= th) return false;
-            const int dy = p >> 6, dx = p & 63;
-            const int s = m - 1;
-#pragma unroll
-            for (int oy = -1; oy <= 1; oy++) {
-#pragma unroll
-                for (int ox = -1; ox <= 1; ox++) {
-                    if (ox == 0 && oy == 0) continue;
-                    const int ny = dy + oy, nx = dx + ox;
-                    if (ny < 0 || ny >= dh || nx < 0 || nx >= dw) continue;
-                    const int mn = sM[ny * 64 + nx];
-                    const int sn = mn > th ? mn - 1 : 0;
-                    if (!(s > sn)) return false;
-                }
-            }
-            return true;
-        };
-        int mine = 0;
-        for (int i = tid; i < nlist; i += 256) {
-            const bool k = keep(sList[i], g->iniTh);
-            sKeep[i] = k;
-            mine += k;
-        }
-        if (mine) atomicAdd(&s_cnt, mine);
-        __syncthreads();
-        if (s_cnt == 0) {   // :812-816 fallback to minThFAST, evaluated after NMS
-            for (int i = tid; i < nlist; i += 256) sKeep[i] = keep(sList[i], g->minTh);
-            __syncthreads();
-        }
-        // emission in raster order (FAST emission order)
-        const LevelGeom& L = g->L[c.l];
-        uint32_t* out = cands + (long long)c.f * g->ncand + L.cand_base + (long long)(c.cell - L.cell_base) * L.cell_cap;
-        int running = 0;
-        for (int b0 = 0; b0 < nlist; b0 += 256) {
-            const int i = b0 + tid;
-            const bool k = i < nlist && sKeep[i];
-            int pos;
-            running = chunk_append(k, running, s_wave, pos);
-            if (k) {
-                const int p = sList[i];
-                const uint32_t xr = (uint32_t)((p & 63) + 3 + c.cj * L.wCell);
-                const uint32_t yr = (uint32_t)((p >> 6) + 3 + c.ci * L.hCell);
-                out[pos] = xr | (yr << 12) | ((uint32_t)(sM[p] - 1) << 24);
-            }
-        }
-        if (tid == 0) *cntOut = running;
-    }
 }
 
 // wave-level scans (DPP) for the wave-per-cell FAST kernel below
@@ -704,17 +468,18 @@ __device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, cons
 
 // One cell after its ROI is in the tile: prefilter, exact arc strength, cell-local NMS with the
 // minThFAST fallback, raster-order emission (see k_fast above for the semantics).
-template <int TP, int SP, int PX>
+template <int TP, int SP>
 __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane, int xoff,
                                                uint8_t* tile, uint8_t* sM, uint16_t* sList,
                                                uint32_t* __restrict__ cands,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
+    constexpr int PX = 8;
     const int dw = c.dw, dh = c.dh;
     // (16-byte stores; the map's LDS carve is rounded up to 16 bytes)
     for (int i = lane; i < ((dh + 2) * SP + 15) / 16; i += 64) reinterpret_cast<uint4*>(sM)[i] = make_uint4(0u, 0u, 0u, 0u);
     wave_lds_sync();
     ORBGPU_STAMP(1);
-    // lane -> (run of PX pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
+    // lane -> (run of PX = 8 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
     const int nruns = (dw + PX - 1) / PX;
     const int rpi = 64 / nruns;                          // rows per iteration
     const int lrow = (int)div20(lane, recip20(nruns));
@@ -730,14 +495,14 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
     int th = g->iniTh;
     int kept = 0;
     for (int pass = 0; pass < 2; pass++) {
-        // ---- stage 1: compass prefilter at th, 4 pixels per lane in packed 16-bit lanes, per-bit
+        // ---- stage 1: compass prefilter at th, 8 pixels per lane in packed 16-bit lanes, per-bit
         // ballot compaction into sList
         const uint32_t tt = (uint32_t)th | ((uint32_t)th << 16);
         int nlist = 0;
         for (int r0 = 0; r0 < dh; r0 += rpi) {
             const int dy = r0 + lrow;
             int pm = 0;
-            if (PX == 8 && lane_on && dy < dh) {
+            if (lane_on && dy < dh) {
                 // 8 pixels: centre bytes x0-3 .. x0+12 (5 dwords), rows +-3 bytes x0 .. x0+7 (3 dwords each)
                 const int sc = (dy + 3) * TP + x0 + xoff;
                 const int s0 = (dy + 6) * TP + x0 + 3 + xoff;
@@ -768,27 +533,6 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const uint32_t Y = __builtin_amdgcn_perm(rob, reb, 0x07030501u);
                 const uint32_t Z = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
                 pm = (int)(((Z * 0x01020408u) >> 24) & xvalid);
-            }
-            if (PX == 4 && lane_on && dy < dh) {
-                const int sc = (dy + 3) * TP + x0 + xoff;       // centre row, from pixel x0-3
-                const int s0 = (dy + 6) * TP + x0 + 3 + xoff;   // row +3
-                const int s8 = dy * TP + x0 + 3 + xoff;         // row -3
-                const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
-                const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3];
-                const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);   // pixels x0-3 .. x0
-                const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);   // x0+1 .. x0+4
-                const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);   // x0+5 .. x0+8
-                const uint32_t P0 = __builtin_amdgcn_alignbyte(t32[d0 + 1], t32[d0], s0 & 3);
-                const uint32_t P8 = __builtin_amdgcn_alignbyte(t32[d8 + 1], t32[d8], s8 & 3);
-                const uint32_t V = __builtin_amdgcn_alignbyte(A1, A0, 3);     // centres x0 .. x0+3
-                const uint32_t P4 = __builtin_amdgcn_alignbyte(A2, A1, 2);    // x0+3 .. x0+6
-                const uint32_t P12 = A0;                                      // x0-3 .. x0
-                // bytes 0, 2 / 1, 3 into 16-bit lanes: one v_perm_b32 each (0x0c selects a zero byte)
-                auto ev = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c00u); };
-                auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
-                const uint32_t re = compass2(ev(V), ev(P0), ev(P4), ev(P8), ev(P12), tt);   // px 0, 2
-                const uint32_t ro = compass2(od(V), od(P0), od(P4), od(P8), od(P12), tt);   // px 1, 3
-                pm = (int)((((re >> 15) & 1u) | ((ro >> 14) & 2u) | ((re >> 29) & 4u) | ((ro >> 28) & 8u)) & xvalid);
             }
             // compaction: one wave prefix sum of the per-lane survivor counts, then each lane writes
             // its (<= 4) entries at its offset
@@ -866,23 +610,20 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
  * per-wave LDS carve is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors
  * are compacted by one wave scan into a raster-ordered list, so corners keep that order and the NMS
  * pass emits the kept ones directly (FAST emission order) by ballot compaction. */
-template <int TP, int SP, int PX>
+template <int TP, int SP>
 __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
-                                                   int cbeg, int cnum, int remap, unsigned long long* __restrict__ stamps,
+                                                   int cbeg, int cnum, unsigned long long* __restrict__ stamps,
                                                    int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
     if (err && blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // k_octree's overflow flag (set after this kernel)
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (8 cells each)
-    int blk = blockIdx.x;
-    if (remap) {
-        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-        blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     const int item0 = (blk * (int)(blockDim.x >> 6) + wv) * 2;
     if (item0 >= total) return;   // whole wave; nothing below uses a block barrier
     const int wb = g->fast_wave_bytes;
@@ -910,7 +651,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         wave_lds_sync();   // the previous cell's last LDS reads happen before this one's writes
         const int xoff = fast_roi_store<TP>(c, lane, k == 0 ? v0 : v1, tile);
         ORBGPU_STAMP(6);
-        fast_cell_body<TP, SP, PX>(g, c, lane, xoff, tile, sM, sList, cands, cntOut, stamps, item);
+        fast_cell_body<TP, SP>(g, c, lane, xoff, tile, sM, sList, cands, cntOut, stamps, item);
     }
 }
 
@@ -1566,8 +1307,10 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
 #pragma unroll
     for (int gq = 0; gq < 4; gq++) {   // test pair lane + 64 gq: (x0, y0, x1, y1) = pf[gq]
         const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
-        const uint32_t r0 = sample(px0 * a - py0 * b, px0 * b + py0 * a);
-        const uint32_t r1 = sample(px1 * a - py1 * b, px1 * b + py1 * a);
+        // the sample offsets as the reference's -O3 -march=native build contracts them (:119-120;
+        // tools/ref_flags_probe.cpp): x = fma(px, a, -(py*b)), y = fma(px, b, py*a)
+        const uint32_t r0 = sample(__builtin_fmaf(px0, a, -(py0 * b)), __builtin_fmaf(px0, b, py0 * a));
+        const uint32_t r1 = sample(__builtin_fmaf(px1, a, -(py1 * b)), __builtin_fmaf(px1, b, py1 * a));
         // saturate_cast<uchar>: only the right-hand side needs the clamp (t0 = 256 compares as 255 would)
         const unsigned long long m = __ballot((r0 >> 16) < min(r1 >> 16, 255u));
         if (lane == 0) dst[gq] = m;
@@ -1596,7 +1339,6 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
     }
 }
 
-template <bool SMP>
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
                                           const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const float (&pf)[4][4],
                                           orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
@@ -1697,84 +1439,25 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     wave_lds_sync();
     DESC_STAMP(3);
 
-    // ---- column pass: item = (column bx, 4 outputs by = 4g..4g+3) over RT[bx][4g .. 4g+9],
-    // v_dot2_u32_u16 on row pairs; rounding as the pinned OpenCV 3.2 8U path: half-to-even where the
-    // SSE2 body runs (x < W & ~3), half-up in the scalar tail.  Result stored transposed,
-    // blurT[bx][by] at bx*40 + by, over the (now dead) window buffer.
+    // ---- column pass: evaluated only at the 512 BRIEF sample pixels (brief_sampled), v_dot2_u32_u16 on
+    // row pairs of RT; rounding as the pinned OpenCV 3.2 8U path: half-to-even where the SSE2 body runs
+    // (x < W & ~3), half-up in the scalar tail.
     const int xsimd = L.w & ~3;
     const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4], k5 = g->gk[5],
               k6 = g->gk[6];
     const ushort2_t K01 = {(unsigned short)k0, (unsigned short)k1}, K23 = {(unsigned short)k2, (unsigned short)k3},
-                    K45 = {(unsigned short)k4, (unsigned short)k5}, K60 = {(unsigned short)k6, 0},
-                    K0s = {0, (unsigned short)k0}, K12 = {(unsigned short)k1, (unsigned short)k2},
-                    K34 = {(unsigned short)k3, (unsigned short)k4}, K56 = {(unsigned short)k5, (unsigned short)k6};
-    if constexpr (!SMP) {
-    uint32_t outw[6];
-    int outa[6];
-#pragma unroll
-    for (int r = 0; r < 6; r++) {   // 37 columns x 10 groups = 370 <= 6 x 64
-        const int it = lane + 64 * r;
-        outa[r] = -1;
-        if (it < kDescBlur * 10) {
-            const int bx = it / 10, gq = it - bx * 10;
-            const uint32_t* rp = reinterpret_cast<const uint32_t*>(rt + __umul24((unsigned)bx, (unsigned)kRtPitch) + 4 * gq);
-            ushort2_t D[5];
-#pragma unroll
-            for (int i = 0; i < 5; i++) D[i] = __builtin_bit_cast(ushort2_t, rp[i]);
-            uint32_t S[4];
-            S[0] = __builtin_amdgcn_udot2(K60, D[3], __builtin_amdgcn_udot2(K45, D[2],
-                     __builtin_amdgcn_udot2(K23, D[1], __builtin_amdgcn_udot2(K01, D[0], 0u, false), false), false), false);
-            S[1] = __builtin_amdgcn_udot2(K56, D[3], __builtin_amdgcn_udot2(K34, D[2],
-                     __builtin_amdgcn_udot2(K12, D[1], __builtin_amdgcn_udot2(K0s, D[0], 0u, false), false), false), false);
-            S[2] = __builtin_amdgcn_udot2(K60, D[4], __builtin_amdgcn_udot2(K45, D[3],
-                     __builtin_amdgcn_udot2(K23, D[2], __builtin_amdgcn_udot2(K01, D[1], 0u, false), false), false), false);
-            S[3] = __builtin_amdgcn_udot2(K56, D[4], __builtin_amdgcn_udot2(K34, D[3],
-                     __builtin_amdgcn_udot2(K12, D[2], __builtin_amdgcn_udot2(K0s, D[1], 0u, false), false), false), false);
-            const bool even = x - 18 + bx < xsimd;
-            uint32_t packed = 0;
-#pragma unroll
-            for (int o = 0; o < 4; o++) {
-                // round(S / 65536): half-to-even = (S + 32767 + q&1) >> 16, half-up = (S + 32768) >> 16
-                const uint32_t bias = even ? 32767u + ((S[o] >> 16) & 1u) : 32768u;
-                const uint32_t v = min((S[o] + bias) >> 16, 255u);
-                packed |= v << (8 * o);
-            }
-            outw[r] = packed;
-            outa[r] = (int)(__umul24((unsigned)bx, (unsigned)kDescBlurPitch) + 4 * gq) >> 2;
-        }
-    }
-    wave_lds_sync();   // every lane has finished reading the window before it is overwritten
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-        if (outa[r] >= 0) w32[outa[r]] = outw[r];
-    wave_lds_sync();
-    }
+                    K45 = {(unsigned short)k4, (unsigned short)k5}, K60 = {(unsigned short)k6, 0};
     DESC_STAMP(4);
 
-    // ---- rBRIEF (:108-147): pinned correctly-rounded cos/sin; 256 tests as
-    // four 64-lane ballots; sample (ix, iy) of the blurred patch at blurT[(18+ix)*40 + 18+iy]
+    // ---- rBRIEF (:108-147): cos/sin as glibc's cosf/sinf compute them (:113, glibc_trig.h); 256 tests
+    // as four 64-lane ballots; sample (ix, iy) of the blurred patch at blurT[(18+ix)*40 + 18+iy]
     const float ang = angle * kFactorPI;
-    double sd, cd;
-    sincos((double)ang, &sd, &cd);
-    const float a = (float)cd, b = (float)sd;
+    float a, b;
+    glibc_sincosf(ang, &b, &a);
     DESC_STAMP(5);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(outD + ((long long)f * kpCap + outIdx) * 32);
-    if constexpr (SMP) {
-        if (x + 18 < xsimd) brief_sampled<true>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
-        else brief_sampled<false>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
-    } else {
-        const uint8_t* ctr = wbase + 18 * kDescBlurPitch + 18;
-#pragma unroll
-        for (int gq = 0; gq < 4; gq++) {
-            const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
-            const float u0 = px0 * b, u1 = py0 * a, u2 = px0 * a, u3 = py0 * b;
-            const float w0 = px1 * b, w1 = py1 * a, w2 = px1 * a, w3 = py1 * b;
-            const int t0 = ctr[__mul24(__float2int_rn(u2 - u3), kDescBlurPitch) + __float2int_rn(u0 + u1)];
-            const int t1 = ctr[__mul24(__float2int_rn(w2 - w3), kDescBlurPitch) + __float2int_rn(w0 + w1)];
-            const unsigned long long m = __ballot(t0 < t1);
-            if (lane == 0) dst[gq] = m;
-        }
-    }
+    if (x + 18 < xsimd) brief_sampled<true>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
+    else brief_sampled<false>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
     if (lane == 0) {
         orb_keypoint o;
         o.x = (float)x;
@@ -1794,27 +1477,20 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 #undef DESC_STAMP
 }
 
-/* Fused IC angle + 7x7 blur + rBRIEF, one wavefront per keypoint slot; a wavefront owns NPW consecutive
+/* Fused IC angle + 7x7 blur + rBRIEF, one wavefront per keypoint slot; a wavefront owns two consecutive
  * slots and issues the second interior window's loads before processing the first. */
-template <int WPB, bool SMP, int NPW>
+constexpr int kDescWaves = 4, kDescSlotsPerWave = 2;
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
-                                                  int remap, unsigned long long* __restrict__ dstamps) {
+                                                  unsigned long long* __restrict__ dstamps) {
     // per wave: 43x48 window (+16 B pad) and the transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch;
     // pitch 50 spreads the transposed stores of the 10 column groups over distinct banks)
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[WPB][kDescWin * kDescWinPitch + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t s_rt[WPB][40 * kRtPitch];
-    int f = blockIdx.y, bx = blockIdx.x;
-    if (remap) {   // workgroups are dealt round-robin over the 8 XCDs: give each XCD a contiguous range of frames
-        const int gx = gridDim.x, nb = gx * gridDim.y, q = nb >> 3, r = nb & 7;
-        const int hw = blockIdx.y * gx + blockIdx.x, xcd = hw & 7, j = hw >> 3;
-        const int lg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-        f = lg / gx;
-        bx = lg - f * gx;
-    }
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[kDescWaves][kDescWin * kDescWinPitch + 16];
+    __shared__ __attribute__((aligned(16))) uint16_t s_rt[kDescWaves][40 * kRtPitch];
+    const int f = blockIdx.y, bx = blockIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int nl = g->nlevels;
     const int* cnts = lvlCount + f * nl;
@@ -1823,14 +1499,14 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         for (int i = 0; i < nl; i++) tot += cnts[i];
         outN[f] = tot;
     }
-    const int s0 = (bx * WPB + wv) * NPW;
+    const int s0 = (bx * kDescWaves + wv) * kDescSlotsPerWave;
     if (s0 >= g->nkpcap) return;
     const DescSlot d0 = desc_slot(g, f, s0, cnts, lvlKps, frames, framePitch, rowStride, pyr);
-    const DescSlot d1 = NPW > 1 ? desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr) : DescSlot{};
-    if (!d0.ok && !(NPW > 1 && d1.ok)) return;   // (the two slots may straddle a level boundary)
+    const DescSlot d1 = desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr);
+    if (!d0.ok && !d1.ok) return;   // (the two slots may straddle a level boundary)
     uint32_t v0[9], v1[9];
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
-    if (NPW > 1 && d1.ok && d1.interior) desc_issue(d1, lane, v1);
+    if (d1.ok && d1.interior) desc_issue(d1, lane, v1);
     // BRIEF test pairs of this lane (lane + 64 gq), fetched now so their latency hides under the window's
     float pf[4][4];
 #pragma unroll
@@ -1841,12 +1517,30 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         pf[gq][2] = (float)pp.z;
         pf[gq][3] = (float)pp.w;
     }
-    if (d0.ok) desc_body<SMP>(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
-    if (NPW > 1 && d1.ok) {
+    if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
+    if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
-        desc_body<SMP>(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
+        desc_body(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
     }
+}
+
+/* glibc_sincosf over an array of angles (the C-ABI's orb_debug_sincosf: the GPU test pins the device
+ * restatement against the oracle's and libm on the host) */
+__global__ __launch_bounds__(256) void k_debug_sincosf(const float* __restrict__ x, int n, float* __restrict__ s,
+                                                       float* __restrict__ c) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float sv, cv;
+    glibc_sincosf(x[i], &sv, &cv);
+    s[i] = sv;
+    c[i] = cv;
+}
+
+hipError_t launch_debug_sincosf(const float* d_x, int n, float* d_s, float* d_c, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_debug_sincosf, dim3((n + 255) / 256), dim3(256), 0, stream, d_x, n, d_s, d_c);
+    return hipGetLastError();
 }
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -1865,84 +1559,37 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                           int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
     if (nframes <= 0) return hipSuccess;
-    const bool wave_fast = !(b.fast_block || (size_t)g.fast_wave_bytes * 4 > 65536);
-    auto launch_fast = [&](int cbeg, int cnum, hipStream_t s) {
-        const int items = cnum * nframes;
-        if (!wave_fast) {   // very large cells: block-per-cell kernel (all cells)
-            if (b.zero_err) (void)hipMemsetAsync(b.d_err, 0, sizeof(int), s);
-            hipLaunchKernelGGL(k_fast, dim3(items), dim3(256), 0, s, b.d_geom, d_frames, frame_pitch, row_stride,
-                               b.d_pyr, b.d_cands, b.d_cellCount, items, b.fast_remap);
-        }
-        else {
-            // b.fast_wpb waves per workgroup: a workgroup's LDS is released only when its slowest wave
-            // ends, so fewer waves per workgroup waste less of the CU on uneven cells
-            const int wpb = b.fast_wpb;
-            const unsigned nblk = cdiv(items, 2 * wpb);
-            const size_t lds = (size_t)g.fast_wave_bytes * wpb;
-            auto kern = g.fast_compact ? (b.fast_px == 8 ? k_fast_wave<56, 40, 8> : k_fast_wave<56, 40, 4>)
-                                       : (b.fast_px == 8 ? k_fast_wave<kFastTilePitch, 64, 8>
-                                                         : k_fast_wave<kFastTilePitch, 64, 4>);
-            hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * wpb), lds, s, b.d_geom, b.d_cells, d_frames, frame_pitch,
-                               row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum, b.fast_remap,
-                               b.d_stamps, cbeg == 0 && b.zero_err ? b.d_err : nullptr);
-        }
-    };
-    auto resize_levels = [&](int l0, int l1, hipStream_t s) {
-        for (int l = l0; l < l1; l++) {
-            const int t = g.L[l].rs_tiled;
-            const int want = b.resize_th >= 64 ? 2 : b.resize_th >= 32 ? 1 : 0;
-            int sel = -1;
-            for (int i = want; i >= 0 && sel < 0; i--)
-                if (t & (1 << i)) sel = i;
-            if (sel >= 0 && !b.resize_direct) {
-                const int th = 16 << sel;
-                dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
-                const ResizeCoef* cf = b.d_rcoef + b.rcoef_off[l];
-                if (sel == 2)
-                    hipLaunchKernelGGL(k_resize_tiled<64>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames,
-                                       frame_pitch, row_stride, b.d_pyr);
-                else if (sel == 1)
-                    hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames,
-                                       frame_pitch, row_stride, b.d_pyr);
-                else
-                    hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames,
-                                       frame_pitch, row_stride, b.d_pyr);
-            } else {
-                dim3 grid(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes);
-                hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, b.d_geom, b.d_rcoef + b.rcoef_off[l], l,
-                                   d_frames, frame_pitch, row_stride, b.d_pyr);
-            }
-        }
-    };
-    // Pyramid tail split (ORBGPU_RESIZE_SPLIT = s): the small levels s+1.. are latency-bound launches,
-    // so they run on the side stream while FAST processes the cells of levels 0..s; FAST of the
-    // remaining levels waits for them.
-    const int sp = b.resize_split;
-    const bool split = b.side && wave_fast && sp >= 1 && sp + 1 < g.nlevels;
-    hipError_t e;
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);
-    resize_levels(1, split ? sp + 1 : g.nlevels, stream);
-    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
-    if (split) {
-        if ((e = hipEventRecord(b.side_fork, stream)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(b.side, b.side_fork, 0)) != hipSuccess) return e;
-        if (marker) marker(user, ORB_K_RESIZE, 1, b.side);
-        resize_levels(sp + 1, g.nlevels, b.side);
-        if (marker) marker(user, ORB_K_RESIZE, 0, b.side);
-        if ((e = hipEventRecord(b.side_join, b.side)) != hipSuccess) return e;
-        const int ncs = g.L[sp + 1].cell_base;   // cells of levels 0..sp
-        if (marker) marker(user, ORB_K_FAST, 1, stream);
-        launch_fast(0, ncs, stream);
-        if (marker) marker(user, ORB_K_FAST, 0, stream);
-        if ((e = hipStreamWaitEvent(stream, b.side_join, 0)) != hipSuccess) return e;
-        if (marker) marker(user, ORB_K_FAST, 1, stream);
-        launch_fast(ncs, g.ncells - ncs, stream);
-        if (marker) marker(user, ORB_K_FAST, 0, stream);
-    } else {
-        if (marker) marker(user, ORB_K_FAST, 1, stream);
-        launch_fast(0, g.ncells, stream);
-        if (marker) marker(user, ORB_K_FAST, 0, stream);
+    for (int l = 1; l < g.nlevels; l++) {
+        // 32-row tiles where the level's source spans fit the LDS tile, else 16-row tiles, else the
+        // untiled kernel (large scale factors): chosen per level from the geometry (LevelGeom::rs_tiled)
+        const int t = g.L[l].rs_tiled;
+        const ResizeCoef* cf = b.d_rcoef + b.rcoef_off[l];
+        if (t & 3) {
+            const int th = (t & 2) ? 32 : 16;
+            const dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
+            if (th == 32)
+                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames, frame_pitch,
+                                   row_stride, b.d_pyr);
+            else
+                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames, frame_pitch,
+                                   row_stride, b.d_pyr);
+        } else {
+            hipLaunchKernelGGL(k_resize, dim3(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes), dim3(256), 0, stream,
+                               b.d_geom, cf, l, d_frames, frame_pitch, row_stride, b.d_pyr);
+        }
     }
+    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
+    if (marker) marker(user, ORB_K_FAST, 1, stream);
+    {   // one-wave workgroups, two (frame, cell) items per wave (a workgroup's LDS is held until its
+        // slowest wave ends, so single waves waste the least of a CU on uneven cells)
+        const int items = g.ncells * nframes;
+        auto kern = g.fast_compact ? k_fast_wave<56, 40> : k_fast_wave<kFastTilePitch, 64>;
+        hipLaunchKernelGGL(kern, dim3(cdiv(items, 2)), dim3(64), (size_t)g.fast_wave_bytes, stream, b.d_geom, b.d_cells,
+                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, 0, g.ncells,
+                           b.d_stamps, b.zero_err ? b.d_err : nullptr);
+    }
+    if (marker) marker(user, ORB_K_FAST, 0, stream);
     if (marker) marker(user, ORB_K_OCTREE, 1, stream);
     {
         const int lk = octree_lds_keys(g.node_cap);
@@ -1953,16 +1600,11 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     }
     if (marker) marker(user, ORB_K_OCTREE, 0, stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
-    {   // b.desc_wpb keypoint wavefronts per workgroup
+    {
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
-        const int wpb = b.desc_wpb;
-        auto kern = b.desc_npw >= 2 ? (b.desc_sampled ? k_describe<4, true, 2> : k_describe<4, false, 2>)
-                    : b.desc_sampled ? (wpb == 1 ? k_describe<1, true, 1> : wpb == 2 ? k_describe<2, true, 1> : k_describe<4, true, 1>)
-                                     : (wpb == 1 ? k_describe<1, false, 1> : wpb == 2 ? k_describe<2, false, 1> : k_describe<4, false, 1>);
-        const int per = (b.desc_npw >= 2 ? 4 : wpb) * (b.desc_npw >= 2 ? 2 : 1);
-        hipLaunchKernelGGL(kern, dim3(cdiv(g.nkpcap, per), nframes), dim3(64 * (b.desc_npw >= 2 ? 4 : wpb)), 0, stream, b.d_geom, d_frames,
-                           frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
-                           b.desc_remap, dst);
+        hipLaunchKernelGGL(k_describe, dim3(cdiv(g.nkpcap, kDescWaves * kDescSlotsPerWave), nframes), dim3(64 * kDescWaves),
+                           0, stream, b.d_geom, d_frames, frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount,
+                           d_kps, d_desc, d_counts, kp_cap, dst);
     }
     if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);
     return hipGetLastError();

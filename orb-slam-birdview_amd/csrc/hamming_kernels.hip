@@ -92,50 +92,10 @@ __global__ __launch_bounds__(256) void k_topk(const uint8_t* __restrict__ q, int
     if (lane == 0 && out_nvalid) out_nvalid[qi] = nvalid;
 }
 
-/* Batched all-pairs top-2 over many (query set, train set) pairs in one launch.  Lane = query, one
- * wavefront = 64 queries x one train slice; the train descriptors of the slice are wave-uniform and
- * read through the scalar cache (s_load), so the inner loop is 8 v_xor + 8 v_bcnt (accumulating)
- * and a 3-op top-2 update on keys dist << 16 | train index: min keeps the first index on ties, and
- * second = min(second, max(best, key)) is the second-smallest key.  Slices are merged by
- * k_top2b_merge (keys compose the same way).  Counts may be read on the device (an extraction
- * batch's d_counts), so a whole batch of frame pairs needs no host round trip. */
-__global__ __launch_bounds__(256) void k_top2_batch(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
-                                                    int* __restrict__ idx_o, int* __restrict__ second_o) {
-    const int p = blockIdx.z, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
-    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
-    const int qw = (blockIdx.x * 4 + wv) * 64;
-    if (qw >= nq) return;   // whole wave (no block barriers below)
-    const int qi = qw + lane;
-    const int t0 = blockIdx.y * a.slice, t1 = min(nt, t0 + a.slice);
-    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
-    if (qi < nq) {
-        const uint4* qp = reinterpret_cast<const uint4*>(a.q + ((long long)fr.x * a.q_stride + qi) * 32);
-        qa = qp[0];
-        qb = qp[1];
-    }
-    const uint4* __restrict__ T = reinterpret_cast<const uint4*>(a.t + (long long)fr.y * a.t_stride * 32);
-    unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-#pragma unroll 4
-    for (int j = t0; j < t1; j++) {
-        const uint4 x = T[2 * j], y = T[2 * j + 1];
-        const unsigned d = __popc(qa.x ^ x.x) + __popc(qa.y ^ x.y) + __popc(qa.z ^ x.z) + __popc(qa.w ^ x.w) +
-            __popc(qb.x ^ y.x) + __popc(qb.y ^ y.y) + __popc(qb.z ^ y.z) + __popc(qb.w ^ y.w);
-        const unsigned key = (d << 16) | (unsigned)j;
-        s2 = min(s2, max(b, key));
-        b = min(b, key);
-    }
-    if (qi >= nq) return;
-    const long long o = (long long)p * a.out_stride + qi;
-    if (gridDim.y == 1) {
-        best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
-        idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
-        second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
-    } else {
-        part[((long long)p * gridDim.y + blockIdx.y) * a.out_stride + qi] = make_uint2(b, s2);
-    }
-}
-
+/* Slices of one (query set, train set) pair's top-2 (k_top2_mfma with gridDim.y > 1) are merged here:
+ * keys dist << 16 | train index compose by min (first index on ties) and second = the second-smallest
+ * key.  Counts may be read on the device (an extraction batch's d_counts), so a whole batch of frame
+ * pairs needs no host round trip. */
 __global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, const uint2* __restrict__ part,
                                                      int* __restrict__ best_o, int* __restrict__ idx_o,
                                                      int* __restrict__ second_o) {
@@ -164,7 +124,7 @@ __global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, c
  * double-buffered; rows padded to 272 bytes so the 16-byte fragment reads are conflict-free).  The
  * accumulator puts trains on the registers and queries on the lanes (row = (r&3) + 8(r>>2) + 4(lane>>5),
  * column = lane & 31), so the top-2 update is lane-local; the two lane halves are merged at the end.
- * Keys, tie order and outputs are those of k_top2_batch. */
+ * Keys: dist << 16 | train index, so min keeps the first index on ties (SearchByBoW's strict `<`). */
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 constexpr int kMfTr = 32;      // trains per tile (MFMA rows)
@@ -294,25 +254,13 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
     const int ns = top2_batch_slices(npairs, max_nq, max_nt);   // the partial buffer is sized for this many
-    static const bool mfma = [] {
-        const char* e = std::getenv("ORBGPU_TOP2_MFMA");
-        return !(e && e[0] == '0');
-    }();
-    int nsu;
-    if (mfma) {   // matrix-core form: >= 2048 workgroups, slices of whole 32-train tiles
-        const int qb = (max_nq + kMfQ - 1) / kMfQ;
-        int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
-        want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
-        a.slice = ((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr;
-        nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
-        hipLaunchKernelGGL(k_top2_mfma, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
-                           d_second);
-    } else {
-        a.slice = std::max(1, (max_nt + ns - 1) / ns);
-        nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
-        hipLaunchKernelGGL(k_top2_batch, dim3((max_nq + 255) / 256, nsu, npairs), dim3(256), 0, stream, a, d_part,
-                           d_best, d_best_idx, d_second);
-    }
+    // matrix-core form: >= 2048 workgroups, slices of whole 32-train tiles
+    const int qb = (max_nq + kMfQ - 1) / kMfQ;
+    int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
+    want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
+    a.slice = ((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr;
+    const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
+    hipLaunchKernelGGL(k_top2_mfma, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx, d_second);
     if (nsu > 1)
         hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,
                            d_best, d_best_idx, d_second);
@@ -342,10 +290,12 @@ __global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict
     const orb_keypoint kp1 = kps1[idx1];
     const bool st1 = ur1[idx1] >= 0;
     const float* F = tp.F;
-    const float la = kp1.x * F[0] + kp1.y * F[3] + F[6];
-    const float lb = kp1.x * F[1] + kp1.y * F[4] + F[7];
-    const float lc = kp1.x * F[2] + kp1.y * F[5] + F[8];
-    const float den = la * la + lb * lb;
+    // CheckDistEpipolarLine's float expressions with the contractions the reference's -O3 -march=native
+    // build applies (tools/ref_flags_probe.cpp fixes each form)
+    const float la = __builtin_fmaf(kp1.x, F[0], kp1.y * F[3]) + F[6];
+    const float lb = __builtin_fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
+    const float lc = __builtin_fmaf(kp1.y, F[5], kp1.x * F[2]) + F[8];
+    const float den = __builtin_fmaf(la, la, lb * lb);
     unsigned long long bestKey = ~0ull;
     const int c0 = ranges[it].x, c1 = ranges[it].y;
     for (int pos = c0 + lane; pos < c1; pos += 64) {
@@ -359,10 +309,10 @@ __global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict
         const orb_keypoint kp2 = kps2[idx2];
         if (!st1 && !st2) {
             const float dex = tp.ex - kp2.x, dey = tp.ey - kp2.y;
-            if (dex * dex + dey * dey < 100 * tp.scale2[kp2.octave]) continue;
+            if (__builtin_fmaf(dex, dex, dey * dey) < 100 * tp.scale2[kp2.octave]) continue;
         }
         if (den == 0) continue;
-        const float num = la * kp2.x + lb * kp2.y + lc;
+        const float num = __builtin_fmaf(lb, kp2.y, la * kp2.x) + lc;
         const float dsqr = num * num / den;
         if (!((double)dsqr < 3.84 * (double)tp.sigma2[kp2.octave])) continue;
         const unsigned long long key = ((unsigned long long)dist << 32) | (unsigned)(0x7FFFFFFF - (pos - c0));

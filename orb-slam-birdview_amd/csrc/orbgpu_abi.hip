@@ -179,7 +179,7 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
     nc = (nc + 63) & ~63;
     g.node_cap = nc;
     fast_wave_layout(g);
-    if (octree_lds_bytes(nc) > 160 * 1024) return ORB_ERR_GEOMETRY;
+    if (g.fast_wave_bytes > 64 * 1024 || octree_lds_bytes(nc) > 160 * 1024) return ORB_ERR_GEOMETRY;
     return ORB_OK;
 }
 
@@ -264,21 +264,7 @@ ExtractBuffers Ctx::buffers() const {
     b.d_lvlCount = d_lvlCount;
     b.d_err = d_err;
     b.zero_err = 1;
-    b.fast_remap = fast_remap ? 1 : 0;
-    b.resize_direct = resize_direct ? 1 : 0;
-    b.resize_th = resize_th;
-    b.fast_block = fast_block ? 1 : 0;
-    b.fast_wpb = fast_wpb;
-    b.desc_wpb = desc_wpb;
-    b.desc_npw = desc_npw;
-    b.desc_remap = desc_remap ? 1 : 0;
-    b.desc_sampled = desc_sampled ? 1 : 0;
-    b.fast_px = fast_px;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
-    b.side = side_stream;
-    b.resize_split = resize_split;
-    b.side_fork = ev_side_fork;
-    b.side_join = ev_side_join;
     return b;
 }
 
@@ -295,17 +281,15 @@ void Ctx::marker(void* user, int id, int begin, hipStream_t s) {
 int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
                      uint8_t* d_desc, int* d_counts, int kp_cap) {
     hipError_t e;
-    const int ns = std::min(std::min(nsub, kMaxSubStreams), nframes);
-    if (ns <= 1 && use_graph && !prof_on && !fast_stamps && resize_split == 0) {
-        // HIP graph replay: one submission per batch instead of 11
-        const std::array<uintptr_t, 40> key = {
+    if (use_graph && !prof_on && !fast_stamps) {
+        // HIP graph replay: one submission per batch instead of 10 launches; captured on the first batch
+        // with a given set of buffers / arguments and re-instantiated when any of them changes
+        const std::array<uintptr_t, 24> key = {
             (uintptr_t)d_frames, (uintptr_t)nframes, (uintptr_t)frame_pitch, (uintptr_t)row_stride, (uintptr_t)d_kps,
             (uintptr_t)d_desc, (uintptr_t)d_counts, (uintptr_t)kp_cap, (uintptr_t)geom.W, (uintptr_t)geom.H,
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
-            (uintptr_t)d_lvlCount, (uintptr_t)d_err, (uintptr_t)resize_th, (uintptr_t)resize_direct,
-            (uintptr_t)fast_block, (uintptr_t)fast_wpb, (uintptr_t)desc_wpb, (uintptr_t)desc_npw, (uintptr_t)desc_sampled, (uintptr_t)fast_px, (uintptr_t)fast_remap, (uintptr_t)desc_remap,
-            (uintptr_t)stream};
+            (uintptr_t)d_lvlCount, (uintptr_t)d_err, (uintptr_t)stream, 0};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -331,39 +315,10 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             gkey = key;
         }
         if ((e = hipGraphLaunch(gexec, stream)) != hipSuccess) return set_error("graph launch", e), ORB_ERR_HIP;
-    } else {
-    if (ns <= 1) {
+    } else {   // ORBGPU_GRAPH=0, per-kernel profiling or stamps: direct launches (same kernels, same order)
         e = launch_extract(geom, buffers(), d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
                            stream, &Ctx::marker, this);
         if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
-    } else {
-        // fork: sub-batch s (frames [f0, f0+nf)) runs on sub[s] with its own frame slots; join on `stream`
-        if ((e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess) return set_error("memset", e), ORB_ERR_HIP;
-        if ((e = hipEventRecord(ev_fork, stream)) != hipSuccess) return set_error("event record", e), ORB_ERR_HIP;
-        const Geom& g = geom;
-        const size_t nl = g.nlevels;
-        for (int si = 0; si < ns; si++) {
-            const int f0 = (int)((long long)nframes * si / ns), f1 = (int)((long long)nframes * (si + 1) / ns);
-            if ((e = hipStreamWaitEvent(sub[si], ev_fork, 0)) != hipSuccess) return set_error("wait", e), ORB_ERR_HIP;
-            ExtractBuffers b = buffers();
-            b.side = nullptr;
-            b.zero_err = 0;
-            b.d_pyr += (size_t)f0 * g.pyr_bytes;
-            b.d_cands += (size_t)f0 * g.ncand;
-            b.d_cellCount += (size_t)f0 * g.ncells;
-            b.d_keys += (size_t)f0 * nl * g.max_level_cand;
-            b.d_knode += (size_t)f0 * nl * g.max_level_cand;
-            b.d_lvlKps += (size_t)f0 * g.nkpcap;
-            b.d_lvlCount += (size_t)f0 * nl;
-            e = launch_extract(g, b, d_frames + (size_t)f0 * frame_pitch, frame_pitch, row_stride, f1 - f0,
-                               d_kps + (size_t)f0 * kp_cap, d_desc + (size_t)f0 * kp_cap * 32, d_counts + f0, kp_cap,
-                               sub[si], &Ctx::marker, this);
-            if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
-            if ((e = hipEventRecord(ev_join[si], sub[si])) != hipSuccess ||
-                (e = hipStreamWaitEvent(stream, ev_join[si], 0)) != hipSuccess)
-                return set_error("join", e), ORB_ERR_HIP;
-        }
-    }
     }
     last_frames = d_frames;
     last_frame_pitch = frame_pitch;
@@ -425,41 +380,13 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
         c->num_cu < 1)
         c->num_cu = 256;
-    if (const char* e = std::getenv("ORBGPU_FAST_REMAP")) c->fast_remap = e[0] == '1';
-    if (const char* e = std::getenv("ORBGPU_RESIZE_DIRECT")) c->resize_direct = e[0] == '1';
-    if (const char* e = std::getenv("ORBGPU_RESIZE_TH")) c->resize_th = std::atoi(e);
-    if (const char* e = std::getenv("ORBGPU_FAST_BLOCK")) c->fast_block = e[0] == '1';
-    if (const char* e = std::getenv("ORBGPU_FAST_WPB")) {
-        const int v = std::atoi(e);
-        c->fast_wpb = v <= 1 ? 1 : v <= 2 ? 2 : 4;
-    }
-    if (const char* e = std::getenv("ORBGPU_DESC_REMAP")) c->desc_remap = e[0] == '1';
-    if (const char* e = std::getenv("ORBGPU_DESC_NPW")) c->desc_npw = std::atoi(e) >= 2 ? 2 : 1;
-    if (const char* e = std::getenv("ORBGPU_DESC_SAMPLED")) c->desc_sampled = e[0] == '1';
-    if (const char* e = std::getenv("ORBGPU_FAST_PX")) c->fast_px = std::atoi(e) == 8 ? 8 : 4;
-    if (const char* e = std::getenv("ORBGPU_DESC_WPB")) {
-        const int v = std::atoi(e);
-        c->desc_wpb = v <= 1 ? 1 : v <= 2 ? 2 : 4;
-    }
+    // diagnostics only (tests/test_gpu_extract.py checks both leave the results unchanged):
+    // ORBGPU_FAST_STAMPS=1 records kernel phase timestamps, ORBGPU_GRAPH=0 launches without graph replay
     if (const char* e = std::getenv("ORBGPU_FAST_STAMPS")) c->fast_stamps = e[0] == '1';
+    if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);
-        return fail(ORB_ERR_HIP);
-    }
-    if (const char* ev = std::getenv("ORBGPU_STREAMS")) c->nsub = std::min(std::max(std::atoi(ev), 1), kMaxSubStreams);
-    bool sub_ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; i < kMaxSubStreams && sub_ok; i++)
-        sub_ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
-                 hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) == hipSuccess;
-    if (const char* ev = std::getenv("ORBGPU_RESIZE_SPLIT")) c->resize_split = std::atoi(ev);
-    if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
-    sub_ok = sub_ok && hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_side_fork, hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_side_join, hipEventDisableTiming) == hipSuccess;
-    if (!sub_ok) {
-        orb_destroy(reinterpret_cast<orb_ctx*>(c));
-        set_error("hipStreamCreate (sub-batch streams)", hipErrorOutOfMemory);
         return fail(ORB_ERR_HIP);
     }
     compute_tables(c);
@@ -495,16 +422,8 @@ void orb_destroy(orb_ctx* h) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
-    for (int i = 0; i < kMaxSubStreams; i++) {
-        if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
-        if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
-    }
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
-    if (c->ev_side_fork) (void)hipEventDestroy(c->ev_side_fork);
-    if (c->ev_side_join) (void)hipEventDestroy(c->ev_side_join);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -671,6 +590,23 @@ int orb_debug_fast_stamps(orb_ctx* h, uint64_t* out, int cap) {
     const int n = std::min((int)c->stamps_cap, cap);
     hipError_t e = hipMemcpy(out, c->d_stamps, (size_t)n * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? n : ORB_ERR_HIP;
+}
+
+int orb_debug_sincosf(orb_ctx* h, const float* x, int n, float* s, float* c) {
+    Ctx* ctx = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(ctx);
+    if (n < 0 || (n > 0 && (!x || !s || !c))) return set_error("orb_debug_sincosf: bad arguments", hipSuccess), ORB_ERR_ARG;
+    if (n == 0) return ORB_OK;
+    float* d = nullptr;
+    hipError_t e = hipMalloc((void**)&d, (size_t)n * 12);
+    if (e != hipSuccess) return set_error("hipMalloc", e), ORB_ERR_NOMEM;
+    if ((e = hipMemcpyAsync(d, x, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream)) == hipSuccess &&
+        (e = launch_debug_sincosf(d, n, d + n, d + 2 * (size_t)n, ctx->stream)) == hipSuccess &&
+        (e = hipMemcpyAsync(s, d + n, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream)) == hipSuccess &&
+        (e = hipMemcpyAsync(c, d + 2 * (size_t)n, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream)) == hipSuccess)
+        e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d);
+    return e == hipSuccess ? ORB_OK : (set_error("orb_debug_sincosf", e), ORB_ERR_HIP);
 }
 
 int orb_debug_level_image(orb_ctx* h, int frame, int level, uint8_t* out, int* w, int* hgt) {

@@ -19,28 +19,10 @@ struct Ctx {
     orb_params p{};
     int device = 0;
     int num_cu = 256;
-    bool fast_remap = true;   // ORBGPU_FAST_REMAP=0 disables the XCD-contiguous cell remap (A/B switch)
-    bool resize_direct = false;   // ORBGPU_RESIZE_DIRECT=1 forces the untiled resize kernel (A/B switch)
-    int resize_th = 32;           // rows per resize tile (ORBGPU_RESIZE_TH = 16 | 32 | 64; 32 measured fastest)
-    bool fast_block = false;      // ORBGPU_FAST_BLOCK=1 uses the block-per-cell FAST kernel (A/B switch)
-    bool desc_sampled = true;     // blur column pass only at the 512 BRIEF samples (ORBGPU_DESC_SAMPLED=0: whole 37x37 patch)
-    int desc_npw = 2;             // keypoints per describe wave, second window prefetched (ORBGPU_DESC_NPW=1|2; 2: -2 %)
-    bool desc_remap = false;      // ORBGPU_DESC_REMAP=1: each XCD describes a contiguous range of frames (its L2 holds their pyramids)
-    int desc_wpb = 4;             // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
-    int fast_px = 8;              // k_fast_wave prefilter pixels per lane (ORBGPU_FAST_PX = 4 | 8; 8: -2 % fast)
-    int fast_wpb = 1;             // k_fast_wave wavefronts per workgroup (ORBGPU_FAST_WPB = 1 | 2 | 4; 1 measured fastest)
-    bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: k_fast_wave records phase timestamps (diagnostic)
+    bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: the kernels record phase timestamps (diagnostic)
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
-    // a batch of frames is split over `nsub` streams so that one sub-batch's low-occupancy phases
-    // (short pyramid levels, the per-level octree) overlap another's kernels (ORBGPU_STREAMS, 1..4)
-    int nsub = 1;   // measured: 2 and 4 are slower at B = 64 (every phase already fills the GPU)
-    hipStream_t sub[kMaxSubStreams]{};
-    hipEvent_t ev_fork = nullptr, ev_join[kMaxSubStreams]{};
-    int resize_split = 0;          // ORBGPU_RESIZE_SPLIT=s: levels s+1.. resized on side_stream during FAST of levels 0..s
-    hipStream_t side_stream = nullptr;
-    hipEvent_t ev_side_fork = nullptr, ev_side_join = nullptr;
 
     // ORBextractor tables (ORBextractor.cc:410-470)
     float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},
@@ -114,7 +96,7 @@ struct Ctx {
     unsigned geom_serial = 0;
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    std::array<uintptr_t, 40> gkey{};
+    std::array<uintptr_t, 24> gkey{};
     hipEvent_t prof_open[ORB_K_COUNT]{};
     std::vector<ProfPair> prof_pairs;
 

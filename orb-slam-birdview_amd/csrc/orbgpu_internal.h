@@ -98,27 +98,12 @@ struct ExtractBuffers {
     uint32_t* d_lvlKps;            // nframes * nkpcap
     int* d_lvlCount;               // nframes * nlevels
     int* d_err;                    // 1 int: internal overflow flag
-    int zero_err;                  // FAST zeroes d_err (0: the caller did, e.g. before a sub-batch fork)
-    int fast_remap;                // XCD-contiguous block->cell remap in k_fast (speed only)
-    int resize_direct;             // force the untiled k_resize (A/B switch, ORBGPU_RESIZE_DIRECT=1)
-    int resize_th;                 // output rows per k_resize_tiled tile: 16, 32 or 64 (ORBGPU_RESIZE_TH)
-    int fast_block;                // use the block-per-cell k_fast (A/B switch, ORBGPU_FAST_BLOCK=1)
-    int fast_wpb;                  // k_fast_wave wavefronts per workgroup (ORBGPU_FAST_WPB = 1 | 2 | 4)
-    int desc_wpb;
-    int desc_npw;                  // keypoint slots per k_describe wavefront (ORBGPU_DESC_NPW = 1 | 2)
-    int desc_remap;                // k_describe workgroups dealt to XCDs as contiguous frame ranges (ORBGPU_DESC_REMAP)
-    int desc_sampled;              // k_describe: column pass only at the BRIEF samples (ORBGPU_DESC_SAMPLED)
-    int fast_px;                   // k_fast_wave prefilter pixels per lane (ORBGPU_FAST_PX = 4 | 8)                  // k_describe wavefronts per workgroup (ORBGPU_DESC_WPB = 1 | 2 | 4)
-    unsigned long long* d_stamps;  // k_fast_wave phase timestamps, 8 per (frame, cell) (ORBGPU_FAST_STAMPS=1)
-    // Side stream for the pyramid tail split: levels resize_split+1.. are resized there while FAST runs
-    // on the cells of levels 0..resize_split (0 = no split; ORBGPU_RESIZE_SPLIT)
-    hipStream_t side;
-    hipEvent_t side_fork, side_join;
-    int resize_split;
+    int zero_err;                  // FAST zeroes d_err (0: the caller did)
+    unsigned long long* d_stamps;  // phase timestamps (ORBGPU_FAST_STAMPS=1 diagnostic): 8 per (frame, cell),
+                                   // 32 per (frame, level), 8 per keypoint slot
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin, hipStream_t stream);
-constexpr int kMaxSubStreams = 4;   // a batch is split over up to this many streams (kernel overlap)
 
 hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
@@ -178,6 +163,9 @@ size_t stereo_scratch_ints(const Geom& g, int npairs, long long out_stride);
 hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L, const StereoSide& R, int npairs,
                          float mb, float mbf, float* d_uright, float* d_depth, int* d_scratch, long long out_stride,
                          int* d_nmatched, hipStream_t stream);
+
+// glibc sinf/cosf (glibc_trig.h) over n angles, for the trig pin test (orb_debug_sincosf)
+hipError_t launch_debug_sincosf(const float* d_x, int n, float* d_s, float* d_c, hipStream_t stream);
 
 // OpenCV 3.2 resize INTER_LINEAR coefficients for sw -> dw (orbgpu_abi.hip), appended to `out`
 void resize_coefs(int sw, int dw, std::vector<ResizeCoef>& out, bool vertical);

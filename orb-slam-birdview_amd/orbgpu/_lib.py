@@ -58,6 +58,7 @@ SIGNATURES = {
     "orb_debug_level_keypoints": (ci, [vp, ci, ci, vp, ci]),
     "orb_debug_level_image": (ci, [vp, ci, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci)]),
     "orb_debug_fast_stamps": (ci, [vp, vp, ci]),
+    "orb_debug_sincosf": (ci, [vp, vp, ci, vp, vp]),
     "orb_descriptor_distance": (ci, [vp, vp]),
     "orb_hamming_topk": (ci, [vp, vp, ci, vp, ci, vp, vp, vp, ci, vp, vp, vp]),
     "orb_hamming_top2_device": (ci, [vp, vp, ci, vp, ci, vp, vp, vp]),

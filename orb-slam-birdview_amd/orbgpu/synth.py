@@ -118,6 +118,15 @@ def synth_batch(w, h, n, first=0, kind="scene"):
     return np.stack([synth_frame(w, h, first + i, kind) for i in range(n)])
 
 
+def bench_frames(w, h, count, first=0, distinct=64):
+    """The bench's batch (bench.py): `distinct` seeded frames first .. first+distinct-1 (the generator
+    costs ~0.1 s per 1280x720 frame), then circularly shifted copies by (7k, 13k) px, k = 1, 2, ..., so
+    every frame of the batch is a distinct image that is fully processed."""
+    base = synth_batch(w, h, min(count, distinct), first=first)
+    reps = [base] + [np.roll(base, (7 * k, 13 * k), axis=(1, 2)) for k in range(1, (count + len(base) - 1) // len(base))]
+    return np.ascontiguousarray(np.concatenate(reps)[:count])
+
+
 def write_synth_vocab(path, k=10, L=3, seed=0, scoring=0, weighting=0, stop_frac=0.05):
     """Write a synthetic DBoW2 ORB vocabulary in ORBvoc.bin's binary format
     (TemplatedVocabulary::saveToBinaryFile, TemplatedVocabulary.h:1512-1531): a complete k-ary tree of

@@ -198,3 +198,65 @@ def test_two_contexts_interleaved(orbgpu_mod, oracle_mod):
     ol3(left)
     assert np.array_equal(gl.mvImagePyramid[3], ol3.level(3))
     assert np.array_equal(gr.mvImagePyramid[3], o.level(3))
+
+
+def test_device_sincosf_matches_glibc_restatement(orbgpu_mod, oracle_mod):
+    """csrc/glibc_trig.h on the GPU == oracle/glibc_sincosf.inc (== libm, tests/test_trig_pin.py) on a
+    strided sweep of every float in [0, 2*pi] plus every float degree value the BRIEF path can form."""
+    from orbgpu import _lib
+    u = np.arange(0, 0x40C90FDB, 97, dtype=np.uint32)
+    x = np.concatenate([u.view(np.float32),
+                        (np.arange(0, 360 * 4096, dtype=np.float32) / np.float32(4096)) * np.float32(np.pi / 180)])
+    x = np.ascontiguousarray(x, np.float32)
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    s, c = np.zeros_like(x), np.zeros_like(x)
+    assert _lib.lib().orb_debug_sincosf(g.h, x.ctypes.data, len(x), s.ctypes.data, c.ctypes.data) == 0
+    os_, oc = oracle_mod.sincosf(x)
+    assert np.array_equal(s.view(np.uint32), os_.view(np.uint32))
+    assert np.array_equal(c.view(np.uint32), oc.view(np.uint32))
+
+
+@pytest.mark.parametrize("env", [{"ORBGPU_GRAPH": "0"}, {"ORBGPU_FAST_STAMPS": "1"}])
+def test_diagnostic_switches_leave_results_unchanged(orbgpu_mod, oracle_mod, monkeypatch, env):
+    """The two environment switches liborbgpu still reads are diagnostics: direct launches instead of
+    graph replay, and kernel phase timestamps.  Both must give the default path's bytes."""
+    from orbgpu.synth import synth_batch
+    frames = synth_batch(1280, 720, 3, first=50)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    b = orbgpu_mod.BatchExtractor(2000, 1280, 720, 3)
+    b.upload(frames)
+    b.launch()
+    b.sync()
+    o = oracle_mod.OracleExtractor(2000)
+    for f in range(3):
+        gk, gd = b.results(f)
+        ok, od = o(frames[f])
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), (env, f)
+    b.close()
+
+
+def test_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
+    """The exact configuration bench.py times: C3, B = 256 frames per batch, two extractor contexts
+    (own stream and buffers) launched alternately with several batches in flight, through the hipGraph
+    path.  Frames {0, 63, 64, 127, 255} of both contexts' last batch vs the oracle, byte for byte."""
+    from orbgpu.synth import bench_frames
+    B = 256
+    frames = bench_frames(1280, 720, B, first=0)
+    exs = [orbgpu_mod.BatchExtractor(2000, 1280, 720, B) for _ in range(2)]
+    for e in exs:
+        e.upload(frames)
+    for step in range(5):   # bench: warm-up, then steps alternate over the contexts without syncing
+        exs[step % 2].launch()
+    for e in exs:
+        e.sync()
+    o = oracle_mod.OracleExtractor(2000)
+    ref = {f: o(frames[f]) for f in (0, 63, 64, 127, 255)}
+    for e in exs:
+        counts = e.counts()
+        for f, (ok, od) in ref.items():
+            gk, gd = e.results(f)
+            assert counts[f] == len(ok)
+            assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
+    for e in exs:
+        e.close()
