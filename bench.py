@@ -3,27 +3,42 @@
 "ORB features/sec per GPU (1280x720, 2000 kp, 8 levels) + Hamming matches/sec".
 
 One step = one batched pass of the extraction hot path (pyramid -> per-cell FAST+NMS ->
-DistributeOctTree -> IC angle + Gaussian + rBRIEF) over `--batch` synthetic 1280x720 frames already
-resident in HBM, on each GPU.  Frames shard across GPUs (one process per GPU, no data-path
-collective: scaling "weak"); value = keypoints produced by all ranks / max-over-ranks time.
+DistributeOctTree -> IC angle + Gaussian + rBRIEF) over `--batch` synthetic frames already resident in
+HBM, on each GPU.  Frames shard across GPUs (one process per GPU, no data-path collective); value =
+keypoints produced by all ranks / max-over-ranks time of the K timed steps.
 
-Also reported on the same line:
-  roofline      dominant kernel's algorithmic bytes per launch / its HIP-event-timed duration
-                (events on liborbgpu's own stream, recorded inside the timed region)
-  cpu_baseline  the oracle restatement of ORBextractor (oracle/, kind "port") on the box's host
-                cores, rank 0 at N=1 only, bounded sample
-  hamming       all-pairs top-2 Hamming between consecutive frames' descriptors (SearchByBoW's
-                brute-force inner loop), matches/s = distance evaluations per second
+Configs (BASELINE.json):
+  c3 (default)  1280x720, 2000 features, B = 256 frames per GPU per step, weak scaling
+  c2            640x480, 1000 features, B = 256 per GPU, weak scaling
+  c5            BASELINE config 5: ONE 8-frame batch of 1280x720 @ 4000 features per step, sharded over the
+                N GPUs (8/N frames each), strong scaling
+  c4 is a leg of every run (`c4_frame`): left / right / bird 1280x720 streams, each on its own GPU when
+  the process sees >= 3 devices (stereo pyramid + descriptors moved over xGMI), else all on one.
 
-Usage: python bench.py [--gpus N --steps K --warmup W --batch B --config c3|c2|c5 --no-cpu]
+Multi-GPU: `python bench.py --gpus N` spawns N ranks itself (before any GPU call) when WORLD_SIZE is
+unset; under torch.distributed.run the ranks come from the environment and must number --gpus.
+
+Also on the same line:
+  roofline      dominant kernel's algorithmic bytes per launch / its HIP-event-timed duration (events on
+                liborbgpu's own stream, a separate pass of the same steps); PMC traffic from profiles/
+  cpu_baseline  the oracle restatement of ORBextractor (oracle/, kind "port") rebuilt -march=native on
+                the box, rank 0 at N=1 only: single thread (5 warm-up + 50 timed frames, median, per-stage
+                times) and frame-parallel on every CPU this process may use
+  hamming       all-pairs top-2 Hamming between consecutive frames' descriptors on the matrix cores (the
+                brute-force SearchByBoW inner loop), matches/s = distance evaluations per second, its I8
+                MFMA fraction, and the restated CPU loops beside it
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B --config c3|c2|c5 --no-cpu --only-extract]
 """
 import argparse
-import resource
 import json
 import os
 import platform
+import resource
+import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -31,11 +46,15 @@ sys.path.insert(0, os.path.join(ROOT, "orb-slam-birdview_amd"))
 
 METRIC = "ORB features/sec per GPU (1280×720, 2000 kp, 8 levels) + Hamming matches/sec"
 CONFIGS = {   # BASELINE.json configs; C3 is the headline single-GPU workload
-    "c2": dict(w=640, h=480, nfeatures=1000, name="C2 640x480 synthetic, 1000 features, 8 levels"),
-    "c3": dict(w=1280, h=720, nfeatures=2000, name="C3 1280x720 KITTI-style synthetic, 2000 features, 8 levels"),
-    "c5": dict(w=1280, h=720, nfeatures=4000, name="C5 1280x720 synthetic, 4000 features, 8 levels"),
+    "c2": dict(w=640, h=480, nfeatures=1000, batch=256, scaling="weak",
+               name="C2 640x480 synthetic, 1000 features, 8 levels"),
+    "c3": dict(w=1280, h=720, nfeatures=2000, batch=256, scaling="weak",
+               name="C3 1280x720 KITTI-style synthetic, 2000 features, 8 levels"),
+    "c5": dict(w=1280, h=720, nfeatures=4000, global_batch=8, scaling="strong",
+               name="C5 8-frame batch of 1280x720 synthetic, 4000 features each, sharded over the GPUs"),
 }
-PEAK_HBM_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+PEAK_I8_OPS = 5.0e15             # MI355X_MICROARCH.md: I8 MFMA = 2x the ~2.5 PF dense BF16 rate per clock
 KNAMES = ["resize", "fast", "octree", "describe", "hamming", "stereo"]   # ORB_K_* order
 
 
@@ -73,9 +92,41 @@ def reduce_max_sum(dist, tmax, vsum):
     return float(t.item()), float(v.item())
 
 
+def gather(dist, obj):
+    if dist is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def frame_range(rank, batch):
     """Synthetic frame indices of a rank: each GPU extracts its own distinct frames."""
     return rank * batch, batch
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(nranks, argv):
+    """`--gpus N` without a launcher: start N rank processes of this script (one per GPU, env rendezvous on
+    127.0.0.1) before this process touches the GPU, and exit with the first failing rank's status."""
+    port = free_port()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks), LOCAL_WORLD_SIZE=str(nranks),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
 
 
 # ---------------------------------------------------------------- algorithmic bytes
@@ -89,7 +140,7 @@ def level_sizes(w, h, nl=8, sf=1.2):
 
 
 def algorithmic_bytes(w, h, kps_per_frame, cands_per_frame):
-    """Per-frame compulsory bytes by kernel (DESIGN.md §Roofline)."""
+    """Per-frame compulsory bytes by kernel (DESIGN.md §4)."""
     lv = level_sizes(w, h)
     P = [a * b for a, b in lv]
     Ptot = sum(P)
@@ -108,11 +159,8 @@ PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD-32 x 2.4 GHz (MI3
 
 
 def read_pmc(kernel, batch):
-    """(HBM bytes per launch, VALU instructions per launch, source commit) of `kernel` from the
-    committed rocprofv3 PMC summary (tools/pmc.sh -> profiles/pmc_traffic.json), scaled from the
-    summary's frames per launch to `batch` (both are per-frame linear), or Nones."""
-    # ORBGPU_PMC_JSON: a summary measured in the same GPU session (tools/gpu_round.sh runs the PMC passes
-    # before the bench and points here at their report)
+    """(HBM bytes per launch, VALU instructions per launch, source) of `kernel` from the rocprofv3 PMC
+    summary (tools/pmc.sh -> profiles/pmc_traffic.json), scaled to `batch` frames per launch, or Nones."""
     path = os.environ.get("ORBGPU_PMC_JSON") or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -137,26 +185,165 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(cfg, frames_np):
+def cpu_budget():
+    """CPUs this process may run on: its affinity mask, capped by a cgroup CPU quota if one is set
+    (os.cpu_count() shows the whole host on the GPU box)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+_ORACLE = None
+
+
+def oracle_native():
+    """The oracle rebuilt -march=native on this host (the reference's own flag, CMakeLists.txt:10-11), in a
+    temporary directory; falls back to the in-tree x86-64-v3 build if the compile fails."""
+    global _ORACLE
+    if _ORACLE is not None:
+        return _ORACLE
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle   # test infrastructure: used ONLY as the timed CPU baseline here
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"orbgpu_oracle_native_{os.getpid()}", "liborb_oracle.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "MARCH=native", f"OUT={out}"], check=True,
+                       timeout=300, capture_output=True)
+        oracle.use_library(out)
+        oracle.BUILD = "-O3 -march=native -ffp-contract=off (built on this host)"
+    except Exception as e:   # keep the baseline, say which build it is
+        oracle.BUILD = f"-O3 -march=x86-64-v3 (in-tree; native rebuild failed: {type(e).__name__})"
+    oracle.lib()
+    _ORACLE = oracle
+    return oracle
+
+
+def cpu_baseline(cfg, frames_np):
+    import numpy as np
+    oracle = oracle_native()
+    cores, aff, quota = cpu_budget()
     nf = cfg["nfeatures"]
-    n1 = min(8, len(frames_np))
-    oracle.time_extract(frames_np[:2], nf, 1, 1)   # warm-up
-    t1, k1 = oracle.time_extract(frames_np[:n1], nf, nthreads=1, iters=1)
-    iters = max(1, (16 * threads) // len(frames_np))
-    tN, kN = oracle.time_extract(frames_np, nf, nthreads=threads, iters=iters)
-    single = k1 / t1
-    allcore = kN * iters / tN
-    return {"value": round(allcore, 1), "unit": "features/s", "cores": threads, "kind": "port",
-            "single_thread_value": round(single, 1), "single_thread_frames_per_s": round(n1 / t1, 2),
-            "frames_per_s": round(len(frames_np) * iters / tN, 2),
-            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
-            "sample": f"{len(frames_np) * iters} frames ({len(frames_np)} distinct, {cfg['w']}x{cfg['h']}, "
-                      f"{nf} features) frame-parallel on {threads} threads + {n1} frames single-thread; "
-                      f"oracle/orb_oracle.cpp -O3 -march=x86-64-v3 (restated CPU baseline, not OpenCV)"}
+    frames = np.ascontiguousarray(frames_np[:16])
+    fm, stages, kps1 = oracle.bench_single(frames, nf, warmup=5, timed=50)
+    med = float(np.median(fm))
+    single = kps1 / 50 / (med / 1e3)
+    total = max(16 * cores, 256)
+    secs, kpsN = oracle.bench_parallel(frames, nf, cores, 1, total)
+    allcore = kpsN / secs
+    out = {"value": round(allcore, 1), "unit": "features/s", "cores": cores, "kind": "port",
+           "frames_per_s": round(total / secs, 2),
+           "single_thread_value": round(single, 1), "single_thread_median_ms_per_frame": round(med, 3),
+           "single_thread_stage_ms_per_frame": {k: round(v / 50, 3) for k, v in stages.items()},
+           "cpu_model": cpu_model(), "affinity_cpus": aff, "cgroup_quota_cpus": quota, "host_cpus": os.cpu_count(),
+           "build": oracle.BUILD,
+           "sample": f"single thread: 5 warm-up + 50 timed frames (median); frame-parallel: {cores} threads x 1 "
+                     f"warm-up frame, then {total} frames ({len(frames)} distinct {cfg['w']}x{cfg['h']}, {nf} "
+                     f"features); oracle/orb_oracle.cpp (restated CPU baseline, not OpenCV)"}
+    if aff > cores:   # a CPU quota caps this process below the host's CPUs: state the full-host estimate too
+        out["host_estimate_value"] = round(allcore / cores * aff, 1)
+        out["host_estimate_note"] = f"measured {cores}-thread rate scaled to the {aff} CPUs of the affinity mask"
+    return out
+
+
+def hamming_cpu(ex, B, oracle):
+    """Restated DescriptorDistance + SearchByBoW selection (ORBmatcher.cc:159-288, 1647-1663) on the
+    same consecutive-frame pairs, single thread and every usable CPU."""
+    import numpy as np
+    cores, _, _ = cpu_budget()
+    npairs = min(8, B - 1)
+    counts = ex.counts()[:npairs + 1].astype(np.int32)
+    desc = np.zeros((npairs + 1, ex.kp_cap, 32), np.uint8)
+    ang = np.zeros((npairs + 1, ex.kp_cap), np.float32)
+    for f in range(npairs + 1):
+        k, d = ex.results(f)
+        desc[f, :len(d)] = d
+        ang[f, :len(k)] = k["angle"]
+    qf, tf = np.arange(npairs), np.arange(1, npairs + 1)
+    res = {}
+    for mode, name in ((1, "bruteforce_top2"), (0, "search_by_bow_single_node")):
+        s1, ev = oracle.bench_hamming(desc, ang, counts, qf, tf, mode, 1, 1)
+        sN, _ = oracle.bench_hamming(desc, ang, counts, qf, tf, mode, cores, max(1, (2 * cores) // npairs))
+        itN = max(1, (2 * cores) // npairs)
+        res[name] = {"single_thread_matches_per_s": round(ev / s1, 1), "allcore_matches_per_s": round(ev * itN / sN, 1),
+                     "cores": cores}
+    res["note"] = (f"{npairs} consecutive-frame pairs (~{int(counts.mean())} descriptors each); matches/s = nq*nt "
+                   f"distance evaluations per second; SearchByBoW skips already-matched frame features, so its "
+                   f"nominal rate is an upper bound of the work it does; {oracle.BUILD}")
+    return res
+
+
+# ---------------------------------------------------------------- C4: three streams, one GPU each
+def c4_leg(cfg, frames, first, dist, rank, world, local):
+    """Per tracking frame (Frame.cc:124-127, 320-342, 662-836): ORBextractor on the rectified left and right
+    images concurrently (the reference's two std::threads), the birdview cv::ORB stream at the same time,
+    then ComputeStereoMatches on the left GPU and the bird(t) x bird(t-1) all-pairs Hamming top-2 on the
+    bird GPU.  Host images in and results out (the drop-in caller's boundary).  With >= 3 GPUs visible,
+    left / right / bird each get a GPU (rank 0 runs the leg while the other ranks wait)."""
+    import numpy as np
+    import orbgpu
+    from orbgpu.synth import bench_frames, synth_bird_mask, synth_stereo_right
+    ndev = orbgpu.device_count()
+    if world > 1 and rank != 0:
+        barrier(dist)
+        return None
+    devs = (0, 1, 2) if ndev >= 3 else (local, local, local)
+    w, h, nf = 1280, 720, 2000   # BASELINE C4: three 1280x720 streams, 2000 features
+    if frames.shape[1:] != (h, w) or len(frames) < 17:
+        frames = bench_frames(w, h, 17, first=first)
+    exl = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=devs[0])
+    exr = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=devs[1])
+    bo = orbgpu.BirdORB(2000, device=devs[2])
+    mt = orbgpu.ORBmatcher(0.7, True, device=devs[2])
+    nc4 = min(16, len(frames) - 1)
+    lefts = [np.ascontiguousarray(frames[i]) for i in range(nc4 + 1)]
+    rights = [synth_stereo_right(lefts[i], first + i) for i in range(nc4 + 1)]
+    bmask = synth_bird_mask(w, h, first)
+    birds = [np.ascontiguousarray(frames[(i + nc4 // 2) % len(frames)]) for i in range(nc4 + 1)]
+
+    def c4_frame(i, prev_desc):
+        out = {}
+
+        def run(key, fn):
+            out[key] = fn()
+        th = [threading.Thread(target=run, args=("l", lambda: exl(lefts[i]))),
+              threading.Thread(target=run, args=("r", lambda: exr(rights[i]))),
+              threading.Thread(target=run, args=("b", lambda: bo.extract(birds[i], bmask)))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        (kl, dl), (kr, dr), (kb, db) = out["l"], out["r"], out["b"]
+        _u, _d, nst = orbgpu.compute_stereo_matches(exl, exr, kl, dl, kr, dr, 0.54, 0.54 * 721.5)
+        nm = 0
+        if prev_desc is not None and len(db) and len(prev_desc):
+            dist_, _idx, _nv = mt.hamming_topk(db, prev_desc, 2)
+            nm = int((dist_[:, 0] <= 50).sum())
+        return db, len(kl) + len(kr), nst, len(kb), nm
+    prev, _, _, _, _ = c4_frame(0, None)
+    tc0 = time.perf_counter()
+    tot = [0, 0, 0, 0]
+    for i in range(1, nc4 + 1):
+        prev, a, b_, c_, d_ = c4_frame(i, prev)
+        tot = [tot[0] + a, tot[1] + b_, tot[2] + c_, tot[3] + d_]
+    tc1 = time.perf_counter()
+    for o in (exl, exr, bo):
+        o.close()
+    if world > 1:
+        barrier(dist)
+    return {"ms_per_frame": round((tc1 - tc0) / nc4 * 1e3, 3), "frames_per_s": round(nc4 / (tc1 - tc0), 1),
+            "devices": {"left": devs[0], "right": devs[1], "bird": devs[2]},
+            "stereo_keypoints_per_frame": tot[0] // nc4, "left_with_depth_per_frame": tot[1] // nc4,
+            "bird_keypoints_per_frame": tot[2] // nc4, "bird_matches_le_th_low_per_frame": tot[3] // nc4,
+            "note": "host images: left + right ORBextractor and the birdview cv::ORB + cornerSubPix concurrently "
+                    "(one host thread per stream), then ComputeStereoMatches (right pyramid over xGMI when on "
+                    "another GPU) and bird(t) x bird(t-1) Hamming top-2; synchronous per tracking frame"}
 
 
 # ---------------------------------------------------------------- main
@@ -165,7 +352,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256)   # frames per step per GPU (measured: 64 -> 256 is +6 %)
+    ap.add_argument("--batch", type=int, default=0, help="frames per step per GPU (default: the config's)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hamming", action="store_true")
@@ -173,37 +360,53 @@ def main():
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-bird", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-profile-pass", action="store_true",
+                    help="skip the per-kernel HIP-event pass (a rocprofv3 trace then holds only the timed launches)")
+    ap.add_argument("--only-extract", action="store_true", help="the extraction steps only (no other leg)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher plumbing only (tests/test_dist_cpu.py): ranks, rendezvous, reductions, the rank-0 "
+                         "line; no GPU is touched")
     ap.add_argument("--pipelines", type=int, default=int(os.environ.get("ORBGPU_BENCH_PIPELINES", "2")),
                     help="batches in flight: consecutive steps alternate over this many extractor contexts "
                          "(own stream and buffers each), so one batch's latency-bound phases overlap another's")
     args = ap.parse_args()
+    if args.only_extract:
+        args.no_cpu = args.no_hamming = args.no_stereo = args.no_host_path = args.no_bird = args.no_c4 = True
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args.gpus, sys.argv[1:]))   # before anything touches the GPU
     rank, world, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = dist_init(world)
+    if args.dry_run:
+        tmax, total = reduce_max_sum(dist, 1.0 + rank, 100.0 * (rank + 1))
+        ranks = gather(dist, {"rank": rank, "device": local, "host": socket.gethostname()})
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "value": total / tmax, "ranks": ranks}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     if os.environ.get("ORBGPU_BENCH_ONE_DEVICE") == "1":   # rehearsal of the N-rank path on a 1-GPU box
         local = 0
     import numpy as np
     import orbgpu
-    from orbgpu.synth import synth_batch
+    from orbgpu.synth import bench_frames
 
     cfg = CONFIGS[args.config]
-    w, h, nf, B = cfg["w"], cfg["h"], cfg["nfeatures"], args.batch
-    first, count = frame_range(rank, B)
-    # 64 distinct synthetic frames (the generator costs ~0.1 s per 1280x720 frame on the host); larger
-    # batches append circularly shifted copies (every frame is still a distinct image, fully processed)
-    base = synth_batch(w, h, min(count, 64), first=first)
-    frames = np.concatenate([base] + [np.roll(base, (7 * k, 13 * k), axis=(1, 2))
-                                      for k in range(1, (count + len(base) - 1) // len(base))])[:count]
-    frames = np.ascontiguousarray(frames)
+    w, h, nf = cfg["w"], cfg["h"], cfg["nfeatures"]
+    if cfg["scaling"] == "strong":   # C5: one global batch sharded over the ranks
+        G = cfg["global_batch"]
+        if G % world:
+            raise SystemExit(f"bench.py: config {args.config} shards {G} frames; --gpus must divide it")
+        B = args.batch or G // world
+        first = rank * B
+    else:
+        B = args.batch or cfg["batch"]
+        first, _ = frame_range(rank, B)
+    frames = bench_frames(w, h, B, first=first)
     ex = orbgpu.BatchExtractor(nf, w, h, B, device=local)
     ex.upload(frames)                         # inputs resident in HBM before timing
-
-    try:
-        import torch
-        has_torch_cuda = torch.cuda.is_available()
-    except Exception:
-        torch, has_torch_cuda = None, False
-
     exs = [ex]
     for _ in range(1, max(1, args.pipelines)):
         e2 = orbgpu.BatchExtractor(nf, w, h, B, device=local)
@@ -213,8 +416,6 @@ def main():
     def sync():
         for e in exs:
             e.sync()
-        if has_torch_cuda:
-            torch.cuda.synchronize(local)
 
     for _ in range(args.warmup):
         for e in exs:
@@ -223,8 +424,7 @@ def main():
     kps_per_step = int(ex.counts().sum())
     assert all(int(e.counts().sum()) == kps_per_step for e in exs)
 
-    # timed region: no per-kernel events (they add a marker packet per kernel boundary); step s runs
-    # on context s mod pipelines
+    # timed region: graph replays only; step s runs on context s mod pipelines
     barrier(dist)
     sync()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
@@ -237,23 +437,27 @@ def main():
     # host cores this rank kept busy during the timed steps (host utilisation beside the 1->N curve)
     host_busy = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / max(t1 - t0, 1e-9)
     barrier(dist)
-    # per-kernel breakdown (HIP events on the library's stream) from a separate pass of the same steps
-    ex.profile(True)
-    for _ in range(args.steps):
-        ex.launch()
-    sync()
-    kms, klaunch = ex.profile_read()
-    ex.profile(False)
     local_time = t1 - t0
     _, host_busy_sum = reduce_max_sum(dist, 0.0, host_busy)
-    local_kps = kps_per_step * args.steps
-    tmax, total_kps = reduce_max_sum(dist, local_time, local_kps)
+    tmax, total_kps = reduce_max_sum(dist, local_time, float(kps_per_step * args.steps))
     _, total_frames = reduce_max_sum(dist, 0.0, float(B * args.steps))
+    ranks = gather(dist, {"rank": rank, "device": local, "host": socket.gethostname(),
+                          "frames_per_step": B, "seconds": round(local_time, 6)})
+
+    # per-kernel breakdown (HIP events on the library's stream) from a separate pass of the same steps
+    kms = None
+    if not args.no_profile_pass:
+        ex.profile(True)
+        for _ in range(args.steps):
+            ex.launch()
+        sync()
+        kms, klaunch = ex.profile_read()
+        ex.profile(False)
 
     # ---- Hamming: all-pairs top-2 between consecutive frames' descriptors (device-resident, one
-    # launch for all B-1 pairs: orb_hamming_top2_frames_device, counts read on the device)
+    # launch for all B-1 pairs: orb_hamming_top2_frames_device on the matrix cores)
     ham = None
-    if not args.no_hamming:
+    if not args.no_hamming and B >= 2:
         counts = ex.counts()
         L = orbgpu._lib.lib()
         pairs = B - 1
@@ -284,10 +488,13 @@ def main():
                "queries_per_s": round(hevals / float(np.mean(counts)) / htmax, 1),
                "pair": f"frame f vs f+1 descriptors (~{int(np.mean(counts))} each), {pairs} pairs per launch",
                "kernel_avg_us": round(kt * 1e6, 2),
-               "kernel_valu_ops_per_s": round(16.0 * evals_step / kt, 1) if kt > 0 else None,
-               "valu_frac": round(16.0 * evals_step / kt / PEAK_VALU_LANE_OPS, 4) if kt > 0 else None,
+               # k_top2_mfma: one +-1 int8 32x32x32 MFMA tile per 32x32 pairs x 256 bits = 512 ops per pair
+               "mfma_i8": ({"achieved_ops_per_s": round(512.0 * evals_step / kt, 1), "peak_ops_per_s": PEAK_I8_OPS,
+                            "frac": round(512.0 * evals_step / kt / PEAK_I8_OPS, 4)} if kt > 0 else None),
                "kernel_hbm_gbs": round((32.0 * 2 * float(counts.sum()) + 12 * float(counts.sum())) / kt / 1e9, 2)
                if kt > 0 else None}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            ham["cpu_baseline"] = hamming_cpu(ex, B, oracle_native())
 
     # ---- roofline of the dominant kernel (per-step algorithmic bytes / per-step kernel time)
     per_frame_kps = kps_per_step / B
@@ -296,29 +503,33 @@ def main():
         n = orbgpu._lib.lib().orb_debug_candidates(ex.h, 0, l, None, 0)
         cands_per_frame += (-n - 1) if n < 0 else n
     ab = algorithmic_bytes(w, h, per_frame_kps, cands_per_frame)
-    steps = args.steps
-    ms_per_step_k = {KNAMES[i]: kms[i] / steps for i in range(4)}
-    dom = max(ms_per_step_k, key=ms_per_step_k.get)
-    dom_bytes = ab[dom] * B
-    dom_s = ms_per_step_k[dom] / 1e3
-    achieved = dom_bytes / dom_s / 1e9
-    launches_per_step = klaunch[KNAMES.index(dom)] / steps
-    traffic, valu_insts, pmc_commit = read_pmc(dom, B)
-    sum_k_s = sum(ms_per_step_k.values()) / 1e3
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 5),
-                "traffic": (round(traffic) if traffic is not None else None),   # HBM bytes per launch (PMC)
-                "algorithmic_bytes_per_frame": int(ab[dom]), "launches_per_step": launches_per_step,
-                "kernel_avg_launch_us": round(dom_s / launches_per_step * 1e6, 2),
-                # the kernel's real limiter is VALU issue: PMC SQ_INSTS_VALU x 64 lanes per launch / launch time
-                "valu": ({"achieved_lane_ops_per_s": round(valu_insts * 64 / (dom_s / launches_per_step), 1),
-                          "peak_lane_ops_per_s": PEAK_VALU_LANE_OPS,
-                          "frac": round(valu_insts * 64 / (dom_s / launches_per_step) / PEAK_VALU_LANE_OPS, 4),
-                          "valu_insts_per_launch": valu_insts, "pmc_commit": pmc_commit}
-                         if valu_insts else None),
-                "pipeline": {"bytes_per_frame": int(ab["pipeline"]),
-                             "achieved": round(ab["pipeline"] * B / sum_k_s / 1e9, 2),
-                             "frac": round(ab["pipeline"] * B / sum_k_s / 1e9 / PEAK_HBM_GBS, 5)}}
+    roofline, ms_per_step_k = None, None
+    if kms is not None:
+        steps = args.steps
+        ms_per_step_k = {KNAMES[i]: kms[i] / steps for i in range(4)}
+        dom = max(ms_per_step_k, key=ms_per_step_k.get)
+        dom_bytes = ab[dom] * B
+        dom_s = ms_per_step_k[dom] / 1e3
+        achieved = dom_bytes / dom_s / 1e9
+        launches_per_step = klaunch[KNAMES.index(dom)] / steps
+        traffic, valu_insts, pmc_src = read_pmc(dom, B)
+        sum_k_s = sum(ms_per_step_k.values()) / 1e3
+        launch_s = dom_s / launches_per_step
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 5),
+                    "traffic": (round(traffic) if traffic is not None else None),   # HBM bytes per launch (PMC)
+                    "algorithmic_bytes_per_launch": int(ab[dom] * B / launches_per_step),
+                    "algorithmic_bytes_per_frame": int(ab[dom]), "launches_per_step": launches_per_step,
+                    "kernel_avg_launch_us": round(launch_s * 1e6, 2),
+                    # the kernel's real limiter is VALU issue: PMC SQ_INSTS_VALU x 64 lanes per launch / launch time
+                    "valu": ({"achieved_lane_ops_per_s": round(valu_insts * 64 / launch_s, 1),
+                              "peak_lane_ops_per_s": PEAK_VALU_LANE_OPS,
+                              "frac": round(valu_insts * 64 / launch_s / PEAK_VALU_LANE_OPS, 4),
+                              "valu_insts_per_launch": valu_insts, "pmc_source": pmc_src}
+                             if valu_insts else None),
+                    "pipeline": {"bytes_per_frame": int(ab["pipeline"]),
+                                 "achieved": round(ab["pipeline"] * B / sum_k_s / 1e9, 2),
+                                 "frac": round(ab["pipeline"] * B / sum_k_s / 1e9 / PEAK_HBM_GBS, 5)}}
 
     # ---- Frame::ComputeStereoMatches on the GPU (BASELINE C4's stereo leg): a
     # separate batch of rectified synthetic pairs (frames 2p, 2p+1) extracted once, then the stereo
@@ -329,7 +540,7 @@ def main():
         npairs = max(1, B // 4)
         sf = []
         for i in range(npairs):
-            left = frames[i]
+            left = frames[i % len(frames)]
             sf += [left, synth_stereo_right(left, first + i)]
         sx = orbgpu.BatchExtractor(nf, w, h, 2 * npairs, device=local)
         sx.upload(np.stack(sf))
@@ -369,8 +580,9 @@ def main():
     host_path = None
     if not args.no_host_path:
         hx = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=local)
-        nh = min(16, len(frames))
+        nh = min(32, len(frames))
         hx(frames[0])
+        hx(frames[1 % len(frames)])
         t0h = time.perf_counter()
         nkp = 0
         for i in range(nh):
@@ -379,13 +591,12 @@ def main():
         t1h = time.perf_counter()
         host_path = {"frames_per_s": round(nh / (t1h - t0h), 1), "features_per_s": round(nkp / (t1h - t0h), 1),
                      "ms_per_frame": round((t1h - t0h) / nh * 1e3, 3),
-                     "note": "orb_extract per host frame: upload + 10 launches + download, one frame in flight"}
+                     "note": "orb_extract per host frame: upload + graph replay + one download, one frame in flight"}
         hx.close()
 
     # ---- birdview stream (BASELINE C4's bird stream): Frame.cc:320-342 fused on one
-    # device-resident 1280x720 image + mask per call (orb_bird_extract_device): pyramid + mask pyramid,
-    # FAST/NMS/Harris candidates, host retainBest (libstdc++ nth_element, as the reference), IC angle,
-    # cornerSubPix, blur, rBRIEF; synchronous per frame (the host selection sits mid-pipeline)
+    # device-resident image + mask per call (orb_bird_extract_device); synchronous per frame (the host
+    # selection, libstdc++ nth_element as the reference, sits mid-pipeline)
     bird = None
     if not args.no_bird:
         from orbgpu.synth import synth_bird_mask
@@ -411,8 +622,7 @@ def main():
                 "note": "cv::ORB(2000) masked detect + cornerSubPix + compute (Frame.cc:320-342), image and "
                         "mask resident, keypoints + descriptors downloaded per frame"}
         if rank == 0 and world == 1 and not args.no_cpu:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import oracle   # test infrastructure: used ONLY as the timed CPU baseline here
+            oracle = oracle_native()
             ob = oracle.OracleCvORB(2000)
             ob.extract(bimg, bmask)
             tc0 = time.perf_counter()
@@ -425,70 +635,34 @@ def main():
         for ptr in (di, dm):
             L.orb_device_free(ex.h, ptr)
 
-    # ---- C4 end to end through the reference's own host-image boundary, one GPU: per tracking frame,
-    # ORBextractor on the rectified left and right images (Frame.cc:124-127), ComputeStereoMatches
-    # (:662-836), the birdview cv::ORB stream (:320-342) and the bird(t) x bird(t-1) all-pairs Hamming
-    # top-2 — synchronous per frame, uploads and downloads included (latency a drop-in caller sees)
     c4 = None
     if not args.no_c4:
-        from orbgpu.synth import synth_bird_mask, synth_stereo_right
-        exl = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=local)
-        exr = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7, device=local)
-        bo = orbgpu.BirdORB(2000, device=local)
-        mt = orbgpu.ORBmatcher(0.7, True, device=local)
-        nc4 = min(16, len(frames) - 1)
-        lefts = [np.ascontiguousarray(frames[i]) for i in range(nc4 + 1)]
-        rights = [synth_stereo_right(lefts[i], first + i) for i in range(nc4 + 1)]
-        bmask = synth_bird_mask(w, h, first)
-        birds = [np.ascontiguousarray(frames[(i + nc4 // 2) % len(frames)]) for i in range(nc4 + 1)]
-
-        def c4_frame(i, prev_desc):
-            kl, dl = exl(lefts[i])
-            kr, dr = exr(rights[i])
-            _u, _d, nst = orbgpu.compute_stereo_matches(exl, exr, kl, dl, kr, dr, 0.54, 0.54 * 721.5)
-            kb, db = bo.extract(birds[i], bmask)
-            nm = 0
-            if prev_desc is not None and len(db) and len(prev_desc):
-                dist, _idx, _nv = mt.hamming_topk(db, prev_desc, 2)
-                nm = int((dist[:, 0] <= 50).sum())
-            return db, len(kl) + len(kr), nst, len(kb), nm
-        prev, _, _, _, _ = c4_frame(0, None)
-        barrier(dist)
-        tc0 = time.perf_counter()
-        tot = [0, 0, 0, 0]
-        for i in range(1, nc4 + 1):
-            prev, a, b_, c_, d_ = c4_frame(i, prev)
-            tot = [tot[0] + a, tot[1] + b_, tot[2] + c_, tot[3] + d_]
-        tc1 = time.perf_counter()
-        c4 = {"ms_per_frame": round((tc1 - tc0) / nc4 * 1e3, 3), "frames_per_s": round(nc4 / (tc1 - tc0), 1),
-              "stereo_keypoints_per_frame": tot[0] // nc4, "left_with_depth_per_frame": tot[1] // nc4,
-              "bird_keypoints_per_frame": tot[2] // nc4, "bird_matches_le_th_low_per_frame": tot[3] // nc4,
-              "note": "host images: left + right ORBextractor, ComputeStereoMatches, birdview cv::ORB + cornerSubPix, "
-                      "bird(t) x bird(t-1) Hamming top-2; synchronous per frame on one GPU"}
-        for o in (exl, exr, bo):
-            o.close()
+        c4 = c4_leg(cfg, frames, first, dist, rank, world, local)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(cfg, frames[:32])
+        cpu = cpu_baseline(cfg, frames[:16])
 
     if rank == 0:
         value = total_kps / tmax
         out = {"metric": METRIC, "value": round(value, 1), "unit": "features/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+               "scaling": cfg["scaling"], "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": cfg["name"], "width": w, "height": h, "nfeatures": nf, "nlevels": 8,
                           "scale_factor": 1.2, "ini_th_fast": 20, "min_th_fast": 7, "batch_per_gpu": B,
                           "global_batch": B * world, "parallelism": f"frame-sharded x{world} (no collective)",
                           "batches_in_flight": len(exs)},
+               "ranks": ranks,
                "frames_per_s": round(total_frames / tmax, 1),
                "host_cores_busy": round(host_busy_sum, 3),   # all ranks' processes, timed region
                "keypoints_per_frame": round(per_frame_kps, 1),
-               "kernels_ms_per_step": {k: round(v, 4) for k, v in ms_per_step_k.items()},
+               "kernels_ms_per_step": ({k: round(v, 4) for k, v in ms_per_step_k.items()} if ms_per_step_k else None),
                "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo,
                "bird": bird, "c4_frame": c4, "host_path": host_path}
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
+            if "host_estimate_value" in cpu:
+                out["speedup_vs_cpu_host_estimate"] = round(value / cpu["host_estimate_value"], 2)
         print(json.dumps(out), flush=True)
     for e in exs:
         e.close()

@@ -256,8 +256,10 @@ int orb_features_in_area(int n, const orb_keypoint* kps_un, float min_x, float m
 
 /* void Frame::ComputeStereoMatches()  Frame.cc:662-836, for one rectified pair.  `left` / `right` are
  * the contexts that extracted the left / right image last (orb_extract; the reference's
- * mpORBextractorLeft/Right, whose mvImagePyramid the window search reads) — same device, same image
- * size.  kpsL/descL = mvKeys/mDescriptors (nL), kpsR/descR = mvKeysRight/mDescriptorsRight (nR);
+ * mpORBextractorLeft/Right, whose mvImagePyramid the window search reads), same image size.  They may sit
+ * on different GPUs (one GPU per camera stream): the right image and pyramid are then copied to the left
+ * device with hipMemcpyPeerAsync and the search runs there.  kpsL/descL = mvKeys/mDescriptors (nL),
+ * kpsR/descR = mvKeysRight/mDescriptorsRight (nR);
  * mb = baseline, mbf = baseline * fx.  uright / depth (nL each) receive mvuRight / mvDepth
  * (-1 = no match); *nmatched = number of left keypoints with a depth.  Synchronous. */
 int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_keypoint* kpsL, const uint8_t* descL,

@@ -33,10 +33,20 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+def use_library(path):
+    """Load the oracle from `path` instead of the in-tree build (bench.py: a -march=native rebuild)."""
+    global _LIB, _PATH
+    assert _LIB is None, "oracle library already loaded"
+    _PATH = path
+
+
+_PATH = None
+
+
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liborb_oracle.so")
+        path = _PATH or os.path.join(_HERE, "liborb_oracle.so")
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)
@@ -62,6 +72,11 @@ def lib():
         L.oracle_blur.argtypes = [vp, ci, ci, vp, ci]
         L.oracle_pattern.argtypes = [vp]
         L.oracle_sincosf.argtypes = [vp, ci, vp, vp]
+        L.oracle_bench_single.argtypes = [vp, ci, ci, ci, ci, ci, ci, vp, vp, vp]
+        L.oracle_bench_parallel.restype = ctypes.c_double
+        L.oracle_bench_parallel.argtypes = [vp, ci, ci, ci, ci, ci, ci, ci, vp]
+        L.oracle_bench_hamming.restype = ctypes.c_double
+        L.oracle_bench_hamming.argtypes = [vp, vp, vp, ci, ci, vp, vp, ci, ci, ci, vp]
         L.oracle_time_extract.restype = ctypes.c_double
         L.oracle_time_extract.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ci, vp]
         L.oracle_search_by_bow_kf_f.argtypes = [cf, ci, ci, vp, vp, vp, FeatVec, ci, vp, vp, FeatVec, vp]
@@ -234,6 +249,41 @@ def time_extract(frames, nfeatures, nthreads=1, iters=1, scale_factor=1.2, nleve
     secs = lib().oracle_time_extract(_p(frames), n, w, h, nfeatures, scale_factor, nlevels, ini_th, min_th,
                                      nthreads, iters, ctypes.byref(tot))
     return secs, tot.value
+
+
+STAGES = ("pyramid", "fast", "octree", "ic_angle", "blur", "brief")
+
+
+def bench_single(frames, nfeatures, warmup=5, timed=50):
+    """Single-thread protocol: per-frame ms of `timed` frames after `warmup`, per-stage totals (ms)."""
+    frames = np.ascontiguousarray(frames, np.uint8)
+    n, h, w = frames.shape
+    fm = np.zeros(timed, np.float64)
+    st = np.zeros(6, np.float64)
+    kps = ctypes.c_longlong()
+    lib().oracle_bench_single(_p(frames), n, w, h, nfeatures, warmup, timed, _p(fm), _p(st), ctypes.byref(kps))
+    return fm, dict(zip(STAGES, st.tolist())), kps.value
+
+
+def bench_parallel(frames, nfeatures, nthreads, warmup, total):
+    frames = np.ascontiguousarray(frames, np.uint8)
+    n, h, w = frames.shape
+    kps = ctypes.c_longlong()
+    secs = lib().oracle_bench_parallel(_p(frames), n, w, h, nfeatures, nthreads, warmup, total, ctypes.byref(kps))
+    return secs, kps.value
+
+
+def bench_hamming(desc, angles, counts, qf, tf, mode, nthreads, iters=1):
+    """desc (F, stride, 32) u8, angles (F, stride) f32, counts (F,): seconds, evaluations per pass."""
+    desc = np.ascontiguousarray(desc, np.uint8)
+    angles = np.ascontiguousarray(angles, np.float32)
+    counts = np.ascontiguousarray(counts, np.int32)
+    qf = np.ascontiguousarray(qf, np.int32)
+    tf = np.ascontiguousarray(tf, np.int32)
+    ev = ctypes.c_longlong()
+    secs = lib().oracle_bench_hamming(_p(desc), _p(angles), _p(counts), desc.shape[1], len(qf), _p(qf), _p(tf), mode,
+                                      nthreads, iters, ctypes.byref(ev))
+    return secs, ev.value
 
 
 def make_featvec(node_ids, groups):

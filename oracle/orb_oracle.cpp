@@ -136,29 +136,39 @@ void gauss7_blur(const Img& src, Img& dst, int flags) {
     int k[7];
     gaussian_kernel_q8(k);
     const int W = src.w, H = src.h;
+    // R: the exact integer row pass (RowFilter<uchar,int>), REFLECT_101 at the clone's edges.  The
+    // interior loop has no border logic so the compiler vectorises it (the oracle is also the timed
+    // CPU baseline); the arithmetic is unchanged.
     std::vector<int> R((size_t)W * H);
-    for (int y = 0; y < H; y++) {             // RowFilter<uchar,int>: exact integer
+    for (int y = 0; y < H; y++) {
         const uint8_t* s = src.row(y);
         int* r = &R[(size_t)y * W];
-        for (int x = 0; x < W; x++) {
+        auto edge = [&](int x) {
             int acc = 0;
             for (int j = 0; j < 7; j++) acc += k[j] * s[reflect101(x + j - 3, W)];
             r[x] = acc;
-        }
+        };
+        const int x0 = std::min(3, W), x1 = std::max(x0, W - 3);
+        for (int x = 0; x < x0; x++) edge(x);
+        for (int x = x0; x < x1; x++)
+            r[x] = k[0] * s[x - 3] + k[1] * s[x - 2] + k[2] * s[x - 1] + k[3] * s[x] + k[4] * s[x + 1] + k[5] * s[x + 2] +
+                   k[6] * s[x + 3];
+        for (int x = x1; x < W; x++) edge(x);
     }
     dst.create(W, H);
-    const int xsimd = W & ~3;                 // SymmColumnVec_32s8u covers multiples of 4
+    const int xsimd = (flags & ORACLE_BLUR_ALL_HALFUP) ? 0 : (W & ~3);   // SymmColumnVec_32s8u covers multiples of 4
     for (int y = 0; y < H; y++) {
+        const int* rr[7];
+        for (int i = 0; i < 7; i++) rr[i] = &R[(size_t)reflect101(y + i - 3, H) * W];
         uint8_t* o = dst.row(y);
         for (int x = 0; x < W; x++) {
-            int S = 0;
-            for (int i = 0; i < 7; i++) S += k[i] * R[(size_t)reflect101(y + i - 3, H) * W + x];
-            int q = S >> 16, rem = S & 0xFFFF, v;
-            if (x < xsimd && !(flags & ORACLE_BLUR_ALL_HALFUP))
-                v = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));   // _mm_cvtps_epi32
-            else
-                v = (S + 32768) >> 16;                                       // FixedPtCastEx
-            o[x] = sat_u8(v);
+            const int S = k[0] * rr[0][x] + k[1] * rr[1][x] + k[2] * rr[2][x] + k[3] * rr[3][x] + k[4] * rr[4][x] +
+                          k[5] * rr[5][x] + k[6] * rr[6][x];
+            const int q = S >> 16, rem = S & 0xFFFF;
+            // SSE2 body (x < W & ~3): _mm_cvtps_epi32, half to even; scalar tail: FixedPtCastEx, half up
+            const int even = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));
+            const int v = x < xsimd ? even : (S + 32768) >> 16;
+            o[x] = (uint8_t)std::min(std::max(v, 0), 255);
         }
     }
 }
@@ -661,6 +671,16 @@ struct Extractor {
     std::vector<std::vector<KP>> cand, lvlKps;
     std::vector<KP> outKps;
     std::vector<uint8_t> outDesc;
+    // per-stage wall time (ms), accumulated over run() calls: pyramid, FAST (+NMS), octree, IC angle,
+    // blur, BRIEF (the CPU baseline reports where its time goes)
+    double stage_ms[6] = {0, 0, 0, 0, 0, 0};
+    typedef std::chrono::steady_clock Clock;
+    static double ms_since(Clock::time_point& t) {
+        const Clock::time_point n = Clock::now();
+        const double d = std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+        return d;
+    }
 
     Extractor(int nf, float sf, int nl, int ini, int mn, int fl)
         : nfeatures(nf), nlevels(nl), iniThFAST(ini), minThFAST(mn), flags(fl), scaleFactor(sf) {
@@ -721,6 +741,7 @@ struct Extractor {
         std::vector<Corner> corners;
         corners.reserve(4096);
         for (int level = 0; level < nlevels; ++level) {
+            Clock::time_point t = Clock::now();
             const Img& im = pyr[level];
             const int minBorderX = EDGE_THRESHOLD - 3;
             const int minBorderY = minBorderX;
@@ -763,6 +784,7 @@ struct Extractor {
             }
             if ((float)(maxBorderX - minBorderX) / (maxBorderY - minBorderY) < 0.5f) return false;  // nIni==0
             std::vector<KP>& keypoints = lvlKps[level];
+            stage_ms[1] += ms_since(t);
             if (literal) {
                 keypoints.reserve(nfeatures);   // :832
                 keypoints = DistributeOctTreeLiteral(vToDistributeKeys, minBorderX, maxBorderX, minBorderY, maxBorderY,
@@ -771,6 +793,7 @@ struct Extractor {
                 keypoints = DistributeOctTree(vToDistributeKeys, minBorderX, maxBorderX, minBorderY, maxBorderY,
                                               mnFeaturesPerLevel[level], (flags & ORACLE_TIE_REVERSE_SEQ) != 0);
             }
+            stage_ms[2] += ms_since(t);
             const int scaledPatchSize = (int)(PATCH_SIZE * mvScaleFactor[level]);
             for (KP& kp : keypoints) {
                 kp.x += minBorderX;
@@ -779,15 +802,20 @@ struct Extractor {
                 kp.size = (float)scaledPatchSize;
             }
         }
+        Clock::time_point t = Clock::now();
         for (int level = 0; level < nlevels; ++level)                             // :851-852
             for (KP& kp : lvlKps[level]) kp.angle = IC_Angle(pyr[level], kp.x, kp.y, umax);
+        stage_ms[3] += ms_since(t);
         return true;
     }
 
     int run(const Img& image) {                                                     // :1043-1105
         if (image.w == 0 || image.h == 0) return -1;
+        Clock::time_point t = Clock::now();
         if (!ComputePyramid(image)) return -2;
+        stage_ms[0] += ms_since(t);
         if (!ComputeKeyPointsOctTree()) return -2;
+        t = Clock::now();
         int nkeypoints = 0;
         for (int level = 0; level < nlevels; ++level) nkeypoints += (int)lvlKps[level].size();
         outKps.clear();
@@ -799,8 +827,10 @@ struct Extractor {
             const int nkl = (int)keypoints.size();
             if (nkl == 0) continue;
             gauss7_blur(pyr[level], blurred[level], flags);
+            stage_ms[4] += ms_since(t);
             for (int i = 0; i < nkl; i++)
                 computeOrbDescriptor(keypoints[i], blurred[level], kPattern, &outDesc[(size_t)(offset + i) * 32], flags);
+            stage_ms[5] += ms_since(t);
             offset += nkl;
             if (level != 0) {
                 float scale = mvScaleFactor[level];
@@ -1039,6 +1069,123 @@ double oracle_time_extract(const uint8_t* frames, int nframes, int w, int h, int
     auto t1 = std::chrono::steady_clock::now();
     if (total_kps) *total_kps = kps.load();
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+/* ---- CPU baseline protocol: single thread, warm-up then individually timed frames
+ * (per-frame ms and per-stage ms out), and frame-parallel over nthreads (one extractor per thread,
+ * `warmup` frames each before the clock starts, then `total` frames from a shared counter). ---- */
+int oracle_bench_single(const uint8_t* frames, int nframes, int w, int h, int nfeatures, int warmup, int timed,
+                        double* frame_ms, double* stage_ms6, long long* total_kps) {
+    std::vector<Img> imgs(nframes);
+    for (int f = 0; f < nframes; f++) {
+        imgs[f].create(w, h);
+        std::memcpy(imgs[f].d.data(), frames + (size_t)f * w * h, (size_t)w * h);
+    }
+    Extractor e(nfeatures, 1.2f, 8, 20, 7, 0);
+    for (int i = 0; i < warmup; i++) e.run(imgs[i % nframes]);
+    for (double& v : e.stage_ms) v = 0;
+    long long kps = 0;
+    for (int i = 0; i < timed; i++) {
+        auto t0 = std::chrono::steady_clock::now();
+        const int n = e.run(imgs[(warmup + i) % nframes]);
+        frame_ms[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        kps += n > 0 ? n : 0;
+    }
+    for (int k = 0; k < 6; k++) stage_ms6[k] = e.stage_ms[k];
+    if (total_kps) *total_kps = kps;
+    return 0;
+}
+
+double oracle_bench_parallel(const uint8_t* frames, int nframes, int w, int h, int nfeatures, int nthreads, int warmup,
+                             int total, long long* total_kps) {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<Img> imgs(nframes);
+    for (int f = 0; f < nframes; f++) {
+        imgs[f].create(w, h);
+        std::memcpy(imgs[f].d.data(), frames + (size_t)f * w * h, (size_t)w * h);
+    }
+    std::atomic<long long> kps{0};
+    std::atomic<int> next{0}, ready{0};
+    std::atomic<bool> go{false};
+    auto worker = [&](int tid) {
+        Extractor e(nfeatures, 1.2f, 8, 20, 7, 0);   // one instance per thread (ORBextractor.h:85)
+        for (int i = 0; i < warmup; i++) e.run(imgs[(tid + i) % nframes]);
+        ready++;
+        while (!go.load()) std::this_thread::yield();
+        for (;;) {
+            const int k = next.fetch_add(1);
+            if (k >= total) break;
+            const int n = e.run(imgs[k % nframes]);
+            kps += n > 0 ? n : 0;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++) th.emplace_back(worker, t);
+    while (ready.load() < nthreads) std::this_thread::yield();
+    auto t0 = std::chrono::steady_clock::now();
+    go = true;
+    for (auto& t : th) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    if (total_kps) *total_kps = kps.load();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+/* Hamming CPU baseline: for each (query frame, train frame) pair, either ORBmatcher::SearchByBoW(KF, F)
+ * with one FeatureVector node holding every feature (the C4 brute-force semantics, SURVEY §8(d):
+ * nnratio 0.7, checkOri on, all MapPoints valid; ORBmatcher.cc:159-288) or the plain all-pairs top-2
+ * DescriptorDistance loop the GPU kernel computes (mode 1).  Pairs are spread over nthreads; `iters`
+ * passes.  Returns wall seconds; *evals = sum of nq * nt over one pass. */
+double oracle_bench_hamming(const uint8_t* desc, const float* angles, const int* counts, int stride, int npairs,
+                            const int* qf, const int* tf, int mode, int nthreads, int iters, long long* evals) {
+    if (nthreads < 1) nthreads = 1;
+    long long ev = 0;
+    for (int p = 0; p < npairs; p++) ev += (long long)counts[qf[p]] * counts[tf[p]];
+    if (evals) *evals = ev;
+    std::atomic<int> next{0};
+    std::atomic<long long> sink{0};
+    const int total = npairs * iters;
+    auto worker = [&]() {
+        std::vector<int> idxq, idxt, match, best(1), second(1);
+        long long local = 0;
+        for (;;) {
+            const int k = next.fetch_add(1);
+            if (k >= total) break;
+            const int p = k % npairs;
+            const int nq = counts[qf[p]], nt = counts[tf[p]];
+            const uint8_t* dq = desc + (size_t)qf[p] * stride * 32;
+            const uint8_t* dt = desc + (size_t)tf[p] * stride * 32;
+            if (mode == 0) {
+                idxq.resize(nq);
+                idxt.resize(nt);
+                for (int i = 0; i < nq; i++) idxq[i] = i;
+                for (int i = 0; i < nt; i++) idxt[i] = i;
+                std::vector<uint8_t> mp(nq, 1);
+                const uint32_t node = 0;
+                const int offq[2] = {0, nq}, offt[2] = {0, nt};
+                OracleFeatVec fq{1, &node, offq, idxq.data()}, ft{1, &node, offt, idxt.data()};
+                match.resize(std::max(nt, 1));
+                local += oracle_search_by_bow_kf_f(0.7f, 1, nq, dq, angles + (size_t)qf[p] * stride, mp.data(), fq, nt, dt,
+                                                   angles + (size_t)tf[p] * stride, ft, match.data());
+            } else {
+                for (int i = 0; i < nq; i++) {
+                    int b1 = 256, b2 = 256, bi = -1;
+                    for (int j = 0; j < nt; j++) {
+                        const int d = DescriptorDistance(dq + (size_t)i * 32, dt + (size_t)j * 32);
+                        if (d < b1) { b2 = b1; b1 = d; bi = j; }
+                        else if (d < b2) b2 = d;
+                    }
+                    local += bi + b2;
+                }
+            }
+        }
+        sink += local;
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++) th.emplace_back(worker);
+    for (auto& t : th) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count() + (sink.load() == -1 ? 1 : 0);
 }
 
 /* SearchByBoW(KF, F)  ORBmatcher.cc:159-288 */

@@ -76,6 +76,19 @@ double oracle_time_extract(const uint8_t* frames, int nframes, int w, int h, int
                            float scaleFactor, int nlevels, int iniTh, int minTh,
                            int nthreads, int iters, long long* total_kps);
 
+/* ---- CPU baseline protocol ---- */
+/* single thread: `warmup` frames, then `timed` frames each timed (frame_ms[timed]); stage_ms6 = total ms of
+ * the timed frames per stage: pyramid, FAST+NMS, octree, IC angle, blur, BRIEF */
+int    oracle_bench_single(const uint8_t* frames, int nframes, int w, int h, int nfeatures, int warmup, int timed,
+                           double* frame_ms, double* stage_ms6, long long* total_kps);
+/* frame-parallel: nthreads extractors, `warmup` frames each off the clock, then `total` frames; seconds */
+double oracle_bench_parallel(const uint8_t* frames, int nframes, int w, int h, int nfeatures, int nthreads, int warmup,
+                             int total, long long* total_kps);
+/* Hamming over frame pairs (desc/angles: `stride` slots per frame, counts per frame): mode 0 = SearchByBoW(KF,F)
+ * with one node holding every feature, 1 = all-pairs top-2; seconds for `iters` passes, *evals = sum nq*nt */
+double oracle_bench_hamming(const uint8_t* desc, const float* angles, const int* counts, int stride, int npairs,
+                            const int* qf, const int* tf, int mode, int nthreads, int iters, long long* evals);
+
 /* ---- matchers (ORBmatcher.cc). FeatureVector = CSR over ascending node ids. ---- */
 typedef struct {
     int nnodes;

@@ -13,44 +13,32 @@
 
 namespace orbgpu {
 
-struct SinCosTable {
-    double sign[4], hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
-};
-
-// sincosf_data.c: entry 1 negates the cosine polynomial (quadrants 2, 3)
-__device__ __forceinline__ SinCosTable glibc_sincos_table(int neg) {
-    SinCosTable t;
-    t.sign[0] = 1.0; t.sign[1] = -1.0; t.sign[2] = -1.0; t.sign[3] = 1.0;
-    t.hpi_inv = 0x1.45F306DC9C883p+23;
-    t.hpi = 0x1.921FB54442D18p0;
-    const double sg = neg ? -1.0 : 1.0;
-    t.c0 = sg * 0x1p0;
-    t.c1 = sg * -0x1.ffffffd0c621cp-2;
-    t.c2 = sg * 0x1.55553e1068f19p-5;
-    t.c3 = sg * -0x1.6c087e89a359dp-10;
-    t.c4 = sg * 0x1.99343027bf8c3p-16;
-    t.s1 = -0x1.555545995a603p-3;
-    t.s2 = 0x1.1107605230bc4p-7;
-    t.s3 = -0x1.994eb3774cf24p-13;
-    return t;
-}
+// sincosf_data.c, as constants: __sincosf_table[1] is entry 0 with the cosine polynomial negated
+// (quadrants 2 and 3), expressed here as a sign applied to c0..c4 (multiplying by -1 is exact).  No table
+// in memory: a dynamically indexed one lands in scratch.
+constexpr double kTrigHpiInv = 0x1.45F306DC9C883p+23;   // 2/pi * 2^24 (x86-64: no TOINT_INTRINSICS)
+constexpr double kTrigHpi = 0x1.921FB54442D18p0;
+constexpr double kTrigC0 = 0x1p0, kTrigC1 = -0x1.ffffffd0c621cp-2, kTrigC2 = 0x1.55553e1068f19p-5,
+                 kTrigC3 = -0x1.6c087e89a359dp-10, kTrigC4 = 0x1.99343027bf8c3p-16;
+constexpr double kTrigS1 = -0x1.555545995a603p-3, kTrigS2 = 0x1.1107605230bc4p-7, kTrigS3 = -0x1.994eb3774cf24p-13;
 
 __device__ __forceinline__ uint32_t trig_abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
 
-// sinf_poly: n even -> sine polynomial, odd -> cosine polynomial (fma = the FMA build's contractions)
-__device__ __forceinline__ float glibc_sinf_poly(double x, double x2, const SinCosTable& p, int n) {
+// sinf_poly: n even -> sine polynomial, odd -> cosine polynomial scaled by cs (+-1: the table entry);
+// every a + b*c of the FMA build is one fused multiply-add
+__device__ __forceinline__ float glibc_sinf_poly(double x, double x2, double cs, int n) {
     if ((n & 1) == 0) {
         const double x3 = x * x2;
-        const double s1 = __builtin_fma(x2, p.s3, p.s2);
+        const double s1 = __builtin_fma(x2, kTrigS3, kTrigS2);
         const double x7 = x3 * x2;
-        const double s = __builtin_fma(x3, p.s1, x);
+        const double s = __builtin_fma(x3, kTrigS1, x);
         return (float)__builtin_fma(x7, s1, s);
     }
     const double x4 = x2 * x2;
-    const double c2 = __builtin_fma(x2, p.c4, p.c3);
-    const double c1 = __builtin_fma(x2, p.c1, p.c0);
+    const double c2 = __builtin_fma(x2, cs * kTrigC4, cs * kTrigC3);
+    const double c1 = __builtin_fma(x2, cs * kTrigC1, cs * kTrigC0);
     const double x6 = x4 * x2;
-    const double c = __builtin_fma(x4, p.c2, c1);
+    const double c = __builtin_fma(x4, cs * kTrigC2, c1);
     return (float)__builtin_fma(x6, c2, c);
 }
 
@@ -64,19 +52,18 @@ __device__ __forceinline__ void glibc_sincosf(float y, float* s, float* c) {
             *c = 1.0f;
             return;
         }
-        const SinCosTable p = glibc_sincos_table(0);
-        *s = glibc_sinf_poly(x, x2, p, 0);
-        *c = glibc_sinf_poly(x, x2, p, 1);
+        *s = glibc_sinf_poly(x, x2, 1.0, 0);
+        *c = glibc_sinf_poly(x, x2, 1.0, 1);
         return;
     }
     // reduce_fast (!TOINT_INTRINSICS): n = round(x * 2/pi) by the shift trick, x - n*pi/2 fused
-    const double r = x * 0x1.45F306DC9C883p+23;
+    const double r = x * kTrigHpiInv;
     const int n = ((int32_t)r + 0x800000) >> 24;
-    x = __builtin_fma(-(double)n, 0x1.921FB54442D18p0, x);
-    const SinCosTable p = glibc_sincos_table((n & 2) != 0);
-    const double sg = p.sign[n & 3];
-    *s = glibc_sinf_poly(x * sg, x * x, p, n);
-    *c = glibc_sinf_poly(x * sg, x * x, p, n ^ 1);
+    x = __builtin_fma(-(double)n, kTrigHpi, x);
+    const double sg = ((n + 1) & 2) ? -1.0 : 1.0;   // sign[n & 3] = {1, -1, -1, 1}
+    const double cs = (n & 2) ? -1.0 : 1.0;         // table entry 1 for quadrants 2, 3
+    *s = glibc_sinf_poly(x * sg, x * x, cs, n);
+    *c = glibc_sinf_poly(x * sg, x * x, cs, n ^ 1);
 }
 
 }  // namespace orbgpu

@@ -418,7 +418,7 @@ void orb_destroy(orb_ctx* h) {
     }
     void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_hout,
-                    c->d_scratch};
+                    c->d_scratch, c->d_peer};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);

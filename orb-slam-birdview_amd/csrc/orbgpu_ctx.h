@@ -75,6 +75,9 @@ struct Ctx {
     // matcher scratch arena (bytes)
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;
+    // the right extractor's frame + pyramid when it runs on another GPU (orb_compute_stereo_matches)
+    uint8_t* d_peer = nullptr;
+    size_t peer_cap = 0;
 
     // last batch (for the mvImagePyramid view and debug reads)
     const uint8_t* last_frames = nullptr;

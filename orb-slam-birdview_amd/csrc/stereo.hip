@@ -12,6 +12,7 @@
 // All window arithmetic is integer (cv::norm NORM_L1 of integer-valued float patches is an exact
 // integer); the parabola and depth use the reference's float expressions, uncontracted.
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <cstring>
 #include <vector>
@@ -361,8 +362,6 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     CTX_GUARD(cl);
     if (!cr || nL < 0 || nR < 0 || (nL && (!kpsL || !descL || !uright || !depth)) || (nR && (!kpsR || !descR)))
         return set_error("orb_compute_stereo_matches: bad arguments", hipSuccess), ORB_ERR_ARG;
-    if (cl->device != cr->device)
-        return set_error("orb_compute_stereo_matches: contexts on different devices", hipSuccess), ORB_ERR_ARG;
     if (cl->last_nframes < 1 || cr->last_nframes < 1 || !same_geometry(cl, cr))
         return set_error("orb_compute_stereo_matches: both contexts must have extracted an image of one size",
                          hipSuccess),
@@ -411,6 +410,37 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
         return set_error("stereo upload", e), ORB_ERR_HIP;
     StereoSide SL{cl->last_frames, cl->last_frame_pitch, cl->last_row_stride, cl->d_pyr, 0, 0, d_kL, d_dL, d_cnt, 0};
     StereoSide SR{cr->last_frames, cr->last_frame_pitch, cr->last_row_stride, cr->d_pyr, 0, 0, d_kR, d_dR, d_cnt + 1, 0};
+    // Left and right extractors on different GPUs (one GPU per camera stream, BASELINE C4): the window
+    // search reads the right image and pyramid, so they move to the left device over xGMI first
+    // (hipMemcpyPeerAsync: the right frame's level 0 and its pyramid slot, ~2.9 MB at 1280x720).
+    // ORBGPU_STEREO_STAGE=1 forces the same staging on one device (tests/test_gpu_stereo.py).
+    const char* force = std::getenv("ORBGPU_STEREO_STAGE");
+    if (cl->device != cr->device || (force && force[0] == '1')) {
+        const size_t f0 = (size_t)cr->last_frame_pitch, pb = (size_t)cr->geom.pyr_bytes;
+        const size_t sneed = ((f0 + 255) & ~(size_t)255) + pb;
+        if (sneed > cl->peer_cap || !cl->d_peer) {
+            if (cl->d_peer) (void)hipFree(cl->d_peer);
+            cl->d_peer = nullptr;
+            cl->peer_cap = 0;
+            if ((e = hipMalloc((void**)&cl->d_peer, sneed)) != hipSuccess) return set_error("stereo peer staging", e), ORB_ERR_NOMEM;
+            cl->peer_cap = sneed;
+        }
+        if (cl->device != cr->device) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, cl->device, cr->device) == hipSuccess && can) {
+                const hipError_t pe = hipDeviceEnablePeerAccess(cr->device, 0);   // direct xGMI copies
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return set_error("peer access", pe), ORB_ERR_HIP;
+                (void)hipGetLastError();
+            }
+        }
+        uint8_t* sf = cl->d_peer;
+        uint8_t* sp = cl->d_peer + ((f0 + 255) & ~(size_t)255);
+        if ((e = hipMemcpyPeerAsync(sf, cl->device, cr->last_frames, cr->device, f0, cl->stream)) != hipSuccess ||
+            (pb && (e = hipMemcpyPeerAsync(sp, cl->device, cr->d_pyr, cr->device, pb, cl->stream)) != hipSuccess))
+            return set_error("stereo peer copy", e), ORB_ERR_HIP;
+        SR.frames = sf;
+        SR.pyr = sp;
+    }
     if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 1, cl->stream);
     e = launch_stereo(cl->d_geom, cl->geom, SL, SR, 1, mb, mbf, d_u, d_d, d_s, scap, d_nm, cl->stream);
     if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 0, cl->stream);

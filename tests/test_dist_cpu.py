@@ -57,3 +57,32 @@ def test_single_rank_needs_no_process_group():
     import bench
     assert bench.dist_init(1) is None
     assert bench.reduce_max_sum(None, 3.0, 5.0) == (3.0, 5.0)
+
+
+def _bench_line(out):
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_gpus_flag_spawns_the_ranks_itself():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts both ranks before any GPU call, they
+    rendezvous on 127.0.0.1 over gloo, and rank 0 alone prints the line with every rank's device."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 2
+    assert [x["rank"] for x in d["ranks"]] == [0, 1] and [x["device"] for x in d["ranks"]] == [0, 1]
+    assert d["value"] == 300.0 / 2.0          # summed work over the max time
+
+
+def test_launcher_world_must_match_gpus_flag():
+    import subprocess
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)

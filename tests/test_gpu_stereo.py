@@ -98,3 +98,25 @@ def test_stereo_no_left_keypoints(orbgpu_mod):
     kb, db = b(synth_frame(640, 480, 1))
     u, d, n = orbgpu_mod.compute_stereo_matches(a, b, ka, da, kb, db, MB, MB * FX)
     assert len(u) == 0 and n == 0
+
+
+@pytest.mark.parametrize("mode", ["staged_one_device", "two_devices"])
+def test_stereo_right_extractor_on_another_device(orbgpu_mod, oracle_mod, monkeypatch, mode):
+    """C4 places each camera stream on its own GPU: the right image and pyramid then move to the left
+    device (hipMemcpyPeerAsync) before the window search.  On a one-GPU box the same staging is forced
+    with ORBGPU_STEREO_STAGE=1; with two GPUs the right extractor runs on device 1."""
+    ndev = orbgpu_mod.device_count()
+    if mode == "two_devices" and ndev < 2:
+        pytest.skip("one GPU visible")
+    if mode == "staged_one_device":
+        monkeypatch.setenv("ORBGPU_STEREO_STAGE", "1")
+    left, right = _pair(1280, 720, 4)
+    kl, dl, kr, dr, ou, od, on = _oracle(oracle_mod, left, right, 2000)
+    gl = orbgpu_mod.ORBextractor(2000, 1.2, 8, 20, 7, device=0)
+    gr = orbgpu_mod.ORBextractor(2000, 1.2, 8, 20, 7, device=1 if mode == "two_devices" else 0)
+    gkl, gdl = gl(left)
+    gkr, gdr = gr(right)
+    assert gkr.tobytes() == kr.tobytes() and np.array_equal(gdr, dr)
+    u, d, n = orbgpu_mod.compute_stereo_matches(gl, gr, gkl, gdl, gkr, gdr, MB, MB * FX)
+    assert n == on > 20
+    assert u.tobytes() == ou.tobytes() and d.tobytes() == od.tobytes()

@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
-"""Copy the summaries of a tools/gpu_round.sh run from gpurun_out/ into profiles/ (tracked).
+"""Copy the summaries of a tools/gpu_round.sh run from gpurun_out/ into profiles/<round>/ (tracked).
 
-Usage: python3 tools/collect_profiles.py <tag>   e.g. r01_v3
-Writes profiles/<tag>_bench.json, <tag>_kernel_stats.csv, <tag>_pytest_gpu.log, <tag>_pmc.json and
-refreshes profiles/pmc_traffic.json (read by bench.py for roofline.traffic / roofline.valu), stamped
-with the git commit the measured code came from.
+Usage: python3 tools/collect_profiles.py r02 v1
+Writes profiles/r02/v1_<bench|bench_c2|bench_c5>.json (the JSON lines), v1_kernel_stats.csv (rocprofv3
+--kernel-trace --stats of the timed loop, two batches in flight), v1_kernel_stats_serial.csv (the same
+loop one batch at a time: the per-launch durations the bench's roofline pass measures), v1_pytest_gpu.txt
+and, when PMC passes ran, v1_pmc.json, refreshing profiles/pmc_traffic.json (read by bench.py for
+roofline.traffic / roofline.valu), stamped with the git commit the measured code came from.
 """
 import json
 import os
@@ -14,34 +16,47 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
-PROF = os.path.join(ROOT, "profiles")
 
 
 def main():
-    tag = sys.argv[1]
+    rnd, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(prof, exist_ok=True)
     commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                             text=True).stdout.strip()
     dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--", "orb-slam-birdview_amd", "include"],
                            capture_output=True, text=True).stdout.strip()
     if dirty:
         commit += "+dirty"
-    lines = [l for l in open(os.path.join(OUT, "bench.log")).read().splitlines() if l.startswith("{")]
-    with open(os.path.join(PROF, f"{tag}_bench.json"), "w") as f:
-        f.write(lines[-1] + "\n")
-    shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_kernel_stats.csv"))
-    shutil.copy(os.path.join(OUT, "pytest_gpu.log"), os.path.join(PROF, f"{tag}_pytest_gpu.log"))
+    main_line = None
+    for name in ("bench", "bench_c2", "bench_c5"):
+        p = os.path.join(OUT, name + ".log")
+        if not os.path.exists(p):
+            continue
+        lines = [l for l in open(p).read().splitlines() if l.startswith("{")]
+        if lines:
+            with open(os.path.join(prof, f"{tag}_{name}.json"), "w") as f:
+                f.write(lines[-1] + "\n")
+            if name == "bench":
+                main_line = json.loads(lines[-1])
+    for src, dst in (("prof", "kernel_stats.csv"), ("prof_serial", "kernel_stats_serial.csv")):
+        p = os.path.join(OUT, src, "run_kernel_stats.csv")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(prof, f"{tag}_{dst}"))
+    if os.path.exists(os.path.join(OUT, "pytest_gpu.log")):
+        shutil.copy(os.path.join(OUT, "pytest_gpu.log"), os.path.join(prof, f"{tag}_pytest_gpu.txt"))
     rep = os.path.join(OUT, "pmc", "report.json")
-    if os.path.exists(rep):
+    if os.path.exists(rep) and main_line:
         d = json.load(open(rep))
         d["commit"] = commit
-        d["batch_frames_per_launch"] = json.loads(lines[-1])["config"]["batch_per_gpu"]
-        d["config"] = "C3 1280x720, 2000 features, bench.py --steps 3 --warmup 1 --no-cpu"
+        d["batch_frames_per_launch"] = main_line["config"]["batch_per_gpu"]
+        d["config"] = "C3 1280x720, 2000 features, bench.py --steps 3 --warmup 1 --only-extract --no-profile-pass"
         d["method"] = ("tools/pmc.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_* --kernel-trace (separate "
                        "passes); tools/pmc_calib.hip known-byte streams give the per-width factor")
-        for name in (f"{tag}_pmc.json", "pmc_traffic.json"):
-            with open(os.path.join(PROF, name), "w") as f:
+        for path in (os.path.join(prof, f"{tag}_pmc.json"), os.path.join(ROOT, "profiles", "pmc_traffic.json")):
+            with open(path, "w") as f:
                 json.dump(d, f, indent=1)
-    print("collected", tag, "commit", commit)
+    print("collected", rnd, tag, "commit", commit)
 
 
 if __name__ == "__main__":

@@ -6,7 +6,7 @@
 OUT=gpurun_out/pmc; mkdir -p $OUT; export TMPDIR=/tmp
 # only the batch launches: the host-path, stereo and C4 legs would mix 1- and 2-frame dispatches
 # into the per-launch means
-ARGS="--steps 3 --warmup 1 --no-cpu --no-host-path --no-stereo --no-c4 ${BENCH_ARGS}"
+ARGS="--steps 3 --warmup 1 --only-extract --no-profile-pass ${BENCH_ARGS}"
 timeout -k 10 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/pmc_calib tools/pmc_calib.hip || { echo "calib build failed"; exit 1; }
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/calib_$ctr -o run -- /tmp/pmc_calib > $OUT/calib_$ctr.log 2>&1 || { echo "calib $ctr failed"; tail -20 $OUT/calib_$ctr.log; exit 1; }
