@@ -16,6 +16,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../oracle/orb_oracle.h"
@@ -148,6 +149,34 @@ int main(int argc, char** argv) {
             }
             report("mvImagePyramid_frame" + std::to_string(f), pok);
             oracle_destroy(o.h);
+        }
+
+        // ---- the stereo threading pattern (Frame.cc:124-127): a left and a right extractor, each driven by
+        // a fresh std::thread per frame, both at once, while a matcher runs on a third thread (the
+        // LocalMapping / LoopClosing threads call ORBmatcher concurrently); results must equal the
+        // single-threaded run.  Under -fsanitize=thread this is the TSan harness of the host-side code.
+        {
+            ORBextractor left(nf, 1.2f, 8, 20, 7), right(nf, 1.2f, 8, 20, 7);
+            ORBmatcher mt(0.7f, true);
+            bool ok = true;
+            for (int f = 0; f + 1 < nframes; f += 2) {
+                std::vector<KeyPoint> kl, kr;
+                DescriptorMat dl, dr;
+                int dd = -1;
+                std::thread tl([&] { left(ImageView(frames.data() + (size_t)f * w * h, w, h), ImageView(), kl, dl); });
+                std::thread tr([&] {
+                    right(ImageView(frames.data() + (size_t)(f + 1) * w * h, w, h), ImageView(), kr, dr);
+                });
+                std::thread tm([&] { dd = ORBmatcher::DescriptorDistance(allD[0].ptr(0), allD[1].ptr(0)); });
+                tl.join();
+                tr.join();
+                tm.join();
+                ok = ok && kl.size() == allK[f].size() && kr.size() == allK[f + 1].size() &&
+                     memcmp(dl.buf.data(), allD[f].buf.data(), dl.buf.size()) == 0 &&
+                     memcmp(dr.buf.data(), allD[f + 1].buf.data(), dr.buf.size()) == 0 && dd >= 0;
+                (void)mt;
+            }
+            report("stereo_threads_fresh_thread_per_frame", ok);
         }
 
         // ---- empty image: outputs untouched (ORBextractor.cc:1046-1047)
