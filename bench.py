@@ -156,6 +156,12 @@ def algorithmic_bytes(w, h, kps_per_frame, cands_per_frame):
 
 
 PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
+# Measured VALU issue ceiling of the integer VOP3 / VOP3P class these kernels are made of (v_perm,
+# v_alignbyte, v_pk_*_u16, v_min3/max3, v_dot4/dot2, v_mul_u32_u24, v_max_i32): 4.33 cycles per wave64
+# instruction per SIMD at the 2.4 GHz nominal clock, 8 waves per SIMD (tools/valu_rate.hip,
+# profiles/r02/valu_rate.txt); v_add_u32 / v_add_f32 / v_fma_f32 issue at 2.5.
+VALU_INT_CYCLES = 4.33
+VALU_INT_CEIL = 256 * 4 * 2.4e9 / VALU_INT_CYCLES   # wave64 instructions per second, whole chip
 
 
 def read_pmc(kernel, batch):
@@ -521,10 +527,14 @@ def main():
                     "algorithmic_bytes_per_launch": int(ab[dom] * B / launches_per_step),
                     "algorithmic_bytes_per_frame": int(ab[dom]), "launches_per_step": launches_per_step,
                     "kernel_avg_launch_us": round(launch_s * 1e6, 2),
-                    # the kernel's real limiter is VALU issue: PMC SQ_INSTS_VALU x 64 lanes per launch / launch time
-                    "valu": ({"achieved_lane_ops_per_s": round(valu_insts * 64 / launch_s, 1),
-                              "peak_lane_ops_per_s": PEAK_VALU_LANE_OPS,
-                              "frac": round(valu_insts * 64 / launch_s / PEAK_VALU_LANE_OPS, 4),
+                    # the kernel's real limiter is VALU issue: PMC SQ_INSTS_VALU per launch / launch time, against
+                    # the measured issue ceiling of the integer instruction class it is made of
+                    "valu": ({"achieved_wave_insts_per_s": round(valu_insts / launch_s, 1),
+                              "ceiling_wave_insts_per_s": round(VALU_INT_CEIL, 1),
+                              "frac": round(valu_insts / launch_s / VALU_INT_CEIL, 4),
+                              "ceiling": "measured: 4.33 cycles per wave64 integer VOP3/VOP3P instruction per SIMD "
+                                         "(tools/valu_rate.hip, profiles/r02/valu_rate.txt)",
+                              "dual_rate_frac": round(valu_insts * 64 / launch_s / PEAK_VALU_LANE_OPS, 4),
                               "valu_insts_per_launch": valu_insts, "pmc_source": pmc_src}
                              if valu_insts else None),
                     "pipeline": {"bytes_per_frame": int(ab["pipeline"]),
