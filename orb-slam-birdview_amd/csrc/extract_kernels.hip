@@ -272,9 +272,11 @@ __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
     }
     int A = 0, Bn = 0;   // clamped at 0: only positive strengths matter (thresholds are >= 0)
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        A = max(A, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));    // dark arc:   all v - p
-        Bn = min(Bn, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15]));  // bright arc: all p - v
+    for (int k = 0; k < 16; k += 2) {   // two arcs per v_max3 / v_min3
+        A = max(max(A, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15])),
+                min(min(m3[k + 1], m3[(k + 4) & 15]), m3[(k + 7) & 15]));   // dark arc:   all v - p
+        Bn = min(min(Bn, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15])),
+                 max(max(x3[k + 1], x3[(k + 4) & 15]), x3[(k + 7) & 15]));  // bright arc: all p - v
     }
     return max(A, -Bn);
 }
@@ -301,6 +303,12 @@ void build_cells(const Geom& g, std::vector<CellDesc>& cells) {
                 d.xoyo = (3 + cj * L.wCell) | ((3 + ci * L.hCell) << 16);
                 d.pitch = L.pitch;
                 d.pyr_off = (int)L.pyr_off;
+                const int x0w = iniX >> 2, nw = std::max(1, ((iniX + rw + 3) >> 2) - x0w);
+                const int nruns = std::max(1, (rw - 6 + 7) / 8);
+                d.roi = nw | ((64 / nw) << 8) | (x0w << 16);
+                d.m_nw = (int)recip20((uint32_t)nw);
+                d.runs = nruns | ((64 / nruns) << 8);
+                d.m_runs = (int)recip20((uint32_t)nruns);
             }
     }
 }
@@ -312,7 +320,7 @@ __device__ __forceinline__ unsigned roi_off(int yy, int stride, int cb) {
 }
 
 struct FastCellT {
-    int f, cell, iniX, rw, rh, dw, dh, x0w, nw, out_off, xo, yo;
+    int f, cell, iniX, rw, rh, dw, dh, x0w, nw, rpr, m_nw, nruns, rpi, m_runs, out_off, xo, yo;
     bool valid, aligned;
     const uint8_t* base;   // ROI row 0, column 0
     int stride;
@@ -339,8 +347,13 @@ __device__ __forceinline__ FastCellT fast_cell_t(const Geom* __restrict__ g, con
     c.stride = l == 0 ? rowStride : d.pitch;
     c.base = lp + (long long)d.iniY * c.stride;
     c.aligned = ((reinterpret_cast<uintptr_t>(lp) | (uintptr_t)c.stride) & 3) == 0;
-    c.x0w = c.iniX >> 2;
-    c.nw = ((c.iniX + c.rw + 3) >> 2) - c.x0w;
+    c.nw = d.roi & 0xFF;
+    c.rpr = (d.roi >> 8) & 0xFF;
+    c.x0w = d.roi >> 16;
+    c.m_nw = d.m_nw;
+    c.nruns = d.runs & 0xFF;
+    c.rpi = (d.runs >> 8) & 0xFF;
+    c.m_runs = d.m_runs;
     return c;
 }
 
@@ -370,8 +383,7 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 
 __device__ __forceinline__ int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
 
-// q = x / n for x < 2^20 / n via a 20-bit reciprocal (wave-uniform n <= 64): two VALU ops, exact.
-__device__ __forceinline__ uint32_t recip20(uint32_t n) { return ((1u << 20) + n - 1) / n; }
+// q = x / n for x < 2^20 / n via the 20-bit reciprocal m = recip20(n) (n <= 64): two VALU ops, exact.
 __device__ __forceinline__ uint32_t div20(uint32_t x, uint32_t m) { return __umul24(x, m) >> 20; }
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
@@ -386,7 +398,7 @@ __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {   // per 
 // set where the pixel may be a corner at threshold t.  Bright: (v+t) - p < 0, dark: p - (v-t) < 0;
 // the four cyclically adjacent compass pairs reduce to (b0|b8) & (b4|b12).
 // As min/max: bright needs min(max(p0, p8), max(p4, p12)) > v + t, dark max(min(p0, p8), min(p4, p12))
-// < v - t (v_pk_max_u16 / v_pk_min_u16: 11 packed ops for the two pixels instead of 16).
+// < v - t, i.e. max(hi - v, v - lo) > t (10 packed ops for the two pixels instead of 16).
 typedef unsigned short ushort2_pk __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p4, uint32_t p8, uint32_t p12,
                                              uint32_t tt) {
@@ -396,8 +408,10 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
                                                                                __builtin_elementwise_max(a4, a12)));
     const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
                                                                                __builtin_elementwise_min(a4, a12)));
-    const uint32_t vt = pk_add16(v, tt), vmt = pk_sub16(v, tt);   // v + t, v - t (per lane)
-    return pk_sub16(vt, hi) | pk_sub16(lo, vmt);
+    // bright (hi > v + t) or dark (lo < v - t)  <=>  max(hi - v, v - lo) > t: the sign of t - max
+    const short2_t d = __builtin_elementwise_max(__builtin_bit_cast(short2_t, pk_sub16(hi, v)),
+                                                 __builtin_bit_cast(short2_t, pk_sub16(v, lo)));
+    return pk_sub16(tt, __builtin_bit_cast(uint32_t, d));
 }
 
 // optional phase timestamps (ORBGPU_FAST_STAMPS=1): s_memtime at the phase boundaries, lane 0
@@ -418,9 +432,8 @@ struct RoiLanes {
 __device__ __forceinline__ RoiLanes roi_lanes(const FastCellT& c, int lane) {
     RoiLanes r;
     const int nw = __builtin_amdgcn_readfirstlane(c.nw), stride = __builtin_amdgcn_readfirstlane(c.stride);
-    const uint32_t m = recip20(nw);
-    r.rpr = (int)div20(64, m);
-    r.yy0 = (int)div20(lane, m);
+    r.rpr = c.rpr;
+    r.yy0 = (int)div20(lane, c.m_nw);
     r.ww = lane - r.yy0 * nw;
     r.off = (int)roi_off(r.yy0, stride, 4 * r.ww);
     // the cell is wave-uniform (readfirstlane returns int: zero-extend both halves)
@@ -480,9 +493,9 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
     wave_lds_sync();
     ORBGPU_STAMP(1);
     // lane -> (run of PX = 8 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
-    const int nruns = (dw + PX - 1) / PX;
-    const int rpi = 64 / nruns;                          // rows per iteration
-    const int lrow = (int)div20(lane, recip20(nruns));
+    const int nruns = c.nruns;                           // (dw + PX - 1) / PX
+    const int rpi = c.rpi;                               // rows per iteration, 64 / nruns
+    const int lrow = (int)div20(lane, c.m_runs);
     const int x0 = PX * (lane - lrow * nruns);
     const bool lane_on = lrow < rpi;
     const uint32_t xvalid = x0 + PX <= dw ? (1u << PX) - 1u : (1u << max(dw - x0, 0)) - 1u;
@@ -578,17 +591,13 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const uint8_t* q = sM + (p >> 6) * SP + (p & 63) + SP + 1;
                 const int m = q[0];
                 const int s = m - 1;
-                k = true;
-#pragma unroll
-                for (int oy = -1; oy <= 1; oy++) {
-#pragma unroll
-                    for (int ox = -1; ox <= 1; ox++) {
-                        if (ox == 0 && oy == 0) continue;
-                        const int mn = q[oy * SP + ox];
-                        const int sn = mn > th ? mn - 1 : 0;
-                        k = k && (s > sn);
-                    }
-                }
+                // the reference keeps score s = M - 1 iff s > sn for every neighbour, sn = Mn - 1 for a
+                // corner neighbour (Mn > th) and 0 otherwise.  A neighbour with Mn <= th < M is below M
+                // anyway, so this is M > max(every Mn, 1)
+                const int n0 = max(max((int)q[-SP - 1], (int)q[-SP]), (int)q[-SP + 1]);
+                const int n1 = max(max((int)q[-1], (int)q[1]), 1);
+                const int n2 = max(max((int)q[SP - 1], (int)q[SP]), (int)q[SP + 1]);
+                k = m > max(max(n0, n1), n2);
                 packed = (uint32_t)((p & 63) + c.xo) | ((uint32_t)((p >> 6) + c.yo) << 12) | ((uint32_t)s << 24);
             }
             const unsigned long long km = __ballot(k);

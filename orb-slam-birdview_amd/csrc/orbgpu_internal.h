@@ -76,7 +76,16 @@ struct CellDesc {
     int xoyo;      // output coordinate offsets (3 + cj*wCell) | (3 + ci*hCell) << 16 (:822-823)
     int pitch;     // level row pitch (levels >= 1)
     int pyr_off;   // level offset in a frame's pyramid slot (levels >= 1)
+    // lane mappings of k_fast_wave, precomputed so the kernel divides nothing (a wave-uniform 32-bit
+    // division costs ~15 VALU instructions, one of them a transcendental v_rcp):
+    int roi;       // ROI load: dwords per row nw | rows per round (64 / nw) << 8 | first dword (iniX >> 2) << 16
+    int m_nw;      // recip20(nw)
+    int runs;      // prefilter: 8-pixel runs per row nruns | rows per round (64 / nruns) << 8
+    int m_runs;    // recip20(nruns)
+    int pad[4];    // 64 bytes: one scalar dwordx16 load
 };
+// q = x / n for x < 2^20 / n, from m = recip20(n) (host and device)
+__host__ __device__ inline uint32_t recip20(uint32_t n) { return ((1u << 20) + n - 1) / n; }
 
 // cv::resize INTER_LINEAR coefficient tables (OpenCV 3.2 imgwarp.cpp), one entry per dst column/row.
 struct ResizeCoef {
