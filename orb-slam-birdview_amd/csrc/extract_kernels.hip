@@ -1226,6 +1226,17 @@ __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
     return lb & ~la;
 }
 
+// The IC_Angle byte masks of lane r < 31 (patch row v = r - 15): bytes of the 8 aligned row dwords with
+// |u| <= umax[|v|], umax (:454-469) packed 4 bits per row [15,15,15,15,14,14,14,13,13,12,11,10,9,8,6,3].
+// The same for every keypoint: computed once per wave.
+__device__ __forceinline__ void ic_masks(int lane, uint32_t (&icm)[8]) {
+    constexpr unsigned long long kUmax = 0x3689ABCDDEEEFFFFull;
+    const int v = min(lane, 30) - 15;
+    const int d = (int)((kUmax >> (4 * abs(v))) & 15);
+#pragma unroll
+    for (int i = 0; i < 8; i++) icm[i] = byte_range_mask(15 - d, 15 + d, i);
+}
+
 // One keypoint slot of k_describe: decoded from the octree output (level, coordinates, output index).
 struct DescSlot {
     bool ok, interior;   // a keypoint; its 48-byte aligned window rows stay inside the level (dword loads)
@@ -1326,23 +1337,48 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
     }
 }
 
+// The 7-tap Gaussian as byte weights shifted to each of the four byte alignments of an output's
+// 7-byte run within aligned window dwords: alignment r uses dwords a, a+1 (and a+2 for r >= 2) with
+// KA[r], KB[r] (, KC[r]), so no byte run is ever realigned (10 v_dot4 per 4 outputs instead of 8 v_dot4
+// and 6 v_alignbyte).
+struct GaussShift {
+    uint32_t ka[4], kb[4], kc[4];
+};
+
+__device__ __forceinline__ GaussShift gauss_shift(const int* gk) {
+    auto b4 = [](int x0, int x1, int x2, int x3) {
+        return (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)x2 << 16) | ((uint32_t)x3 << 24);
+    };
+    GaussShift k;
+    k.ka[0] = b4(gk[0], gk[1], gk[2], gk[3]);
+    k.kb[0] = b4(gk[4], gk[5], gk[6], 0);
+    k.kc[0] = 0;
+    k.ka[1] = b4(0, gk[0], gk[1], gk[2]);
+    k.kb[1] = b4(gk[3], gk[4], gk[5], gk[6]);
+    k.kc[1] = 0;
+    k.ka[2] = b4(0, 0, gk[0], gk[1]);
+    k.kb[2] = b4(gk[2], gk[3], gk[4], gk[5]);
+    k.kc[2] = b4(gk[6], 0, 0, 0);
+    k.ka[3] = b4(0, 0, 0, gk[0]);
+    k.kb[3] = b4(gk[1], gk[2], gk[3], gk[4]);
+    k.kc[3] = b4(gk[5], gk[6], 0, 0);
+    return k;
+}
+
 // k_describe row pass, 8 rounds of one lane: RT[4gq + o][wy] = sum_t k_t * window[wy][SH + 4gq + o + t]
 // (the window row starts SH bytes into its first dword)
 template <int SH>
-__device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, uint32_t K0123, uint32_t K456) {
+__device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, const GaussShift& K) {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         uint32_t w[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) w[i] = rw[72 * r + i];
-        // bytes b .. b+3 of w[0..3]
-        auto run = [&](int b) -> uint32_t {
-            return (b & 3) == 0 ? w[b >> 2] : __builtin_amdgcn_alignbyte(w[(b >> 2) + 1], w[b >> 2], b & 3);
-        };
 #pragma unroll
         for (int o = 0; o < 4; o++) {
-            const uint32_t v = __builtin_amdgcn_udot4(run(SH + o + 4), K456, __builtin_amdgcn_udot4(run(SH + o), K0123, 0u, false),
-                                                      false);
+            const int b = SH + o, a = b >> 2, al = b & 3;
+            uint32_t v = __builtin_amdgcn_udot4(w[a + 1], K.kb[al], __builtin_amdgcn_udot4(w[a], K.ka[al], 0u, false), false);
+            if (al >= 2) v = __builtin_amdgcn_udot4(w[a + 2], K.kc[al], v, false);
             rq[o * kRtPitch + 6 * r] = (uint16_t)v;
         }
     }
@@ -1394,12 +1430,11 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 
     // ---- IC_Angle (:77-104) on the unblurred window: lane r < 31 sums row v = r - 15 over the
     // circular patch |u| <= umax[|v|] with v_dot4_u32_u8 (u*I = (u+16)*I - 16*I).
-    // umax (:454-469) packed 4 bits per row: [15,15,15,15,14,14,14,13,13,12,11,10,9,8,6,3]
-    constexpr unsigned long long kUmax = 0x3689ABCDDEEEFFFFull;
     int m10 = 0, m01 = 0;
     if (lane < 31) {
         const int v = lane - 15;
-        const int d = (int)((kUmax >> (4 * abs(v))) & 15);
+        uint32_t icm[8];
+        ic_masks(lane, icm);
         const int base = (21 + v) * kDescWinPitch + sh + 6;   // byte of u = -15
         const int d0 = base >> 2, bs = base & 3;
         uint32_t w[9];
@@ -1408,7 +1443,7 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
         uint32_t sI = 0, sW = 0;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const uint32_t bytes = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs) & byte_range_mask(15 - d, 15 + d, i);
+            const uint32_t bytes = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs) & icm[i];
             // weights (u + 16) for u = 4i-15 .. 4i-12  ->  4i+1 .. 4i+4
             const uint32_t wt = (uint32_t)(4 * i + 1) | ((uint32_t)(4 * i + 2) << 8) | ((uint32_t)(4 * i + 3) << 16) |
                                 ((uint32_t)(4 * i + 4) << 24);
@@ -1426,9 +1461,7 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass: item = (row wy, 4 outputs
     // rx = 4g..4g+3) over window bytes 4g..4g+9; output o = v_dot4(bytes o..o+3, k0..k3) +
     // v_dot4(bytes o+4..o+7, k4 k5 k6 0) (the 8-bit taps sum to 257, so every sum fits 16 bits).
-    const uint32_t K0123 = (uint32_t)g->gk[0] | ((uint32_t)g->gk[1] << 8) | ((uint32_t)g->gk[2] << 16) |
-                           ((uint32_t)g->gk[3] << 24);
-    const uint32_t K456 = (uint32_t)g->gk[4] | ((uint32_t)g->gk[5] << 8) | ((uint32_t)g->gk[6] << 16);
+    const GaussShift K = gauss_shift(g->gk);
     // lane = (row wy0 = lane / 10, group gq = lane % 10), round r takes row wy0 + 6r: the read and store
     // addresses are the lane's base plus immediate offsets.  8 rounds cover rows 0..47; rows 43..47 are
     // scratch (they read past the window, inside the workgroup's LDS, into RT rows no sample reads
@@ -1439,10 +1472,10 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
         const uint32_t* rw = w32 + wy0 * 12 + gq;
         uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy0;   // RT[4gq + j][wy]
         switch (sh) {
-            case 0: desc_row_pass<0>(rw, rq, K0123, K456); break;
-            case 1: desc_row_pass<1>(rw, rq, K0123, K456); break;
-            case 2: desc_row_pass<2>(rw, rq, K0123, K456); break;
-            default: desc_row_pass<3>(rw, rq, K0123, K456); break;
+            case 0: desc_row_pass<0>(rw, rq, K); break;
+            case 1: desc_row_pass<1>(rw, rq, K); break;
+            case 2: desc_row_pass<2>(rw, rq, K); break;
+            default: desc_row_pass<3>(rw, rq, K); break;
         }
     }
     wave_lds_sync();
