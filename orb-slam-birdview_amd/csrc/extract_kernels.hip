@@ -43,6 +43,14 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
+// (a * b) >> 32 for a, b < 2^24: v_mul_hi_u32_u24 (the compiler does not form it from 64-bit products)
+__device__ __forceinline__ unsigned mul_hi_u24(unsigned a, unsigned b) {
+    unsigned r;
+    asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+typedef unsigned int uint32x4_t __attribute__((ext_vector_type(4)));
+
 /* ------------------------------------------------------------------------------------------------
  * Pyramid: cv::resize(level l-1 -> level l, INTER_LINEAR) for every frame of the batch
  * (ComputePyramid, ORBextractor.cc:1118-1120).  OpenCV-3.x 8U fixed point: 11-bit horizontal
@@ -110,12 +118,17 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         const int nq = ((sx1 - sx0) >> 4) + 1;
         const unsigned magic = (65536u + nq - 1) / nq;                  // i / nq for i < 4096, nq <= 17
         const int total = nr * nq;
+        // a buffer descriptor over the span (SGPRs): 32-bit row offsets (r * stride < 2^24 * 100 fits), no
+        // 64-bit address arithmetic per chunk
+        const uint64_t pb = reinterpret_cast<uint64_t>(base);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pb), 0, 0x7FFFFFFF, 0x00020000);
         uint4 v[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {   // unconditional (clamped) loads: all in flight before the first wait
             const int i = min(tid + 256 * k, total - 1);
-            const int r = (int)(((unsigned)i * magic) >> 16), q = i - r * nq;
-            v[k] = reinterpret_cast<const uint4*>(base + (long long)r * src.stride)[q];
+            const int r = (int)(__umul24((unsigned)i, magic) >> 16), q = i - (int)__umul24((unsigned)r, (unsigned)nq);
+            const uint32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)__umul24((unsigned)r, (unsigned)src.stride) + 16 * q, 0, 0);
+            v[k] = make_uint4(w[0], w[1], w[2], w[3]);
         }
         if (tid < kRsTileW) {
             const ResizeCoef c = coef[x0 + min(tid, nx - 1)];
@@ -128,7 +141,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
 #pragma unroll
         for (int k = 0; k < kPer; k++) {   // clamped duplicates store the same bytes to the same place
             const int i = min(tid + 256 * k, total - 1);
-            const int r = (int)(((unsigned)i * magic) >> 16), q = i - r * nq;
+            const int r = (int)(__umul24((unsigned)i, magic) >> 16), q = i - (int)__umul24((unsigned)r, (unsigned)nq);
             *reinterpret_cast<uint4*>(&s_src[r * kRsPitch + 16 * q]) = v[k];
         }
     } else {
@@ -194,6 +207,9 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
             const int ty = pass * 8 + (tid >> 5);
             if (ty >= ny) break;
             const int4 cy = s_cy[ty];
+            // (c * (h >> 4)) >> 16 == mul_hi_u24(c << 12, h & ~15): c <= 2048 and h < 2^19 keep both
+            // operands within 24 bits
+            const unsigned cy0 = (unsigned)cy.z << 12, cy1 = (unsigned)cy.w << 12;
             const uint32_t* q0 = reinterpret_cast<const uint32_t*>(&s_src[(cy.x - sy0) * kRsPitch]) + bw;
             const uint32_t* q1 = reinterpret_cast<const uint32_t*>(&s_src[(cy.y - sy0) * kRsPitch]) + bw;
             const uint32_t u0 = q0[0], u1 = q0[1], u2 = q0[2], w0 = q1[0], w1 = q1[1], w2 = q1[2];
@@ -206,10 +222,10 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
                                                            __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(a1, a0, sel[i])), 0u, false);
                 const unsigned h1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cc[i]),
                                                            __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(b1, b0, sel[i])), 0u, false);
-                const unsigned v = ((__umul24((unsigned)cy.z, h0 >> 4) >> 16) + (__umul24((unsigned)cy.w, h1 >> 4) >> 16) + 2) >> 2;
+                const unsigned v = (mul_hi_u24(cy0, h0 & ~15u) + mul_hi_u24(cy1, h1 & ~15u) + 2) >> 2;
                 packed |= v << (8 * i);
             }
-            *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + ty) * pitch) = packed;
+            *reinterpret_cast<uint32_t*>(dst + __umul24((unsigned)(y0 + ty), (unsigned)pitch)) = packed;
         }
         return;
     }
