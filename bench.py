@@ -599,10 +599,32 @@ def main():
             k_, d_ = hx(frames[i])
             nkp += len(k_)
         t1h = time.perf_counter()
-        host_path = {"frames_per_s": round(nh / (t1h - t0h), 1), "features_per_s": round(nkp / (t1h - t0h), 1),
-                     "ms_per_frame": round((t1h - t0h) / nh * 1e3, 3),
-                     "note": "orb_extract per host frame: upload + graph replay + one download, one frame in flight"}
+        py_ms = (t1h - t0h) / nh * 1e3
         hx.close()
+        # the same boundary through the C++ mirror (ORB_SLAM2::ORBextractor::operator(), as Frame::ExtractORB
+        # calls it), timed in a child process: the drop-in caller's latency without Python overhead
+        cpp = None
+        exe = os.path.join(ROOT, "tools", "host_latency")
+        if os.path.exists(exe):
+            import tempfile
+            nfr = min(16, len(frames))
+            with tempfile.NamedTemporaryFile(suffix=".raw", delete=False) as tf:
+                for i in range(nfr):
+                    tf.write(np.ascontiguousarray(frames[i]).tobytes())
+                raw = tf.name
+            try:
+                r = subprocess.run([exe, raw, str(w), str(h), str(nfr), str(nf), "200", str(local)],
+                                   capture_output=True, text=True, timeout=120)
+                if r.returncode == 0:
+                    cpp = json.loads(r.stdout.strip().splitlines()[-1])
+            finally:
+                os.unlink(raw)
+        ms = cpp["ms_per_frame_median"] if cpp else py_ms
+        host_path = {"frames_per_s": round(1e3 / ms, 1), "features_per_s": round(per_frame_kps * 1e3 / ms, 1),
+                     "ms_per_frame": round(ms, 4), "caller": "C++ mirror (tools/host_latency)" if cpp else "python",
+                     "cpp": cpp, "python_ms_per_frame": round(py_ms, 4),
+                     "note": "ORBextractor::operator() per host frame: upload + graph replay + one download, one "
+                             "frame in flight, median of 200"}
 
     # ---- birdview stream (BASELINE C4's bird stream): Frame.cc:320-342 fused on one
     # device-resident image + mask per call (orb_bird_extract_device); synchronous per frame (the host

@@ -1163,13 +1163,13 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
                                                            uint16_t* __restrict__ knodeAll,
                                                            uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
                                                            int* __restrict__ err, int lds_keys,
-                                                           unsigned long long* __restrict__ ostamps) {
+                                                           unsigned long long* __restrict__ ostamps, int lbase) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int NC = g->node_cap;
     const int tid = threadIdx.x;
     constexpr int NT = kOctreeThreads;
     // frames along x so that every frame's level-0 block (the longest) is dispatched first
-    const int f = blockIdx.x, l = blockIdx.y;
+    const int f = blockIdx.x, l = lbase + (int)blockIdx.y;
     const LevelGeom& L = g->L[l];
     int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
     int* sv = sc + 32;
@@ -1623,8 +1623,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                           int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
     if (nframes <= 0) return hipSuccess;
-    if (marker) marker(user, ORB_K_RESIZE, 1, stream);
-    for (int l = 1; l < g.nlevels; l++) {
+    auto resize = [&](int l, hipStream_t s) {
         // 32-row tiles where the level's source spans fit the LDS tile, else 16-row tiles, else the
         // untiled kernel (large scale factors): chosen per level from the geometry (LevelGeom::rs_tiled)
         const int t = g.L[l].rs_tiled;
@@ -1633,44 +1632,50 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
             const int th = (t & 2) ? 32 : 16;
             const dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
             if (th == 32)
-                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames, frame_pitch,
+                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames, frame_pitch,
                                    row_stride, b.d_pyr);
             else
-                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, stream, b.d_geom, cf, l, d_frames, frame_pitch,
+                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames, frame_pitch,
                                    row_stride, b.d_pyr);
         } else {
-            hipLaunchKernelGGL(k_resize, dim3(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes), dim3(256), 0, stream,
+            hipLaunchKernelGGL(k_resize, dim3(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes), dim3(256), 0, s,
                                b.d_geom, cf, l, d_frames, frame_pitch, row_stride, b.d_pyr);
         }
-    }
-    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
-    if (marker) marker(user, ORB_K_FAST, 1, stream);
-    {   // one-wave workgroups, two (frame, cell) items per wave (a workgroup's LDS is held until its
-        // slowest wave ends, so single waves waste the least of a CU on uneven cells)
-        const int items = g.ncells * nframes;
+    };
+    // FAST over cells [cbeg, cbeg + cnum) of every frame: one-wave workgroups, two (frame, cell) items per
+    // wave (a workgroup's LDS is held until its slowest wave ends, so single waves waste the least of a
+    // CU on uneven cells)
+    auto fast = [&](int cbeg, int cnum, hipStream_t s, int* zero) {
+        const int items = cnum * nframes;
         auto kern = g.fast_compact ? k_fast_wave<56, 40> : k_fast_wave<kFastTilePitch, 64>;
-        hipLaunchKernelGGL(kern, dim3(cdiv(items, 2)), dim3(64), (size_t)g.fast_wave_bytes, stream, b.d_geom, b.d_cells,
-                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, 0, g.ncells,
-                           b.d_stamps, b.zero_err ? b.d_err : nullptr);
-    }
-    if (marker) marker(user, ORB_K_FAST, 0, stream);
-    if (marker) marker(user, ORB_K_OCTREE, 1, stream);
-    {
+        hipLaunchKernelGGL(kern, dim3(cdiv(items, 2)), dim3(64), (size_t)g.fast_wave_bytes, s, b.d_geom, b.d_cells,
+                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum,
+                           b.d_stamps, zero);
+    };
+    auto octree = [&](int lbase, int nl, hipStream_t s) {
         const int lk = octree_lds_keys(g.node_cap);
-        hipLaunchKernelGGL(k_octree, dim3(nframes, g.nlevels), dim3(kOctreeThreads),
-                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, stream, b.d_geom, b.d_cands, b.d_cellCount,
-                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
-                           b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr);
-    }
-    if (marker) marker(user, ORB_K_OCTREE, 0, stream);
-    if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
-    {
+        hipLaunchKernelGGL(k_octree, dim3(nframes, nl), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap) + (size_t)lk * 6,
+                           s, b.d_geom, b.d_cands, b.d_cellCount, b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err,
+                           lk, b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
+    };
+    auto describe = [&](hipStream_t s) {
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
         const unsigned gx = cdiv(g.nkpcap, kDescWaves * kDescSlotsPerWave);
-        hipLaunchKernelGGL(k_describe, dim3(gx * nframes), dim3(64 * kDescWaves), 0, stream, b.d_geom, d_frames,
-                           frame_pitch, row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap,
-                           dst);
-    }
+        hipLaunchKernelGGL(k_describe, dim3(gx * nframes), dim3(64 * kDescWaves), 0, s, b.d_geom, d_frames, frame_pitch,
+                           row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap, dst);
+    };
+    int* zero = b.zero_err ? b.d_err : nullptr;
+    if (marker) marker(user, ORB_K_RESIZE, 1, stream);
+    for (int l = 1; l < g.nlevels; l++) resize(l, stream);
+    if (marker) marker(user, ORB_K_RESIZE, 0, stream);
+    if (marker) marker(user, ORB_K_FAST, 1, stream);
+    fast(0, g.ncells, stream, zero);
+    if (marker) marker(user, ORB_K_FAST, 0, stream);
+    if (marker) marker(user, ORB_K_OCTREE, 1, stream);
+    octree(0, g.nlevels, stream);
+    if (marker) marker(user, ORB_K_OCTREE, 0, stream);
+    if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
+    describe(stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);
     return hipGetLastError();
 }
