@@ -80,6 +80,19 @@ def test_other_parameters(orbgpu_mod, oracle_mod):
         assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), params
 
 
+def test_threshold_edges(orbgpu_mod, oracle_mod):
+    # iniThFAST / minThFAST of 0 and 1 on a low-contrast frame, where arc strengths M of 1 and 2 decide
+    # corners and the NMS (k_fast_wave keeps a corner iff M > max(neighbour M, 1): score M - 1 > 0 at
+    # threshold 0, ORBextractor.cc:812-816 / cv::FAST nonmax)
+    from orbgpu.synth import synth_frame
+    img = (synth_frame(640, 480, 5) // 24 + 100).astype(np.uint8)
+    for params in [(1000, 1.2, 8, 1, 0), (1000, 1.2, 8, 0, 0), (1000, 1.2, 8, 2, 1)]:
+        ok, od = oracle_mod.OracleExtractor(*params)(img)
+        gk, gd = orbgpu_mod.ORBextractor(*params)(img)
+        assert len(gk) > 100, params
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), params
+
+
 def test_empty_image_leaves_outputs_untouched(orbgpu_mod):
     g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
     sentinel_k, sentinel_d = object(), object()
