@@ -1242,15 +1242,15 @@ __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
     return lb & ~la;
 }
 
-// The IC_Angle byte masks of lane r < 31 (patch row v = r - 15): bytes of the 8 aligned row dwords with
-// |u| <= umax[|v|], umax (:454-469) packed 4 bits per row [15,15,15,15,14,14,14,13,13,12,11,10,9,8,6,3].
-// The same for every keypoint: computed once per wave.
-__device__ __forceinline__ void ic_masks(int lane, uint32_t (&icm)[8]) {
+// The IC_Angle byte masks of lane l: patch row v = (l >> 1) - 15 (l < 62), dwords 4h .. 4h+3 of the row's
+// aligned 32-byte slice (h = l & 1): bytes with |u| <= umax[|v|], umax (:454-469) packed 4 bits per row
+// [15,15,15,15,14,14,14,13,13,12,11,10,9,8,6,3].  The same for every keypoint: computed once per wave.
+__device__ __forceinline__ void ic_masks(int lane, uint32_t (&icm)[4]) {
     constexpr unsigned long long kUmax = 0x3689ABCDDEEEFFFFull;
-    const int v = min(lane, 30) - 15;
+    const int v = min(lane >> 1, 30) - 15, h = lane & 1;
     const int d = (int)((kUmax >> (4 * abs(v))) & 15);
 #pragma unroll
-    for (int i = 0; i < 8; i++) icm[i] = byte_range_mask(15 - d, 15 + d, i);
+    for (int i = 0; i < 4; i++) icm[i] = byte_range_mask(15 - d, 15 + d, 4 * h + i);
 }
 
 // One keypoint slot of k_describe: decoded from the octree output (level, coordinates, output index).
@@ -1402,6 +1402,7 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
 
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
                                           const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const float (&pf)[4][4],
+                                          const uint32_t (&icm)[4],
                                           orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
                                           unsigned long long* __restrict__ dstamps) {
     const int l = d.l, x = d.x, y = d.y, score = d.score, outIdx = d.outIdx;
@@ -1444,27 +1445,25 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     wave_lds_sync();
     DESC_STAMP(1);
 
-    // ---- IC_Angle (:77-104) on the unblurred window: lane r < 31 sums row v = r - 15 over the
-    // circular patch |u| <= umax[|v|] with v_dot4_u32_u8 (u*I = (u+16)*I - 16*I).
+    // ---- IC_Angle (:77-104) on the unblurred window: lanes 2r, 2r+1 (r < 31) sum halves of row v = r - 15
+    // over the circular patch |u| <= umax[|v|] with v_dot4_u32_u8 (u*I = (u+16)*I - 16*I); two lanes per
+    // row halve the wave's instructions
     int m10 = 0, m01 = 0;
-    if (lane < 31) {
-        const int v = lane - 15;
-        uint32_t icm[8];
-        ic_masks(lane, icm);
+    if (lane < 62) {
+        const int v = (lane >> 1) - 15, h = lane & 1;
         const int base = (21 + v) * kDescWinPitch + sh + 6;   // byte of u = -15
-        const int d0 = base >> 2, bs = base & 3;
-        uint32_t w[9];
+        const int d0 = (base >> 2) + 4 * h, bs = base & 3;
+        uint32_t w[5];
 #pragma unroll
-        for (int i = 0; i < 9; i++) w[i] = w32[d0 + i];
+        for (int i = 0; i < 5; i++) w[i] = w32[d0 + i];
+        // weights (u + 16) for u = 4c-15 .. 4c-12, c = 4h + i  ->  4c+1 .. 4c+4
+        const uint32_t wt0 = 0x04030201u + (uint32_t)h * 0x10101010u;
         uint32_t sI = 0, sW = 0;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < 4; i++) {
             const uint32_t bytes = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs) & icm[i];
-            // weights (u + 16) for u = 4i-15 .. 4i-12  ->  4i+1 .. 4i+4
-            const uint32_t wt = (uint32_t)(4 * i + 1) | ((uint32_t)(4 * i + 2) << 8) | ((uint32_t)(4 * i + 3) << 16) |
-                                ((uint32_t)(4 * i + 4) << 24);
             sI = __builtin_amdgcn_udot4(bytes, 0x01010101u, sI, false);
-            sW = __builtin_amdgcn_udot4(bytes, wt, sW, false);
+            sW = __builtin_amdgcn_udot4(bytes, wt0 + (uint32_t)i * 0x04040404u, sW, false);
         }
         m10 = (int)sW - 16 * (int)sI;
         m01 = v * (int)sI;
@@ -1581,11 +1580,13 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         pf[gq][2] = (float)pp.z;
         pf[gq][3] = (float)pp.w;
     }
-    if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
+    uint32_t icm[4];
+    ic_masks(lane, icm);
+    if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, icm, outK, outD, kpCap, dstamps);
     if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
-        desc_body(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pf, outK, outD, kpCap, dstamps);
+        desc_body(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pf, icm, outK, outD, kpCap, dstamps);
     }
 }
 
