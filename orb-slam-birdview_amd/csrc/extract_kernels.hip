@@ -15,6 +15,33 @@
 namespace orbgpu {
 
 __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024] = {ORBGPU_PATTERN31_VALUES};
+// the same pattern as floats (k_describe's BRIEF offsets are float products): one 16-byte load per test
+// pair and lane, no conversions
+__constant__ __attribute__((aligned(16))) float c_pattern_f[1024] = {ORBGPU_PATTERN31_VALUES};
+
+// IC_Angle byte masks per lane (see ic_masks): lane l sums dwords 4h .. 4h+3 (h = l & 1) of patch row
+// v = min(l >> 1, 30) - 15, bytes with |u| <= umax[|v|] (ORBextractor.cc:454-469)
+struct IcMaskTable {
+    uint32_t m[64][4];
+};
+constexpr IcMaskTable make_ic_masks() {
+    IcMaskTable t{};
+    constexpr int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    for (int l = 0; l < 64; l++) {
+        const int r = (l >> 1) < 30 ? (l >> 1) : 30, v = r - 15, h = l & 1;
+        const int d = umax[v < 0 ? -v : v];
+        for (int i = 0; i < 4; i++) {
+            uint32_t m = 0;
+            for (int j = 0; j < 4; j++) {
+                const int u = 4 * (4 * h + i) + j;   // byte of the row slice; u = -15 is byte 0
+                if (u >= 15 - d && u <= 15 + d) m |= 0xFFu << (8 * j);
+            }
+            t.m[l][i] = m;
+        }
+    }
+    return t;
+}
+__constant__ __attribute__((aligned(16))) IcMaskTable c_ic_masks = make_ic_masks();
 
 namespace {
 
@@ -1235,23 +1262,6 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {   // cv::fastAta
 }
 
 
-// IC_Angle row sums: bytes of the aligned 32-byte row slice that lie in [lo, hi] (inclusive)
-__device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi, int i) {
-    const int a = min(max(lo - 4 * i, 0), 4), b = min(max(hi - 4 * i + 1, 0), 4);
-    const uint32_t la = (uint32_t)((1ull << (8 * a)) - 1), lb = (uint32_t)((1ull << (8 * b)) - 1);
-    return lb & ~la;
-}
-
-// The IC_Angle byte masks of lane l: patch row v = (l >> 1) - 15 (l < 62), dwords 4h .. 4h+3 of the row's
-// aligned 32-byte slice (h = l & 1): bytes with |u| <= umax[|v|], umax (:454-469) packed 4 bits per row
-// [15,15,15,15,14,14,14,13,13,12,11,10,9,8,6,3].  The same for every keypoint: computed once per wave.
-__device__ __forceinline__ void ic_masks(int lane, uint32_t (&icm)[4]) {
-    constexpr unsigned long long kUmax = 0x3689ABCDDEEEFFFFull;
-    const int v = min(lane >> 1, 30) - 15, h = lane & 1;
-    const int d = (int)((kUmax >> (4 * abs(v))) & 15);
-#pragma unroll
-    for (int i = 0; i < 4; i++) icm[i] = byte_range_mask(15 - d, 15 + d, 4 * h + i);
-}
 
 // One keypoint slot of k_describe: decoded from the octree output (level, coordinates, output index).
 struct DescSlot {
@@ -1390,13 +1400,18 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
         uint32_t w[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) w[i] = rw[72 * r + i];
+        // the four outputs' dot4 chains interleaved level by level (independent neighbours, no dependent
+        // back-to-back v_dot4 that needs wait states)
+        uint32_t acc[4];
 #pragma unroll
-        for (int o = 0; o < 4; o++) {
-            const int b = SH + o, a = b >> 2, al = b & 3;
-            uint32_t v = __builtin_amdgcn_udot4(w[a + 1], K.kb[al], __builtin_amdgcn_udot4(w[a], K.ka[al], 0u, false), false);
-            if (al >= 2) v = __builtin_amdgcn_udot4(w[a + 2], K.kc[al], v, false);
-            rq[o * kRtPitch + 6 * r] = (uint16_t)v;
-        }
+        for (int o = 0; o < 4; o++) acc[o] = __builtin_amdgcn_udot4(w[(SH + o) >> 2], K.ka[(SH + o) & 3], 0u, false);
+#pragma unroll
+        for (int o = 0; o < 4; o++) acc[o] = __builtin_amdgcn_udot4(w[((SH + o) >> 2) + 1], K.kb[(SH + o) & 3], acc[o], false);
+#pragma unroll
+        for (int o = 0; o < 4; o++)
+            if (((SH + o) & 3) >= 2) acc[o] = __builtin_amdgcn_udot4(w[((SH + o) >> 2) + 2], K.kc[(SH + o) & 3], acc[o], false);
+#pragma unroll
+        for (int o = 0; o < 4; o++) rq[o * kRtPitch + 6 * r] = (uint16_t)acc[o];
     }
 }
 
@@ -1574,14 +1589,14 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     float pf[4][4];
 #pragma unroll
     for (int gq = 0; gq < 4; gq++) {
-        const char4 pp = reinterpret_cast<const char4*>(c_pattern)[lane + 64 * gq];
-        pf[gq][0] = (float)pp.x;
-        pf[gq][1] = (float)pp.y;
-        pf[gq][2] = (float)pp.z;
-        pf[gq][3] = (float)pp.w;
+        const float4 pp = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * gq];
+        pf[gq][0] = pp.x;
+        pf[gq][1] = pp.y;
+        pf[gq][2] = pp.z;
+        pf[gq][3] = pp.w;
     }
-    uint32_t icm[4];
-    ic_masks(lane, icm);
+    const uint4 mm = reinterpret_cast<const uint4*>(&c_ic_masks.m[0][0])[lane];
+    const uint32_t icm[4] = {mm.x, mm.y, mm.z, mm.w};
     if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, icm, outK, outD, kpCap, dstamps);
     if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
