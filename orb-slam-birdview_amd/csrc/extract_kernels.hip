@@ -576,7 +576,8 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const uint32_t Va = __builtin_amdgcn_alignbyte(A1, A0, 3), Vb = __builtin_amdgcn_alignbyte(A2, A1, 3);
                 const uint32_t P4a = __builtin_amdgcn_alignbyte(A2, A1, 2), P4b = __builtin_amdgcn_alignbyte(A3, A2, 2);
                 const uint32_t P12a = A0, P12b = A1;
-                auto ev = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c00u); };
+                // even bytes as 16-bit lanes: an AND (logic class, 3.3 cycles) instead of a v_perm (4.4)
+                auto ev = [](uint32_t x) { return x & 0x00FF00FFu; };
                 auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
                 const uint32_t rea = compass2(ev(Va), ev(P0a), ev(P4a), ev(P8a), ev(P12a), tt);
                 const uint32_t roa = compass2(od(Va), od(P0a), od(P4a), od(P8a), od(P12a), tt);
