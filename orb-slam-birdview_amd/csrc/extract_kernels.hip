@@ -522,6 +522,39 @@ __device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, cons
     return 0;
 }
 
+// Survivor bits (bit k = pixel x0 + k) of the compass prefilter at threshold t (tt = t | t << 16) for 8
+// pixels of domain row dy, in a tile where domain pixel (x, y) sits at byte (y + 3) * TP + x + 3 + B (B =
+// the ROI's byte offset in its first dword, wave-uniform: one instantiation per value).  Every 4-byte run
+// is taken straight from the row's dwords, so a run starting on a dword boundary costs no v_alignbyte
+// (7.5 instead of 12 per 8 pixels on average over B).
+template <int TP, int B>
+__device__ __forceinline__ uint32_t prefilter8(const uint32_t* t32, int dy, int x0, uint32_t tt) {
+    const uint32_t* c = t32 + (((dy + 3) * TP + x0) >> 2);   // x0 is a multiple of 8, TP of 4
+    const uint32_t* p = t32 + (((dy + 6) * TP + x0) >> 2);
+    const uint32_t* m = t32 + ((dy * TP + x0) >> 2);
+    auto run = [](const uint32_t* w, int off) -> uint32_t {   // bytes off .. off+3 (off is a constant)
+        return (off & 3) == 0 ? w[off >> 2] : __builtin_amdgcn_alignbyte(w[(off >> 2) + 1], w[off >> 2], off & 3);
+    };
+    // centre row: pixel x0 + k at byte 3 + B + k; rows +-3: the same columns
+    const uint32_t P12a = run(c, B), P12b = run(c, B + 4), Va = run(c, B + 3), Vb = run(c, B + 7);
+    const uint32_t P4a = run(c, B + 6), P4b = run(c, B + 10);
+    const uint32_t P0a = run(p, B + 3), P0b = run(p, B + 7), P8a = run(m, B + 3), P8b = run(m, B + 7);
+    // even bytes as 16-bit lanes: an AND (logic class, 3.3 cycles) instead of a v_perm (4.4)
+    auto ev = [](uint32_t x) { return x & 0x00FF00FFu; };
+    auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
+    const uint32_t rea = compass2(ev(Va), ev(P0a), ev(P4a), ev(P8a), ev(P12a), tt);
+    const uint32_t roa = compass2(od(Va), od(P0a), od(P4a), od(P8a), od(P12a), tt);
+    const uint32_t reb = compass2(ev(Vb), ev(P0b), ev(P4b), ev(P8b), ev(P12b), tt);
+    const uint32_t rob = compass2(od(Vb), od(P0b), od(P4b), od(P8b), od(P12b), tt);
+    // sign bits 15 / 31 of the four results -> pixel bits 0..7: gather the high bytes (one v_perm per
+    // pair), put pixel i and i+4 in byte i's bits 0 and 4, and fold the four bytes into the top byte
+    // with one multiply
+    const uint32_t X = __builtin_amdgcn_perm(roa, rea, 0x07030501u);   // rea.b1 roa.b1 rea.b3 roa.b3
+    const uint32_t Y = __builtin_amdgcn_perm(rob, reb, 0x07030501u);
+    const uint32_t Z = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
+    return (Z * 0x01020408u) >> 24;
+}
+
 // One cell after its ROI is in the tile: prefilter, exact arc strength, cell-local NMS with the
 // minThFAST fallback, raster-order emission (see k_fast above for the semantics).
 template <int TP, int SP>
@@ -559,37 +592,14 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             const int dy = r0 + lrow;
             int pm = 0;
             if (lane_on && dy < dh) {
-                // 8 pixels: centre bytes x0-3 .. x0+12 (5 dwords), rows +-3 bytes x0 .. x0+7 (3 dwords each)
-                const int sc = (dy + 3) * TP + x0 + xoff;
-                const int s0 = (dy + 6) * TP + x0 + 3 + xoff;
-                const int s8 = dy * TP + x0 + 3 + xoff;
-                const int dc = sc >> 2, d0 = s0 >> 2, d8 = s8 >> 2;
-                const uint32_t w0 = t32[dc], w1 = t32[dc + 1], w2 = t32[dc + 2], w3 = t32[dc + 3], w4 = t32[dc + 4];
-                const uint32_t A0 = __builtin_amdgcn_alignbyte(w1, w0, sc & 3);   // x0-3 .. x0
-                const uint32_t A1 = __builtin_amdgcn_alignbyte(w2, w1, sc & 3);   // x0+1 .. x0+4
-                const uint32_t A2 = __builtin_amdgcn_alignbyte(w3, w2, sc & 3);   // x0+5 .. x0+8
-                const uint32_t A3 = __builtin_amdgcn_alignbyte(w4, w3, sc & 3);   // x0+9 .. x0+12
-                const uint32_t q0 = t32[d0], q1 = t32[d0 + 1], q2 = t32[d0 + 2];
-                const uint32_t r0 = t32[d8], r1 = t32[d8 + 1], r2 = t32[d8 + 2];
-                const uint32_t P0a = __builtin_amdgcn_alignbyte(q1, q0, s0 & 3), P0b = __builtin_amdgcn_alignbyte(q2, q1, s0 & 3);
-                const uint32_t P8a = __builtin_amdgcn_alignbyte(r1, r0, s8 & 3), P8b = __builtin_amdgcn_alignbyte(r2, r1, s8 & 3);
-                const uint32_t Va = __builtin_amdgcn_alignbyte(A1, A0, 3), Vb = __builtin_amdgcn_alignbyte(A2, A1, 3);
-                const uint32_t P4a = __builtin_amdgcn_alignbyte(A2, A1, 2), P4b = __builtin_amdgcn_alignbyte(A3, A2, 2);
-                const uint32_t P12a = A0, P12b = A1;
-                // even bytes as 16-bit lanes: an AND (logic class, 3.3 cycles) instead of a v_perm (4.4)
-                auto ev = [](uint32_t x) { return x & 0x00FF00FFu; };
-                auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
-                const uint32_t rea = compass2(ev(Va), ev(P0a), ev(P4a), ev(P8a), ev(P12a), tt);
-                const uint32_t roa = compass2(od(Va), od(P0a), od(P4a), od(P8a), od(P12a), tt);
-                const uint32_t reb = compass2(ev(Vb), ev(P0b), ev(P4b), ev(P8b), ev(P12b), tt);
-                const uint32_t rob = compass2(od(Vb), od(P0b), od(P4b), od(P8b), od(P12b), tt);
-                // sign bits 15 / 31 of the four results -> pixel bits 0..7: gather the high bytes (one
-                // v_perm per pair), put pixel i and i+4 in byte i's bits 0 and 4, and fold the four bytes
-                // into the top byte with one multiply
-                const uint32_t X = __builtin_amdgcn_perm(roa, rea, 0x07030501u);   // rea.b1 roa.b1 rea.b3 roa.b3
-                const uint32_t Y = __builtin_amdgcn_perm(rob, reb, 0x07030501u);
-                const uint32_t Z = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
-                pm = (int)(((Z * 0x01020408u) >> 24) & xvalid);
+                uint32_t bits;
+                switch (xoff) {   // wave-uniform
+                    case 0: bits = prefilter8<TP, 0>(t32, dy, x0, tt); break;
+                    case 1: bits = prefilter8<TP, 1>(t32, dy, x0, tt); break;
+                    case 2: bits = prefilter8<TP, 2>(t32, dy, x0, tt); break;
+                    default: bits = prefilter8<TP, 3>(t32, dy, x0, tt); break;
+                }
+                pm = (int)(bits & xvalid);
             }
             // compaction: one wave prefix sum of the per-lane survivor counts, then each lane writes
             // its (<= 4) entries at its offset
