@@ -286,26 +286,28 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
  * buffers do for a ROI).  Survivors are emitted in raster order (FAST emission order), packed
  * x_rel | y_rel<<12 | score<<24 with coordinates relative to minBorder (:822-823).
  * --------------------------------------------------------------------------------------------- */
-template <int P = kFastTilePitch>
+// c = the centre pixel's byte; pixels CS bytes apart in a row, rows P bytes apart (the 16-bit tile's
+// low bytes: CS = 2)
+template <int P, int CS>
 __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
     const int v = c[0];
     int d[16];
-    d[0] = v - c[3 * P];
-    d[1] = v - c[1 + 3 * P];
-    d[2] = v - c[2 + 2 * P];
-    d[3] = v - c[3 + 1 * P];
-    d[4] = v - c[3];
-    d[5] = v - c[3 - 1 * P];
-    d[6] = v - c[2 - 2 * P];
-    d[7] = v - c[1 - 3 * P];
-    d[8] = v - c[-3 * P];
-    d[9] = v - c[-1 - 3 * P];
-    d[10] = v - c[-2 - 2 * P];
-    d[11] = v - c[-3 - 1 * P];
-    d[12] = v - c[-3];
-    d[13] = v - c[-3 + 1 * P];
-    d[14] = v - c[-2 + 2 * P];
-    d[15] = v - c[-1 + 3 * P];
+    d[0] = v - c[0 * CS + 3 * P];
+    d[1] = v - c[1 * CS + 3 * P];
+    d[2] = v - c[2 * CS + 2 * P];
+    d[3] = v - c[3 * CS + 1 * P];
+    d[4] = v - c[3 * CS + 0 * P];
+    d[5] = v - c[3 * CS + -1 * P];
+    d[6] = v - c[2 * CS + -2 * P];
+    d[7] = v - c[1 * CS + -3 * P];
+    d[8] = v - c[0 * CS + -3 * P];
+    d[9] = v - c[-1 * CS + -3 * P];
+    d[10] = v - c[-2 * CS + -2 * P];
+    d[11] = v - c[-3 * CS + -1 * P];
+    d[12] = v - c[-3 * CS + 0 * P];
+    d[13] = v - c[-3 * CS + 1 * P];
+    d[14] = v - c[-2 * CS + 2 * P];
+    d[15] = v - c[-1 * CS + 3 * P];
     // 9-arc [k, k+8] = three 3-runs: v_min3/v_max3 over runs, then over the arcs
     int m3[16], x3[16];
 #pragma unroll
@@ -477,7 +479,7 @@ __device__ __forceinline__ RoiLanes roi_lanes(const FastCellT& c, int lane) {
     const int nw = __builtin_amdgcn_readfirstlane(c.nw), stride = __builtin_amdgcn_readfirstlane(c.stride);
     r.rpr = c.rpr;
     r.yy0 = (int)div20(lane, c.m_nw);
-    r.ww = lane - r.yy0 * nw;
+    r.ww = lane - (int)__umul24((unsigned)r.yy0, (unsigned)nw);
     r.off = (int)roi_off(r.yy0, stride, 4 * r.ww);
     // the cell is wave-uniform (readfirstlane returns int: zero-extend both halves)
     const uint64_t pb = reinterpret_cast<uint64_t>(c.base + 4 * c.x0w);
@@ -498,75 +500,152 @@ __device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uin
         v[k] = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, roi_row_ok(c, r, k) ? r.off : 0x40000000, k * r.rpr * c.stride, 0);
 }
 
-// ROI -> LDS tile (rows TP apart): the prefetched dwords, the rows of a tall ROI past them, or bytes
-// for a level whose base / stride is not dword aligned.  Returns the tile column of ROI x = 0.
-template <int TP>
-__device__ __forceinline__ int fast_roi_store(const FastCellT& c, int lane, const uint32_t (&v)[8], uint8_t* tile) {
+// ROI -> 16-bit LDS tile (rows TQ elements apart): ROI column c at element c + 1, so that every
+// prefilter window starts on a 16-byte boundary (see prefilter16).  The bytes are widened as they are
+// stored.  ROI column c is byte c + B of the loaded row (B = the ROI's byte offset in its first dword),
+// so a lane's dword (bytes 4 ww .. 4 ww + 3) goes to elements 4 ww - B + 1 .. 4 ww - B + 4, i.e. the
+// pixel pairs at dwords 2 ww - (B >> 1) and + 1 are (b0, b1), (b2, b3) for B odd and (prev b3, b0),
+// (b1, b2) for B even — prev = the row's previous dword, lane - 1's (DPP wave_shr), and the row's last
+// dword also stores (b3, 0).  Dword -1 of row 0 lies in the carve's 16-byte lead pad, that of a later row
+// in the previous row's unused tail (TQ >= rw + 6).  Rows of a tall ROI past the prefetched ones are
+// loaded here; a level whose base / stride is not dword aligned is stored per byte.
+__device__ __forceinline__ uint32_t dpp_prev_lane(uint32_t v) {   // lane - 1's value (lane 0: 0)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, true);
+}
+
+template <bool ODD>
+__device__ __forceinline__ void widen_store(uint32_t* q, uint32_t v, uint32_t pv, bool last) {
+    if (ODD) {
+        q[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
+        q[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
+    } else {
+        q[0] = __builtin_amdgcn_perm(v, pv, 0x0c040c03u);
+        q[1] = __builtin_amdgcn_perm(0u, v, 0x0c020c01u);
+        if (last) q[2] = v >> 24;
+    }
+}
+
+// the prefetched rows (round k: ROI row yy0 + k * rpr) and, for a tall ROI, the rows past them
+template <int TQ, bool ODD>
+__device__ __forceinline__ void widen_rows(const FastCellT& c, const RoiLanes& r, const uint32_t (&v)[8], uint32_t* t32,
+                                           int B, bool last) {
+    uint32_t* t = t32 + (r.yy0 * (TQ / 2) + 2 * r.ww - (B >> 1));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (k * r.rpr >= c.rh) break;   // wave-uniform
+        const uint32_t pv = ODD ? 0u : dpp_prev_lane(v[k]);
+        if (roi_row_ok(c, r, k)) widen_store<ODD>(t + k * r.rpr * (TQ / 2), v[k], pv, last);
+    }
+    if (r.yy0 < r.rpr)
+        for (int yy = r.yy0 + 8 * r.rpr; yy < c.rh; yy += r.rpr) {   // lanes of one row iterate together
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + r.ww) * 4));
+            const uint32_t pw = ODD ? 0u : dpp_prev_lane(w);
+            widen_store<ODD>(t32 + (yy * (TQ / 2) + 2 * r.ww - (B >> 1)), w, pw, last);
+        }
+}
+
+template <int TQ>
+__device__ __forceinline__ void fast_roi_store(const FastCellT& c, int lane, const uint32_t (&v)[8], uint16_t* tile) {
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(tile);
     if (c.aligned) {
         const RoiLanes r = roi_lanes(c, lane);
-        uint32_t* t = reinterpret_cast<uint32_t*>(&tile[r.yy0 * TP + 4 * r.ww]);
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (roi_row_ok(c, r, k)) t[k * r.rpr * (TP / 4)] = v[k];
-        if (r.yy0 < r.rpr)
-            for (int yy = r.yy0 + 8 * r.rpr; yy < c.rh; yy += r.rpr)
-                *reinterpret_cast<uint32_t*>(&tile[yy * TP + 4 * r.ww]) =
-                    *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + r.ww) * 4));
-        return c.iniX & 3;
+        const int B = c.iniX & 3;
+        const bool last = r.ww == __builtin_amdgcn_readfirstlane(c.nw) - 1;
+        if (B & 1) widen_rows<TQ, true>(c, r, v, t32, B, last);
+        else widen_rows<TQ, false>(c, r, v, t32, B, last);
+        return;
     }
     const uint32_t mrw = recip20(c.rw);
     for (int idx = lane; idx < c.rh * c.rw; idx += 64) {
         const int yy = (int)div20(idx, mrw), xx = idx - (int)__umul24((unsigned)yy, (unsigned)c.rw);
-        tile[yy * TP + xx] = c.base[roi_off(yy, c.stride, c.iniX + xx)];
+        tile[yy * TQ + xx + 1] = c.base[roi_off(yy, c.stride, c.iniX + xx)];
     }
-    return 0;
 }
 
 // Survivor bits (bit k = pixel x0 + k) of the compass prefilter at threshold t (tt = t | t << 16) for 8
-// pixels of domain row dy, in a tile where domain pixel (x, y) sits at byte (y + 3) * TP + x + 3 + B (B =
-// the ROI's byte offset in its first dword, wave-uniform: one instantiation per value).  Every 4-byte run
-// is taken straight from the row's dwords, so a run starting on a dword boundary costs no v_alignbyte
-// (7.5 instead of 12 per 8 pixels on average over B).
-template <int TP, int B>
-__device__ __forceinline__ uint32_t prefilter8(const uint32_t* t32, int dy, int x0, uint32_t tt) {
-    const uint32_t* c = t32 + (((dy + 3) * TP + x0) >> 2);   // x0 is a multiple of 8, TP of 4
-    const uint32_t* p = t32 + (((dy + 6) * TP + x0) >> 2);
-    const uint32_t* m = t32 + ((dy * TP + x0) >> 2);
-    auto run = [](const uint32_t* w, int off) -> uint32_t {   // bytes off .. off+3 (off is a constant)
-        return (off & 3) == 0 ? w[off >> 2] : __builtin_amdgcn_alignbyte(w[(off >> 2) + 1], w[off >> 2], off & 3);
-    };
-    // centre row: pixel x0 + k at byte 3 + B + k; rows +-3: the same columns
-    const uint32_t P12a = run(c, B), P12b = run(c, B + 4), Va = run(c, B + 3), Vb = run(c, B + 7);
-    const uint32_t P4a = run(c, B + 6), P4b = run(c, B + 10);
-    const uint32_t P0a = run(p, B + 3), P0b = run(p, B + 7), P8a = run(m, B + 3), P8b = run(m, B + 7);
-    // even bytes as 16-bit lanes: an AND (logic class, 3.3 cycles) instead of a v_perm (4.4)
-    auto ev = [](uint32_t x) { return x & 0x00FF00FFu; };
-    auto od = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };
-    const uint32_t rea = compass2(ev(Va), ev(P0a), ev(P4a), ev(P8a), ev(P12a), tt);
-    const uint32_t roa = compass2(od(Va), od(P0a), od(P4a), od(P8a), od(P12a), tt);
-    const uint32_t reb = compass2(ev(Vb), ev(P0b), ev(P4b), ev(P8b), ev(P12b), tt);
-    const uint32_t rob = compass2(od(Vb), od(P0b), od(P4b), od(P8b), od(P12b), tt);
-    // sign bits 15 / 31 of the four results -> pixel bits 0..7: gather the high bytes (one v_perm per
-    // pair), put pixel i and i+4 in byte i's bits 0 and 4, and fold the four bytes into the top byte
-    // with one multiply
-    const uint32_t X = __builtin_amdgcn_perm(roa, rea, 0x07030501u);   // rea.b1 roa.b1 rea.b3 roa.b3
-    const uint32_t Y = __builtin_amdgcn_perm(rob, reb, 0x07030501u);
+// pixels of domain row dy, in the 16-bit tile where domain pixel (x, y) is element (y + 3) * TQ + x + 4.
+// Each tile dword is a pixel pair, so the centre row's 8 dwords from element x0 (two 16-byte reads) hold
+// the centre pairs (x0 + 2j, x0 + 2j + 1) at dwords j + 2 and the pairs at columns -3 / +3 (odd
+// elements) as one v_alignbyte each; rows -3 / +3 are two 8-byte reads each.  No byte unpacking.
+typedef const uint32_t __attribute__((address_space(3))) lds_cu32;
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef const u32x2_t __attribute__((address_space(3))) lds_cu32x2;
+typedef const uint32x4_t __attribute__((address_space(3))) lds_cu32x4;
+
+template <int TQ, bool CLEAN>   // CLEAN: drop the high bytes (a pass-0 arc strength may sit there)
+__device__ __forceinline__ uint32_t prefilter16(lds_cu32* w, uint32_t tt) {   // w: element dy * TQ + x0
+    static_assert(TQ % 8 == 0, "tile rows must keep 16-byte alignment");
+    const uint32x4_t c0 = *(lds_cu32x4*)(w + 3 * TQ / 2), c1 = *(lds_cu32x4*)(w + 3 * TQ / 2 + 4);
+    // rows +3 / -3: four 8-byte reads (volatile: merged into ds_read2_b64 they would take 8 LDS cycles
+    // instead of 2 x 2)
+    const u32x2_t p0 = *(volatile lds_cu32x2*)(w + 6 * TQ / 2 + 2), p1 = *(volatile lds_cu32x2*)(w + 6 * TQ / 2 + 4);
+    const u32x2_t m0 = *(volatile lds_cu32x2*)(w + 2), m1 = *(volatile lds_cu32x2*)(w + 4);
+    uint32_t D[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    uint32_t P[4] = {p0[0], p0[1], p1[0], p1[1]}, M[4] = {m0[0], m0[1], m1[0], m1[1]};
+    if (CLEAN) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) D[j] &= 0x00FF00FFu;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            P[j] &= 0x00FF00FFu;
+            M[j] &= 0x00FF00FFu;
+        }
+    }
+    uint32_t r[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t P12 = __builtin_amdgcn_alignbyte(D[j + 1], D[j], 2);   // column -3
+        const uint32_t P4 = __builtin_amdgcn_alignbyte(D[j + 4], D[j + 3], 2);  // column +3
+        r[j] = compass2(D[j + 2], P[j], P4, M[j], P12, tt);
+    }
+    // sign bits 15 / 31 of r[j] are pixels 2j / 2j + 1: gather the high bytes (one v_perm per two
+    // results), put pixel i and i+4 in byte i's bits 0 and 4, and weight the four bytes by 1, 2, 4, 8
+    // with one v_dot4 (a 32-bit multiply is quarter rate)
+    const uint32_t X = __builtin_amdgcn_perm(r[1], r[0], 0x07050301u);
+    const uint32_t Y = __builtin_amdgcn_perm(r[3], r[2], 0x07050301u);
     const uint32_t Z = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
-    return (Z * 0x01020408u) >> 24;
+    return __builtin_amdgcn_udot4(Z, 0x08040201u, 0u, false);
+}
+
+// Stage 1 of a cell at threshold tt: the prefilter over every domain row, survivors compacted into
+// sList in raster order (one wave prefix sum of the per-lane counts per row round, then each lane
+// writes its entries at its offset).  Returns the list length.
+template <int TQ, bool CLEAN>
+__device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int rpi, int lrow, bool lane_on, int x0,
+                                              uint32_t xvalid, uint32_t tt, uint16_t* sList) {
+    int nlist = 0;
+    for (int r0 = 0; r0 < dh; r0 += rpi) {
+        const int dy = r0 + lrow;
+        int pm = 0;
+        if (lane_on && dy < dh) {
+            // one VGPR address per row round (the asm keeps the compiler from re-deriving it per load)
+            lds_cu32* w = (lds_cu32*)(t32 + r0 * (TQ / 2));
+            asm volatile("" : "+v"(w));
+            pm = (int)(prefilter16<TQ, CLEAN>(w, tt) & xvalid);
+        }
+        const int cnt = __popc(pm);
+        const int incl = wave_incl_scan(cnt);
+        int pos = nlist + incl - cnt;
+        const int base = dy * 64 + x0;
+        // one iteration per set bit (survivors are sparse: the wave runs max-popcount iterations)
+        for (uint32_t b = (uint32_t)pm; b; b &= b - 1) sList[pos++] = (uint16_t)(base + __builtin_ctz(b));
+        nlist += __builtin_amdgcn_readlane(incl, 63);
+    }
+    return nlist;
 }
 
 // One cell after its ROI is in the tile: prefilter, exact arc strength, cell-local NMS with the
-// minThFAST fallback, raster-order emission (see k_fast above for the semantics).
-template <int TP, int SP>
-__device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane, int xoff,
-                                               uint8_t* tile, uint8_t* sM, uint16_t* sList,
+// minThFAST fallback, raster-order emission (see k_fast above for the semantics).  The arc strength M
+// of a scored pixel is kept in the high byte of its tile element (pixels are < 256, and the widening
+// store leaves every high byte 0), so the NMS reads neighbours' M from the tile: no separate map to
+// clear, and unscored pixels read 0.
+template <int TQ>
+__device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane,
+                                               uint16_t* tile, uint16_t* sList,
                                                uint32_t* __restrict__ cands,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
-    constexpr int PX = 8;
+    constexpr int PX = 8, TB = 2 * TQ;   // TB: tile row pitch in bytes
     const int dw = c.dw, dh = c.dh;
-    // (16-byte stores; the map's LDS carve is rounded up to 16 bytes)
-    for (int i = lane; i < ((dh + 2) * SP + 15) / 16; i += 64) reinterpret_cast<uint4*>(sM)[i] = make_uint4(0u, 0u, 0u, 0u);
-    wave_lds_sync();
     ORBGPU_STAMP(1);
     // lane -> (run of PX = 8 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
     const int nruns = c.nruns;                           // (dw + PX - 1) / PX
@@ -575,42 +654,21 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
     const int x0 = PX * (lane - lrow * nruns);
     const bool lane_on = lrow < rpi;
     const uint32_t xvalid = x0 + PX <= dw ? (1u << PX) - 1u : (1u << max(dw - x0, 0)) - 1u;
-    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
-    const uint8_t* t0 = &tile[3 * TP + 3 + xoff];
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile) + ((lrow * TQ + x0) >> 1);   // row step TQ / 2
+    uint8_t* t0 = reinterpret_cast<uint8_t*>(&tile[3 * TQ + 4]);   // domain pixel (0, 0), low byte
     // Pass 0 runs the whole cell at iniThFAST; only a cell left with no keypoint (:812-816) runs pass 1
     // at minThFAST.  The prefilter is a necessary condition for M > th at the pass threshold, so a
     // pass only scores the pixels that can matter at its threshold: everything else reads 0 in the map
-    // (M <= th counts 0 in the NMS), and pass 1's survivors are a superset that overwrites pass 0's.
+    // (M <= th counts 0 in the NMS), and pass 1's survivors are a superset that overwrites pass 0's
+    // (pass 1's prefilter masks the high bytes pass 0 wrote).
     int th = g->iniTh;
     int kept = 0;
     for (int pass = 0; pass < 2; pass++) {
-        // ---- stage 1: compass prefilter at th, 8 pixels per lane in packed 16-bit lanes, per-bit
-        // ballot compaction into sList
+        // ---- stage 1: compass prefilter at th, 8 pixels per lane as 16-bit pixel pairs, survivors
+        // compacted into sList by one wave scan
         const uint32_t tt = (uint32_t)th | ((uint32_t)th << 16);
-        int nlist = 0;
-        for (int r0 = 0; r0 < dh; r0 += rpi) {
-            const int dy = r0 + lrow;
-            int pm = 0;
-            if (lane_on && dy < dh) {
-                uint32_t bits;
-                switch (xoff) {   // wave-uniform
-                    case 0: bits = prefilter8<TP, 0>(t32, dy, x0, tt); break;
-                    case 1: bits = prefilter8<TP, 1>(t32, dy, x0, tt); break;
-                    case 2: bits = prefilter8<TP, 2>(t32, dy, x0, tt); break;
-                    default: bits = prefilter8<TP, 3>(t32, dy, x0, tt); break;
-                }
-                pm = (int)(bits & xvalid);
-            }
-            // compaction: one wave prefix sum of the per-lane survivor counts, then each lane writes
-            // its (<= 4) entries at its offset
-            const int cnt = __popc(pm);
-            const int incl = wave_incl_scan(cnt);
-            int pos = nlist + incl - cnt;
-            const int base = dy * 64 + x0;
-            // one iteration per set bit (survivors are sparse: the wave runs max-popcount iterations)
-            for (uint32_t b = (uint32_t)pm; b; b &= b - 1) sList[pos++] = (uint16_t)(base + __builtin_ctz(b));
-            nlist += __builtin_amdgcn_readlane(incl, 63);
-        }
+        const int nlist = pass == 0 ? prefilter_cell<TQ, false>(t32, dh, rpi, lrow, lane_on, x0, xvalid, tt, sList)
+                                    : prefilter_cell<TQ, true>(t32, dh, rpi, lrow, lane_on, x0, xvalid, tt, sList);
         wave_lds_sync();
         ORBGPU_STAMP(2);
         // ---- stage 2: exact arc strength for the survivors; corners at th are compacted in place
@@ -621,8 +679,9 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             int p = 0, m = 0;
             if (i < nlist) {
                 p = sList[i];
-                m = fast_arc_strength<TP>(t0 + (p >> 6) * TP + (p & 63));
-                sM[(p >> 6) * SP + (p & 63) + SP + 1] = (uint8_t)m;
+                uint8_t* e = t0 + (p >> 6) * TB + 2 * (p & 63);
+                m = fast_arc_strength<TB, 2>(e);
+                e[1] = (uint8_t)m;
             }
             const bool corner = m > th;
             const unsigned long long cm = __ballot(corner);
@@ -631,8 +690,8 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         }
         wave_lds_sync();
         ORBGPU_STAMP(3);
-        // ---- cell-local NMS at th.  Neighbours outside the domain read the zero border; M <= th
-        // counts 0.  The corner list is in raster order (the prefilter compacts rows in order, pixels
+        // ---- cell-local NMS at th.  Neighbours outside the domain are ROI border pixels (M = 0);
+        // M <= th counts 0.  The corner list is in raster order (the prefilter compacts rows in order, pixels
         // ascending within a lane's run, runs in lane order), so the kept corners are emitted as they
         // are found: one ballot compaction per chunk of 64, FAST emission order.
         kept = 0;
@@ -642,15 +701,15 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             uint32_t packed = 0;
             if (i < ncorner) {
                 const int p = sList[i];
-                const uint8_t* q = sM + (p >> 6) * SP + (p & 63) + SP + 1;
+                const uint8_t* q = t0 + (p >> 6) * TB + 2 * (p & 63) + 1;
                 const int m = q[0];
                 const int s = m - 1;
                 // the reference keeps score s = M - 1 iff s > sn for every neighbour, sn = Mn - 1 for a
                 // corner neighbour (Mn > th) and 0 otherwise.  A neighbour with Mn <= th < M is below M
                 // anyway, so this is M > max(every Mn, 1)
-                const int n0 = max(max((int)q[-SP - 1], (int)q[-SP]), (int)q[-SP + 1]);
-                const int n1 = max(max((int)q[-1], (int)q[1]), 1);
-                const int n2 = max(max((int)q[SP - 1], (int)q[SP]), (int)q[SP + 1]);
+                const int n0 = max(max((int)q[-TB - 2], (int)q[-TB]), (int)q[-TB + 2]);
+                const int n1 = max(max((int)q[-2], (int)q[2]), 1);
+                const int n2 = max(max((int)q[TB - 2], (int)q[TB]), (int)q[TB + 2]);
                 k = m > max(max(n0, n1), n2);
                 packed = (uint32_t)((p & 63) + c.xo) | ((uint32_t)((p >> 6) + c.yo) << 12) | ((uint32_t)s << 24);
             }
@@ -673,7 +732,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
  * per-wave LDS carve is sized on the host from the level grids (Geom::fast_*).  Prefilter survivors
  * are compacted by one wave scan into a raster-ordered list, so corners keep that order and the NMS
  * pass emits the kept ones directly (FAST emission order) by ballot compaction. */
-template <int TP, int SP>
+template <int TQ>
 __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
@@ -690,10 +749,9 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     const int item0 = (blk * (int)(blockDim.x >> 6) + wv) * 2;
     if (item0 >= total) return;   // whole wave; nothing below uses a block barrier
     const int wb = g->fast_wave_bytes;
-    uint8_t* tile = smem + (size_t)wv * wb;
-    // arc-strength map with a zero border: pixel (dy, dx) of the domain at sM[(dy+1)*SP + dx+1]
-    uint8_t* sM = tile + ((g->fast_rows * TP + 16 + 15) & ~15);
-    uint16_t* sList = reinterpret_cast<uint16_t*>(sM + (((g->fast_drows + 2) * SP + 15) & ~15));
+    // 16-bit pixel tile, TQ per row, after a 16-byte lead pad (fast_roi_store's dword -1 of row 0)
+    uint16_t* tile = reinterpret_cast<uint16_t*>(smem + (size_t)wv * wb + 16);
+    uint16_t* sList = reinterpret_cast<uint16_t*>(smem + (size_t)wv * wb + ((g->fast_rows * TQ * 2 + 32 + 15) & ~15));
     const bool has1 = item0 + 1 < total;
     const FastCellT c0 = fast_cell_t(g, cells, item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
     const FastCellT c1 = fast_cell_t(g, cells, has1 ? item0 + 1 : item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
@@ -712,15 +770,18 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         }
         ORBGPU_STAMP(0);
         wave_lds_sync();   // the previous cell's last LDS reads happen before this one's writes
-        const int xoff = fast_roi_store<TP>(c, lane, k == 0 ? v0 : v1, tile);
+        fast_roi_store<TQ>(c, lane, k == 0 ? v0 : v1, tile);
         ORBGPU_STAMP(6);
-        fast_cell_body<TP, SP>(g, c, lane, xoff, tile, sM, sList, cands, cntOut, stamps, item);
+        fast_cell_body<TQ>(g, c, lane, tile, sList, cands, cntOut, stamps, item);
     }
 }
 
 // Per-wave LDS carve of k_fast_wave.  Cells at most 36 px wide (every BASELINE config) use the
-// compact pitches <56, 40>: the tile row must hold the prefilter's dword window (4*ceil(dw/4) + 14
-// bytes) and the ROI's dwords, the score map a zero column either side of the domain.
+// compact tile pitch of 48 elements, wider ones 80: a tile row holds the
+// widened ROI (rw + 2 elements) and an unused tail for the next row's dword -1, a multiple of 8 elements
+// (16-byte reads), with row strides of 24 / 40 dwords (2-way LDS bank conflicts at most for the
+// prefilter's 16- and 8-byte reads).
+// Prefilter windows of pixels past the domain may read into the next row: those bits are masked.
 void fast_wave_layout(Geom& g) {
     int rows = 1, drows = 1, list = 1, maxw = 1;
     for (int l = 0; l < g.nlevels; l++) {
@@ -734,8 +795,8 @@ void fast_wave_layout(Geom& g) {
     g.fast_drows = drows;
     g.fast_list = list;
     g.fast_compact = maxw <= 36 ? 1 : 0;
-    const int tp = g.fast_compact ? 56 : kFastTilePitch, sp = g.fast_compact ? 40 : 64;
-    g.fast_wave_bytes = ((rows * tp + 16 + 15) & ~15) + (((drows + 2) * sp + 15) & ~15) + ((list * 2 + 15) & ~15);
+    const int tq = g.fast_compact ? 48 : kFastTilePitch;
+    g.fast_wave_bytes = ((rows * tq * 2 + 32 + 15) & ~15) + ((list * 2 + 15) & ~15);
     g.fast_wave_bytes = (g.fast_wave_bytes + 15) & ~15;
 }
 
@@ -1674,7 +1735,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     // CU on uneven cells)
     auto fast = [&](int cbeg, int cnum, hipStream_t s, int* zero) {
         const int items = cnum * nframes;
-        auto kern = g.fast_compact ? k_fast_wave<56, 40> : k_fast_wave<kFastTilePitch, 64>;
+        auto kern = g.fast_compact ? k_fast_wave<48> : k_fast_wave<kFastTilePitch>;
         hipLaunchKernelGGL(kern, dim3(cdiv(items, 2)), dim3(64), (size_t)g.fast_wave_bytes, s, b.d_geom, b.d_cells,
                            d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum,
                            b.d_stamps, zero);

@@ -14,7 +14,7 @@ constexpr int kMinBorder = kEdgeThreshold - 3;   // :773
 constexpr int kPatchSize = 31;        // :72
 constexpr int kHalfPatch = 15;        // :73
 constexpr int kMaxDim = 4096;         // candidate coordinates are packed in 12 bits
-constexpr int kFastTilePitch = 72;    // LDS pitch of a FAST cell ROI (ROI <= 66 px + 3 align)
+constexpr int kFastTilePitch = 80;    // 16-bit elements per FAST tile row (ROI <= 66 px, prefilter window <= 74)
 constexpr int kFastMaxRoi = 66;
 constexpr int kOctreeThreads = 512;
 constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3 (blur taps)
@@ -59,7 +59,7 @@ struct Geom {
     int fast_rows;       // k_fast_wave per-wave LDS carve (max over levels): ROI rows,
     int fast_drows;      //   detection-domain rows,
     int fast_list;       //   prefilter-survivor list entries (domain pixels)
-    int fast_wave_bytes; //   bytes per wave (tile | arc strength | list | keep bits)
+    int fast_wave_bytes; //   bytes per wave (lead pad | 16-bit tile | survivor list)
     int fast_compact;    //   every cell <= 36 px wide: compact LDS pitches (tile 56, score map 40)
     int umax[16];        // ORBextractor.cc:454-469
     int gk[8];           // 7-tap Gaussian, sigma 2, 8-bit fixed point (getGaussianKernel x 256)
