@@ -466,9 +466,9 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
 // ROI dwords of a cell (aligned levels) issued into registers, so that the next cell's loads are in
 // flight while the current one is processed.  lane = (row yy0 = lane / nw, dword ww = lane % nw);
 // round k takes row yy0 + k * rpr (rpr = 64 / nw rows per round): the lane's offset is computed once
-// and each round adds a wave-uniform row step, the soffset of a buffer load whose descriptor (SGPRs)
-// starts at the ROI's first dword.  Rows past the ROI and lanes past rpr rows take an out-of-range
-// voffset (read 0).  Rows from 8 * rpr on (tall cells) are loaded by fast_roi_store.
+// and each round adds a wave-uniform row step to the voffset of a buffer load whose descriptor (SGPRs)
+// starts at the ROI's first dword.  Rows past the ROI and lanes past rpr rows are out of the
+// descriptor's range (read 0).  Rows from 8 * rpr on (tall cells) are loaded by fast_roi_store.
 struct RoiLanes {
     int yy0, ww, rpr, off;
     __amdgpu_buffer_rsrc_t rsrc;
@@ -495,9 +495,13 @@ __device__ __forceinline__ bool roi_row_ok(const FastCellT& c, const RoiLanes& r
 
 __device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uint32_t (&v)[8]) {
     const RoiLanes r = roi_lanes(c, lane);
+    // rows past the ROI lie past the descriptor's num_records ((rh - 1) * stride + 4 nw <= rh * stride
+    // + 4 ww) and read 0 without a per-row test: the row step goes into voffset, which the range check
+    // covers (soffset would not be checked); lanes past rpr rows start out of range
+    const int off = r.yy0 < r.rpr ? r.off : 0x40000000;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-        v[k] = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, roi_row_ok(c, r, k) ? r.off : 0x40000000, k * r.rpr * c.stride, 0);
+        v[k] = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, off + k * r.rpr * c.stride, 0, 0);
 }
 
 // ROI -> 16-bit LDS tile (rows TQ elements apart): ROI column c at element c + 1, so that every
