@@ -287,43 +287,45 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
  * x_rel | y_rel<<12 | score<<24 with coordinates relative to minBorder (:822-823).
  * --------------------------------------------------------------------------------------------- */
 // c = the centre pixel's byte; pixels CS bytes apart in a row, rows P bytes apart (the 16-bit tile's
-// low bytes: CS = 2)
+// low bytes: CS = 2).  On the raw circle values p: the dark strength max over arcs of min (v - p) is
+// v - X with X = min over arcs of max p, the bright one Y - v with Y = max over arcs of min p, so
+// M = max(v - X, Y - v, 0) needs no per-pixel differences.
 template <int P, int CS>
 __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
     const int v = c[0];
-    int d[16];
-    d[0] = v - c[0 * CS + 3 * P];
-    d[1] = v - c[1 * CS + 3 * P];
-    d[2] = v - c[2 * CS + 2 * P];
-    d[3] = v - c[3 * CS + 1 * P];
-    d[4] = v - c[3 * CS + 0 * P];
-    d[5] = v - c[3 * CS + -1 * P];
-    d[6] = v - c[2 * CS + -2 * P];
-    d[7] = v - c[1 * CS + -3 * P];
-    d[8] = v - c[0 * CS + -3 * P];
-    d[9] = v - c[-1 * CS + -3 * P];
-    d[10] = v - c[-2 * CS + -2 * P];
-    d[11] = v - c[-3 * CS + -1 * P];
-    d[12] = v - c[-3 * CS + 0 * P];
-    d[13] = v - c[-3 * CS + 1 * P];
-    d[14] = v - c[-2 * CS + 2 * P];
-    d[15] = v - c[-1 * CS + 3 * P];
+    int p[16];
+    p[0] = c[0 * CS + 3 * P];
+    p[1] = c[1 * CS + 3 * P];
+    p[2] = c[2 * CS + 2 * P];
+    p[3] = c[3 * CS + 1 * P];
+    p[4] = c[3 * CS + 0 * P];
+    p[5] = c[3 * CS + -1 * P];
+    p[6] = c[2 * CS + -2 * P];
+    p[7] = c[1 * CS + -3 * P];
+    p[8] = c[0 * CS + -3 * P];
+    p[9] = c[-1 * CS + -3 * P];
+    p[10] = c[-2 * CS + -2 * P];
+    p[11] = c[-3 * CS + -1 * P];
+    p[12] = c[-3 * CS + 0 * P];
+    p[13] = c[-3 * CS + 1 * P];
+    p[14] = c[-2 * CS + 2 * P];
+    p[15] = c[-1 * CS + 3 * P];
     // 9-arc [k, k+8] = three 3-runs: v_min3/v_max3 over runs, then over the arcs
     int m3[16], x3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        m3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-        x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        m3[k] = min(min(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
+        x3[k] = max(max(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
     }
-    int A = 0, Bn = 0;   // clamped at 0: only positive strengths matter (thresholds are >= 0)
+    int X = 255, Y = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k += 2) {   // two arcs per v_max3 / v_min3
-        A = max(max(A, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15])),
-                min(min(m3[k + 1], m3[(k + 4) & 15]), m3[(k + 7) & 15]));   // dark arc:   all v - p
-        Bn = min(min(Bn, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15])),
-                 max(max(x3[k + 1], x3[(k + 4) & 15]), x3[(k + 7) & 15]));  // bright arc: all p - v
+    for (int k = 0; k < 16; k += 2) {   // two arcs per v_min3 / v_max3
+        X = min(min(X, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15])),
+                max(max(x3[k + 1], x3[(k + 4) & 15]), x3[(k + 7) & 15]));   // dark arcs:   max p
+        Y = max(max(Y, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15])),
+                min(min(m3[k + 1], m3[(k + 4) & 15]), m3[(k + 7) & 15]));   // bright arcs: min p
     }
-    return max(A, -Bn);
+    return max(max(v - X, Y - v), 0);
 }
 
 // Host table of the cells (ComputeKeyPointsOctTree's grid, ORBextractor.cc:781-806), frame independent.
@@ -675,6 +677,10 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                                     : prefilter_cell<TQ, true>(t32, dh, rpi, lrow, lane_on, x0, xvalid, tt, sList);
         wave_lds_sync();
         ORBGPU_STAMP(2);
+#if defined(ORBGPU_FAST_CUT) && ORBGPU_FAST_CUT == 2
+        if (lane == 0) *cntOut = nlist & 0;
+        return;
+#endif
         // ---- stage 2: exact arc strength for the survivors; corners at th are compacted in place
         // (each chunk is read into registers before any lane writes, and writes land at or before it)
         int ncorner = 0;
@@ -694,6 +700,10 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         }
         wave_lds_sync();
         ORBGPU_STAMP(3);
+#if defined(ORBGPU_FAST_CUT) && ORBGPU_FAST_CUT == 3
+        if (lane == 0) *cntOut = ncorner & 0;
+        return;
+#endif
         // ---- cell-local NMS at th.  Neighbours outside the domain are ROI border pixels (M = 0);
         // M <= th counts 0.  The corner list is in raster order (the prefilter compacts rows in order, pixels
         // ascending within a lane's run, runs in lane order), so the kept corners are emitted as they
@@ -776,6 +786,11 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         wave_lds_sync();   // the previous cell's last LDS reads happen before this one's writes
         fast_roi_store<TQ>(c, lane, k == 0 ? v0 : v1, tile);
         ORBGPU_STAMP(6);
+#if defined(ORBGPU_FAST_CUT) && ORBGPU_FAST_CUT == 1   // instruction-count diagnostics only (tools/diag_cut.sh)
+        wave_lds_sync();
+        if (lane == 0) *cntOut = (int)tile[lane] & 0;
+        continue;
+#endif
         fast_cell_body<TQ>(g, c, lane, tile, sList, cands, cntOut, stamps, item);
     }
 }
