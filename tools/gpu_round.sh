@@ -12,6 +12,12 @@ if [ -z "$SKIP_TESTS" ]; then
   step pytest_gpu 480 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu || exit 1
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 fi
+# PMC passes first, so the bench line's roofline.traffic / roofline.valu come from this same build
+if [ -n "$PMC" ]; then
+  bash tools/pmc.sh > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $OUT/pmc.log; exit 1; }
+  echo "pmc ok"
+  export ORBGPU_PMC_JSON=$OUT/pmc/report.json
+fi
 step bench 600 python bench.py --steps 20 --warmup 3 || exit 1
 step bench_c2 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu --no-c4 --no-bird || exit 1
 step bench_c5 300 python bench.py --config c5 --steps 50 --warmup 5 --no-cpu --no-c4 --no-bird --no-stereo || exit 1
@@ -19,8 +25,4 @@ step bench_c5 300 python bench.py --config c5 --steps 50 --warmup 5 --no-cpu --n
 step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --only-extract --no-profile-pass --steps 20 --warmup 3 || exit 1
 # the same loop one batch at a time: per-launch durations comparable with the bench's HIP-event roofline pass
 step rocprof_serial 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_serial -o run -- python3 bench.py --only-extract --no-profile-pass --pipelines 1 --steps 20 --warmup 3 || exit 1
-if [ -n "$PMC" ]; then
-  bash tools/pmc.sh > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $OUT/pmc.log; exit 1; }
-  echo "pmc ok"
-fi
 exit 0
