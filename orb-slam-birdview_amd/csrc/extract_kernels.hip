@@ -351,7 +351,7 @@ void build_cells(const Geom& g, std::vector<CellDesc>& cells) {
                 d.pitch = L.pitch;
                 d.pyr_off = (int)L.pyr_off;
                 const int x0w = iniX >> 2, nw = std::max(1, ((iniX + rw + 3) >> 2) - x0w);
-                const int nruns = std::max(1, (rw - 6 + 7) / 8);
+                const int nruns = std::max(1, (rw - 6 + 15) / 16);   // 16-pixel prefilter runs
                 d.roi = nw | ((64 / nw) << 8) | (x0w << 16);
                 d.m_nw = (int)recip20((uint32_t)nw);
                 d.runs = nruns | ((64 / nruns) << 8);
@@ -627,7 +627,7 @@ __device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int r
             // one VGPR address per row round (the asm keeps the compiler from re-deriving it per load)
             lds_cu32* w = (lds_cu32*)(t32 + r0 * (TQ / 2));
             asm volatile("" : "+v"(w));
-            pm = (int)(prefilter16<TQ, CLEAN>(w, tt) & xvalid);
+            pm = (int)((prefilter16<TQ, CLEAN>(w, tt) | (prefilter16<TQ, CLEAN>(w + 4, tt) << 8)) & xvalid);
         }
         const int cnt = __popc(pm);
         const int incl = wave_incl_scan(cnt);
@@ -650,10 +650,10 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                                                uint16_t* tile, uint16_t* sList,
                                                uint32_t* __restrict__ cands,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
-    constexpr int PX = 8, TB = 2 * TQ;   // TB: tile row pitch in bytes
+    constexpr int PX = 16, TB = 2 * TQ;   // PX: pixels per lane and row round; TB: tile row pitch in bytes
     const int dw = c.dw, dh = c.dh;
     ORBGPU_STAMP(1);
-    // lane -> (run of PX = 8 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
+    // lane -> (run of PX = 16 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
     const int nruns = c.nruns;                           // (dw + PX - 1) / PX
     const int rpi = c.rpi;                               // rows per iteration, 64 / nruns
     const int lrow = (int)div20(lane, c.m_runs);

@@ -80,7 +80,7 @@ struct CellDesc {
     // division costs ~15 VALU instructions, one of them a transcendental v_rcp):
     int roi;       // ROI load: dwords per row nw | rows per round (64 / nw) << 8 | first dword (iniX >> 2) << 16
     int m_nw;      // recip20(nw)
-    int runs;      // prefilter: 8-pixel runs per row nruns | rows per round (64 / nruns) << 8
+    int runs;      // prefilter: 16-pixel runs per row nruns | rows per round (64 / nruns) << 8
     int m_runs;    // recip20(nruns)
     int pad[4];    // 64 bytes: one scalar dwordx16 load
 };
