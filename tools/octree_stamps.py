@@ -16,7 +16,7 @@ from orbgpu.synth import synth_batch  # noqa: E402
 
 
 def main():
-    B, NL, NCELLS = 64, 8, 2656
+    B, NL, NCELLS = int(sys.argv[1]) if len(sys.argv) > 1 else 64, 8, 2656
     bx = orbgpu.BatchExtractor(2000, 1280, 720, B)
     bx.upload(synth_batch(1280, 720, B))
     for _ in range(3):
