@@ -519,14 +519,25 @@ __device__ __forceinline__ uint32_t dpp_prev_lane(uint32_t v) {   // lane - 1's 
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, true);
 }
 
+// v_perm selectors as SGPRs (a VOP3 takes no literal on gfx9: left to itself the compiler re-materialises
+// one per store with a v_mov)
+struct WidenSel {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ uint32_t sgpr_const(uint32_t x) {
+    uint32_t r;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(x));
+    return r;
+}
+
 template <bool ODD>
-__device__ __forceinline__ void widen_store(uint32_t* q, uint32_t v, uint32_t pv, bool last) {
-    if (ODD) {
-        q[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
-        q[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
-    } else {
-        q[0] = __builtin_amdgcn_perm(v, pv, 0x0c040c03u);
-        q[1] = __builtin_amdgcn_perm(0u, v, 0x0c020c01u);
+__device__ __forceinline__ void widen_store(uint32_t* q, uint32_t v, uint32_t pv, bool last, const WidenSel& S) {
+    if (ODD) {   // (b0, b1), (b2, b3)
+        q[0] = __builtin_amdgcn_perm(0u, v, S.lo);
+        q[1] = __builtin_amdgcn_perm(0u, v, S.hi);
+    } else {     // (prev b3, b0), (b1, b2) [, (b3, 0)]
+        q[0] = __builtin_amdgcn_perm(v, pv, S.lo);
+        q[1] = __builtin_amdgcn_perm(0u, v, S.hi);
         if (last) q[2] = v >> 24;
     }
 }
@@ -535,18 +546,23 @@ __device__ __forceinline__ void widen_store(uint32_t* q, uint32_t v, uint32_t pv
 template <int TQ, bool ODD>
 __device__ __forceinline__ void widen_rows(const FastCellT& c, const RoiLanes& r, const uint32_t (&v)[8], uint32_t* t32,
                                            int B, bool last) {
+    const WidenSel S = ODD ? WidenSel{sgpr_const(0x0c010c00u), sgpr_const(0x0c030c02u)}
+                           : WidenSel{sgpr_const(0x0c040c03u), sgpr_const(0x0c020c01u)};
     uint32_t* t = t32 + (r.yy0 * (TQ / 2) + 2 * r.ww - (B >> 1));
+    const bool on = r.yy0 < r.rpr;
+    const int rpr = __builtin_amdgcn_readfirstlane(r.rpr), rh = __builtin_amdgcn_readfirstlane(c.rh);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        if (k * r.rpr >= c.rh) break;   // wave-uniform
+        const int k0 = k * rpr;
+        if (k0 >= rh) break;   // wave-uniform
         const uint32_t pv = ODD ? 0u : dpp_prev_lane(v[k]);
-        if (roi_row_ok(c, r, k)) widen_store<ODD>(t + k * r.rpr * (TQ / 2), v[k], pv, last);
+        if (on && r.yy0 + k0 < rh) widen_store<ODD>(t + k0 * (TQ / 2), v[k], pv, last, S);
     }
-    if (r.yy0 < r.rpr)
-        for (int yy = r.yy0 + 8 * r.rpr; yy < c.rh; yy += r.rpr) {   // lanes of one row iterate together
+    if (on)
+        for (int yy = r.yy0 + 8 * rpr; yy < rh; yy += rpr) {   // lanes of one row iterate together
             const uint32_t w = *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + r.ww) * 4));
             const uint32_t pw = ODD ? 0u : dpp_prev_lane(w);
-            widen_store<ODD>(t32 + (yy * (TQ / 2) + 2 * r.ww - (B >> 1)), w, pw, last);
+            widen_store<ODD>(t32 + (yy * (TQ / 2) + 2 * r.ww - (B >> 1)), w, pw, last, S);
         }
 }
 
