@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
                                                    int cbeg, int cnum, unsigned long long* __restrict__ stamps,
-                                                   int* __restrict__ err) {
+                                                   int* __restrict__ err, int ipw) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
     if (err && blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // k_octree's overflow flag (set after this kernel)
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
@@ -776,13 +776,13 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (8 cells each)
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    const int item0 = (blk * (int)(blockDim.x >> 6) + wv) * 2;
+    const int item0 = (blk * (int)(blockDim.x >> 6) + wv) * ipw;   // ipw = items per wave, 2 (1 for latency)
     if (item0 >= total) return;   // whole wave; nothing below uses a block barrier
     const int wb = g->fast_wave_bytes;
     // 16-bit pixel tile, TQ per row, after a 16-byte lead pad (fast_roi_store's dword -1 of row 0)
     uint16_t* tile = reinterpret_cast<uint16_t*>(smem + (size_t)wv * wb + 16);
     uint16_t* sList = reinterpret_cast<uint16_t*>(smem + (size_t)wv * wb + ((g->fast_rows * TQ * 2 + 32 + 15) & ~15));
-    const bool has1 = item0 + 1 < total;
+    const bool has1 = ipw == 2 && item0 + 1 < total;
     const FastCellT c0 = fast_cell_t(g, cells, item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
     const FastCellT c1 = fast_cell_t(g, cells, has1 ? item0 + 1 : item0, frames, framePitch, rowStride, pyr, cbeg, cnum);
     uint32_t v0[8], v1[8];
@@ -1664,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
-                                                  unsigned long long* __restrict__ dstamps) {
+                                                  unsigned long long* __restrict__ dstamps, int spw) {
     // per wave: 43x48 window (+16 B pad) and the transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch;
     // pitch 50 spreads the transposed stores of the 10 column groups over distinct banks)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[kDescWaves][kDescWin * kDescWinPitch + 16];
@@ -1672,7 +1672,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     // 1-D grid, blocks dealt round-robin over the 8 XCDs: XCD x takes a contiguous run of the (frame,
     // slot-block) sequence, so a frame's windows are fetched into one L2 (PMC: 0.71 GB per 256 C3
     // frames against 1.96 GB with the frames spread over every XCD)
-    const int gx = (g->nkpcap + kDescWaves * kDescSlotsPerWave - 1) / (kDescWaves * kDescSlotsPerWave);
+    const int gx = (g->nkpcap + kDescWaves * spw - 1) / (kDescWaves * spw);   // spw: slots per wave, 2 (1 for latency)
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int lb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     const int f = lb / gx, bx = lb - f * gx;
@@ -1684,10 +1684,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
         for (int i = 0; i < nl; i++) tot += cnts[i];
         outN[f] = tot;
     }
-    const int s0 = (bx * kDescWaves + wv) * kDescSlotsPerWave;
+    const int s0 = (bx * kDescWaves + wv) * spw;
     if (s0 >= g->nkpcap) return;
     const DescSlot d0 = desc_slot(g, f, s0, cnts, lvlKps, frames, framePitch, rowStride, pyr);
-    const DescSlot d1 = desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr);
+    const DescSlot d1 = spw == 2 ? desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr)
+                                 : DescSlot{};
     if (!d0.ok && !d1.ok) return;   // (the two slots may straddle a level boundary)
     uint32_t v0[9], v1[9];
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
@@ -1771,9 +1772,11 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     auto fast = [&](int cbeg, int cnum, hipStream_t s, int* zero) {
         const int items = cnum * nframes;
         auto kern = g.fast_compact ? k_fast_wave<48> : k_fast_wave<kFastTilePitch>;
-        hipLaunchKernelGGL(kern, dim3(cdiv(items, 2)), dim3(64), (size_t)g.fast_wave_bytes, s, b.d_geom, b.d_cells,
+        // a single frame (the host path's latency) takes one cell per wave: twice the waves, half each one's chain
+        const int ipw = nframes == 1 ? 1 : 2;
+        hipLaunchKernelGGL(kern, dim3(cdiv(items, ipw)), dim3(64), (size_t)g.fast_wave_bytes, s, b.d_geom, b.d_cells,
                            d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum,
-                           b.d_stamps, zero);
+                           b.d_stamps, zero, ipw);
     };
     auto octree = [&](int lbase, int nl, hipStream_t s) {
         const int lk = octree_lds_keys(g.node_cap);
@@ -1783,9 +1786,10 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     };
     auto describe = [&](hipStream_t s) {
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
-        const unsigned gx = cdiv(g.nkpcap, kDescWaves * kDescSlotsPerWave);
+        const int spw = nframes == 1 ? 1 : kDescSlotsPerWave;   // a single frame: one keypoint per wave
+        const unsigned gx = cdiv(g.nkpcap, kDescWaves * spw);
         hipLaunchKernelGGL(k_describe, dim3(gx * nframes), dim3(64 * kDescWaves), 0, s, b.d_geom, d_frames, frame_pitch,
-                           row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap, dst);
+                           row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap, dst, spw);
     };
     int* zero = b.zero_err ? b.d_err : nullptr;
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);
