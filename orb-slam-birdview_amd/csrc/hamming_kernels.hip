@@ -119,12 +119,15 @@ __global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, c
 
 /* The same all-pairs top-2 on the matrix cores.  With descriptor bits as +-1 int8 values,
  * q . t = 256 - 2 popcount(q ^ t), so a tile of Hamming distances is one 32x32 i8 GEMM over K = 256:
- * eight v_mfma_i32_32x32x32_i8.  A workgroup owns 128 queries (4 waves x 32, the B operand, expanded
- * once into registers) and walks its train slice in tiles of 32 (the A operand, expanded into LDS,
- * double-buffered; rows padded to 272 bytes so the 16-byte fragment reads are conflict-free).  The
- * accumulator puts trains on the registers and queries on the lanes (row = (r&3) + 8(r>>2) + 4(lane>>5),
- * column = lane & 31), so the top-2 update is lane-local; the two lane halves are merged at the end.
- * Keys: dist << 16 | train index, so min keeps the first index on ties (SearchByBoW's strict `<`). */
+ * eight v_mfma_i32_32x32x32_i8 in one accumulator chain.  A workgroup owns 128 queries (4 waves x 32,
+ * the B operand, expanded once into registers as -16 / +16, so the tile's results come out as
+ * tile-local keys, see kc) and walks its train slice in tiles of 32 (the A operand: trains expanded to
+ * +-1 once per launch by k_expand_pm1, copied into LDS, double-buffered; rows padded to 272 bytes so
+ * the 16-byte fragment reads are conflict-free).  The accumulator puts trains on the registers and
+ * queries on the lanes (row = (r&3) + 8(r>>2) + 4(lane>>5), column = lane & 31), so the top-2 update is
+ * lane-local; the two lane halves are merged at the end.  Running keys: dist << 16 | train index, so
+ * min keeps the first index on ties (SearchByBoW's strict `<`).  The accumulators live in VGPRs
+ * (-amdgpu-mfma-vgpr-form: no v_accvgpr_read per result). */
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 constexpr int kMfTr = 32;      // trains per tile (MFMA rows)
@@ -151,7 +154,38 @@ __device__ __forceinline__ v4i_t pm1x16(uint32_t w) {   // bits 0..15 of w -> 16
     r.w = pm1x4(w >> 12);
     return r;
 }
+// 4 query bits -> 4 bytes: -16 (0xF0) where the bit is set, +16 (0x10) where it is clear.  Against +-1
+// trains the MFMA then sums -16 * dot, and from an initial 4096 + row each result is its tile-local key.
+__device__ __forceinline__ int pm16x4(uint32_t n) {
+    const uint32_t s = __umul24(n & 15u, 0x00204081u) & 0x01010101u;
+    const uint32_t m = (s << 8) - s;                                    // 0xFF in the set bytes
+    return (int)(0x10101010u ^ (m & 0xE0E0E0E0u));
+}
+__device__ __forceinline__ v4i_t pm16x16(uint32_t w) {
+    v4i_t r;
+    r.x = pm16x4(w);
+    r.y = pm16x4(w >> 4);
+    r.z = pm16x4(w >> 8);
+    r.w = pm16x4(w >> 12);
+    return r;
+}
 
+/* The pairs' train descriptors expanded to +-1 int8 once per launch (thread = one descriptor dword ->
+ * 32 bytes), so k_top2_mfma's train tiles are plain copies: without it every query workgroup of a pair
+ * re-expands every train tile (~40 VALU per thread and tile, more than the tile's top-2 updates). */
+__global__ __launch_bounds__(256) void k_expand_pm1(Top2Batch a, int max_nt) {
+    const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int row = i >> 3, s = i & 7;
+    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
+    const int nt = a.counts ? a.counts[fr.y] : a.nt;
+    if (row >= min(nt, max_nt)) return;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(a.t + ((long long)fr.y * a.t_stride + row) * 32)[s];
+    v4i_t* d = reinterpret_cast<v4i_t*>(const_cast<uint8_t*>(a.tx) + ((long long)p * a.tx_stride + row) * 256 + 32 * s);
+    d[0] = pm1x16(w);
+    d[1] = pm1x16(w >> 16);
+}
+
+template <bool PRE>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx)
 __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
                                                    int* __restrict__ idx_o, int* __restrict__ second_o) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[2][kMfTr * kMfPitch];
@@ -174,53 +208,83 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
         }
         const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-        for (int s = 0; s < 8; s++) qf[s] = pm1x16(qd[s] >> (16 * h));
+        for (int s = 0; s < 8; s++) qf[s] = pm16x16(qd[s] >> (16 * h));
     }
     const uint32_t* __restrict__ T = reinterpret_cast<const uint32_t*>(a.t + (long long)fr.y * a.t_stride * 32);
-    const int er = tid >> 3, es = tid & 7;   // staging: thread -> (train row, descriptor dword)
-    auto stage = [&](int buf, uint32_t w) {
+    // PRE: this pair's expanded trains through a buffer descriptor (SGPRs), 32-bit offsets
+    const uint64_t txb = PRE ? reinterpret_cast<uint64_t>(a.tx + (long long)p * a.tx_stride * 256) : 0;
+    const auto TXR = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(txb >> 32)) << 32) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)txb)),
+        0, 0x7FFFFFFF, 0x00020000);
+    const int er = tid >> 3, es = tid & 7;   // staging: thread -> (train row, descriptor dword = 32 expanded bytes)
+    struct Chunk {
+        uint32_t w;    // !PRE: the descriptor dword
+        v4i_t x0, x1;  // PRE: its 32 expanded bytes
+    };
+    auto fetch = [&](int row) -> Chunk {
+        Chunk k;
+        if (PRE) {
+            const int o = row * 256 + 32 * es;
+            k.x0 = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, o, 0, 0));
+            k.x1 = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, o + 16, 0, 0));
+        } else {
+            k.w = T[(long long)row * 8 + es];
+        }
+        return k;
+    };
+    auto stage = [&](int buf, const Chunk& k) {
         v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * kMfPitch + es * 32]);
-        d[0] = pm1x16(w);
-        d[1] = pm1x16(w >> 16);
+        d[0] = PRE ? k.x0 : pm1x16(k.w);
+        d[1] = PRE ? k.x1 : pm1x16(k.w >> 16);
     };
     unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
+    // the MFMA's initial accumulator: 4096 + row, so that with the queries scaled to -16 / +16 every result
+    // is already its tile-local key 4096 - 16 dot + row = dist * 32 + row (dist = (256 - dot) / 2)
+    v16i_t kc;
+#pragma unroll
+    for (int r = 0; r < 16; r++) kc[r] = 4096 + (r & 3) + 8 * (r >> 2);
     const int ntile = t1 > t0 ? (t1 - t0 + kMfTr - 1) / kMfTr : 0;   // uniform
     if (ntile > 0) {
-        stage(0, t0 + er < t1 ? T[(long long)(t0 + er) * 8 + es] : 0u);
+        // rows past the slice load the slice's last row (their keys are masked): no zeroing, no branch
+        stage(0, fetch(min(t0 + er, t1 - 1)));
         __syncthreads();
         for (int j = 0; j < ntile; j++) {
             const int tb = t0 + kMfTr * j;
             const bool more = j + 1 < ntile;
-            uint32_t wn = 0;
-            if (more && tb + kMfTr + er < t1) wn = T[(long long)(tb + kMfTr + er) * 8 + es];
+            Chunk wn;
+            if (more) wn = fetch(min(tb + kMfTr + er, t1 - 1));
             const uint8_t* A = &s_t[j & 1][c * kMfPitch + 16 * h];
-            v16i_t acc0 = {}, acc1 = {};
+            v16i_t acc = kc;
 #pragma unroll
-            for (int s = 0; s < 8; s += 2) {   // two accumulators: independent MFMA chains
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s], acc0, 0,
-                                                             0, 0);
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s + 32),
-                                                             qf[s + 1], acc1, 0, 0, 0);
-            }
-            // key = dist << 16 | train = (256 - dot) * 2^15 + train (256 - dot is even); with b <= s2,
-            // min(s2, max(b, key)) is med3(b, key, s2)
-            const int kb = (256 << 15) + tb + 4 * h;
+            for (int s = 0; s < 8; s++)   // one chain: the other waves on the SIMD hide its latency
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s], acc, 0, 0, 0);
+            // the results are tile-local keys dist * 32 + row (row = (r&3) + 8(r>>2) < 32; dist = (256 - dot)
+            // / 2, see kc): the tile's top-2 by med3 / min (2 ops per distance), then merged
+            // into the running keys dist << 16 | train index once per tile
+            unsigned lb = 0xFFFFFFFFu, ls = 0xFFFFFFFFu;
             if (tb + kMfTr <= t1) {
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
-                    const unsigned key = (unsigned)(__mul24(acc0[r] + acc1[r], -32768) + kb + (r & 3) + 8 * (r >> 2));
-                    s2 = umed3(b, key, s2);
-                    b = min(b, key);
+                    const unsigned key = (unsigned)acc[r];
+                    ls = umed3(lb, key, ls);
+                    lb = min(lb, key);
                 }
             } else {   // the slice's last, partial tile
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const int tr = tb + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const unsigned key = tr < t1
-                        ? (unsigned)(__mul24(acc0[r] + acc1[r], -32768) + kb + (r & 3) + 8 * (r >> 2)) : 0xFFFFFFFFu;
-                    s2 = umed3(b, key, s2);
-                    b = min(b, key);
+                    const unsigned key = tr < t1 ? (unsigned)acc[r] : 0xFFFFFFFFu;
+                    ls = umed3(lb, key, ls);
+                    lb = min(lb, key);
                 }
+            }
+            if (lb != 0xFFFFFFFFu) {   // (only a partial tile leaves a lane without keys)
+                const unsigned gb = ((lb << 11) & 0xFFFF0000u) + (lb & 31u) + (unsigned)(tb + 4 * h);
+                s2 = umed3(b, gb, s2);
+                b = min(b, gb);
+                // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
+                if (ls != 0xFFFFFFFFu) s2 = min(s2, (ls << 11) | 0xFFFFu);
             }
             if (more) stage((j + 1) & 1, wn);
             __syncthreads();
@@ -260,7 +324,14 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
     a.slice = ((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr;
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
-    hipLaunchKernelGGL(k_top2_mfma, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx, d_second);
+    if (a.tx) {
+        hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, npairs), dim3(256), 0, stream, a, max_nt);
+        hipLaunchKernelGGL(k_top2_mfma<true>, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
+                           d_second);
+    } else {
+        hipLaunchKernelGGL(k_top2_mfma<false>, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best,
+                           d_best_idx, d_second);
+    }
     if (nsu > 1)
         hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,
                            d_best, d_best_idx, d_second);

@@ -273,10 +273,11 @@ int orb_hamming_top2_device(orb_ctx* h, const uint8_t* d_q, int nq, const uint8_
     if (nt > 65535) return set_error("orb_hamming_top2_device: more than 65535 trains", hipSuccess), ORB_ERR_ARG;
     Arena a{c};
     const int ns = top2_batch_slices(1, nq, nt);
-    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(uint2)) + 256);
+    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(uint2)) + Arena::align((size_t)nt * 256) + 512);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     uint2* part = a.take<uint2>((size_t)ns * nq);
-    Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq};
+    uint8_t* tx = a.take<uint8_t>((size_t)nt * 256);   // trains expanded to +-1 int8 once (k_expand_pm1)
+    Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq, tx, nt};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2_batch(tb, 1, nq, nt, d_best, d_best_idx, d_second, part, c->stream);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
@@ -295,16 +296,18 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     Arena a{c};
     const int ns = top2_batch_slices(npairs, kp_cap, kp_cap);
     hipError_t e = a.reserve(Arena::align((size_t)npairs * sizeof(int2)) +
-                             Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) + 512);
+                             Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) +
+                             Arena::align((size_t)npairs * kp_cap * 256) + 768);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     int2* d_frames = a.take<int2>(npairs);
     uint2* part = a.take<uint2>((size_t)npairs * ns * kp_cap);
+    uint8_t* tx = a.take<uint8_t>((size_t)npairs * kp_cap * 256);   // each pair's trains expanded once
     if (c->frames_host.size() < (size_t)npairs) c->frames_host.resize(npairs);
     for (int p = 0; p < npairs; p++) c->frames_host[p] = make_int2(q_frames[p], t_frames[p]);
     if ((e = hipMemcpyAsync(d_frames, c->frames_host.data(), (size_t)npairs * sizeof(int2), hipMemcpyHostToDevice,
                             c->stream)) != hipSuccess)
         return set_error("upload pairs", e), ORB_ERR_HIP;
-    Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap};
+    Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap, tx, kp_cap};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2_batch(tb, npairs, kp_cap, kp_cap, d_best, d_best_idx, d_second, part, c->stream);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);

@@ -136,6 +136,10 @@ struct Top2Batch {
     const int2* frames;
     int slice;
     long long out_stride;   // outputs / partials of pair p at p * out_stride + query
+    // trains already expanded to +-1 int8 (256 B each; pair p's at tx + p * tx_stride * 256), or NULL:
+    // k_top2_mfma then expands every train tile itself
+    const uint8_t* tx;
+    long long tx_stride;
 };
 int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,

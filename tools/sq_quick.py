@@ -5,7 +5,8 @@ import glob
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_fast_wave": "fast", "k_describe": "describe", "k_resize_tiled": "resize", "k_octree": "octree"}
+KERNELS = {"k_fast_wave": "fast", "k_describe": "describe", "k_resize_tiled": "resize", "k_octree": "octree",
+           "k_expand_pm1": "expand_pm1", "k_top2_mfma": "top2_mfma", "k_top2b_merge": "top2b_merge"}
 
 
 def main(d):
