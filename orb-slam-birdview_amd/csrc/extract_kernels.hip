@@ -1566,6 +1566,10 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     }
     wave_lds_sync();
     DESC_STAMP(1);
+#if defined(ORBGPU_DESC_CUT) && ORBGPU_DESC_CUT == 1   // instruction-count diagnostics only (tools/diag_cut.sh)
+    if (lane == 0) outD[((long long)f * kpCap + outIdx) * 32] = wbase[lane];
+    return;
+#endif
 
     // ---- IC_Angle (:77-104) on the unblurred window: lanes 2r, 2r+1 (r < 31) sum halves of row v = r - 15
     // over the circular patch |u| <= umax[|v|] with v_dot4_u32_u8 (u*I = (u+16)*I - 16*I); two lanes per
@@ -1594,6 +1598,10 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     m01 = wave_sum(m01);
     const float angle = fast_atan2((float)m01, (float)m10);
     DESC_STAMP(2);
+#if defined(ORBGPU_DESC_CUT) && ORBGPU_DESC_CUT == 2
+    if (lane == 0) outD[((long long)f * kpCap + outIdx) * 32] = (uint8_t)angle;
+    return;
+#endif
 
     // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass: item = (row wy, 4 outputs
     // rx = 4g..4g+3) over window bytes 4g..4g+9; output o = v_dot4(bytes o..o+3, k0..k3) +
@@ -1617,6 +1625,10 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     }
     wave_lds_sync();
     DESC_STAMP(3);
+#if defined(ORBGPU_DESC_CUT) && ORBGPU_DESC_CUT == 3
+    if (lane == 0) outD[((long long)f * kpCap + outIdx) * 32] = (uint8_t)(angle + rt[lane]);
+    return;
+#endif
 
     // ---- column pass: evaluated only at the 512 BRIEF sample pixels (brief_sampled), v_dot2_u32_u16 on
     // row pairs of RT; rounding as the pinned OpenCV 3.2 8U path: half-to-even where the SSE2 body runs
