@@ -1446,8 +1446,10 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         // +18 centre offset is folded into the constant (it is even, so ties still go to even)
         const uint32_t xb = __builtin_bit_cast(uint32_t, fx + 12582930.0f) & 0xFFFFu;
         const uint32_t yb = __builtin_bit_cast(uint32_t, fy + 12582930.0f);
-        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + __umul24(xb, 2u * kRtPitch) + ((yb & 0xFFFEu) << 1));
-        const uint32_t sh = yb << 4;   // v_alignbit reads bits 4:0: 16 for an odd row, realigning the u16 pairs
+        // RT element (xb, yb); the pitch is odd, so an element's dword parity depends on both
+        const uint32_t idx = __umul24(xb, (unsigned)kRtPitch) + (yb & 0xFFFFu);
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + ((idx & ~1u) << 1));
+        const uint32_t sh = idx << 4;   // v_alignbit reads bits 4:0: 16 for an odd element, realigning the u16 pairs
         const uint32_t d0 = rp[0], d1 = rp[1], d2 = rp[2], d3 = rp[3], d4 = rp[4];
         uint32_t S = __builtin_amdgcn_udot2(K01, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d1, d0, sh)), 0u, false);
         S = __builtin_amdgcn_udot2(K23, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d2, d1, sh)), S, false);
@@ -1678,7 +1680,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
                                                   unsigned long long* __restrict__ dstamps, int spw) {
     // per wave: 43x48 window (+16 B pad) and the transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch;
-    // pitch 50 spreads the transposed stores of the 10 column groups over distinct banks)
+    // an odd pitch spreads the transposed stores of the 10 column groups over distinct banks)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[kDescWaves][kDescWin * kDescWinPitch + 16];
     __shared__ __attribute__((aligned(16))) uint16_t s_rt[kDescWaves][40 * kRtPitch];
     // 1-D grid, blocks dealt round-robin over the 8 XCDs: XCD x takes a contiguous run of the (frame,
