@@ -117,6 +117,13 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
  * base or stride is not 16-byte aligned), the coefficients of the tile's columns/rows are staged
  * once, and each thread then produces 4 output pixels per row pass (one dword store) from LDS byte
  * reads. */
+// s_cy entry of one output row: the LDS byte offsets of its two source rows and the vertical weights
+// pre-shifted for the vertical pass, (c * (h >> 4)) >> 16 == mul_hi_u24(c << 12, h & ~15) (c <= 2048 and
+// h < 2^19 keep both operands within 24 bits)
+__device__ __forceinline__ int4 rs_row_entry(const ResizeCoef& c, int sy0) {
+    return make_int4((c.s0 - sy0) * kRsPitch, (c.s1 - sy0) * kRsPitch, c.c0 << 12, c.c1 << 12);
+}
+
 template <int kRsTileH>
 __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
                                                       const ResizeCoef* __restrict__ coef, int level,
@@ -163,7 +170,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         }
         if (tid < kRsTileH) {
             const ResizeCoef c = coef[dw + y0 + min(tid, ny - 1)];
-            cyv = make_int4(c.s0, c.s1, c.c0, c.c1);
+            cyv = rs_row_entry(c, sy0);
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++) {   // clamped duplicates store the same bytes to the same place
@@ -178,7 +185,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         }
         if (tid < kRsTileH) {
             const ResizeCoef c = coef[dw + y0 + min(tid, ny - 1)];
-            cyv = make_int4(c.s0, c.s1, c.c0, c.c1);
+            cyv = rs_row_entry(c, sy0);
         }
         if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
             const int nw = (sx1 - sx0 + 4) >> 2;
@@ -212,8 +219,14 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         c0[i] = cx.z;
         c1[i] = cx.w;
     }
-    uint8_t* dst = pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off + x0 + tx;
+    // the level's rows through a buffer descriptor (block-uniform base in SGPRs): 32-bit store offsets
+    const uint64_t lb = reinterpret_cast<uint64_t>(pyr + (long long)f * g->pyr_bytes + g->L[level].pyr_off);
+    const auto dsr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(lb >> 32)) << 32) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)lb)),
+        0, 0x7FFFFFFF, 0x00020000);
     const int pitch = g->L[level].pitch;
+    const unsigned dcol = (unsigned)(x0 + tx);
     if (tx >= nx) return;
     // The 4 pixels' source bytes lie within 8 bytes from o0[0] (scale factor <= ~1.6; otherwise the
     // byte path below): a row's 3 dwords from LDS, realigned to o0[0], give each pixel's byte pair as
@@ -233,12 +246,10 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         for (int pass = 0; pass < kRsTileH / 8; pass++) {
             const int ty = pass * 8 + (tid >> 5);
             if (ty >= ny) break;
-            const int4 cy = s_cy[ty];
-            // (c * (h >> 4)) >> 16 == mul_hi_u24(c << 12, h & ~15): c <= 2048 and h < 2^19 keep both
-            // operands within 24 bits
-            const unsigned cy0 = (unsigned)cy.z << 12, cy1 = (unsigned)cy.w << 12;
-            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(&s_src[(cy.x - sy0) * kRsPitch]) + bw;
-            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(&s_src[(cy.y - sy0) * kRsPitch]) + bw;
+            const int4 cy = s_cy[ty];   // (LDS offsets of the two source rows, c0 << 12, c1 << 12)
+            const unsigned cy0 = (unsigned)cy.z, cy1 = (unsigned)cy.w;
+            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(&s_src[cy.x]) + bw;
+            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(&s_src[cy.y]) + bw;
             const uint32_t u0 = q0[0], u1 = q0[1], u2 = q0[2], w0 = q1[0], w1 = q1[1], w2 = q1[2];
             const uint32_t a0 = __builtin_amdgcn_alignbyte(u1, u0, bsh), a1 = __builtin_amdgcn_alignbyte(u2, u1, bsh);
             const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, bsh), b1 = __builtin_amdgcn_alignbyte(w2, w1, bsh);
@@ -252,7 +263,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
                 const unsigned v = (mul_hi_u24(cy0, h0 & ~15u) + mul_hi_u24(cy1, h1 & ~15u) + 2) >> 2;
                 packed |= v << (8 * i);
             }
-            *reinterpret_cast<uint32_t*>(dst + __umul24((unsigned)(y0 + ty), (unsigned)pitch)) = packed;
+            __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
         }
         return;
     }
@@ -261,17 +272,17 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         const int ty = pass * 8 + (tid >> 5);
         if (ty >= ny) break;
         const int4 cy = s_cy[ty];
-        const uint8_t* r0 = &s_src[(cy.x - sy0) * kRsPitch];
-        const uint8_t* r1 = &s_src[(cy.y - sy0) * kRsPitch];
+        const uint8_t* r0 = &s_src[cy.x];
+        const uint8_t* r1 = &s_src[cy.y];
         uint32_t packed = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const unsigned h0 = __umul24(r0[o0[i]], c0[i]) + __umul24(r0[o1[i]], c1[i]);
             const unsigned h1 = __umul24(r1[o0[i]], c0[i]) + __umul24(r1[o1[i]], c1[i]);
-            const unsigned v = ((__umul24((unsigned)cy.z, h0 >> 4) >> 16) + (__umul24((unsigned)cy.w, h1 >> 4) >> 16) + 2) >> 2;
+            const unsigned v = (mul_hi_u24((unsigned)cy.z, h0 & ~15u) + mul_hi_u24((unsigned)cy.w, h1 & ~15u) + 2) >> 2;
             packed |= v << (8 * i);
         }
-        *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + ty) * pitch) = packed;
+        __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
     }
 }
 
