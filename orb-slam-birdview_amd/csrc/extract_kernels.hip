@@ -1761,10 +1761,11 @@ static inline unsigned cdiv(unsigned a, unsigned b) { return (a + b - 1) / b; }
 
 size_t octree_lds_bytes(int node_cap) { return (size_t)node_cap * (16 * 4) + (32 + 8) * 4; }
 
-// Keys (u32 + u16 node index) that fit in LDS after the node tables with the block at <= 78 KiB, so
-// that two octree workgroups share a CU.
+// Keys (u32 + u16 node index) that fit in LDS after the node tables with the block at <= 52 KiB, so
+// that three octree workgroups share a CU (a level with more candidates keeps them in the global
+// scratch: the KeysInLds = false instantiation).
 static int octree_lds_keys(int node_cap) {
-    const long long room = 78 * 1024 - (long long)octree_lds_bytes(node_cap);
+    const long long room = 52 * 1024 - (long long)octree_lds_bytes(node_cap);
     return room > 0 ? (int)((room / 6) & ~7LL) : 0;
 }
 
