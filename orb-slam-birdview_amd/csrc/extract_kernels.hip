@@ -132,7 +132,9 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
     constexpr int kRows = rs_rows(kRsTileH);
     constexpr int kQ = kRsPitch / 16;                                  // 16-byte chunks per LDS row
     constexpr int kPer = (kRows * kQ + 255) / 256;                     // chunks per thread (upper bound)
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[kRows * kRsPitch];
+    // the source tile, sized on the host to the level's largest span (LevelGeom::rs_span_rows <= kRows)
+    // rather than kRows: a smaller block footprint, more resident blocks
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
     __shared__ int4 s_cx[kRsTileW];
     __shared__ int4 s_cy[kRsTileH];
     const int f = blockIdx.z;
@@ -1781,11 +1783,12 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         if (t & 3) {
             const int th = (t & 2) ? 32 : 16;
             const dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
+            const size_t lds = (size_t)g.L[l].rs_span_rows * kRsPitch;
             if (th == 32)
-                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames, frame_pitch,
+                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), lds, s, b.d_geom, cf, l, d_frames, frame_pitch,
                                    row_stride, b.d_pyr);
             else
-                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), 0, s, b.d_geom, cf, l, d_frames, frame_pitch,
+                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), lds, s, b.d_geom, cf, l, d_frames, frame_pitch,
                                    row_stride, b.d_pyr);
         } else {
             hipLaunchKernelGGL(k_resize, dim3(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes), dim3(256), 0, s,

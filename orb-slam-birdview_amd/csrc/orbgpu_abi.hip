@@ -131,15 +131,19 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
                 xfits = cx[x1].s1 - (cx[x0].s0 & ~15) + 1 <= kRsPitch;   // 16-byte aligned span start
             }
             L.rs_tiled = 0;
+            int span_rows[3] = {0, 0, 0};   // the largest source span of a tile, per tile height
             for (int i = 0; i < 3 && xfits; i++) {
                 const int th = 16 << i;
                 bool fits = true;
                 for (int y0 = 0; y0 < L.h && fits; y0 += th) {
                     const int y1 = std::min(y0 + th, L.h) - 1;
+                    span_rows[i] = std::max(span_rows[i], cy[y1].s1 - cy[y0].s0 + 1);
                     fits = cy[y1].s1 - cy[y0].s0 + 1 <= rs_rows(th);
                 }
                 if (fits) L.rs_tiled |= 1 << i;
             }
+            // the LDS source tile is sized to the tile height the launch uses (32 rows when they fit)
+            L.rs_span_rows = (L.rs_tiled & 2) ? span_rows[1] : span_rows[0];
         }
         L.maxBX = L.w - kEdgeThreshold + 3;
         L.maxBY = L.h - kEdgeThreshold + 3;

@@ -45,7 +45,7 @@ struct LevelGeom {
     float hX;            // root width (:545)
     float scale;         // mvScaleFactor
     float patch_size;    // (int)(PATCH_SIZE*scale) (:837)
-    int pad1;
+    int rs_span_rows;    // k_resize_tiled: the largest source span (rows) of a tile: its LDS tile height
 };
 
 struct Geom {
