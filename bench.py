@@ -50,7 +50,10 @@ CONFIGS = {   # BASELINE.json configs; C3 is the headline single-GPU workload
                name="C2 640x480 synthetic, 1000 features, 8 levels"),
     "c3": dict(w=1280, h=720, nfeatures=2000, batch=256, scaling="weak",
                name="C3 1280x720 KITTI-style synthetic, 2000 features, 8 levels"),
-    "c5": dict(w=1280, h=720, nfeatures=4000, global_batch=8, scaling="strong",
+    # C5's 8-frame step (1 frame per GPU at N = 8) is latency-bound: four batches in flight, one per
+    # hardware queue (GPU_MAX_HW_QUEUES = 4), measured 370 vs 290 M features/s at B = 8 and 131 vs 78 at
+    # B = 1 against two; C2 / C3 batches of 256 peak at two
+    "c5": dict(w=1280, h=720, nfeatures=4000, global_batch=8, scaling="strong", pipelines=4,
                name="C5 8-frame batch of 1280x720 synthetic, 4000 features each, sharded over the GPUs"),
 }
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -378,10 +381,13 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher plumbing only (tests/test_dist_cpu.py): ranks, rendezvous, reductions, the rank-0 "
                          "line; no GPU is touched")
-    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("ORBGPU_BENCH_PIPELINES", "2")),
+    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("ORBGPU_BENCH_PIPELINES", "0")),
                     help="batches in flight: consecutive steps alternate over this many extractor contexts "
-                         "(own stream and buffers each), so one batch's latency-bound phases overlap another's")
+                         "(own stream and buffers each), so one batch's latency-bound phases overlap another's "
+                         "(default: the config's, 2 for C2/C3, 4 for C5)")
     args = ap.parse_args()
+    if args.pipelines <= 0:
+        args.pipelines = CONFIGS[args.config].get("pipelines", 2)
     if args.only_extract:
         args.no_cpu = args.no_hamming = args.no_stereo = args.no_host_path = args.no_bird = args.no_c4 = True
 

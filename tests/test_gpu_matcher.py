@@ -244,6 +244,40 @@ def test_top2_device_small_train_sets(orbgpu_mod, nt):
         L.orb_device_free(b.h, p)
 
 
+def test_top2_device_extreme_distances_and_ties(orbgpu_mod):
+    """Distances 0 and 256 (the ends of the MFMA kernel's tile-local key range) and long runs of equal
+    distances across 32-train tiles: the first index wins, the second is the second-smallest distance."""
+    from orbgpu import _lib
+    rng = np.random.default_rng(7)
+    nq = 70
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    q[1] = 0
+    q[2] = 255
+    t = np.concatenate([np.repeat(q[:1], 50, 0), np.repeat(~q[:1], 47, 0), np.zeros((5, 32), np.uint8),
+                        np.full((3, 32), 255, np.uint8)])
+    nt = len(t)
+    b = orbgpu_mod.BatchExtractor(1000, 640, 480, 1)
+    L = _lib.lib()
+    dq, dt = b._alloc(q.nbytes), b._alloc(t.nbytes)
+    out = [b._alloc(nq * 4) for _ in range(3)]
+    L.orb_memcpy_h2d(b.h, dq, q.ctypes.data, q.nbytes)
+    L.orb_memcpy_h2d(b.h, dt, t.ctypes.data, t.nbytes)
+    b.hamming_top2(dq, nq, dt, nt, *out)
+    b.sync()
+    res = [np.zeros(nq, np.int32) for _ in range(3)]
+    for r, d in zip(res, out):
+        L.orb_memcpy_d2h(b.h, r.ctypes.data, d, nq * 4)
+    D = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    srt = np.sort(D, 1)
+    assert np.array_equal(res[0], srt[:, 0]) and np.array_equal(res[1], D.argmin(1))
+    assert np.array_equal(res[2], srt[:, 1])
+    assert (res[0][0], res[1][0], res[2][0]) == (0, 0, 0)
+    assert res[0][1] == 0 and res[1][1] == 97 and res[0][2] == 0 and res[1][2] == 102
+    for p in [dq, dt] + out:
+        L.orb_device_free(b.h, p)
+    b.close()
+
+
 def test_top2_frames_batch_vs_numpy(orbgpu_mod):
     """orb_hamming_top2_frames_device: many frame pairs of an extraction batch in one launch, counts
     read on the device — vs numpy on the downloaded descriptors."""
