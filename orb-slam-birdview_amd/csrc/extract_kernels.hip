@@ -882,8 +882,9 @@ __device__ __forceinline__ void child_rect(uint32_t rx, uint32_t ry, int q, uint
 // buffers (`par` flips on every call, which every thread makes in the same order), and every thread
 // adds the totals of the waves before its own.  The buffer written by call k+2 was last read in
 // call k, before every thread reached call k+1's barrier, so no trailing barrier is needed.
+template <int NT>   // the k_octree block size
 __device__ __forceinline__ int oct_scan(int v, int* sc, int& par, int& total) {
-    constexpr int NW = kOctreeThreads / 64;
+    constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = wave_incl_scan(v);
     int* buf = sc + 16 * par;
@@ -921,7 +922,7 @@ __device__ __forceinline__ int quad_mask(const int* qd) {
 // One (frame, level) of DistributeOctTree once the candidate count C is known.  KeysInLds selects
 // whether keys / knode live in LDS (after the node tables) or in the per-level global scratch; the
 // two instantiations let the compiler use ds_* or global_* accesses instead of flat ones.
-template <bool KeysInLds>
+template <bool KeysInLds, int NT>
 __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const LevelGeom& L, int f, int l, int* smem,
                                              int C, const int* __restrict__ cc, const uint32_t* __restrict__ cs,
                                              uint32_t* keys, uint16_t* knode, uint32_t* __restrict__ lvlKps,
@@ -929,7 +930,6 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                                              unsigned long long* __restrict__ ost) {
     const int NC = g->node_cap;
     const int tid = threadIdx.x;
-    constexpr int NT = kOctreeThreads;
     // LDS carve: tables P and Q (ping-pong: A = current list, B = next), quad, rank, info, ord, nchr,
     // scan buffers, scalars.  Phase 2's dense sort keys alias B's rx/ry, its per-rank d / prefix
     // alias B's cnt/seq (all consumed before B is written).
@@ -962,7 +962,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             const int c = c0 + tid;
             const int n = c < ncl ? coff[c] : 0;
             int tot;
-            const int off = oct_scan(n, sc, par, tot);
+            const int off = oct_scan<NT>(n, sc, par, tot);
             if (c < ncl) coff[c] = base + off;
             base += tot;
         }
@@ -996,7 +996,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             const int c = c0 + tid;
             const int n = c < ncl ? cc[c] : 0;
             int tot;
-            const int off = oct_scan(n, sc, par, tot);
+            const int off = oct_scan<NT>(n, sc, par, tot);
             for (int k = 0; k < n; k++) keys[base + off + k] = cs[(long long)c * L.cell_cap + k];
             base += tot;
         }
@@ -1033,7 +1033,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         const int t = t0 + tid;
         const int n = t < nIni ? cntB[t] : 0;
         int tot;
-        const int pos = S + oct_scan(n > 0 ? 1 : 0, sc, par, tot);
+        const int pos = S + oct_scan<NT>(n > 0 ? 1 : 0, sc, par, tot);
         if (n > 0) {
             const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
             rxA[pos] = (uint32_t)x0 | ((uint32_t)x1 << 16);
@@ -1099,7 +1099,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                     val = 1 | (__popc(mask) << 16);
                 }
                 int tot;
-                const int pre = oct_scan(val, sc, par, tot);
+                const int pre = oct_scan<NT>(val, sc, par, tot);
                 if (t < S) {
                     if (val) {
                         rank[t] = nproc + (pre & 0xFFFF);
@@ -1125,7 +1125,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const int t = t0 + tid;
                 const bool big = t < S && cntA[t] > 1;
                 int tot;
-                const int pos = nsort + oct_scan(big ? 1 : 0, sc, par, tot);
+                const int pos = nsort + oct_scan<NT>(big ? 1 : 0, sc, par, tot);
                 if (big)
                     skey[pos] = ((unsigned long long)cntA[t] << 40) | ((unsigned long long)seqA[t] << 16) |
                                 (unsigned long long)t;
@@ -1166,7 +1166,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const int r = r0 + tid;
                 const int d = r < nsort ? dd[r] : 0;
                 int tot;
-                const int pre = run + oct_scan(d, sc, par, tot);
+                const int pre = run + oct_scan<NT>(d, sc, par, tot);
                 if (r < nsort) dpre[r] = pre;
                 const unsigned long long fail = __ballot(r < nsort && S + pre + d >= N);
                 if (fail && (threadIdx.x & 63) == 0) atomicMin(&sv[2], r0 + (tid & ~63) + __ffsll((long long)fail) - 1);
@@ -1191,7 +1191,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const int t = t0 + tid;
                 const bool keep = t < S && rank[t] < 0;
                 int tot;
-                const int pre = und + oct_scan(keep ? 1 : 0, sc, par, tot);
+                const int pre = und + oct_scan<NT>(keep ? 1 : 0, sc, par, tot);
                 if (keep) info[t] = pre;
                 und += tot;
             }
@@ -1303,7 +1303,8 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
 #undef OCT_STAMP
 }
 
-__global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restrict__ g,
+template <int NT>   // block size: kOctreeThreads for batches, 1024 for one frame (the host path's latency)
+__global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
                                                            const uint32_t* __restrict__ cands,
                                                            const int* __restrict__ cellCount,
                                                            uint32_t* __restrict__ keysAll,
@@ -1314,7 +1315,6 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int NC = g->node_cap;
     const int tid = threadIdx.x;
-    constexpr int NT = kOctreeThreads;
     // frames along x so that every frame's level-0 block (the longest) is dispatched first
     const int f = blockIdx.x, l = lbase + (int)blockIdx.y;
     const LevelGeom& L = g->L[l];
@@ -1337,16 +1337,16 @@ __global__ __launch_bounds__(kOctreeThreads) void k_octree(const Geom* __restric
         if (stage) cstage[c] = n;
     }
     int par = 0, C = 0;
-    (void)oct_scan(mine, sc, par, C);
+    (void)oct_scan<NT>(mine, sc, par, C);
     // keys and their node indices live in LDS after the node tables when they fit (every round
     // re-reads them), else in the per-level global scratch
     if (C <= lds_keys) {
         uint32_t* keys = reinterpret_cast<uint32_t*>(sv + 8);
-        octree_level<true>(g, L, f, l, smem, C, cc, cs, keys, reinterpret_cast<uint16_t*>(keys + lds_keys), lvlKps,
+        octree_level<true, NT>(g, L, f, l, smem, C, cc, cs, keys, reinterpret_cast<uint16_t*>(keys + lds_keys), lvlKps,
                            lvlCount, err, par, ost);
     } else {
         const long long o = ((long long)f * g->nlevels + l) * g->max_level_cand;
-        octree_level<false>(g, L, f, l, smem, C, cc, cs, keysAll + o, knodeAll + o, lvlKps, lvlCount, err, par, ost);
+        octree_level<false, NT>(g, L, f, l, smem, C, cc, cs, keysAll + o, knodeAll + o, lvlKps, lvlCount, err, par, ost);
     }
 }
 
@@ -1809,9 +1809,13 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     };
     auto octree = [&](int lbase, int nl, hipStream_t s) {
         const int lk = octree_lds_keys(g.node_cap);
-        hipLaunchKernelGGL(k_octree, dim3(nframes, nl), dim3(kOctreeThreads), octree_lds_bytes(g.node_cap) + (size_t)lk * 6,
-                           s, b.d_geom, b.d_cands, b.d_cellCount, b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err,
-                           lk, b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
+        // a single frame (the host path) is one block per level, so the level-0 block is the whole latency:
+        // 1024 threads halve its per-key steps; batches keep 512 (three blocks per CU)
+        const bool one = nframes == 1;
+        hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
+                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_cellCount,
+                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
+                           b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
     };
     auto describe = [&](hipStream_t s) {
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
