@@ -1809,9 +1809,10 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     };
     auto octree = [&](int lbase, int nl, hipStream_t s) {
         const int lk = octree_lds_keys(g.node_cap);
-        // a single frame (the host path) is one block per level, so the level-0 block is the whole latency:
-        // 1024 threads halve its per-key steps; batches keep 512 (three blocks per CU)
-        const bool one = nframes == 1;
+        // a small batch (the host path's single frame, C5's 8-frame step) has fewer blocks than CUs, so the
+        // level-0 blocks are the whole latency: 1024 threads halve their per-key steps; larger batches keep
+        // 512 (three blocks per CU)
+        const bool one = nframes * nl <= 256;
         hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
                            octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_cellCount,
                            b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
