@@ -1516,7 +1516,7 @@ __device__ __forceinline__ GaussShift gauss_shift(const int* gk) {
 // k_describe row pass, 8 rounds of one lane: RT[4gq + o][wy] = sum_t k_t * window[wy][SH + 4gq + o + t]
 // (the window row starts SH bytes into its first dword)
 template <int SH>
-__device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, const GaussShift& K) {
+__device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, const GaussShift& K, bool last) {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         uint32_t w[4];
@@ -1532,8 +1532,10 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
 #pragma unroll
         for (int o = 0; o < 4; o++)
             if (((SH + o) & 3) >= 2) acc[o] = __builtin_amdgcn_udot4(w[((SH + o) >> 2) + 2], K.kc[(SH + o) & 3], acc[o], false);
+        if (r < 7 || last) {   // round 7: only row 42 (RT rows stop at 42: pitch 43)
 #pragma unroll
-        for (int o = 0; o < 4; o++) rq[o * kRtPitch + 6 * r] = (uint16_t)acc[o];
+            for (int o = 0; o < 4; o++) rq[o * kRtPitch + 6 * r] = (uint16_t)acc[o];
+        }
     }
 }
 
@@ -1624,18 +1626,18 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     const GaussShift K = gauss_shift(g->gk);
     // lane = (row wy0 = lane / 10, group gq = lane % 10), round r takes row wy0 + 6r: the read and store
     // addresses are the lane's base plus immediate offsets.  8 rounds cover rows 0..47; rows 43..47 are
-    // scratch (they read past the window, inside the workgroup's LDS, into RT rows no sample reads
-    // with a nonzero tap).  The window shift sh is wave-uniform: one instantiation per value, so output
+    // computed (from reads past the window, inside the workgroup's LDS) but not stored: RT's pitch is 43.
+    // The window shift sh is wave-uniform: one instantiation per value, so output
     // o's byte runs start at the compile-time offset sh + o (aligned runs need no v_alignbyte).
     if (lane < 60) {
         const int wy0 = (int)(__umul24((unsigned)lane, 205u) >> 11), gq = lane - wy0 * 10;   // lane / 10, lane < 60
         const uint32_t* rw = w32 + wy0 * 12 + gq;
         uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy0;   // RT[4gq + j][wy]
         switch (sh) {
-            case 0: desc_row_pass<0>(rw, rq, K); break;
-            case 1: desc_row_pass<1>(rw, rq, K); break;
-            case 2: desc_row_pass<2>(rw, rq, K); break;
-            default: desc_row_pass<3>(rw, rq, K); break;
+            case 0: desc_row_pass<0>(rw, rq, K, wy0 == 0); break;
+            case 1: desc_row_pass<1>(rw, rq, K, wy0 == 0); break;
+            case 2: desc_row_pass<2>(rw, rq, K, wy0 == 0); break;
+            default: desc_row_pass<3>(rw, rq, K, wy0 == 0); break;
         }
     }
     wave_lds_sync();

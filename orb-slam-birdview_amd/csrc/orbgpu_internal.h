@@ -21,7 +21,7 @@ constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3
 constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as aligned dwords
 constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
-constexpr int kRtPitch = 49;          // k_describe row-pass sums, u16 per transposed row (odd: the row
+constexpr int kRtPitch = 43;          // k_describe row-pass sums, u16 per transposed row (43 rows, odd: the row
                                       // pass's transposed u16 stores of 10 column groups hit distinct banks)
 constexpr int kRsTileW = 128;         // k_resize_tiled<TH>: output tile 128 x TH, 4 px per thread
 constexpr int kRsPitch = 272;         // LDS source tile: up to 272 bytes (from a 16-B aligned column) x (2*TH + 8) rows
