@@ -1540,8 +1540,7 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
 }
 
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
-                                          const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt, const float (&pf)[4][4],
-                                          const uint32_t (&icm)[4],
+                                          const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt,
                                           orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
                                           unsigned long long* __restrict__ dstamps) {
     const int l = d.l, x = d.x, y = d.y, score = d.score, outIdx = d.outIdx;
@@ -1551,6 +1550,9 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 #define DESC_STAMP(k) \
     if (dst_st && lane == 0) dst_st[(k)] = __builtin_amdgcn_s_memtime();
     DESC_STAMP(0);
+    // the lane's IC_Angle byte masks (constant table), issued before the window is stored
+    const uint4 mm = reinterpret_cast<const uint4*>(&c_ic_masks.m[0][0])[lane];
+    const uint32_t icm[4] = {mm.x, mm.y, mm.z, mm.w};
     uint32_t* w32 = reinterpret_cast<uint32_t*>(wbase);
     int sh;
     if (d.interior) {
@@ -1657,6 +1659,18 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
                     K45 = {(unsigned short)k4, (unsigned short)k5}, K60 = {(unsigned short)k6, 0};
     DESC_STAMP(4);
 
+    // BRIEF test pairs of this lane (lane + 64 gq) from the constant table, issued before the trig so their
+    // latency hides under it; loaded here rather than once per wave to keep them out of the row pass's
+    // live registers
+    float pf[4][4];
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+        const float4 pp = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * gq];
+        pf[gq][0] = pp.x;
+        pf[gq][1] = pp.y;
+        pf[gq][2] = pp.z;
+        pf[gq][3] = pp.w;
+    }
     // ---- rBRIEF (:108-147): cos/sin as glibc's cosf/sinf compute them (:113, glibc_trig.h); 256 tests
     // as four 64-lane ballots; sample (ix, iy) of the blurred patch at blurT[(18+ix)*40 + 18+iy]
     const float ang = angle * kFactorPI;
@@ -1722,23 +1736,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     uint32_t v0[9], v1[9];
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
     if (d1.ok && d1.interior) desc_issue(d1, lane, v1);
-    // BRIEF test pairs of this lane (lane + 64 gq), fetched now so their latency hides under the window's
-    float pf[4][4];
-#pragma unroll
-    for (int gq = 0; gq < 4; gq++) {
-        const float4 pp = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * gq];
-        pf[gq][0] = pp.x;
-        pf[gq][1] = pp.y;
-        pf[gq][2] = pp.z;
-        pf[gq][3] = pp.w;
-    }
-    const uint4 mm = reinterpret_cast<const uint4*>(&c_ic_masks.m[0][0])[lane];
-    const uint32_t icm[4] = {mm.x, mm.y, mm.z, mm.w};
-    if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], pf, icm, outK, outD, kpCap, dstamps);
+    if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
     if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
-        desc_body(g, d1, f, lane, v1, s_win[wv], s_rt[wv], pf, icm, outK, outD, kpCap, dstamps);
+        desc_body(g, d1, f, lane, v1, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
     }
 }
 
