@@ -61,7 +61,7 @@ struct Geom {
     int fast_drows;      //   detection-domain rows,
     int fast_list;       //   prefilter-survivor list entries (domain pixels)
     int fast_wave_bytes; //   bytes per wave (lead pad | 16-bit tile | survivor list)
-    int fast_compact;    //   every cell <= 36 px wide: compact LDS pitches (tile 56, score map 40)
+    int fast_compact;    //   every cell <= 36 px wide: compact tile pitch (48 elements; else kFastTilePitch)
     int umax[16];        // ORBextractor.cc:454-469
     int gk[8];           // 7-tap Gaussian, sigma 2, 8-bit fixed point (getGaussianKernel x 256)
     LevelGeom L[ORBGPU_MAX_LEVELS];
@@ -125,7 +125,7 @@ hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, i
                                int* d_nvalid, hipStream_t stream);
 
 
-// Batched all-pairs top-2 (k_top2_batch): pair p = (query frame frames[p].x, train frame frames[p].y)
+// Batched all-pairs top-2 (k_expand_pm1 + k_top2_mfma): pair p = (query frame frames[p].x, train frame frames[p].y)
 // of descriptor arrays q / t with q_stride / t_stride descriptors per frame; counts[frame] on the
 // device, or nq / nt for every pair when counts == NULL (frames == NULL: one pair, frame 0).
 struct Top2Batch {
