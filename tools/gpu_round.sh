@@ -18,8 +18,8 @@ if [ -n "$PMC" ]; then
   echo "pmc ok"
   export ORBGPU_PMC_JSON=$OUT/pmc/report.json
 fi
-step bench 600 python bench.py --steps 20 --warmup 3 || exit 1
-step bench_c2 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu --no-c4 --no-bird || exit 1
+step bench 600 python bench.py || exit 1
+step bench_c2 300 python bench.py --config c2 --no-cpu --no-c4 --no-bird || exit 1
 step bench_c5 300 python bench.py --config c5 --steps 50 --warmup 5 --no-cpu --no-c4 --no-bird --no-stereo || exit 1
 # the timed loop as the bench runs it (two batches in flight: kernel durations of the two streams overlap)
 step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --only-extract --no-profile-pass --steps 20 --warmup 3 || exit 1
