@@ -80,6 +80,22 @@ def test_other_parameters(orbgpu_mod, oracle_mod):
         assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), params
 
 
+@pytest.mark.parametrize("w,h,params", [
+    (640, 480, (1000, 1.2, 1, 20, 7)),    # one level: no pyramid launches, every feature on level 0
+    (640, 480, (1000, 1.2, 12, 20, 7)),   # 12 levels: the top one is 86x64, one FAST cell
+    (1280, 720, (3000, 1.2, 12, 20, 7)),
+    (1280, 720, (2000, 1.1, 16, 20, 7)),  # ORBGPU_MAX_LEVELS levels
+])
+def test_level_counts(orbgpu_mod, oracle_mod, w, h, params):
+    # nlevels away from the default 8 (ORBextractor.cc:410-470 tables, :1107-1132 pyramid chain)
+    from orbgpu.synth import synth_frame
+    img = synth_frame(w, h, 13)
+    ok, od = oracle_mod.OracleExtractor(*params)(img)
+    gk, gd = orbgpu_mod.ORBextractor(*params)(img)
+    assert len(gk) > 0
+    assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), params
+
+
 def test_threshold_edges(orbgpu_mod, oracle_mod):
     # iniThFAST / minThFAST of 0 and 1 on a low-contrast frame, where arc strengths M of 1 and 2 decide
     # corners and the NMS (k_fast_wave keeps a corner iff M > max(neighbour M, 1): score M - 1 > 0 at
