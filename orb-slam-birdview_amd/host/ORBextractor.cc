@@ -107,7 +107,8 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, s
         memcpy(d.data, dbuf_.data(), (size_t)n * 32);
     }
     _keypoints.resize(n);
-    if (n) memcpy(&_keypoints[0], kbuf_.data(), (size_t)n * sizeof(KeyPoint));
+    // cv::KeyPoint has user constructors (not trivially copyable by type): copy the layout-checked bytes
+    if (n) memcpy(static_cast<void*>(_keypoints.data()), kbuf_.data(), (size_t)n * sizeof(KeyPoint));
 }
 #endif
 

@@ -82,3 +82,32 @@ def test_mirror_parity_on_gpu(mirror_bin, tmp_path, w, h, nf):
     assert rc == 0 and not fails, "\n".join(fails) + "\n" + err[-2000:]
     summary = [l for l in out.splitlines() if l.startswith("SUMMARY")][0].split()
     assert int(summary[1]) >= 20 and int(summary[2]) == 0
+
+
+@pytest.fixture(scope="module")
+def cv_overload_bin():
+    # the mirror's -DORBGPU_WITH_OPENCV overloads, compiled over tests/cpp/cv_api (a model of the OpenCV
+    # 3.2 types: OpenCV is absent in this image)
+    subprocess.check_call(["make", "-s", "-C", CPP, "test_cv_overload"])
+    return os.path.join(CPP, "test_cv_overload")
+
+
+def test_cv_overload_builds_and_fails_loudly_without_gpu(cv_overload_bin, tmp_path):
+    import orbgpu
+    if orbgpu.device_count() > 0:
+        pytest.skip("a GPU is present")
+    rc, out, _ = _run(cv_overload_bin, np.zeros((1, 64, 64), np.uint8), 100, tmp_path)
+    assert rc == 1 and "CHECK exception FAIL" in out
+
+
+@pytest.mark.gpu
+def test_cv_overload_matches_plain_overload(cv_overload_bin, tmp_path):
+    # Frame.cc:414-420's call shape: (*extractor)(im, cv::Mat(), mvKeys, mDescriptors) on a padded cv::Mat,
+    # then mvImagePyramid[l] as cv::Mat; bytes equal to the ImageView overload's (itself bit-exact vs the oracle)
+    from orbgpu.synth import synth_frame
+    frames = np.stack([synth_frame(1280, 720, 3), synth_frame(1280, 720, 6, "noise")])
+    rc, out, err = _run(cv_overload_bin, frames, 2000, tmp_path)
+    fails = [l for l in out.splitlines() if " FAIL" in l]
+    assert rc == 0 and not fails, "\n".join(fails) + "\n" + err[-2000:]
+    summary = [l for l in out.splitlines() if l.startswith("SUMMARY")][0].split()
+    assert int(summary[1]) == 12 and int(summary[2]) == 0
