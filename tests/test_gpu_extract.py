@@ -289,3 +289,27 @@ def test_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
             assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
     for e in exs:
         e.close()
+
+
+def test_c5_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
+    """bench.py --config c5: BASELINE config 5's 8-frame batch at 4,000 features, four extractor contexts
+    in flight (one per hardware queue) through the hipGraph path, the small-batch kernel shapes (1024-thread
+    octree blocks).  Every frame of every context vs the oracle, byte for byte."""
+    from orbgpu.synth import bench_frames
+    B, NF = 8, 4000
+    frames = bench_frames(1280, 720, B, first=0)
+    exs = [orbgpu_mod.BatchExtractor(NF, 1280, 720, B) for _ in range(4)]
+    for e in exs:
+        e.upload(frames)
+    for step in range(10):
+        exs[step % 4].launch()
+    for e in exs:
+        e.sync()
+    o = oracle_mod.OracleExtractor(NF)
+    ref = [o(frames[f]) for f in range(B)]
+    for e in exs:
+        for f, (ok, od) in enumerate(ref):
+            gk, gd = e.results(f)
+            assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
+    for e in exs:
+        e.close()
