@@ -313,3 +313,25 @@ def test_c5_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
             assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
     for e in exs:
         e.close()
+
+
+def test_c2_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
+    """bench.py --config c2: 640x480 at 1,000 features, B = 256, two contexts through the graph path."""
+    from orbgpu.synth import bench_frames
+    B = 256
+    frames = bench_frames(640, 480, B, first=0)
+    exs = [orbgpu_mod.BatchExtractor(1000, 640, 480, B) for _ in range(2)]
+    for e in exs:
+        e.upload(frames)
+    for step in range(5):
+        exs[step % 2].launch()
+    for e in exs:
+        e.sync()
+    o = oracle_mod.OracleExtractor(1000)
+    ref = {f: o(frames[f]) for f in (0, 100, 255)}
+    for e in exs:
+        for f, (ok, od) in ref.items():
+            gk, gd = e.results(f)
+            assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
+    for e in exs:
+        e.close()
