@@ -1472,6 +1472,7 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         if (ALLEVEN) return S + 32767u + ((S >> 16) & 1u);
         return S + (colBase + (int)xb < xsimd ? 32767u + ((S >> 16) & 1u) : 32768u);
     };
+    unsigned long long mq[4];
 #pragma unroll
     for (int gq = 0; gq < 4; gq++) {   // test pair lane + 64 gq: (x0, y0, x1, y1) = pf[gq]
         const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
@@ -1480,9 +1481,10 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         const uint32_t r0 = sample(__builtin_fmaf(px0, a, -(py0 * b)), __builtin_fmaf(px0, b, py0 * a));
         const uint32_t r1 = sample(__builtin_fmaf(px1, a, -(py1 * b)), __builtin_fmaf(px1, b, py1 * a));
         // saturate_cast<uchar>: only the right-hand side needs the clamp (t0 = 256 compares as 255 would)
-        const unsigned long long m = __ballot((r0 >> 16) < min(r1 >> 16, 255u));
-        if (lane == 0) dst[gq] = m;
+        mq[gq] = __ballot((r0 >> 16) < min(r1 >> 16, 255u));
     }
+    // the four 64-test words in one store (lanes 0..3)
+    if (lane < 4) dst[lane] = lane == 0 ? mq[0] : lane == 1 ? mq[1] : lane == 2 ? mq[2] : mq[3];
 }
 
 // The 7-tap Gaussian as byte weights shifted to each of the four byte alignments of an output's
