@@ -474,9 +474,18 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
     return pk_sub16(tt, __builtin_bit_cast(uint32_t, d));
 }
 
-// optional phase timestamps (ORBGPU_FAST_STAMPS=1): s_memtime at the phase boundaries, lane 0
+// optional phase timestamps (a build with -DORBGPU_KERNEL_STAMPS=1, run with ORBGPU_FAST_STAMPS=1):
+// s_memtime at the phase boundaries, lane 0.  Off by default: each stamp is a branch that splits the
+// kernel's scheduling regions (describe 0.533 -> 0.528, octree 0.102 -> 0.100 ms per 256 C3 frames)
+#ifndef ORBGPU_KERNEL_STAMPS
+#define ORBGPU_KERNEL_STAMPS 0
+#endif
+#if ORBGPU_KERNEL_STAMPS
 #define ORBGPU_STAMP(k) \
     if (stamps && lane == 0) stamps[(long long)item * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define ORBGPU_STAMP(k)
+#endif
 
 // ROI dwords of a cell (aligned levels) issued into registers, so that the next cell's loads are in
 // flight while the current one is processed.  lane = (row yy0 = lane / nw, dword ww = lane % nw);
@@ -948,8 +957,12 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
     int* nchr = ord + NC;         // node -> children of the nodes divided before it
     int* sc = nchr + NC;          // 2 x 16 ints of scan buffers
     int* sv = sc + 32;            // scalars
+#if ORBGPU_KERNEL_STAMPS
 #define OCT_STAMP(k) \
     if (ost && tid == 0) ost[(k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OCT_STAMP(k)
+#endif
 
     // 1. gather candidates in cell order (vToDistributeKeys, :818-825)
     const int ncl = L.nCols * L.nRows;
@@ -1056,10 +1069,14 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
     for (int round = 0; round < 4 * NC + 64; round++) {
         const int prevSize = S;
         // sub-step stamps of round 0 (slots 12..16) and of the first phase-2 round (20..28)
-        const int subBase = round == 0 ? 12 : (phase == 2 && !p2seen) ? 20 : -1;
+        [[maybe_unused]] const int subBase = round == 0 ? 12 : (phase == 2 && !p2seen) ? 20 : -1;
         if (phase == 2) p2seen = 1;
+#if ORBGPU_KERNEL_STAMPS
 #define OCT_SUB(k) \
     if (ost && tid == 0 && subBase >= 0 && subBase + (k) < 29) ost[subBase + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OCT_SUB(k)
+#endif
         for (int t = tid; t < 4 * S; t += NT) quad[t] = 0;
         for (int t = tid; t < S; t += NT) rank[t] = -1;
         __syncthreads();
@@ -1324,7 +1341,9 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
     // 3.. end of round r (up to 9), 12.. / 20.. sub-steps of round 0 / the first phase-2 round,
     // 29 = C, 30 = phase-2 start round, 31 done
     unsigned long long* ost = ostamps ? ostamps + ((long long)f * g->nlevels + l) * 32 : nullptr;
+#if ORBGPU_KERNEL_STAMPS
     if (ost && tid == 0) ost[0] = __builtin_amdgcn_s_memtime();
+#endif
     const int ncl = L.nCols * L.nRows;
     const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
     const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
@@ -1548,9 +1567,13 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     const int l = d.l, x = d.x, y = d.y, score = d.score, outIdx = d.outIdx;
     const LevelGeom& L = g->L[l];
     const LevelPtr src = d.src;
-    unsigned long long* dst_st = dstamps ? dstamps + ((long long)f * g->nkpcap + d.s) * 8 : nullptr;
+    [[maybe_unused]] unsigned long long* dst_st = dstamps ? dstamps + ((long long)f * g->nkpcap + d.s) * 8 : nullptr;
+#if ORBGPU_KERNEL_STAMPS
 #define DESC_STAMP(k) \
     if (dst_st && lane == 0) dst_st[(k)] = __builtin_amdgcn_s_memtime();
+#else
+#define DESC_STAMP(k)
+#endif
     DESC_STAMP(0);
     // the lane's IC_Angle byte masks (constant table), issued before the window is stored
     const uint4 mm = reinterpret_cast<const uint4*>(&c_ic_masks.m[0][0])[lane];

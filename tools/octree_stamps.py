@@ -1,4 +1,6 @@
 #!/usr/bin/env python3
+
+Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it).
 """Where a k_octree workgroup spends its time (diagnostic, GPU): runs one C3 batch with
 ORBGPU_FAST_STAMPS=1 and prints, per pyramid level, the mean s_memtime cycles of the candidate
 gather, the root setup, each division round and the final best-key pass, with the candidate
