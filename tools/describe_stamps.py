@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
-
-Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it).
 """Where a k_describe wavefront spends its time (diagnostic, GPU): runs one C3 batch with
 ORBGPU_FAST_STAMPS=1 and prints the mean s_memtime cycles of each phase per keypoint wave:
-window load, IC angle, blur row pass, blur column pass, sin/cos, BRIEF tests + output."""
+window load, IC angle, blur row pass, blur column pass, sin/cos, BRIEF tests + output.
+Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it)."""
 import os
 import sys
 

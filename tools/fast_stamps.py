@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
-
-Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it).
 """Where a k_fast_wave wavefront spends its time (diagnostic, GPU): runs one C3 batch with
 ORBGPU_FAST_STAMPS=1 and prints the mean s_memtime cycles of each phase per (frame, cell) wave,
 overall and per pyramid level.  Phases: ROI wait + LDS store, score-map zeroing, prefilter +
-compaction, exact arc strength, NMS (+ fallback), emission."""
+compaction, exact arc strength, NMS (+ fallback), emission.
+Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it)."""
 import os
 import sys
 

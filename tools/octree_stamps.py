@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
-
-Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it).
 """Where a k_octree workgroup spends its time (diagnostic, GPU): runs one C3 batch with
 ORBGPU_FAST_STAMPS=1 and prints, per pyramid level, the mean s_memtime cycles of the candidate
 gather, the root setup, each division round and the final best-key pass, with the candidate
-count and the round at which phase 2 (sorted division) starts."""
+count and the round at which phase 2 (sorted division) starts.
+Needs a library built with kernel stamps: make -B -C orb-slam-birdview_amd STAMPS=1 (then make -B again without it)."""
 import os
 import sys
 
