@@ -792,7 +792,6 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
                                                    int cbeg, int cnum, unsigned long long* __restrict__ stamps,
                                                    int* __restrict__ err, int ipw) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
-    if (err && blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // k_octree's overflow flag (set after this kernel)
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem_fast);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     // blocks dealt round-robin over the 8 XCDs: give each XCD a contiguous range of blocks (8 cells each)
@@ -810,6 +809,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     uint32_t v0[8], v1[8];
     if (c0.valid && c0.aligned) fast_roi_issue(c0, lane, v0);
     if (has1 && c1.valid && c1.aligned) fast_roi_issue(c1, lane, v1);
+    if (err && blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // k_octree's overflow flag (set after this kernel)
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         if (k == 1 && !has1) break;
@@ -1747,20 +1747,30 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: SALU
     const int nl = g->nlevels;
     const int* cnts = lvlCount + f * nl;
-    if (bx == 0 && threadIdx.x == 0) {
-        int tot = 0;
-        for (int i = 0; i < nl; i++) tot += cnts[i];
-        outN[f] = tot;
-    }
     const int s0 = (bx * kDescWaves + wv) * spw;
-    if (s0 >= g->nkpcap) return;
+    // the frame's keypoint count, by its first block's thread 0 (on every path out of the kernel)
+    auto write_n = [&]() {
+        if (bx == 0 && threadIdx.x == 0) {
+            int tot = 0;
+            for (int i = 0; i < nl; i++) tot += cnts[i];
+            outN[f] = tot;
+        }
+    };
+    if (s0 >= g->nkpcap) {
+        write_n();
+        return;
+    }
     const DescSlot d0 = desc_slot(g, f, s0, cnts, lvlKps, frames, framePitch, rowStride, pyr);
     const DescSlot d1 = spw == 2 ? desc_slot(g, f, s0 + 1, cnts, lvlKps, frames, framePitch, rowStride, pyr)
                                  : DescSlot{};
-    if (!d0.ok && !d1.ok) return;   // (the two slots may straddle a level boundary)
+    if (!d0.ok && !d1.ok) {   // (the two slots may straddle a level boundary)
+        write_n();
+        return;
+    }
     uint32_t v0[9], v1[9];
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
     if (d1.ok && d1.interior) desc_issue(d1, lane, v1);
+    write_n();   // (after the window loads are issued)
     if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
     if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
