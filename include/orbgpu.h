@@ -22,8 +22,21 @@
 extern "C" {
 #endif
 
-#define ORBGPU_ABI_VERSION 1
+#define ORBGPU_ABI_VERSION 2
 #define ORBGPU_MAX_LEVELS 16
+
+/* OpenCV arithmetic variant (orb_params.variant / orb_bird_params.variant, bit flags).  The reference
+ * links whichever OpenCV 2.4.3-3.4 the build machine has (CMakeLists.txt:31-37) and calls its resize
+ * (ORBextractor.cc:1120) and GaussianBlur (:1085-1086); those versions differ in the last bits, and the
+ * octree sort (:684) breaks size ties by heap address.  0 is the pinned default (OpenCV 3.2 x86-64 SSE2
+ * without IPP; ties by node creation sequence; BRIEF offsets contracted to FMA as GCC -march=native
+ * builds them).  The bit values equal the oracle's ORACLE_* flags (oracle/orb_oracle.h). */
+#define ORB_VARIANT_DEFAULT        0
+#define ORB_VARIANT_TIE_REVERSE    1  /* :684 tie: a later-created node counts as the SMALLER pointer      */
+#define ORB_VARIANT_RESIZE_GENERIC 2  /* resize vertical pass = generic FixedPtCast (b0*H0+b1*H1+2^21)>>22 */
+#define ORB_VARIANT_BLUR_HALFUP    4  /* GaussianBlur column pass rounds half-up everywhere (no SSE2 body) */
+#define ORB_VARIANT_NO_FMA         8  /* BRIEF sample offsets (:119-120) uncontracted (no -march=native FMA) */
+#define ORB_VARIANT_MASK          15
 
 typedef enum {
     ORB_OK = 0,
@@ -54,6 +67,7 @@ typedef struct {
     int max_width;    /* capacity hints (contexts grow on demand for host input) */
     int max_height;
     int max_batch;    /* frames per batched launch (device-resident path)       */
+    int variant;      /* ORB_VARIANT_* bits (0 = pinned default); unknown bits: ORB_ERR_ARG */
 } orb_params;
 
 typedef struct orb_ctx orb_ctx;
@@ -134,6 +148,8 @@ typedef struct {
     int edgeThreshold;
     int fastThreshold;
     int device;
+    int variant;      /* ORB_VARIANT_RESIZE_GENERIC | ORB_VARIANT_BLUR_HALFUP apply (cv::ORB's own pyramid
+                         resize and descriptor blur, orb.cpp); other bits: ORB_ERR_ARG */
 } orb_bird_params;
 
 typedef struct orb_bird orb_bird;

@@ -96,6 +96,7 @@ def lib():
         L.oracle_cvorb_create.restype = vp
         L.oracle_cvorb_create.argtypes = [ci, cf, ci, ci, ci]
         L.oracle_cvorb_destroy.argtypes = [vp]
+        L.oracle_cvorb_set_flags.argtypes = [vp, ci]
         L.oracle_cvorb_detect.argtypes = [vp, vp, ci, ci, ci, vp, ci, vp, ci]
         L.oracle_cvorb_candidates.argtypes = [vp, ci, vp, ci]
         L.oracle_cvorb_level.argtypes = [vp, ci, vp, vp, vp]
@@ -411,10 +412,12 @@ class OracleCvORB:
     """Restated OpenCV 3.2 cv::ORB (HARRIS_SCORE) + cornerSubPix of the birdview stream
     (Frame.cc:318-342; oracle/cvorb_oracle.inc).  Parity unpinned against OpenCV itself."""
 
-    def __init__(self, nfeatures=2000, scale_factor=1.2, nlevels=8, edge_threshold=31, fast_threshold=20):
+    def __init__(self, nfeatures=2000, scale_factor=1.2, nlevels=8, edge_threshold=31, fast_threshold=20, flags=0):
         self.nlevels = nlevels
         self.h = lib().oracle_cvorb_create(nfeatures, scale_factor, nlevels, edge_threshold, fast_threshold)
         assert self.h
+        if flags:   # ORACLE_RESIZE_GENERIC / ORACLE_BLUR_ALL_HALFUP
+            lib().oracle_cvorb_set_flags(self.h, flags)
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -166,6 +166,9 @@ int oracle_distinctive_descriptor(const uint8_t* desc, int N);
  * restated in cvorb_oracle.inc.  PARITY UNPINNED (OpenCV absent, no reference fixture). ---- */
 void* oracle_cvorb_create(int nfeatures, float scaleFactor, int nlevels, int edgeThreshold, int fastThreshold);
 void  oracle_cvorb_destroy(void* h);
+/* OpenCV arithmetic variant of the cv::ORB pyramid resize and descriptor blur (ORACLE_RESIZE_GENERIC,
+ * ORACLE_BLUR_ALL_HALFUP; other bits ignored) */
+void  oracle_cvorb_set_flags(void* h, int flags);
 /* cv::ORB::detect(img, kps, mask); mask may be NULL.  Returns n (or -n-1 if cap too small). */
 int   oracle_cvorb_detect(void* h, const uint8_t* img, int w, int hgt, int stride, const uint8_t* mask, int mstride,
                           OracleKeyPoint* out, int cap);

@@ -46,6 +46,7 @@ struct BirdLevel {
 
 struct BirdGeom {
     int nlevels, W, H, edge, fastTh;
+    int variant;           // ORB_VARIANT_RESIZE_GENERIC / ORB_VARIANT_BLUR_HALFUP (orb_bird_params.variant)
     float harris_scale4;   // (1 / (4 * 7 * 255.f))^4
     int gk[8];             // 7-tap Gaussian sigma 2, 8-bit fixed point
     int umax[16];          // orb.cpp computeKeyPoints u_max (halfPatchSize 15)
@@ -87,7 +88,9 @@ __global__ __launch_bounds__(256) void k_bird_resize(const BirdGeom* __restrict_
     const uint8_t* r1 = base + S.off + (long long)cy.s1 * S.pitch;
     const int h0 = r0[cx.s0] * cx.c0 + r0[cx.s1] * cx.c1;
     const int h1 = r1[cx.s0] * cx.c0 + r1[cx.s1] * cx.c1;
-    int v = (((cy.c0 * (h0 >> 4)) >> 16) + ((cy.c1 * (h1 >> 4)) >> 16) + 2) >> 2;
+    int v = (g->variant & ORB_VARIANT_RESIZE_GENERIC)
+                ? min((cy.c0 * h0 + cy.c1 * h1 + (1 << 21)) >> 22, 255)   // generic FixedPtCast
+                : (((cy.c0 * (h0 >> 4)) >> 16) + ((cy.c1 * (h1 >> 4)) >> 16) + 2) >> 2;
     if (blockIdx.z) v = v > 254 ? v : 0;
     base[D.off + (long long)y * D.pitch + x] = (uint8_t)v;
 }
@@ -281,7 +284,8 @@ __global__ __launch_bounds__(256) void k_bird_blur(const BirdGeom* __restrict__ 
     }
     const int q = S >> 16, rem = S & 0xFFFF;
     int v;
-    if (x < (L.w & ~3)) v = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));
+    // ORB_VARIANT_BLUR_HALFUP: half-up everywhere (no SSE2 body)
+    if (x < ((g->variant & ORB_VARIANT_BLUR_HALFUP) ? 0 : (L.w & ~3))) v = rem > 32768 ? q + 1 : (rem < 32768 ? q : q + (q & 1));
     else v = (S + 32768) >> 16;
     blur[L.off + (long long)r.y * L.pitch + x] = (uint8_t)min(max(v, 0), 255);
 }
@@ -582,7 +586,7 @@ void retain_best(std::vector<SelKey>& kps, int n_points) {
 struct Bird {
     int device = 0;
     hipStream_t stream = nullptr;
-    int nfeatures = 2000, nlevels = 8, edge = 31, fastTh = 20;
+    int nfeatures = 2000, nlevels = 8, edge = 31, fastTh = 20, variant = 0;
     double scaleFactor = 1.2f;
     float wmask[kSubW * kSubW]{};
 
@@ -680,6 +684,7 @@ int Bird::ensure_geometry(int W, int H, int nl) {
     G.H = H;
     G.edge = edge;
     G.fastTh = std::min(std::max(fastTh, 0), 255);
+    G.variant = variant;
     const float sc = 1.f / ((1 << 2) * 7 * 255.f);
     G.harris_scale4 = sc * sc * sc * sc;
     {   // getGaussianKernel(7, 2, CV_32F) -> 8-bit fixed point
@@ -1006,7 +1011,8 @@ extern "C" orb_bird* orb_bird_create(const orb_bird_params* p, int* status) {
         return nullptr;
     };
     if (!p || p->nfeatures < 0 || p->nlevels < 1 || p->nlevels > ORBGPU_MAX_LEVELS || !(p->scaleFactor > 1.0f) ||
-        p->edgeThreshold < 4 || p->fastThreshold < 0) {
+        p->edgeThreshold < 4 || p->fastThreshold < 0 ||
+        (p->variant & ~(ORB_VARIANT_RESIZE_GENERIC | ORB_VARIANT_BLUR_HALFUP))) {
         set_error("invalid orb_bird_params", hipSuccess);
         return fail(ORB_ERR_ARG);
     }
@@ -1025,6 +1031,7 @@ extern "C" orb_bird* orb_bird_create(const orb_bird_params* p, int* status) {
     b->nlevels = p->nlevels;
     b->edge = p->edgeThreshold;
     b->fastTh = p->fastThreshold;
+    b->variant = p->variant;
     // cornerSubPix weight mask: exp(-y^2) * exp(-x^2) in float (glibc expf, as the reference's host)
     for (int i = 0; i < kSubW; i++) {
         const float y = (float)(i - kSubWin) / kSubWin;

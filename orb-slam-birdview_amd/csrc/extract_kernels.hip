@@ -84,6 +84,9 @@ typedef unsigned int uint32x4_t __attribute__((ext_vector_type(4)));
  * weights, vertical pass ((b0*(H0>>4))>>16 + (b1*(H1>>4))>>16 + 2)>>2.
  * Only the ROI values matter: the reference's REFLECT_101 padding is never read on the path.
  * --------------------------------------------------------------------------------------------- */
+// GENERIC (ORB_VARIANT_RESIZE_GENERIC): the vertical pass as the generic FixedPtCast,
+// sat_u8((b0*H0 + b1*H1 + 2^21) >> 22), instead of the 3.x `>>4` form
+template <bool GENERIC>
 __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef,
                                                 int level, const uint8_t* __restrict__ frames, long long framePitch,
                                                 int rowStride, uint8_t* __restrict__ pyr) {
@@ -103,7 +106,9 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
         const ResizeCoef cx = coef[x];
         const unsigned h0 = __umul24(r0[cx.s0], (unsigned)cx.c0) + __umul24(r0[cx.s1], (unsigned)cx.c1);
         const unsigned h1 = __umul24(r1[cx.s0], (unsigned)cx.c0) + __umul24(r1[cx.s1], (unsigned)cx.c1);
-        const unsigned v = ((__umul24((unsigned)cy.c0, h0 >> 4) >> 16) + (__umul24((unsigned)cy.c1, h1 >> 4) >> 16) + 2) >> 2;
+        const unsigned v =
+            GENERIC ? min((__umul24((unsigned)cy.c0, h0) + __umul24((unsigned)cy.c1, h1) + (1u << 21)) >> 22, 255u)
+                    : ((__umul24((unsigned)cy.c0, h0 >> 4) >> 16) + (__umul24((unsigned)cy.c1, h1 >> 4) >> 16) + 2) >> 2;
         packed |= (uint32_t)v << (8 * i);
     }
     // the pitch is a multiple of 64, so the dword never leaves the row (pad bytes are never read)
@@ -119,12 +124,20 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
  * reads. */
 // s_cy entry of one output row: the LDS byte offsets of its two source rows and the vertical weights
 // pre-shifted for the vertical pass, (c * (h >> 4)) >> 16 == mul_hi_u24(c << 12, h & ~15) (c <= 2048 and
-// h < 2^19 keep both operands within 24 bits)
+// h < 2^19 keep both operands within 24 bits); unshifted for the generic form
+template <bool GENERIC>
 __device__ __forceinline__ int4 rs_row_entry(const ResizeCoef& c, int sy0) {
-    return make_int4((c.s0 - sy0) * kRsPitch, (c.s1 - sy0) * kRsPitch, c.c0 << 12, c.c1 << 12);
+    return make_int4((c.s0 - sy0) * kRsPitch, (c.s1 - sy0) * kRsPitch, GENERIC ? c.c0 : c.c0 << 12,
+                     GENERIC ? c.c1 : c.c1 << 12);
+}
+// one output pixel's vertical pass from the two rows' horizontal sums (weights from rs_row_entry)
+template <bool GENERIC>
+__device__ __forceinline__ unsigned rs_vpass(unsigned c0, unsigned c1, unsigned h0, unsigned h1) {
+    if (GENERIC) return min((__umul24(c0, h0) + __umul24(c1, h1) + (1u << 21)) >> 22, 255u);
+    return (mul_hi_u24(c0, h0 & ~15u) + mul_hi_u24(c1, h1 & ~15u) + 2) >> 2;
 }
 
-template <int kRsTileH>
+template <int kRsTileH, bool GENERIC>
 __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
                                                       const ResizeCoef* __restrict__ coef, int level,
                                                       const uint8_t* __restrict__ frames, long long framePitch,
@@ -172,7 +185,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         }
         if (tid < kRsTileH) {
             const ResizeCoef c = coef[dw + y0 + min(tid, ny - 1)];
-            cyv = rs_row_entry(c, sy0);
+            cyv = rs_row_entry<GENERIC>(c, sy0);
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++) {   // clamped duplicates store the same bytes to the same place
@@ -187,7 +200,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         }
         if (tid < kRsTileH) {
             const ResizeCoef c = coef[dw + y0 + min(tid, ny - 1)];
-            cyv = rs_row_entry(c, sy0);
+            cyv = rs_row_entry<GENERIC>(c, sy0);
         }
         if (((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 3) == 0) {
             const int nw = (sx1 - sx0 + 4) >> 2;
@@ -262,7 +275,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
                                                            __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(a1, a0, sel[i])), 0u, false);
                 const unsigned h1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cc[i]),
                                                            __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(b1, b0, sel[i])), 0u, false);
-                const unsigned v = (mul_hi_u24(cy0, h0 & ~15u) + mul_hi_u24(cy1, h1 & ~15u) + 2) >> 2;
+                const unsigned v = rs_vpass<GENERIC>(cy0, cy1, h0, h1);
                 packed |= v << (8 * i);
             }
             __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
@@ -281,7 +294,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         for (int i = 0; i < 4; i++) {
             const unsigned h0 = __umul24(r0[o0[i]], c0[i]) + __umul24(r0[o1[i]], c1[i]);
             const unsigned h1 = __umul24(r1[o0[i]], c0[i]) + __umul24(r1[o1[i]], c1[i]);
-            const unsigned v = (mul_hi_u24((unsigned)cy.z, h0 & ~15u) + mul_hi_u24((unsigned)cy.w, h1 & ~15u) + 2) >> 2;
+            const unsigned v = rs_vpass<GENERIC>((unsigned)cy.z, (unsigned)cy.w, h0, h1);
             packed |= v << (8 * i);
         }
         __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
@@ -939,6 +952,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                                              unsigned long long* __restrict__ ost) {
     const int NC = g->node_cap;
     const int tid = threadIdx.x;
+    const int tieMask = (g->variant & ORB_VARIANT_TIE_REVERSE) ? 0xFFFFFF : 0;   // :684 tie policy
     // LDS carve: tables P and Q (ping-pong: A = current list, B = next), quad, rank, info, ord, nchr,
     // scan buffers, scalars.  Phase 2's dense sort keys alias B's rx/ry, its per-rank d / prefix
     // alias B's cnt/seq (all consumed before B is written).
@@ -1143,8 +1157,11 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const bool big = t < S && cntA[t] > 1;
                 int tot;
                 const int pos = nsort + oct_scan<NT>(big ? 1 : 0, sc, par, tot);
+                // seq in 24 bits: creation order, or its complement for ORB_VARIANT_TIE_REVERSE (a later-
+                // created node counts as the smaller pointer); roots (seq < 0) never reach this sort
                 if (big)
-                    skey[pos] = ((unsigned long long)cntA[t] << 40) | ((unsigned long long)seqA[t] << 16) |
+                    skey[pos] = ((unsigned long long)cntA[t] << 40) |
+                                ((unsigned long long)((unsigned)(seqA[t] ^ tieMask) & 0xFFFFFFu) << 16) |
                                 (unsigned long long)t;
                 nsort += tot;
             }
@@ -1465,8 +1482,9 @@ __device__ __forceinline__ void desc_issue(const DescSlot& d, int lane, uint32_t
 // 256 rBRIEF tests of one keypoint, the blurred samples computed at the sample pixels only (the column
 // pass of the 7x7 blur over RT[bx][by .. by+6], rounded as the pinned OpenCV 3.2 8U path: half-to-even
 // where the SSE2 body runs (x < W & ~3), half-up in the scalar tail).  ALLEVEN: every sampled column
-// lies in the SSE2 body (x + 18 < W & ~3), so the per-sample column test drops out.
-template <bool ALLEVEN>
+// lies in the SSE2 body (x + 18 < W & ~3), so the per-sample column test drops out.  FMA: the sample
+// offsets contracted as the reference's -march=native build does (else ORB_VARIANT_NO_FMA: uncontracted).
+template <bool ALLEVEN, bool FMA>
 __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float b, const float (&pf)[4][4], int colBase,
                                               int xsimd, ushort2_t K01, ushort2_t K23, ushort2_t K45, ushort2_t K60,
                                               int lane, unsigned long long* __restrict__ dst) {
@@ -1497,8 +1515,12 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
         // the sample offsets as the reference's -O3 -march=native build contracts them (:119-120;
         // tools/ref_flags_probe.cpp): x = fma(px, a, -(py*b)), y = fma(px, b, py*a)
-        const uint32_t r0 = sample(__builtin_fmaf(px0, a, -(py0 * b)), __builtin_fmaf(px0, b, py0 * a));
-        const uint32_t r1 = sample(__builtin_fmaf(px1, a, -(py1 * b)), __builtin_fmaf(px1, b, py1 * a));
+        // (ORB_VARIANT_NO_FMA: px * a - py * b and px * b + py * a, each product rounded; the kernels build
+        // with -ffp-contract=off)
+        const uint32_t r0 = FMA ? sample(__builtin_fmaf(px0, a, -(py0 * b)), __builtin_fmaf(px0, b, py0 * a))
+                                : sample(px0 * a - py0 * b, px0 * b + py0 * a);
+        const uint32_t r1 = FMA ? sample(__builtin_fmaf(px1, a, -(py1 * b)), __builtin_fmaf(px1, b, py1 * a))
+                                : sample(px1 * a - py1 * b, px1 * b + py1 * a);
         // saturate_cast<uchar>: only the right-hand side needs the clamp (t0 = 256 compares as 255 would)
         mq[gq] = __ballot((r0 >> 16) < min(r1 >> 16, 255u));
     }
@@ -1560,6 +1582,7 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
     }
 }
 
+template <bool FMA>
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
                                           const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt,
                                           orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
@@ -1676,8 +1699,8 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 
     // ---- column pass: evaluated only at the 512 BRIEF sample pixels (brief_sampled), v_dot2_u32_u16 on
     // row pairs of RT; rounding as the pinned OpenCV 3.2 8U path: half-to-even where the SSE2 body runs
-    // (x < W & ~3), half-up in the scalar tail.
-    const int xsimd = L.w & ~3;
+    // (x < W & ~3), half-up in the scalar tail; ORB_VARIANT_BLUR_HALFUP: half-up everywhere (no SSE2 body).
+    const int xsimd = (g->variant & ORB_VARIANT_BLUR_HALFUP) ? 0 : (L.w & ~3);
     const int k0 = g->gk[0], k1 = g->gk[1], k2 = g->gk[2], k3 = g->gk[3], k4 = g->gk[4], k5 = g->gk[5],
               k6 = g->gk[6];
     const ushort2_t K01 = {(unsigned short)k0, (unsigned short)k1}, K23 = {(unsigned short)k2, (unsigned short)k3},
@@ -1703,8 +1726,8 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     glibc_sincosf(ang, &b, &a);
     DESC_STAMP(5);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(outD + ((long long)f * kpCap + outIdx) * 32);
-    if (x + 18 < xsimd) brief_sampled<true>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
-    else brief_sampled<false>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
+    if (x + 18 < xsimd) brief_sampled<true, FMA>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
+    else brief_sampled<false, FMA>(rt, a, b, pf, x - 18, xsimd, K01, K23, K45, K60, lane, dst);
     if (lane == 0) {
         orb_keypoint o;
         o.x = (float)x;
@@ -1727,6 +1750,7 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 /* Fused IC angle + 7x7 blur + rBRIEF, one wavefront per keypoint slot; a wavefront owns two consecutive
  * slots and issues the second interior window's loads before processing the first. */
 constexpr int kDescWaves = 4, kDescSlotsPerWave = 2;
+template <bool FMA>   // false: ORB_VARIANT_NO_FMA
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
@@ -1771,11 +1795,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
     if (d1.ok && d1.interior) desc_issue(d1, lane, v1);
     write_n();   // (after the window loads are issued)
-    if (d0.ok) desc_body(g, d0, f, lane, v0, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
+    if (d0.ok) desc_body<FMA>(g, d0, f, lane, v0, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
     if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
-        desc_body(g, d1, f, lane, v1, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
+        desc_body<FMA>(g, d1, f, lane, v1, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
     }
 }
 
@@ -1819,19 +1843,18 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         // untiled kernel (large scale factors): chosen per level from the geometry (LevelGeom::rs_tiled)
         const int t = g.L[l].rs_tiled;
         const ResizeCoef* cf = b.d_rcoef + b.rcoef_off[l];
+        const bool gen = (g.variant & ORB_VARIANT_RESIZE_GENERIC) != 0;
         if (t & 3) {
             const int th = (t & 2) ? 32 : 16;
             const dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
             const size_t lds = (size_t)g.L[l].rs_span_rows * kRsPitch;
-            if (th == 32)
-                hipLaunchKernelGGL(k_resize_tiled<32>, grid, dim3(256), lds, s, b.d_geom, cf, l, d_frames, frame_pitch,
-                                   row_stride, b.d_pyr);
-            else
-                hipLaunchKernelGGL(k_resize_tiled<16>, grid, dim3(256), lds, s, b.d_geom, cf, l, d_frames, frame_pitch,
-                                   row_stride, b.d_pyr);
+            auto kern = th == 32 ? (gen ? k_resize_tiled<32, true> : k_resize_tiled<32, false>)
+                                 : (gen ? k_resize_tiled<16, true> : k_resize_tiled<16, false>);
+            hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, b.d_geom, cf, l, d_frames, frame_pitch, row_stride,
+                               b.d_pyr);
         } else {
-            hipLaunchKernelGGL(k_resize, dim3(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes), dim3(256), 0, s,
-                               b.d_geom, cf, l, d_frames, frame_pitch, row_stride, b.d_pyr);
+            hipLaunchKernelGGL(gen ? k_resize<true> : k_resize<false>, dim3(cdiv(g.L[l].w, 256), cdiv(g.L[l].h, 4), nframes),
+                               dim3(256), 0, s, b.d_geom, cf, l, d_frames, frame_pitch, row_stride, b.d_pyr);
         }
     };
     // FAST over cells [cbeg, cbeg + cnum) of every frame: one-wave workgroups, two (frame, cell) items per
@@ -1861,7 +1884,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         unsigned long long* dst = b.d_stamps ? b.d_stamps + (size_t)nframes * (g.ncells * 8 + g.nlevels * 32) : nullptr;
         const int spw = nframes == 1 ? 1 : kDescSlotsPerWave;   // a single frame: one keypoint per wave
         const unsigned gx = cdiv(g.nkpcap, kDescWaves * spw);
-        hipLaunchKernelGGL(k_describe, dim3(gx * nframes), dim3(64 * kDescWaves), 0, s, b.d_geom, d_frames, frame_pitch,
+        hipLaunchKernelGGL((g.variant & ORB_VARIANT_NO_FMA) ? k_describe<false> : k_describe<true>, dim3(gx * nframes), dim3(64 * kDescWaves), 0, s, b.d_geom, d_frames, frame_pitch,
                            row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap, dst, spw);
     };
     int* zero = b.zero_err ? b.d_err : nullptr;

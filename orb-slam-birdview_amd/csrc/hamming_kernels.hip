@@ -1,7 +1,12 @@
-// gfx950 Hamming-distance kernels for ORBmatcher (ORBmatcher.cc).  256-bit distance =
-// 8 x (v_xor_b32 + v_bcnt_u32_b32): bitwise VALU work, no MFMA.  The selection logic that depends
-// on the order of earlier accepted matches (SearchByBoW's taken set, SearchForInitialization's
-// vMatchedDistance) is replayed on the host from these exact top-k lists (matcher.cpp).
+// gfx950 Hamming-distance kernels for ORBmatcher (ORBmatcher.cc).  Two forms of the 256-bit distance
+// (DescriptorDistance, ORBmatcher.cc:1647-1663):
+//  - k_topk / k_triangulation: 8 x (v_xor_b32 + v_bcnt_u32_b32) per pair on the VALU, for the
+//    vocabulary-gated candidate lists (CSR);
+//  - k_top2_mfma: the all-pairs top-2 on the matrix cores, bits as +-1 int8 so that
+//    q . t = 256 - 2 popcount(q ^ t) (v_mfma_i32_32x32x32_i8; bound: the I8 MFMA peak).
+// The selection logic that depends on the order of earlier accepted matches (SearchByBoW's taken set,
+// SearchForInitialization's vMatchedDistance) is replayed on the host from these exact top-k lists
+// (matcher.hip).
 #include <algorithm>
 #include <cstdlib>
 
@@ -174,12 +179,13 @@ __device__ __forceinline__ v4i_t pm16x16(uint32_t w) {
  * 32 bytes), so k_top2_mfma's train tiles are plain copies: without it every query workgroup of a pair
  * re-expands every train tile (~40 VALU per thread and tile, more than the tile's top-2 updates). */
 __global__ __launch_bounds__(256) void k_expand_pm1(Top2Batch a, int max_nt) {
+    // blockIdx.y = expansion slot: one per distinct train frame (a.tx_frames) or, without that list, one per pair
     const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
     const int row = i >> 3, s = i & 7;
-    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
-    const int nt = a.counts ? a.counts[fr.y] : a.nt;
+    const int tf = a.tx_frames ? a.tx_frames[p] : (a.frames ? a.frames[p].y : 0);
+    const int nt = a.counts ? a.counts[tf] : a.nt;
     if (row >= min(nt, max_nt)) return;
-    const uint32_t w = reinterpret_cast<const uint32_t*>(a.t + ((long long)fr.y * a.t_stride + row) * 32)[s];
+    const uint32_t w = reinterpret_cast<const uint32_t*>(a.t + ((long long)tf * a.t_stride + row) * 32)[s];
     v4i_t* d = reinterpret_cast<v4i_t*>(const_cast<uint8_t*>(a.tx) + ((long long)p * a.tx_stride + row) * 256 + 32 * s);
     d[0] = pm1x16(w);
     d[1] = pm1x16(w >> 16);
@@ -212,7 +218,8 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
     }
     const uint32_t* __restrict__ T = reinterpret_cast<const uint32_t*>(a.t + (long long)fr.y * a.t_stride * 32);
     // PRE: this pair's expanded trains through a buffer descriptor (SGPRs), 32-bit offsets
-    const uint64_t txb = PRE ? reinterpret_cast<uint64_t>(a.tx + (long long)p * a.tx_stride * 256) : 0;
+    const int txs = a.tx_slot ? a.tx_slot[p] : p;   // the pair's expansion slot
+    const uint64_t txb = PRE ? reinterpret_cast<uint64_t>(a.tx + (long long)txs * a.tx_stride * 256) : 0;
     const auto TXR = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(txb >> 32)) << 32) |
                                 (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)txb)),
@@ -306,6 +313,7 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
 }
 
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
+    npairs = std::max(npairs, 1);
     const int qwaves = std::max(1, (max_nq + 63) / 64);
     int ns = (8192 + npairs * qwaves - 1) / (npairs * qwaves);   // aim for >= 8192 wavefronts
     ns = std::min(ns, std::max(1, (max_nt + 31) / 32));          // >= 32 trains per slice
@@ -324,8 +332,11 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
     a.slice = ((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr;
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
-    if (a.tx) {
-        hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, npairs), dim3(256), 0, stream, a, max_nt);
+    // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
+    // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels
+    if (a.tx && max_nt > 0) {
+        const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
+        hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, nslots), dim3(256), 0, stream, a, max_nt);
         hipLaunchKernelGGL(k_top2_mfma<true>, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
                            d_second);
     } else {

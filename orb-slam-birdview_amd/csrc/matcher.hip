@@ -277,7 +277,7 @@ int orb_hamming_top2_device(orb_ctx* h, const uint8_t* d_q, int nq, const uint8_
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     uint2* part = a.take<uint2>((size_t)ns * nq);
     uint8_t* tx = a.take<uint8_t>((size_t)nt * 256);   // trains expanded to +-1 int8 once (k_expand_pm1)
-    Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq, tx, nt};
+    Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq, tx, nt, nullptr, nullptr, 0};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2_batch(tb, 1, nq, nt, d_best, d_best_idx, d_second, part, c->stream);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
@@ -293,21 +293,46 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     if (!d_desc || !d_counts || kp_cap <= 0 || kp_cap > 65535 || !q_frames || !t_frames || !d_best ||
         !d_best_idx || !d_second)
         return set_error("orb_hamming_top2_frames_device: bad arguments", hipSuccess), ORB_ERR_ARG;
+    for (int p = 0; p < npairs; p++)
+        if (q_frames[p] < 0 || t_frames[p] < 0)
+            return set_error("orb_hamming_top2_frames_device: negative frame index", hipSuccess), ORB_ERR_ARG;
+    // each distinct train frame is expanded to +-1 once (consecutive-frame pairs share their frames), so the
+    // expansion scratch grows with the distinct frames, not with the pairs
+    // host staging in the context (it outlives the asynchronous upload): [pairs (q, t) | slot per pair |
+    // train frame per slot], one upload
+    std::vector<int>& up = c->pairs_upload_host;
+    up.assign((size_t)npairs * 3, 0);
+    {
+        std::vector<std::pair<int, int>> order(npairs);
+        for (int p = 0; p < npairs; p++) order[p] = {t_frames[p], p};
+        std::sort(order.begin(), order.end());
+        int nsl = 0;
+        for (int i = 0; i < npairs; i++) {
+            if (i == 0 || order[i].first != order[i - 1].first) {
+                up.push_back(order[i].first);
+                nsl++;
+            }
+            up[(size_t)2 * npairs + order[i].second] = nsl - 1;
+        }
+        for (int p = 0; p < npairs; p++) {
+            up[2 * p] = q_frames[p];
+            up[2 * p + 1] = t_frames[p];
+        }
+    }
+    const int nslots = (int)up.size() - 3 * npairs;
     Arena a{c};
     const int ns = top2_batch_slices(npairs, kp_cap, kp_cap);
-    hipError_t e = a.reserve(Arena::align((size_t)npairs * sizeof(int2)) +
-                             Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) +
-                             Arena::align((size_t)npairs * kp_cap * 256) + 768);
+    hipError_t e = a.reserve(Arena::align(up.size() * 4) + Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) +
+                             Arena::align((size_t)nslots * kp_cap * 256) + 768);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
-    int2* d_frames = a.take<int2>(npairs);
+    int* d_up = a.take<int>(up.size());
     uint2* part = a.take<uint2>((size_t)npairs * ns * kp_cap);
-    uint8_t* tx = a.take<uint8_t>((size_t)npairs * kp_cap * 256);   // each pair's trains expanded once
-    if (c->frames_host.size() < (size_t)npairs) c->frames_host.resize(npairs);
-    for (int p = 0; p < npairs; p++) c->frames_host[p] = make_int2(q_frames[p], t_frames[p]);
-    if ((e = hipMemcpyAsync(d_frames, c->frames_host.data(), (size_t)npairs * sizeof(int2), hipMemcpyHostToDevice,
-                            c->stream)) != hipSuccess)
+    uint8_t* tx = a.take<uint8_t>((size_t)nslots * kp_cap * 256);   // each distinct train frame expanded once
+    if ((e = hipMemcpyAsync(d_up, up.data(), up.size() * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return set_error("upload pairs", e), ORB_ERR_HIP;
-    Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap, tx, kp_cap};
+    const int2* d_frames = reinterpret_cast<const int2*>(d_up);
+    Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap, tx, kp_cap,
+                 d_up + 2 * npairs, d_up + 3 * npairs, nslots};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2_batch(tb, npairs, kp_cap, kp_cap, d_best, d_best_idx, d_second, part, c->stream);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);

@@ -106,6 +106,7 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
     g.H = H;
     g.iniTh = std::min(std::max(c->p.iniThFAST, 0), 255);
     g.minTh = std::min(std::max(c->p.minThFAST, 0), 255);
+    g.variant = c->p.variant;
     for (int i = 0; i < 16; i++) g.umax[i] = c->umax[i];
     for (int i = 0; i < 7; i++) g.gk[i] = c->gk[i];
     long long pyr = 0;
@@ -375,6 +376,10 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
         set_error("invalid orb_params", hipSuccess);
         return fail(ORB_ERR_ARG);
     }
+    if (p->variant & ~ORB_VARIANT_MASK) {
+        set_error("invalid orb_params.variant (unknown ORB_VARIANT_* bits)", hipSuccess);
+        return fail(ORB_ERR_ARG);
+    }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || p->device < 0 || p->device >= ndev) {
@@ -393,6 +398,8 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     // ORBGPU_FAST_STAMPS=1 records kernel phase timestamps, ORBGPU_GRAPH=0 launches without graph replay
     if (const char* e = std::getenv("ORBGPU_FAST_STAMPS")) c->fast_stamps = e[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
+    // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
+    if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);

@@ -20,6 +20,7 @@ struct Ctx {
     int device = 0;
     int num_cu = 256;
     bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: the kernels record phase timestamps (diagnostic)
+    bool stereo_stage = false;    // ORBGPU_STEREO_STAGE=1: stereo stages the right side as for a peer GPU (test)
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
@@ -71,7 +72,7 @@ struct Ctx {
     void* h_pinned = nullptr;     // pinned staging for orb_extract's single download (count, flag, keypoints, descriptors)
     size_t pinned_cap = 0;
 
-    std::vector<int2> frames_host;   // staging for orb_hamming_top2_frames_device pair lists
+    std::vector<int> pairs_upload_host;   // staging for orb_hamming_top2_frames_device pair lists / slots
     // matcher scratch arena (bytes)
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;

@@ -55,6 +55,7 @@ struct Geom {
     int nkpcap;          // octree output slots per frame
     long long pyr_bytes; // pyramid bytes per frame (levels >= 1)
     int iniTh, minTh;
+    int variant;         // ORB_VARIANT_* bits (orb_params.variant): the OpenCV arithmetic variant
     int node_cap;        // octree LDS node capacity
     int max_level_cand;  // max cand_cap over levels (octree key scratch per level)
     int fast_rows;       // k_fast_wave per-wave LDS carve (max over levels): ROI rows,
@@ -137,10 +138,15 @@ struct Top2Batch {
     const int2* frames;
     int slice;
     long long out_stride;   // outputs / partials of pair p at p * out_stride + query
-    // trains already expanded to +-1 int8 (256 B each; pair p's at tx + p * tx_stride * 256), or NULL:
-    // k_top2_mfma then expands every train tile itself
+    // trains already expanded to +-1 int8 (256 B each; pair p's at tx + slot * tx_stride * 256 with
+    // slot = tx_slot[p], or p when tx_slot is NULL), or NULL: k_top2_mfma then expands every train tile
+    // itself.  tx_frames (n_tx_frames entries): the train frame of each slot, so that a frame shared by
+    // several pairs is expanded once (NULL: one slot per pair, frames[p].y)
     const uint8_t* tx;
     long long tx_stride;
+    const int* tx_slot;
+    const int* tx_frames;
+    int n_tx_frames;
 };
 int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,

@@ -414,8 +414,7 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     // search reads the right image and pyramid, so they move to the left device over xGMI first
     // (hipMemcpyPeerAsync: the right frame's level 0 and its pyramid slot, ~2.9 MB at 1280x720).
     // ORBGPU_STEREO_STAGE=1 forces the same staging on one device (tests/test_gpu_stereo.py).
-    const char* force = std::getenv("ORBGPU_STEREO_STAGE");
-    if (cl->device != cr->device || (force && force[0] == '1')) {
+    if (cl->device != cr->device || cl->stereo_stage) {
         const size_t f0 = (size_t)cr->last_frame_pitch, pb = (size_t)cr->geom.pyr_bytes;
         const size_t sneed = ((f0 + 255) & ~(size_t)255) + pb;
         if (sneed > cl->peer_cap || !cl->d_peer) {

@@ -16,6 +16,9 @@ static int env_device() {
     return e ? atoi(e) : 0;
 }
 
+int env_variant();   // ORBextractor.cc: ORBGPU_VARIANT
+
+
 std::shared_ptr<BirdviewORB> BirdviewORB::create(int nfeatures, float scaleFactor, int nlevels, int edgeThreshold,
                                                  int firstLevel, int WTA_K, int scoreType, int patchSize,
                                                  int fastThreshold) {
@@ -27,7 +30,10 @@ std::shared_ptr<BirdviewORB> BirdviewORB::create(int nfeatures, float scaleFacto
 BirdviewORB::BirdviewORB(int nfeatures, float scaleFactor, int nlevels, int edgeThreshold, int fastThreshold,
                          int device)
     : nfeatures_(nfeatures) {
-    orb_bird_params p{nfeatures, scaleFactor, nlevels, edgeThreshold, fastThreshold, device};
+    // cv::ORB's pyramid resize and descriptor blur follow the same OpenCV build as ORBextractor's: the
+    // resize / blur bits of ORBGPU_VARIANT
+    orb_bird_params p{nfeatures, scaleFactor, nlevels, edgeThreshold, fastThreshold, device,
+                      env_variant() & (ORB_VARIANT_RESIZE_GENERIC | ORB_VARIANT_BLUR_HALFUP)};
     int st = ORB_OK;
     h_ = orb_bird_create(&p, &st);
     if (!h_) throw OrbGpuError(st, "orb_bird_create");

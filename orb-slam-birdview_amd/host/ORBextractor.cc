@@ -20,20 +20,32 @@ static int env_device() {
     return e ? atoi(e) : 0;
 }
 
+int env_variant() {
+    const char* e = getenv("ORBGPU_VARIANT");
+    return e ? (int)strtol(e, nullptr, 0) : ORB_VARIANT_DEFAULT;
+}
+
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
       minThFAST(_minThFAST) {
-    init(env_device());
+    init(env_device(), env_variant());
 }
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST,
                            int device)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
       minThFAST(_minThFAST) {
-    init(device);
+    init(device, env_variant());
 }
 
-void ORBextractor::init(int device) {
+ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST,
+                           int device, int variant)
+    : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
+      minThFAST(_minThFAST) {
+    init(device, variant);
+}
+
+void ORBextractor::init(int device, int variant) {
     orb_params p;
     memset(&p, 0, sizeof p);
     p.nfeatures = nfeatures;
@@ -43,6 +55,7 @@ void ORBextractor::init(int device) {
     p.minThFAST = minThFAST;
     p.device = device;
     p.max_batch = 1;
+    p.variant = variant;
     int st = ORB_OK;
     ctx_ = orb_create(&p, &st);
     if (!ctx_) throw OrbGpuError(st, "orb_create");

@@ -103,9 +103,13 @@ class ORBextractor {
 public:
     enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
 
-    // ORBextractor.cc:410-470.  The device is ORBGPU_DEVICE (default 0) unless given.
+    // ORBextractor.cc:410-470.  The device is ORBGPU_DEVICE (default 0) unless given; the OpenCV arithmetic
+    // variant (ORB_VARIANT_* bits of include/orbgpu.h, matching the OpenCV the reference build links) is
+    // ORBGPU_VARIANT (default 0 = OpenCV 3.2) unless given, so Tracking.cc:121-127 constructs it unchanged.
     ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST);
     ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int device);
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int device,
+                 int variant);
     ~ORBextractor();
     ORBextractor(const ORBextractor&) = delete;
     ORBextractor& operator=(const ORBextractor&) = delete;
@@ -147,7 +151,7 @@ protected:
 
 private:
     friend class ImagePyramid;
-    void init(int device);
+    void init(int device, int variant);
     int extract_raw(const uint8_t* data, int cols, int rows, size_t step);   // returns #keypoints in kbuf_/dbuf_
     orb_ctx* ctx_ = nullptr;
     std::vector<KeyPoint> kbuf_;

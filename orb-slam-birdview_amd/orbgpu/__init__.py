@@ -10,11 +10,13 @@ import ctypes
 
 import numpy as np
 
-from ._lib import OrbBirdParams, OrbError, OrbFeatVec, OrbParams, check, lib
+from ._lib import (VARIANT_BLUR_HALFUP, VARIANT_DEFAULT, VARIANT_NO_FMA, VARIANT_RESIZE_GENERIC,
+                   VARIANT_TIE_REVERSE, OrbBirdParams, OrbError, OrbFeatVec, OrbParams, check, lib)
 
 __all__ = ["ORBextractor", "ORBmatcher", "BatchExtractor", "KP_DTYPE", "OrbError", "device_count",
            "features_in_area", "compute_stereo_matches", "ORBVocabulary", "BirdORB", "cornerSubPix",
-           "bird_footprint_mask"]
+           "bird_footprint_mask", "VARIANT_DEFAULT", "VARIANT_TIE_REVERSE", "VARIANT_RESIZE_GENERIC",
+           "VARIANT_BLUR_HALFUP", "VARIANT_NO_FMA"]
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -33,9 +35,9 @@ def device_count():
 
 class _Ctx:
     def __init__(self, nfeatures, scale_factor, nlevels, ini_th, min_th, device=0, max_width=0,
-                 max_height=0, max_batch=1):
+                 max_height=0, max_batch=1, variant=0):
         self.params = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th, device, max_width,
-                                max_height, max_batch)
+                                max_height, max_batch, variant)
         st = ctypes.c_int()
         self.h = lib().orb_create(ctypes.byref(self.params), ctypes.byref(st))
         if not self.h:
@@ -52,10 +54,11 @@ class _Ctx:
 
 
 class ORBextractor(_Ctx):
-    """ORB_SLAM2::ORBextractor (ORBextractor.cc:410-470, 1043-1132) on one MI355X."""
+    """ORB_SLAM2::ORBextractor (ORBextractor.cc:410-470, 1043-1132) on one MI355X.  `variant` selects the
+    OpenCV arithmetic the reference build links (VARIANT_* bits; 0 = the pinned OpenCV 3.2 default)."""
 
-    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0):
-        super().__init__(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device)
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0, variant=0):
+        super().__init__(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device, variant=variant)
         n = nlevels
         self._t = [np.zeros(n, np.float32) for _ in range(4)]
         self._npl = np.zeros(n, np.int32)
@@ -153,8 +156,8 @@ class BatchExtractor(_Ctx):
     """Device-resident batched extraction (orb_extract_batch_device): frames already in HBM."""
 
     def __init__(self, nfeatures, width, height, batch, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
-                 device=0):
-        super().__init__(nfeatures, scale_factor, nlevels, ini_th, min_th, device, width, height, batch)
+                 device=0, variant=0):
+        super().__init__(nfeatures, scale_factor, nlevels, ini_th, min_th, device, width, height, batch, variant)
         self.w, self.hgt, self.batch = width, height, batch
         self.kp_cap = lib().orb_batch_kp_cap(self.h, width, height)
         if self.kp_cap < 0:
@@ -451,8 +454,9 @@ class BirdORB:
     scaleFactor 1.2, nlevels 8, edgeThreshold 31, HARRIS_SCORE, patchSize 31, fastThreshold 20),
     plus cornerSubPix and the fused Frame.cc:320-342 sequence, on one MI355X (orb_bird_* C-ABI)."""
 
-    def __init__(self, nfeatures=2000, scaleFactor=1.2, nlevels=8, edgeThreshold=31, fastThreshold=20, device=0):
-        self.params = OrbBirdParams(nfeatures, scaleFactor, nlevels, edgeThreshold, fastThreshold, device)
+    def __init__(self, nfeatures=2000, scaleFactor=1.2, nlevels=8, edgeThreshold=31, fastThreshold=20, device=0,
+                 variant=0):
+        self.params = OrbBirdParams(nfeatures, scaleFactor, nlevels, edgeThreshold, fastThreshold, device, variant)
         st = ctypes.c_int()
         self.h = lib().orb_bird_create(ctypes.byref(self.params), ctypes.byref(st))
         if not self.h:

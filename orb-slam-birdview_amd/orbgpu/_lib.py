@@ -15,18 +15,21 @@ HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "orbgpu.h")
 
 _LIB = None
 
+# OpenCV arithmetic variant bits (include/orbgpu.h ORB_VARIANT_*; equal to the oracle's ORACLE_* flags)
+VARIANT_DEFAULT, VARIANT_TIE_REVERSE, VARIANT_RESIZE_GENERIC, VARIANT_BLUR_HALFUP, VARIANT_NO_FMA = 0, 1, 2, 4, 8
+
 vp, ci, cf, csz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
 
 
 class OrbParams(ctypes.Structure):
     _fields_ = [("nfeatures", ci), ("scaleFactor", cf), ("nlevels", ci), ("iniThFAST", ci),
                 ("minThFAST", ci), ("device", ci), ("max_width", ci), ("max_height", ci),
-                ("max_batch", ci)]
+                ("max_batch", ci), ("variant", ci)]
 
 
 class OrbBirdParams(ctypes.Structure):
     _fields_ = [("nfeatures", ci), ("scaleFactor", cf), ("nlevels", ci), ("edgeThreshold", ci),
-                ("fastThreshold", ci), ("device", ci)]
+                ("fastThreshold", ci), ("device", ci), ("variant", ci)]
 
 
 class OrbFeatVec(ctypes.Structure):

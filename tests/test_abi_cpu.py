@@ -30,8 +30,25 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_keypoint_layout(orbgpu_mod):
     from orbgpu import _lib
-    assert _lib.lib().orb_abi_version() == 1
+    assert _lib.lib().orb_abi_version() == 2   # 2: orb_params / orb_bird_params gained `variant`
     assert orbgpu_mod.KP_DTYPE.itemsize == 28   # cv::KeyPoint
+    # the ctypes structs match the header's field lists
+    assert [f for f, _ in _lib.OrbParams._fields_][-1] == "variant"
+    assert [f for f, _ in _lib.OrbBirdParams._fields_][-1] == "variant"
+
+
+def test_variant_bits_match_header_and_oracle(orbgpu_mod):
+    """ORB_VARIANT_* (include/orbgpu.h) == the Python constants == the oracle's ORACLE_* flags, so a parity
+    test passes one value to both sides."""
+    hdr = open(os.path.join(ROOT, "include", "orbgpu.h")).read()
+    ora = open(os.path.join(ROOT, "oracle", "orb_oracle.h")).read()
+    v = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define ORB_VARIANT_([A-Z_]+)\s+(\d+)", hdr)}
+    o = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define ORACLE_([A-Z_]+)\s+(\d+)", ora)}
+    assert v["TIE_REVERSE"] == o["TIE_REVERSE_SEQ"] == orbgpu_mod.VARIANT_TIE_REVERSE
+    assert v["RESIZE_GENERIC"] == o["RESIZE_GENERIC"] == orbgpu_mod.VARIANT_RESIZE_GENERIC
+    assert v["BLUR_HALFUP"] == o["BLUR_ALL_HALFUP"] == orbgpu_mod.VARIANT_BLUR_HALFUP
+    assert v["NO_FMA"] == o["NO_FMA"] == orbgpu_mod.VARIANT_NO_FMA
+    assert v["MASK"] == v["TIE_REVERSE"] | v["RESIZE_GENERIC"] | v["BLUR_HALFUP"] | v["NO_FMA"]
 
 
 def test_no_cpu_fallback_without_gpu(orbgpu_mod):
@@ -46,6 +63,8 @@ def test_invalid_params_rejected(orbgpu_mod):
         orbgpu_mod.ORBextractor(1000, 1.0, 8, 20, 7)   # scaleFactor must be > 1
     with pytest.raises(orbgpu_mod.OrbError):
         orbgpu_mod.ORBextractor(1000, 1.2, 40, 20, 7)  # > ORBGPU_MAX_LEVELS
+    with pytest.raises(orbgpu_mod.OrbError):
+        orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7, variant=32)   # unknown ORB_VARIANT_* bit
 
 
 def test_descriptor_distance_host_helper(orbgpu_mod, oracle_mod):
