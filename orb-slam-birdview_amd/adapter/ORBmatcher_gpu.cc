@@ -1,0 +1,286 @@
+/*
+ * ORBmatcher_gpu.cc — the reference's descriptor-matcher methods with their exact signatures
+ * (include/ORBmatcher.h:65-73, 87-89 of donglinb/ORB-SLAM-BIRDVIEW), computed by liborbgpu.
+ *
+ * This file is compiled INSIDE the reference's libORB_SLAM2, next to src/ORBmatcher.cc, from which
+ * the maintainer removes the six bodies defined here:
+ *
+ *   int ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)              ORBmatcher.cc:159-288
+ *   int ORBmatcher::SearchForInitialization(Frame&, Frame&, vector<cv::Point2f>&,
+ *                                           vector<int>&, int)                      :405-520
+ *   int ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)           :522-655
+ *   int ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat,
+ *                                          vector<pair<size_t,size_t>>&, const bool) :657-823
+ *   int ORBmatcher::BirdviewMatch(Frame&, Frame&, vector<int>&, vector<cv::Point2f>&, int)  :1667-1786
+ *   int ORBmatcher::BirdviewMatch(const Frame&, const Frame&, vector<int>&, int)          :1788-1899
+ *
+ * Everything else in ORBmatcher (the projection-gated searches, Fuse, SearchBySim3, DescriptorDistance,
+ * CheckDistEpipolarLine, ComputeThreeMaxima) stays the reference's own CPU code.  Callers
+ * (Tracking.cc:739,1032,1938; LocalMapping.cc:278; LoopClosing.cc:265) are unchanged.
+ *
+ * Each method reads the same Frame / KeyFrame / MapPoint members as the reference body, hands them to
+ * the C-ABI (include/orbgpu.h) as flat views, and maps the returned indices back to the reference's
+ * outputs (MapPoint* for the BoW searches).  The GPU computes the distances and candidate filtering;
+ * the order-dependent acceptance (taken sets, vMatchedDistance stealing, ratio test, rotation
+ * histogram + ComputeThreeMaxima) is replayed by liborbgpu in the reference's iteration order, so the
+ * outputs are the reference's.  The candidate windows come from the reference's own
+ * Frame::GetFeaturesInArea / GetFeaturesInAreaBirdview, and the epipole from the reference's own
+ * expression (:664-670).  A GPU failure throws std::runtime_error (the reference has no error path;
+ * there is no CPU fallback).
+ *
+ * Thread safety: the reference calls these from the Tracking, LocalMapping and LoopClosing threads at
+ * once; each host thread gets its own liborbgpu context (device ORBGPU_DEVICE, default 0).
+ */
+#include "ORBmatcher.h"
+
+#include <limits.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/orbgpu.h"
+
+namespace ORB_SLAM2 {
+
+namespace orbgpu_adapter {
+
+static_assert(sizeof(cv::KeyPoint) == sizeof(orb_keypoint), "cv::KeyPoint must keep its 28-byte layout");
+
+void check(int st, const char* what) {
+    if (st != ORB_OK) throw std::runtime_error(std::string("liborbgpu ") + what + ": " + orb_last_error());
+}
+
+struct ThreadCtx {
+    int device = -1;
+    orb_ctx* ctx = nullptr;
+    ~ThreadCtx() {
+        if (ctx) orb_destroy(ctx);
+    }
+};
+
+// one context per (host thread, device): the matchers are stack objects called from several threads
+orb_ctx* ctx() {
+    static thread_local ThreadCtx tc;
+    const char* e = getenv("ORBGPU_DEVICE");
+    const int dev = e ? atoi(e) : 0;
+    if (tc.ctx && tc.device == dev) return tc.ctx;
+    if (tc.ctx) orb_destroy(tc.ctx);
+    tc.ctx = nullptr;
+    orb_params p;
+    memset(&p, 0, sizeof p);
+    p.nfeatures = 1000;   // extraction parameters are unused by the matcher entry points
+    p.scaleFactor = 1.2f;
+    p.nlevels = 8;
+    p.iniThFAST = 20;
+    p.minThFAST = 7;
+    p.device = dev;
+    int st = ORB_OK;
+    tc.ctx = orb_create(&p, &st);
+    if (!tc.ctx) check(st, "orb_create");
+    tc.device = dev;
+    return tc.ctx;
+}
+
+// An n x 32 CV_8U descriptor matrix as one contiguous block (mDescriptors is continuous in the reference:
+// ORBextractor allocates it with create(); a strided view is copied row by row).
+const uint8_t* desc_rows(const cv::Mat& M, int n, std::vector<uint8_t>& tmp) {
+    static const uint8_t dummy[32] = {0};
+    if (n <= 0 || M.empty()) return dummy;
+    if ((size_t)M.step == 32) return M.ptr(0);
+    tmp.resize((size_t)n * 32);
+    for (int r = 0; r < n; r++) memcpy(&tmp[(size_t)r * 32], M.ptr(r), 32);
+    return tmp.data();
+}
+
+const orb_keypoint* keys_of(const std::vector<cv::KeyPoint>& k) {
+    static const orb_keypoint dummy = {0, 0, 0, 0, 0, 0, 0};
+    return k.empty() ? &dummy : reinterpret_cast<const orb_keypoint*>(k.data());
+}
+
+std::vector<float> angles_of(const std::vector<cv::KeyPoint>& k) {
+    std::vector<float> a(k.size() ? k.size() : 1, 0.f);
+    for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
+    return a;
+}
+
+// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>) as the C-ABI's CSR; std::map order
+// is the reference's iteration order
+struct FeatCsr {
+    std::vector<uint32_t> ids;
+    std::vector<int> off, idx;
+    orb_featvec fv;
+    explicit FeatCsr(const DBoW2::FeatureVector& f) {
+        off.push_back(0);
+        for (DBoW2::FeatureVector::const_iterator it = f.begin(); it != f.end(); ++it) {
+            ids.push_back(it->first);
+            for (size_t j = 0; j < it->second.size(); j++) idx.push_back((int)it->second[j]);
+            off.push_back((int)idx.size());
+        }
+        if (idx.empty()) idx.push_back(0);
+        fv.nnodes = (int)ids.size();
+        fv.node_ids = ids.empty() ? nullptr : ids.data();
+        fv.offsets = off.data();
+        fv.indices = idx.data();
+    }
+};
+
+// pMP && !pMP->isBad() per feature (the BoW searches' admission test, :191-197, :558-562, :574-580)
+std::vector<uint8_t> good_points(const std::vector<MapPoint*>& v) {
+    std::vector<uint8_t> f(v.size() ? v.size() : 1, 0);
+    for (size_t i = 0; i < v.size(); i++) f[i] = v[i] && !v[i]->isBad();
+    return f;
+}
+
+}  // namespace orbgpu_adapter
+
+using namespace orbgpu_adapter;
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+    const std::vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
+    vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL));
+    const std::vector<uint8_t> mp = good_points(vpMapPointsKF);
+    const std::vector<float> aKF = angles_of(pKF->mvKeysUn), aF = angles_of(F.mvKeys);
+    FeatCsr fkf(pKF->mFeatVec), ff(F.mFeatVec);
+    std::vector<uint8_t> t1, t2;
+    std::vector<int> match(F.N > 0 ? F.N : 1, -1);
+    int nmatches = 0;
+    check(orb_search_by_bow_kf_f(ctx(), mfNNratio, mbCheckOrientation, pKF->N, desc_rows(pKF->mDescriptors, pKF->N, t1),
+                                 aKF.data(), mp.data(), fkf.fv, F.N, desc_rows(F.mDescriptors, F.N, t2), aF.data(),
+                                 ff.fv, match.data(), &nmatches),
+          "SearchByBoW(KeyFrame*, Frame&)");
+    for (int iF = 0; iF < F.N; iF++)
+        if (match[iF] >= 0) vpMapPointMatches[iF] = vpMapPointsKF[match[iF]];
+    return nmatches;
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12) {
+    const std::vector<MapPoint*> vpMapPoints1 = pKF1->GetMapPointMatches();
+    const std::vector<MapPoint*> vpMapPoints2 = pKF2->GetMapPointMatches();
+    vpMatches12 = std::vector<MapPoint*>(vpMapPoints1.size(), static_cast<MapPoint*>(NULL));
+    const std::vector<uint8_t> mp1 = good_points(vpMapPoints1), mp2 = good_points(vpMapPoints2);
+    const std::vector<float> a1 = angles_of(pKF1->mvKeysUn), a2 = angles_of(pKF2->mvKeysUn);
+    FeatCsr f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
+    std::vector<uint8_t> t1, t2;
+    const int n1 = (int)vpMapPoints1.size(), n2 = (int)vpMapPoints2.size();
+    std::vector<int> match(n1 > 0 ? n1 : 1, -1);
+    int nmatches = 0;
+    check(orb_search_by_bow_kf_kf(ctx(), mfNNratio, mbCheckOrientation, n1, desc_rows(pKF1->mDescriptors, n1, t1),
+                                  a1.data(), mp1.data(), f1.fv, n2, desc_rows(pKF2->mDescriptors, n2, t2), a2.data(),
+                                  mp2.data(), f2.fv, match.data(), &nmatches),
+          "SearchByBoW(KeyFrame*, KeyFrame*)");
+    for (int i1 = 0; i1 < n1; i1++)
+        if (match[i1] >= 0) vpMatches12[i1] = vpMapPoints2[match[i1]];
+    return nmatches;
+}
+
+int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
+                                       std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo) {
+    // epipole of KF1's camera centre in KF2, the reference's own expressions (:664-670)
+    cv::Mat Cw = pKF1->GetCameraCenter();
+    cv::Mat R2w = pKF2->GetRotation();
+    cv::Mat t2w = pKF2->GetTranslation();
+    cv::Mat C2 = R2w * Cw + t2w;
+    const float invz = 1.0f / C2.at<float>(2);
+    const float ex = pKF2->fx * C2.at<float>(0) * invz + pKF2->cx;
+    const float ey = pKF2->fy * C2.at<float>(1) * invz + pKF2->cy;
+
+    const int n1 = pKF1->N, n2 = pKF2->N;
+    std::vector<uint8_t> mp1(n1 > 0 ? n1 : 1, 0), mp2(n2 > 0 ? n2 : 1, 0);   // GetMapPoint(idx) != NULL (:699, :722)
+    for (int i = 0; i < n1; i++) mp1[i] = pKF1->GetMapPoint(i) != NULL;
+    for (int i = 0; i < n2; i++) mp2[i] = pKF2->GetMapPoint(i) != NULL;
+    float F[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) F[3 * r + c] = F12.at<float>(r, c);   // CheckDistEpipolarLine (:143-147)
+    std::vector<float> ur1(pKF1->mvuRight.begin(), pKF1->mvuRight.end()), ur2(pKF2->mvuRight.begin(), pKF2->mvuRight.end());
+    ur1.resize(n1 > 0 ? n1 : 1, -1.f);
+    ur2.resize(n2 > 0 ? n2 : 1, -1.f);
+    FeatCsr f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
+    std::vector<uint8_t> t1, t2;
+    std::vector<int> pairs(2 * (size_t)(n1 > 0 ? n1 : 1));
+    int np = 0;
+    check(orb_search_for_triangulation(ctx(), mbCheckOrientation, bOnlyStereo, n1, desc_rows(pKF1->mDescriptors, n1, t1),
+                                       keys_of(pKF1->mvKeysUn), mp1.data(), ur1.data(), f1.fv, n2,
+                                       desc_rows(pKF2->mDescriptors, n2, t2), keys_of(pKF2->mvKeysUn), mp2.data(),
+                                       ur2.data(), f2.fv, F, ex, ey, pKF2->mvScaleFactors.data(),
+                                       pKF2->mvLevelSigma2.data(), (int)pKF2->mvScaleFactors.size(), pairs.data(),
+                                       n1 > 0 ? n1 : 1, &np),
+          "SearchForTriangulation");
+    vMatchedPairs.clear();   // :812-820
+    vMatchedPairs.reserve(np);
+    for (int i = 0; i < np; i++) vMatchedPairs.push_back(std::make_pair((size_t)pairs[2 * i], (size_t)pairs[2 * i + 1]));
+    return np;
+}
+
+namespace orbgpu_adapter {
+
+// The window searches (:405-520, :1667-1899): candidate list per query from the reference's own grid
+// lookup, in its order; `area(i1)` returns the query's candidates or an empty list for a skipped query.
+template <class Area>
+int window_match(float nnratio, bool checkOri, bool level0_only, const std::vector<cv::KeyPoint>& k1,
+                 const cv::Mat& d1, const std::vector<cv::KeyPoint>& k2, const cv::Mat& d2, Area area,
+                 std::vector<int>& vnMatches12) {
+    const int n1 = (int)k1.size(), n2 = (int)k2.size();
+    std::vector<int> off(n1 + 1, 0), idx;
+    for (int i1 = 0; i1 < n1; i1++) {
+        const std::vector<size_t> v = area(i1);
+        for (size_t j = 0; j < v.size(); j++) idx.push_back((int)v[j]);
+        off[i1 + 1] = (int)idx.size();
+    }
+    if (idx.empty()) idx.push_back(0);
+    std::vector<uint8_t> t1, t2;
+    std::vector<int> out(n1 > 0 ? n1 : 1, -1);
+    int nmatches = 0;
+    check(orb_window_match(ctx(), nnratio, checkOri, level0_only, n1, desc_rows(d1, n1, t1), keys_of(k1), n2,
+                           desc_rows(d2, n2, t2), keys_of(k2), off.data(), idx.data(), out.data(), &nmatches),
+          "window match");
+    vnMatches12.assign(out.begin(), out.begin() + n1);
+    return nmatches;
+}
+
+}  // namespace orbgpu_adapter
+
+int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
+                                        std::vector<int>& vnMatches12, int windowSize) {
+    const int nm = window_match(
+        mfNNratio, mbCheckOrientation, true, F1.mvKeysUn, F1.mDescriptors, F2.mvKeysUn, F2.mDescriptors,
+        [&](int i1) {
+            const int level1 = F1.mvKeysUn[i1].octave;   // :421-423: level-0 queries only
+            if (level1 > 0) return std::vector<size_t>();
+            return F2.GetFeaturesInArea(vbPrevMatched[i1].x, vbPrevMatched[i1].y, windowSize, level1, level1);
+        },
+        vnMatches12);
+    for (size_t i1 = 0, iend1 = vnMatches12.size(); i1 < iend1; i1++)   // :514-517
+        if (vnMatches12[i1] >= 0) vbPrevMatched[i1] = F2.mvKeysUn[vnMatches12[i1]].pt;
+    return nm;
+}
+
+int ORBmatcher::BirdviewMatch(Frame& F1, Frame& F2, std::vector<int>& vnMatches12, std::vector<cv::Point2f>& vPrevMatched,
+                              int windowSize) {
+    const int nm = window_match(
+        mfNNratio, mbCheckOrientation, true, F1.mvKeysBird, F1.mDescriptorsBird, F2.mvKeysBird, F2.mDescriptorsBird,
+        [&](int i1) {
+            const int level1 = F1.mvKeysBird[i1].octave;   // :1683-1685
+            if (level1 > 0) return std::vector<size_t>();
+            return F2.GetFeaturesInAreaBirdview(vPrevMatched[i1].x, vPrevMatched[i1].y, windowSize, level1, level1);
+        },
+        vnMatches12);
+    for (size_t i1 = 0, iend1 = vnMatches12.size(); i1 < iend1; i1++)   // :1778-1781
+        if (vnMatches12[i1] >= 0) vPrevMatched[i1] = F2.mvKeysBird[vnMatches12[i1]].pt;
+    return nm;
+}
+
+int ORBmatcher::BirdviewMatch(const Frame& F1, const Frame& F2, std::vector<int>& vnMatches12, int windowSize) {
+    return window_match(
+        mfNNratio, mbCheckOrientation, false, F1.mvKeysBird, F1.mDescriptorsBird, F2.mvKeysBird, F2.mDescriptorsBird,
+        [&](int i1) {
+            const cv::KeyPoint& kp1 = F1.mvKeysBird[i1];   // :1803-1808: every level, window around kp1
+            return F2.GetFeaturesInAreaBirdview(kp1.pt.x, kp1.pt.y, windowSize, kp1.octave, kp1.octave);
+        },
+        vnMatches12);
+}
+
+}  // namespace ORB_SLAM2

@@ -330,7 +330,8 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     const int qb = (max_nq + kMfQ - 1) / kMfQ;
     int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
     want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
-    a.slice = ((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr;
+    // (max_nt == 0: one empty slice of one tile width, so that nothing below divides by zero)
+    a.slice = std::max(((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr, kMfTr);
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
     // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
     // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels

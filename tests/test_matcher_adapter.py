@@ -1,0 +1,76 @@
+"""The ORBmatcher adapter (orb-slam-birdview_amd/adapter/ORBmatcher_gpu.cc): the reference's own method
+signatures -- SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&), SearchByBoW(KeyFrame*, KeyFrame*, ...),
+SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12, ...), SearchForInitialization(Frame&, Frame&,
+...), BirdviewMatch x2 (include/ORBmatcher.h:65-73, 87-89) -- compiled against models of Frame / KeyFrame /
+MapPoint / DBoW2::FeatureVector (tests/cpp/slam_api) and cv::Mat (tests/cpp/cv_api).  CPU: it compiles
+and defines exactly those symbols.  GPU: tests/cpp/test_matcher_adapter calls them the way Tracking,
+LocalMapping and LoopClosing do and checks every output (MapPoint* vectors, index pairs, vbPrevMatched)
+against the oracle restatement of the reference bodies."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPP = os.path.join(ROOT, "tests", "cpp")
+BIN = os.path.join(CPP, "test_matcher_adapter")
+
+
+@pytest.fixture(scope="module")
+def adapter_bin():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    subprocess.check_call(["make", "-s", "-C", CPP, "test_matcher_adapter"])
+    return BIN
+
+
+def test_adapter_defines_the_reference_signatures(adapter_bin):
+    out = subprocess.run(["nm", "-C", "--defined-only", adapter_bin], capture_output=True, text=True,
+                         check=True).stdout
+    for sym in [
+        "ORB_SLAM2::ORBmatcher::SearchByBoW(ORB_SLAM2::KeyFrame*, ORB_SLAM2::Frame&, "
+        "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&)",
+        "ORB_SLAM2::ORBmatcher::SearchByBoW(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, "
+        "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&)",
+        "ORB_SLAM2::ORBmatcher::SearchForTriangulation(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, cv::Mat, "
+        "std::vector<std::pair<unsigned long, unsigned long>, std::allocator<std::pair<unsigned long, unsigned long> > >&,"
+        " bool)",
+        "ORB_SLAM2::ORBmatcher::SearchForInitialization(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, "
+        "std::vector<cv::Point2f, std::allocator<cv::Point2f> >&, std::vector<int, std::allocator<int> >&, int)",
+        "ORB_SLAM2::ORBmatcher::BirdviewMatch(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, std::vector<int, "
+        "std::allocator<int> >&, std::vector<cv::Point2f, std::allocator<cv::Point2f> >&, int)",
+        "ORB_SLAM2::ORBmatcher::BirdviewMatch(ORB_SLAM2::Frame const&, ORB_SLAM2::Frame const&, std::vector<int, "
+        "std::allocator<int> >&, int)",
+    ]:
+        assert sym in out, sym
+
+
+def _frames(w, h, idx, shift):
+    from orbgpu.synth import synth_frame
+    a = synth_frame(w, h, idx)
+    b = np.empty_like(a)   # the second view: a horizontal shift (epipolar lines stay rows)
+    b[:, shift:] = a[:, :w - shift]
+    b[:, :shift] = a[:, :1]
+    return np.stack([a, b])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,nf,idx,shift", [(1280, 720, 2000, 3, 6), (640, 480, 1000, 5, 4)])
+def test_adapter_matches_the_oracle(adapter_bin, tmp_path, w, h, nf, idx, shift):
+    raw = tmp_path / "pair.raw"
+    raw.write_bytes(_frames(w, h, idx, shift).tobytes())
+    p = subprocess.run([adapter_bin, str(raw), str(w), str(h), str(nf)], capture_output=True, text=True, timeout=300)
+    print(p.stdout)
+    fails = [l for l in p.stdout.splitlines() if l.startswith("CHECK") and " FAIL" in l]
+    assert p.returncode == 0 and not fails and "SUMMARY" in p.stdout, (p.stdout[-3000:], p.stderr[-2000:])
+
+
+def test_adapter_without_gpu_throws(adapter_bin, tmp_path):
+    """No device: the adapter fails loudly (std::runtime_error from orb_create), never a CPU path."""
+    import orbgpu
+    if orbgpu.device_count() > 0:
+        pytest.skip("a GPU is present")
+    raw = tmp_path / "pair.raw"
+    raw.write_bytes(_frames(640, 480, 5, 4).tobytes())
+    p = subprocess.run([adapter_bin, str(raw), "640", "480", "1000"], capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "CHECK exception FAIL" in p.stdout and "orb_create" in p.stdout
