@@ -1,5 +1,6 @@
 // gfx950 kernels of the ORB extractor: pyramid, per-cell FAST+NMS, DistributeOctTree, and the fused
-// IC-angle + 7x7 Gaussian + rBRIEF descriptor.  Integer/byte work: no MFMA anywhere; the bounds
+// IC-angle + 7x7 Gaussian + rBRIEF descriptor.  Integer/byte work: no MFMA in these kernels (the
+// all-pairs Hamming top-2 in hamming_kernels.hip is the one MFMA user); the bounds
 // are HBM bytes and VALU issue.
 //
 // Compiled with -ffp-contract=off and correctly-rounded fp32 divide, so every float expression on the
