@@ -362,6 +362,41 @@ def c4_leg(cfg, frames, first, dist, rank, world, local):
 
 
 # ---------------------------------------------------------------- main
+def matcher_leg(img, w, h, nf, device):
+    """Per-call latency of SearchByBoW (KF,F) / (KF,KF), SearchForTriangulation, SearchForInitialization
+    and Frame::ComputeBoW on two C3 frames (the second shifted by (2, 3) px), FeatureVectors from a
+    synthetic ORBvoc-sized vocabulary (k = 10, L = 6, levelsup 4), GPU adapter vs oracle CPU loop."""
+    import tempfile
+    import numpy as np
+    from orbgpu.synth import write_synth_vocab_large
+    exe = os.path.join(ROOT, "tools", "matcher_latency")
+    if not os.path.exists(exe):
+        return {"error": "tools/matcher_latency not built"}
+    tmp = tempfile.mkdtemp(prefix="orbgpu_matcher_")
+    raw, voc = os.path.join(tmp, "frames.raw"), os.path.join(tmp, "voc.bin")
+    try:
+        a = np.ascontiguousarray(img)
+        b = np.ascontiguousarray(np.roll(a, (2, 3), axis=(0, 1)))
+        with open(raw, "wb") as f:
+            f.write(a.tobytes() + b.tobytes())
+        write_synth_vocab_large(voc, 10, 6)
+        r = subprocess.run([exe, raw, str(w), str(h), str(nf), voc, "50", "10"], capture_output=True, text=True,
+                           timeout=300, env=dict(os.environ, ORBGPU_DEVICE=str(device)))
+        if r.returncode not in (0, 1) or not r.stdout.strip():
+            return {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        out["note"] = ("median us per call, one call per frame / keyframe pair as Tracking.cc:1029-1032, "
+                       "LoopClosing.cc:265, LocalMapping.cc:278, Tracking.cc:738-739 and Frame.cc:562-569 make them; "
+                       "GPU = adapter/ORBmatcher_gpu.cc (host inputs, upload + kernels + host replay), CPU = the "
+                       "oracle's restatement of each body, single thread, same inputs; outputs compared equal")
+        return out
+    finally:
+        for p in (raw, voc):
+            if os.path.exists(p):
+                os.unlink(p)
+        os.rmdir(tmp)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -378,6 +413,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true",
                     help="skip the per-kernel HIP-event pass (a rocprofv3 trace then holds only the timed launches)")
+    ap.add_argument("--no-matcher", action="store_true", help="skip the per-call ORBmatcher / ComputeBoW leg")
     ap.add_argument("--only-extract", action="store_true", help="the extraction steps only (no other leg)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher plumbing only (tests/test_dist_cpu.py): ranks, rendezvous, reductions, the rank-0 "
@@ -391,6 +427,7 @@ def main():
         args.pipelines = CONFIGS[args.config].get("pipelines", 2)
     if args.only_extract:
         args.no_cpu = args.no_hamming = args.no_stereo = args.no_host_path = args.no_bird = args.no_c4 = True
+        args.no_matcher = True
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn(args.gpus, sys.argv[1:]))   # before anything touches the GPU
@@ -639,6 +676,13 @@ def main():
                      "note": "ORBextractor::operator() per host frame: upload + graph replay + one download, one "
                              "frame in flight, median of 200"}
 
+    # ---- the ORBmatcher drop-ins per call (SURVEY 8(a) rows a9-a13 at the reference's granularity: one call
+    # per frame / keyframe pair) and Frame::ComputeBoW, through the reference-signature adapter, against
+    # the oracle's single-thread CPU loops on the same inputs (tools/matcher_latency.cc; rank 0 at N = 1)
+    matcher = None
+    if rank == 0 and world == 1 and not args.no_matcher:
+        matcher = matcher_leg(frames[0], w, h, nf, local)
+
     # ---- birdview stream (BASELINE C4's bird stream): Frame.cc:320-342 fused on one
     # device-resident image + mask per call (orb_bird_extract_device); synchronous per frame (the host
     # selection, libstdc++ nth_element as the reference, sits mid-pipeline)
@@ -703,7 +747,7 @@ def main():
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": ({k: round(v, 4) for k, v in ms_per_step_k.items()} if ms_per_step_k else None),
                "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo,
-               "bird": bird, "c4_frame": c4, "host_path": host_path}
+               "bird": bird, "c4_frame": c4, "host_path": host_path, "matcher": matcher}
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
             if "host_estimate_value" in cpu:

@@ -263,6 +263,28 @@ int orb_window_match(orb_ctx* ctx, float nnratio, int check_ori, int level0_only
                      int n2, const uint8_t* desc2, const orb_keypoint* kps2,
                      const int* cand_off, const int* cand_idx, int* match12, int* nmatches);
 
+/* The Frame grid as the reference holds it (Frame.h:211 mGrid[FRAME_GRID_COLS][FRAME_GRID_ROWS], filled by
+ * Frame::AssignFeaturesToGrid, Frame.cc:378-413) flattened column-major: the keypoints of cell (ix, iy)
+ * are cell_idx[cell_off[ix * 48 + iy] .. cell_off[ix * 48 + iy + 1]) in the cell vector's order; the cell
+ * arithmetic of Frame::GetFeaturesInArea (:494-547) uses min_x / min_y and the inverse cell sizes.  The
+ * birdview grid (GetFeaturesInAreaBirdview, :891-945) is the same with min_x = min_y = 0. */
+typedef struct orb_frame_grid {
+    float min_x, min_y;          /* mnMinX, mnMinY */
+    float inv_w, inv_h;          /* mfGridElementWidthInv, mfGridElementHeightInv */
+    const int* cell_off;         /* 64 * 48 + 1 */
+    const int* cell_idx;         /* cell_off[64 * 48] entries */
+} orb_frame_grid;
+
+/* The window searches with the candidate lists computed on the GPU from F2's grid: the same matches
+ * as orb_window_match with cand = GetFeaturesInArea(centre, window, octave1, octave1) per query.
+ * centres: n1 (x, y) pairs (SearchForInitialization's vbPrevMatched, BirdviewMatch's vPrevMatched), or
+ * NULL = each query's own keypoint position (BirdviewMatch(const Frame&, const Frame&, ...), :1803-1808).
+ * level0_only: queries with octave > 0 are skipped (:420-423, :1683-1685).  match12 out. */
+int orb_window_match_grid(orb_ctx* ctx, float nnratio, int check_ori, int level0_only,
+                          int n1, const uint8_t* desc1, const orb_keypoint* kps1, const float* centres,
+                          float window, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
+                          orb_frame_grid grid2, int* match12, int* nmatches);
+
 /* Frame::GetFeaturesInArea over the 64x48 Frame grid (Frame.cc:378-412, 494-560): host helper the
  * C++ mirror uses to build window candidate lists. Returns count or -(needed)-1. */
 int orb_features_in_area(int n, const orb_keypoint* kps_un, float min_x, float max_x, float min_y, float max_y,

@@ -23,9 +23,9 @@
  * outputs (MapPoint* for the BoW searches).  The GPU computes the distances and candidate filtering;
  * the order-dependent acceptance (taken sets, vMatchedDistance stealing, ratio test, rotation
  * histogram + ComputeThreeMaxima) is replayed by liborbgpu in the reference's iteration order, so the
- * outputs are the reference's.  The candidate windows come from the reference's own
- * Frame::GetFeaturesInArea / GetFeaturesInAreaBirdview, and the epipole from the reference's own
- * expression (:664-670).  A GPU failure throws std::runtime_error (the reference has no error path;
+ * outputs are the reference's.  The window searches' candidate lists are Frame::GetFeaturesInArea /
+ * GetFeaturesInAreaBirdview evaluated on the GPU over the grid the Frame constructor built (mGrid /
+ * mGridBirdview, read here); the epipole is the reference's own expression (:664-670).  A GPU failure throws std::runtime_error (the reference has no error path;
  * there is no CPU fallback).
  *
  * Thread safety: the reference calls these from the Tracking, LocalMapping and LoopClosing threads at
@@ -217,25 +217,44 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
 
 namespace orbgpu_adapter {
 
-// The window searches (:405-520, :1667-1899): candidate list per query from the reference's own grid
-// lookup, in its order; `area(i1)` returns the query's candidates or an empty list for a skipped query.
-template <class Area>
-int window_match(float nnratio, bool checkOri, bool level0_only, const std::vector<cv::KeyPoint>& k1,
-                 const cv::Mat& d1, const std::vector<cv::KeyPoint>& k2, const cv::Mat& d2, Area area,
-                 std::vector<int>& vnMatches12) {
-    const int n1 = (int)k1.size(), n2 = (int)k2.size();
-    std::vector<int> off(n1 + 1, 0), idx;
-    for (int i1 = 0; i1 < n1; i1++) {
-        const std::vector<size_t> v = area(i1);
-        for (size_t j = 0; j < v.size(); j++) idx.push_back((int)v[j]);
-        off[i1 + 1] = (int)idx.size();
+// The window searches (:405-520, :1667-1899).  The candidate lists are GetFeaturesInArea(Birdview) over
+// F2's grid, computed on the GPU (orb_window_match_grid) from the grid the Frame constructor built
+// (mGrid / mGridBirdview, Frame.cc:378-413) and its cell geometry: the same lists, in the same order.
+struct GridCsr {
+    std::vector<int> off, idx;
+    orb_frame_grid g;
+    GridCsr(const std::vector<std::size_t> (&grid)[FRAME_GRID_COLS][FRAME_GRID_ROWS], float min_x, float min_y,
+            float inv_w, float inv_h) {
+        off.resize(FRAME_GRID_COLS * FRAME_GRID_ROWS + 1);
+        off[0] = 0;
+        for (int ix = 0; ix < FRAME_GRID_COLS; ix++)
+            for (int iy = 0; iy < FRAME_GRID_ROWS; iy++) {
+                const std::vector<std::size_t>& cell = grid[ix][iy];
+                for (size_t j = 0; j < cell.size(); j++) idx.push_back((int)cell[j]);
+                off[ix * FRAME_GRID_ROWS + iy + 1] = (int)idx.size();
+            }
+        if (idx.empty()) idx.push_back(0);
+        g.min_x = min_x;
+        g.min_y = min_y;
+        g.inv_w = inv_w;
+        g.inv_h = inv_h;
+        g.cell_off = off.data();
+        g.cell_idx = idx.data();
     }
-    if (idx.empty()) idx.push_back(0);
+};
+
+int window_match(float nnratio, bool checkOri, bool level0_only, const std::vector<cv::KeyPoint>& k1,
+                 const cv::Mat& d1, const std::vector<cv::KeyPoint>& k2, const cv::Mat& d2, const GridCsr& grid2,
+                 const std::vector<cv::Point2f>* centres, int windowSize, std::vector<int>& vnMatches12) {
+    static_assert(sizeof(cv::Point2f) == 8, "cv::Point2f must be two floats");
+    const int n1 = (int)k1.size(), n2 = (int)k2.size();
     std::vector<uint8_t> t1, t2;
     std::vector<int> out(n1 > 0 ? n1 : 1, -1);
     int nmatches = 0;
-    check(orb_window_match(ctx(), nnratio, checkOri, level0_only, n1, desc_rows(d1, n1, t1), keys_of(k1), n2,
-                           desc_rows(d2, n2, t2), keys_of(k2), off.data(), idx.data(), out.data(), &nmatches),
+    const float* cen = centres && !centres->empty() ? reinterpret_cast<const float*>(centres->data()) : nullptr;
+    check(orb_window_match_grid(ctx(), nnratio, checkOri, level0_only, n1, desc_rows(d1, n1, t1), keys_of(k1), cen,
+                                (float)windowSize, n2, desc_rows(d2, n2, t2), keys_of(k2), grid2.g, out.data(),
+                                &nmatches),
           "window match");
     vnMatches12.assign(out.begin(), out.begin() + n1);
     return nmatches;
@@ -245,14 +264,10 @@ int window_match(float nnratio, bool checkOri, bool level0_only, const std::vect
 
 int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
                                         std::vector<int>& vnMatches12, int windowSize) {
-    const int nm = window_match(
-        mfNNratio, mbCheckOrientation, true, F1.mvKeysUn, F1.mDescriptors, F2.mvKeysUn, F2.mDescriptors,
-        [&](int i1) {
-            const int level1 = F1.mvKeysUn[i1].octave;   // :421-423: level-0 queries only
-            if (level1 > 0) return std::vector<size_t>();
-            return F2.GetFeaturesInArea(vbPrevMatched[i1].x, vbPrevMatched[i1].y, windowSize, level1, level1);
-        },
-        vnMatches12);
+    // :416-437: level-0 queries, GetFeaturesInArea(vbPrevMatched[i1], windowSize, level1, level1)
+    const GridCsr g2(F2.mGrid, F2.mnMinX, F2.mnMinY, F2.mfGridElementWidthInv, F2.mfGridElementHeightInv);
+    const int nm = window_match(mfNNratio, mbCheckOrientation, true, F1.mvKeysUn, F1.mDescriptors, F2.mvKeysUn,
+                                F2.mDescriptors, g2, &vbPrevMatched, windowSize, vnMatches12);
     for (size_t i1 = 0, iend1 = vnMatches12.size(); i1 < iend1; i1++)   // :514-517
         if (vnMatches12[i1] >= 0) vbPrevMatched[i1] = F2.mvKeysUn[vnMatches12[i1]].pt;
     return nm;
@@ -260,27 +275,20 @@ int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Po
 
 int ORBmatcher::BirdviewMatch(Frame& F1, Frame& F2, std::vector<int>& vnMatches12, std::vector<cv::Point2f>& vPrevMatched,
                               int windowSize) {
-    const int nm = window_match(
-        mfNNratio, mbCheckOrientation, true, F1.mvKeysBird, F1.mDescriptorsBird, F2.mvKeysBird, F2.mDescriptorsBird,
-        [&](int i1) {
-            const int level1 = F1.mvKeysBird[i1].octave;   // :1683-1685
-            if (level1 > 0) return std::vector<size_t>();
-            return F2.GetFeaturesInAreaBirdview(vPrevMatched[i1].x, vPrevMatched[i1].y, windowSize, level1, level1);
-        },
-        vnMatches12);
+    // :1680-1700: level-0 queries around vPrevMatched[i1] in the birdview grid
+    const GridCsr g2(F2.mGridBirdview, 0.f, 0.f, F2.mfGridElementWidthInvBirdview, F2.mfGridElementHeightInvBirdview);
+    const int nm = window_match(mfNNratio, mbCheckOrientation, true, F1.mvKeysBird, F1.mDescriptorsBird, F2.mvKeysBird,
+                                F2.mDescriptorsBird, g2, &vPrevMatched, windowSize, vnMatches12);
     for (size_t i1 = 0, iend1 = vnMatches12.size(); i1 < iend1; i1++)   // :1778-1781
         if (vnMatches12[i1] >= 0) vPrevMatched[i1] = F2.mvKeysBird[vnMatches12[i1]].pt;
     return nm;
 }
 
 int ORBmatcher::BirdviewMatch(const Frame& F1, const Frame& F2, std::vector<int>& vnMatches12, int windowSize) {
-    return window_match(
-        mfNNratio, mbCheckOrientation, false, F1.mvKeysBird, F1.mDescriptorsBird, F2.mvKeysBird, F2.mDescriptorsBird,
-        [&](int i1) {
-            const cv::KeyPoint& kp1 = F1.mvKeysBird[i1];   // :1803-1808: every level, window around kp1
-            return F2.GetFeaturesInAreaBirdview(kp1.pt.x, kp1.pt.y, windowSize, kp1.octave, kp1.octave);
-        },
-        vnMatches12);
+    // :1801-1812: every query, window around its own keypoint, candidates at its octave
+    const GridCsr g2(F2.mGridBirdview, 0.f, 0.f, F2.mfGridElementWidthInvBirdview, F2.mfGridElementHeightInvBirdview);
+    return window_match(mfNNratio, mbCheckOrientation, false, F1.mvKeysBird, F1.mDescriptorsBird, F2.mvKeysBird,
+                        F2.mDescriptorsBird, g2, nullptr, windowSize, vnMatches12);
 }
 
 }  // namespace ORB_SLAM2

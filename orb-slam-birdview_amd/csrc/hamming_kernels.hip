@@ -97,6 +97,96 @@ __global__ __launch_bounds__(256) void k_topk(const uint8_t* __restrict__ q, int
     if (lane == 0 && out_nvalid) out_nvalid[qi] = nvalid;
 }
 
+// The window searches' candidate lists built on the device (SearchForInitialization :416-437,
+// BirdviewMatch :1680-1700 / :1801-1812): Frame::GetFeaturesInArea(cx, cy, r, lv, lv) with lv = the
+// query's octave (:494-547) over F2's grid in its CSR form.  The reference visits cells ix-major, iy
+// inner, a cell's keypoints in vector order: that is increasing CSR slot, so a candidate's slot is its
+// rank in vIndices2 and (dist, slot) breaks ties as the reference's first minimum does.  One wave per
+// item; the rectangle's column ranges are contiguous slot runs.
+__global__ __launch_bounds__(256) void k_window_topk(const uint8_t* __restrict__ q, const int* __restrict__ item_q,
+                                                     const float2* __restrict__ centre, int nitems,
+                                                     const orb_keypoint* __restrict__ kps1,
+                                                     const uint8_t* __restrict__ t,
+                                                     const orb_keypoint* __restrict__ kps2,
+                                                     const int* __restrict__ cell_off,
+                                                     const int* __restrict__ cell_idx, WinGrid wg,
+                                                     const int* __restrict__ thr, int k, int* __restrict__ out_dist,
+                                                     int* __restrict__ out_idx, int* __restrict__ out_nvalid) {
+    constexpr int COLS = 64, ROWS = 48;   // Frame.h:39-40
+    const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (qi >= nitems) return;
+    const int i1 = item_q[qi];
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)i1 * 32);
+    const uint4 qa = qp[0], qb = qp[1];
+    const int lv = kps1[i1].octave;
+    float x, y;
+    if (centre) {
+        const float2 cc = centre[i1];
+        x = cc.x;
+        y = cc.y;
+    } else {
+        x = kps1[i1].x;
+        y = kps1[i1].y;
+    }
+    const float r = wg.r;
+    // cell rectangle, the reference's float expressions (-ffp-contract=off: no fused forms)
+    const int nMinCellX = max(0, (int)floorf((x - wg.min_x - r) * wg.inv_w));
+    const int nMaxCellX = min(COLS - 1, (int)ceilf((x - wg.min_x + r) * wg.inv_w));
+    const int nMinCellY = max(0, (int)floorf((y - wg.min_y - r) * wg.inv_h));
+    const int nMaxCellY = min(ROWS - 1, (int)ceilf((y - wg.min_y + r) * wg.inv_h));
+    const bool empty = nMinCellX >= COLS || nMaxCellX < 0 || nMinCellY >= ROWS || nMaxCellY < 0;
+    unsigned long long lst[kMaxK];
+#pragma unroll
+    for (int j = 0; j < kMaxK; j++) lst[j] = ~0ull;
+    int nvalid = 0;
+    if (!empty) {
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+            const int s0 = cell_off[ix * ROWS + nMinCellY], s1 = cell_off[ix * ROWS + nMaxCellY + 1];
+            for (int s = s0 + lane; s < s1; s += 64) {
+                const int ti = cell_idx[s];
+                const orb_keypoint kp = kps2[ti];
+                if (kp.octave != lv) continue;                                        // :518-525 with min = max = lv
+                if (!(fabsf(kp.x - x) < r && fabsf(kp.y - y) < r)) continue;          // :530-533
+                const uint4* tp = reinterpret_cast<const uint4*>(t + (long long)ti * 32);
+                const int d = hamming256(qa, qb, tp[0], tp[1]);
+                if (thr && thr[ti] <= d) continue;
+                nvalid++;
+                unsigned long long key = ((unsigned long long)d << 32) | (unsigned)s;
+#pragma unroll
+                for (int j = 0; j < kMaxK; j++) {   // sorted insert (compare-swap chain)
+                    if (j < k && key < lst[j]) {
+                        const unsigned long long tmp = lst[j];
+                        lst[j] = key;
+                        key = tmp;
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nvalid += __shfl_xor(nvalid, o);
+    int head = 0;
+    for (int j = 0; j < k; j++) {
+        unsigned long long mine = ~0ull;
+#pragma unroll
+        for (int s = 0; s < kMaxK; s++)
+            if (s == head) mine = lst[s];
+        const unsigned long long m = wave_min_u64(mine);
+        if (mine == m && m != ~0ull) head++;
+        if (lane == 0) {
+            int dd = -1, ii = -1;
+            if (m != ~0ull) {
+                dd = (int)(m >> 32);
+                ii = cell_idx[(int)(m & 0xFFFFFFFFu)];
+            }
+            out_dist[(long long)qi * k + j] = dd;
+            out_idx[(long long)qi * k + j] = ii;
+        }
+    }
+    if (lane == 0 && out_nvalid) out_nvalid[qi] = nvalid;
+}
+
 /* Slices of one (query set, train set) pair's top-2 (k_top2_mfma with gridDim.y > 1) are merged here:
  * keys dist << 16 | train index compose by min (first index on ties) and second = the second-smallest
  * key.  Counts may be read on the device (an extraction batch's d_counts), so a whole batch of frame
@@ -416,6 +506,17 @@ hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, i
     if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_topk, dim3((nq + 3) / 4), dim3(256), 0, stream, d_q, nq, d_t, nt, d_ranges, d_cand_idx,
                        d_thr, k, d_dist, d_idx, d_nvalid);
+    return hipGetLastError();
+}
+
+hipError_t launch_window_topk(const uint8_t* d_q, const int* d_item_q, const float2* d_centre, int nitems,
+                              const orb_keypoint* d_kps1, const uint8_t* d_t, const orb_keypoint* d_kps2,
+                              const int* d_cell_off, const int* d_cell_idx, const WinGrid& wg, const int* d_thr,
+                              int k, int* d_dist, int* d_idx, int* d_nvalid, hipStream_t stream) {
+    if (nitems <= 0) return hipSuccess;
+    if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_window_topk, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_q, d_item_q, d_centre, nitems,
+                       d_kps1, d_t, d_kps2, d_cell_off, d_cell_idx, wg, d_thr, k, d_dist, d_idx, d_nvalid);
     return hipGetLastError();
 }
 

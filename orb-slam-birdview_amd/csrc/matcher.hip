@@ -20,29 +20,6 @@ constexpr int TH_LOW = 50;          // ORBmatcher.cc:38
 constexpr int HISTO_LENGTH = 30;    // :39
 constexpr int K = 8;
 
-struct Arena {
-    Ctx* c;
-    size_t off = 0;
-    static size_t align(size_t x) { return (x + 255) & ~(size_t)255; }
-    // reserve the total first, then take() pieces
-    hipError_t reserve(size_t bytes) {
-        if (bytes <= c->scratch_cap && c->d_scratch) return hipSuccess;
-        if (c->d_scratch) (void)hipFree(c->d_scratch);
-        c->d_scratch = nullptr;
-        c->scratch_cap = 0;
-        hipError_t e = hipMalloc((void**)&c->d_scratch, bytes);
-        if (e == hipSuccess) c->scratch_cap = bytes;
-        return e;
-    }
-    template <class T>
-    T* take(size_t n) {
-        off = align(off);
-        T* p = (T*)(c->d_scratch + off);
-        off += std::max<size_t>(n, 1) * sizeof(T);
-        return p;
-    }
-};
-
 int rot_bin(float a1, float a2) {   // ORBmatcher.cc:236-243 (round(rot*(1/30)): bins 0..12, upstream quirk)
     const float factor = 1.0f / HISTO_LENGTH;
     float rot = a1 - a2;
@@ -99,72 +76,119 @@ struct TopkSession {
     std::vector<int2> item_rng;      // [begin, end) into cand
     const int* cand = nullptr;       // host candidate list
     int ncand = 0;
-    // device
-    uint8_t* d_q = nullptr;
-    uint8_t* d_t = nullptr;
-    int2* d_rng = nullptr;
-    int* d_cand = nullptr;
-    int* d_thr = nullptr;
-    int* d_dist = nullptr;
-    int* d_idx = nullptr;
-    int* d_nvalid = nullptr;
-    // host results (indexed by item)
-    std::vector<int> dist, idx, nvalid;
+    Stage st{c};
+    // arena offsets: inputs [q | t | rng | cand | thr], outputs [dist | idx | nvalid]
+    size_t o_q = 0, o_t = 0, o_rng = 0, o_cand = 0, o_thr = 0, o_in_end = 0, o_dist = 0, o_idx = 0, o_nv = 0, o_end = 0;
+    bool uploaded = false;
+    // grid mode (orb_window_match_grid): the candidates come from F2's grid on the device
+    bool grid = false;
+    WinGrid wg{};
+    size_t o_item = 0, o_cen = 0, o_k1 = 0, o_k2 = 0, o_coff = 0, o_cidx = 0;
+    // host results (indexed by item), in the pinned mirror
+    const int* dist = nullptr;
+    const int* idx = nullptr;
+    const int* nvalid = nullptr;
 
     int setup(const uint8_t* qdesc, const uint8_t* tdesc, int ntrain) {
         nitems = (int)item_q.size();
         nt = ntrain;
-        Arena a{c};
-        const size_t need = Arena::align((size_t)nitems * 32) + Arena::align((size_t)nt * 32) +
-                            Arena::align((size_t)nitems * 8) + Arena::align((size_t)ncand * 4) +
-                            Arena::align((size_t)nt * 4) + 3 * Arena::align((size_t)nitems * K * 4) + 4096;
-        hipError_t e = a.reserve(need);
-        if (e != hipSuccess) return set_error("matcher scratch", e), ORB_ERR_NOMEM;
-        d_q = a.take<uint8_t>((size_t)nitems * 32);
-        d_t = a.take<uint8_t>((size_t)nt * 32);
-        d_rng = a.take<int2>(nitems);
-        d_cand = a.take<int>(ncand);
-        d_thr = a.take<int>(nt);
-        d_dist = a.take<int>((size_t)nitems * K);
-        d_idx = a.take<int>((size_t)nitems * K);
-        d_nvalid = a.take<int>(nitems);
-        std::vector<uint8_t> qg((size_t)nitems * 32);
-        for (int i = 0; i < nitems; i++) std::memcpy(&qg[(size_t)i * 32], qdesc + (size_t)item_q[i] * 32, 32);
-        if (nitems && (e = hipMemcpyAsync(d_q, qg.data(), qg.size(), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-            return set_error("upload queries", e), ORB_ERR_HIP;
-        if (nt && (e = hipMemcpyAsync(d_t, tdesc, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-            return set_error("upload trains", e), ORB_ERR_HIP;
-        if (nitems && (e = hipMemcpyAsync(d_rng, item_rng.data(), (size_t)nitems * sizeof(int2), hipMemcpyHostToDevice,
-                                          c->stream)) != hipSuccess)
-            return set_error("upload ranges", e), ORB_ERR_HIP;
-        if (ncand && (e = hipMemcpyAsync(d_cand, cand, (size_t)ncand * 4, hipMemcpyHostToDevice, c->stream)) !=
-                         hipSuccess)
-            return set_error("upload candidates", e), ORB_ERR_HIP;
-        dist.assign((size_t)nitems * K, -1);
-        idx.assign((size_t)nitems * K, -1);
-        nvalid.assign(nitems, 0);
+        if (nitems == 0) return ORB_OK;   // nothing to rank: no GPU work at all
+        st.c = c;
+        o_q = st.add((size_t)nitems * 32);
+        o_t = st.add((size_t)nt * 32);
+        o_rng = st.add((size_t)nitems * 8);
+        o_cand = st.add((size_t)ncand * 4);
+        o_thr = st.add((size_t)nt * 4);
+        o_in_end = st.off;
+        o_dist = st.add((size_t)nitems * K * 4);
+        o_idx = st.add((size_t)nitems * K * 4);
+        o_nv = st.add((size_t)nitems * 4);
+        o_end = st.off;
+        const int r = st.alloc();
+        if (r != ORB_OK) return r;
+        uint8_t* hq = st.h<uint8_t>(o_q);
+        for (int i = 0; i < nitems; i++) std::memcpy(hq + (size_t)i * 32, qdesc + (size_t)item_q[i] * 32, 32);
+        if (nt) std::memcpy(st.h<uint8_t>(o_t), tdesc, (size_t)nt * 32);
+        std::memcpy(st.h<int2>(o_rng), item_rng.data(), (size_t)nitems * 8);
+        if (ncand) std::memcpy(st.h<int>(o_cand), cand, (size_t)ncand * 4);
+        dist = st.h<int>(o_dist);
+        idx = st.h<int>(o_idx);
+        nvalid = st.h<int>(o_nv);
         return ORB_OK;
     }
 
-    // Re-rank items [from, nitems) with train thresholds thr (NULL = admit all).
+    // Grid mode: queries = desc1 rows item_q[i] (uploaded whole, indexed on the device), candidates from
+    // the window around centres[item_q[i]] (NULL: kps1) in F2's grid.
+    int setup_grid(const uint8_t* desc1, int n1, const orb_keypoint* kps1, const float* centres, const uint8_t* desc2,
+                   int n2, const orb_keypoint* kps2, const orb_frame_grid& g, float r) {
+        nitems = (int)item_q.size();
+        nt = n2;
+        if (nitems == 0) return ORB_OK;
+        grid = true;
+        wg = WinGrid{g.min_x, g.min_y, g.inv_w, g.inv_h, r};
+        const int ncells = 64 * 48, nslots = g.cell_off[ncells];
+        st.c = c;
+        o_q = st.add((size_t)n1 * 32);
+        o_item = st.add((size_t)nitems * 4);
+        o_cen = st.add(centres ? (size_t)n1 * 8 : 0);
+        o_k1 = st.add((size_t)n1 * sizeof(orb_keypoint));
+        o_t = st.add((size_t)n2 * 32);
+        o_k2 = st.add((size_t)n2 * sizeof(orb_keypoint));
+        o_coff = st.add((size_t)(ncells + 1) * 4);
+        o_cidx = st.add((size_t)nslots * 4);
+        o_thr = st.add((size_t)n2 * 4);
+        o_in_end = st.off;
+        o_dist = st.add((size_t)nitems * K * 4);
+        o_idx = st.add((size_t)nitems * K * 4);
+        o_nv = st.add((size_t)nitems * 4);
+        o_end = st.off;
+        const int rr = st.alloc();
+        if (rr != ORB_OK) return rr;
+        auto put = [&](size_t o, const void* src, size_t bytes) {
+            if (bytes) std::memcpy(c->h_mstage + o, src, bytes);
+        };
+        put(o_q, desc1, (size_t)n1 * 32);
+        put(o_item, item_q.data(), (size_t)nitems * 4);
+        if (centres) put(o_cen, centres, (size_t)n1 * 8);
+        put(o_k1, kps1, (size_t)n1 * sizeof(orb_keypoint));
+        put(o_t, desc2, (size_t)n2 * 32);
+        put(o_k2, kps2, (size_t)n2 * sizeof(orb_keypoint));
+        put(o_coff, g.cell_off, (size_t)(ncells + 1) * 4);
+        put(o_cidx, g.cell_idx, (size_t)nslots * 4);
+        cen = centres != nullptr;
+        dist = st.h<int>(o_dist);
+        idx = st.h<int>(o_idx);
+        nvalid = st.h<int>(o_nv);
+        return ORB_OK;
+    }
+    bool cen = false;
+
+    // Rank items [from, nitems) with train thresholds thr (NULL = admit all).
     int run(int from, const int* thr) {
         const int n = nitems - from;
         if (n <= 0) return ORB_OK;
         hipError_t e;
-        if (thr && (e = hipMemcpyAsync(d_thr, thr, (size_t)nt * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-            return set_error("upload thresholds", e), ORB_ERR_HIP;
+        if (thr) std::memcpy(st.h<int>(o_thr), thr, (size_t)nt * 4);
+        // first call: the whole input span in one DMA; a re-rank: the thresholds only
+        if ((e = uploaded ? (thr ? st.up(o_thr, o_thr + (size_t)nt * 4) : hipSuccess) : st.up(0, o_in_end)) != hipSuccess)
+            return set_error("upload", e), ORB_ERR_HIP;
+        uploaded = true;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-        e = launch_hamming_topk(d_q + (size_t)from * 32, n, d_t, nt, d_rng + from, d_cand, thr ? d_thr : nullptr, K,
-                                d_dist + (size_t)from * K, d_idx + (size_t)from * K, d_nvalid + from, c->stream);
+        if (grid)
+            e = launch_window_topk(st.d<uint8_t>(o_q), st.d<int>(o_item) + from, cen ? st.d<float2>(o_cen) : nullptr, n,
+                                   st.d<orb_keypoint>(o_k1), st.d<uint8_t>(o_t), st.d<orb_keypoint>(o_k2),
+                                   st.d<int>(o_coff), st.d<int>(o_cidx), wg, thr ? st.d<int>(o_thr) : nullptr, K,
+                                   st.d<int>(o_dist) + (size_t)from * K, st.d<int>(o_idx) + (size_t)from * K,
+                                   st.d<int>(o_nv) + from, c->stream);
+        else
+            e = launch_hamming_topk(st.d<uint8_t>(o_q) + (size_t)from * 32, n, st.d<uint8_t>(o_t), nt,
+                                    st.d<int2>(o_rng) + from, st.d<int>(o_cand), thr ? st.d<int>(o_thr) : nullptr, K,
+                                    st.d<int>(o_dist) + (size_t)from * K, st.d<int>(o_idx) + (size_t)from * K,
+                                    st.d<int>(o_nv) + from, c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("hamming kernel", e), ORB_ERR_HIP;
-        if ((e = hipMemcpyAsync(dist.data() + (size_t)from * K, d_dist + (size_t)from * K, (size_t)n * K * 4,
-                                hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(idx.data() + (size_t)from * K, d_idx + (size_t)from * K, (size_t)n * K * 4,
-                                hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(nvalid.data() + from, d_nvalid + from, (size_t)n * 4, hipMemcpyDeviceToHost,
-                                c->stream)) != hipSuccess ||
-            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        // the output span in one DMA (items before `from` come back unchanged)
+        if ((e = st.down(o_dist, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return set_error("download top-k", e), ORB_ERR_HIP;
         return ORB_OK;
     }
@@ -462,34 +486,29 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     const int ncand = fv2.nnodes ? fv2.offsets[fv2.nnodes] : 0;
     std::vector<int> best(nitems, -1);
     if (nitems) {
-        Arena a{c};
-        hipError_t e = a.reserve(Arena::align((size_t)n1 * 32) + Arena::align((size_t)n1 * sizeof(orb_keypoint)) +
-                                 Arena::align((size_t)n1 * 4) + Arena::align((size_t)n2 * 32) +
-                                 Arena::align((size_t)n2 * sizeof(orb_keypoint)) + Arena::align(n2) +
-                                 Arena::align((size_t)n2 * 4) + Arena::align((size_t)nitems * 4) +
-                                 Arena::align((size_t)nitems * 8) + Arena::align((size_t)ncand * 4) +
-                                 Arena::align((size_t)nitems * 4) + 4096);
-        if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
-        uint8_t* d_d1 = a.take<uint8_t>((size_t)n1 * 32);
-        orb_keypoint* d_k1 = a.take<orb_keypoint>(n1);
-        float* d_u1 = a.take<float>(n1);
-        uint8_t* d_d2 = a.take<uint8_t>((size_t)n2 * 32);
-        orb_keypoint* d_k2 = a.take<orb_keypoint>(n2);
-        uint8_t* d_m2 = a.take<uint8_t>(n2);
-        float* d_u2 = a.take<float>(n2);
-        int* d_q = a.take<int>(nitems);
-        int2* d_r = a.take<int2>(nitems);
-        int* d_c = a.take<int>(ncand);
-        int* d_b = a.take<int>(nitems);
-        auto up = [&](void* d, const void* hsrc, size_t bytes) {
-            return bytes ? hipMemcpyAsync(d, hsrc, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+        Stage st{c};
+        const size_t o_d1 = st.add((size_t)n1 * 32), o_k1 = st.add((size_t)n1 * sizeof(orb_keypoint)),
+                     o_u1 = st.add((size_t)n1 * 4), o_d2 = st.add((size_t)n2 * 32),
+                     o_k2 = st.add((size_t)n2 * sizeof(orb_keypoint)), o_m2 = st.add(n2), o_u2 = st.add((size_t)n2 * 4),
+                     o_q = st.add((size_t)nitems * 4), o_r = st.add((size_t)nitems * 8), o_c = st.add((size_t)ncand * 4);
+        const size_t o_in_end = st.off, o_b = st.add((size_t)nitems * 4), o_end = st.off;
+        int r = st.alloc();
+        if (r != ORB_OK) return r;
+        auto put = [&](size_t o, const void* src, size_t bytes) {
+            if (bytes) std::memcpy(c->h_mstage + o, src, bytes);
         };
-        if ((e = up(d_d1, desc1, (size_t)n1 * 32)) != hipSuccess || (e = up(d_k1, kps1, n1 * sizeof(orb_keypoint))) ||
-            (e = up(d_u1, uright1, (size_t)n1 * 4)) || (e = up(d_d2, desc2, (size_t)n2 * 32)) ||
-            (e = up(d_k2, kps2, n2 * sizeof(orb_keypoint))) || (e = up(d_m2, has_mp2, n2)) ||
-            (e = up(d_u2, uright2, (size_t)n2 * 4)) || (e = up(d_q, item_q.data(), (size_t)nitems * 4)) ||
-            (e = up(d_r, rng.data(), (size_t)nitems * 8)) || (e = up(d_c, fv2.indices, (size_t)ncand * 4)))
-            return set_error("upload", e), ORB_ERR_HIP;
+        put(o_d1, desc1, (size_t)n1 * 32);
+        put(o_k1, kps1, (size_t)n1 * sizeof(orb_keypoint));
+        put(o_u1, uright1, (size_t)n1 * 4);
+        put(o_d2, desc2, (size_t)n2 * 32);
+        put(o_k2, kps2, (size_t)n2 * sizeof(orb_keypoint));
+        put(o_m2, has_mp2, n2);
+        put(o_u2, uright2, (size_t)n2 * 4);
+        put(o_q, item_q.data(), (size_t)nitems * 4);
+        put(o_r, rng.data(), (size_t)nitems * 8);
+        put(o_c, fv2.indices, (size_t)ncand * 4);
+        hipError_t e = st.up(0, o_in_end);
+        if (e != hipSuccess) return set_error("upload", e), ORB_ERR_HIP;
         TriParams tp;
         std::memset(&tp, 0, sizeof tp);
         std::memcpy(tp.F, F12, sizeof tp.F);
@@ -501,13 +520,14 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         }
         tp.only_stereo = only_stereo;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-        e = launch_triangulation(d_d1, d_k1, d_u1, d_d2, d_k2, d_m2, d_u2, d_q, d_r, d_c, nitems, tp, d_b, c->stream);
+        e = launch_triangulation(st.d<uint8_t>(o_d1), st.d<orb_keypoint>(o_k1), st.d<float>(o_u1), st.d<uint8_t>(o_d2),
+                                 st.d<orb_keypoint>(o_k2), st.d<uint8_t>(o_m2), st.d<float>(o_u2), st.d<int>(o_q),
+                                 st.d<int2>(o_r), st.d<int>(o_c), nitems, tp, st.d<int>(o_b), c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
-        if ((e = hipMemcpyAsync(best.data(), d_b, (size_t)nitems * 4, hipMemcpyDeviceToHost, c->stream)) !=
-                hipSuccess ||
-            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        if ((e = st.down(o_b, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return set_error("download", e), ORB_ERR_HIP;
+        std::memcpy(best.data(), st.h<int>(o_b), (size_t)nitems * 4);
     }
     std::vector<int> vMatches12(n1, -1);
     std::vector<int> rotHist[HISTO_LENGTH];
@@ -542,24 +562,15 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     return ORB_OK;
 }
 
-/* SearchForInitialization (:405-520) / BirdviewMatch(const Frame&, const Frame&, ...) (:1790-1899) */
-int orb_window_match(orb_ctx* h, float nnratio, int check_ori, int level0_only, int n1, const uint8_t* desc1,
-                     const orb_keypoint* kps1, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
-                     const int* cand_off, const int* cand_idx, int* match12, int* nmatches_out) {
-    Ctx* c = reinterpret_cast<Ctx*>(h);
-    CTX_GUARD(c);
-    if (n1 < 0 || n2 < 0 || !match12 || !cand_off) return ORB_ERR_ARG;
-    TopkSession s{c};
-    s.cand = cand_idx;
-    s.ncand = cand_off[n1];
-    for (int i1 = 0; i1 < n1; i1++) {
-        if (level0_only && kps1[i1].octave > 0) continue;   // :420-423
-        if (cand_off[i1 + 1] == cand_off[i1]) continue;     // :427-428
-        s.item_q.push_back(i1);
-        s.item_rng.push_back(make_int2(cand_off[i1], cand_off[i1 + 1]));
-    }
-    int st = s.setup(desc1, desc2, n2);
-    if (st == ORB_OK) st = s.run(0, nullptr);
+}  // extern "C"
+
+namespace orbgpu {
+namespace {
+// The window searches' acceptance, replayed in the reference's query order (:440-498): first / second
+// admissible candidate, vMatchedDistance stealing, rotation histogram.
+int window_replay(TopkSession& s, float nnratio, int check_ori, int n1, const orb_keypoint* kps1, int n2,
+                  const orb_keypoint* kps2, int* match12, int* nmatches_out) {
+    int st = s.run(0, nullptr);
     if (st != ORB_OK) return st;
     std::vector<int> vnMatches12(n1, -1), vnMatches21(n2, -1), vMatchedDistance(n2, INT_MAX);
     std::vector<int> rotHist[HISTO_LENGTH];
@@ -588,6 +599,54 @@ int orb_window_match(orb_ctx* h, float nnratio, int check_ori, int level0_only, 
     std::memcpy(match12, vnMatches12.data(), (size_t)n1 * sizeof(int));
     if (nmatches_out) *nmatches_out = nmatches;
     return ORB_OK;
+}
+}  // namespace
+}  // namespace orbgpu
+
+extern "C" {
+
+/* SearchForInitialization (:405-520) / BirdviewMatch(const Frame&, const Frame&, ...) (:1790-1899) */
+int orb_window_match(orb_ctx* h, float nnratio, int check_ori, int level0_only, int n1, const uint8_t* desc1,
+                     const orb_keypoint* kps1, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
+                     const int* cand_off, const int* cand_idx, int* match12, int* nmatches_out) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || n2 < 0 || !match12 || !cand_off) return ORB_ERR_ARG;
+    TopkSession s{c};
+    s.cand = cand_idx;
+    s.ncand = cand_off[n1];
+    for (int i1 = 0; i1 < n1; i1++) {
+        if (level0_only && kps1[i1].octave > 0) continue;   // :420-423
+        if (cand_off[i1 + 1] == cand_off[i1]) continue;     // :427-428
+        s.item_q.push_back(i1);
+        s.item_rng.push_back(make_int2(cand_off[i1], cand_off[i1 + 1]));
+    }
+    const int st = s.setup(desc1, desc2, n2);
+    if (st != ORB_OK) return st;
+    return window_replay(s, nnratio, check_ori, n1, kps1, n2, kps2, match12, nmatches_out);
+}
+
+/* The same searches with GetFeaturesInArea computed on the device from F2's grid (orbgpu.h). */
+int orb_window_match_grid(orb_ctx* h, float nnratio, int check_ori, int level0_only, int n1, const uint8_t* desc1,
+                          const orb_keypoint* kps1, const float* centres, float window, int n2,
+                          const uint8_t* desc2, const orb_keypoint* kps2, orb_frame_grid grid2, int* match12,
+                          int* nmatches_out) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || n2 < 0 || !match12 || (n1 && (!desc1 || !kps1)) || (n2 && (!desc2 || !kps2)) ||
+        !grid2.cell_off || (grid2.cell_off[64 * 48] && !grid2.cell_idx))
+        return set_error("orb_window_match_grid: bad arguments", hipSuccess), ORB_ERR_ARG;
+    for (int i = 0, nslots = grid2.cell_off[64 * 48]; i < nslots; i++)   // the device indexes kps2 by these
+        if (grid2.cell_idx[i] < 0 || grid2.cell_idx[i] >= n2)
+            return set_error("orb_window_match_grid: grid index out of range", hipSuccess), ORB_ERR_ARG;
+    TopkSession s{c};
+    for (int i1 = 0; i1 < n1; i1++) {
+        if (level0_only && kps1[i1].octave > 0) continue;   // :420-423 (a query without candidates ranks nothing)
+        s.item_q.push_back(i1);
+    }
+    const int st = s.setup_grid(desc1, n1, kps1, centres, desc2, n2, kps2, grid2, window);
+    if (st != ORB_OK) return st;
+    return window_replay(s, nnratio, check_ori, n1, kps1, n2, kps2, match12, nmatches_out);
 }
 
 /* Frame::GetFeaturesInArea over the Frame grid (Frame.cc:378-392, 494-560) */

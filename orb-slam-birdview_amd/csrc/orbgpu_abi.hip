@@ -439,6 +439,7 @@ void orb_destroy(orb_ctx* h) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->h_mstage) (void)hipHostFree(c->h_mstage);
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     if (c->stream) (void)hipStreamDestroy(c->stream);

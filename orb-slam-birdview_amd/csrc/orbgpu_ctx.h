@@ -1,7 +1,9 @@
 // liborbgpu context (the object behind the opaque orb_ctx*).
 #pragma once
-#include <string>
+#include <algorithm>
 #include <array>
+#include <cstring>
+#include <string>
 #include <vector>
 
 #include "orbgpu_internal.h"
@@ -76,6 +78,10 @@ struct Ctx {
     // matcher scratch arena (bytes)
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;
+    // pinned mirror of the matcher arena: a call's inputs are packed here at the device offsets and go up
+    // in one DMA, its outputs come back in one (matcher.hip Stage)
+    uint8_t* h_mstage = nullptr;
+    size_t mstage_cap = 0;
     // the right extractor's frame + pyramid when it runs on another GPU (orb_compute_stereo_matches)
     uint8_t* d_peer = nullptr;
     size_t peer_cap = 0;
@@ -112,6 +118,73 @@ struct Ctx {
     int run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err = nullptr);
     static void marker(void* user, int id, int begin, hipStream_t s);
+};
+
+// The context's device scratch arena (Ctx::d_scratch): reserve the total first, then take() pieces.
+struct Arena {
+    Ctx* c;
+    size_t off = 0;
+    static size_t align(size_t x) { return (x + 255) & ~(size_t)255; }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= c->scratch_cap && c->d_scratch) return hipSuccess;
+        if (c->d_scratch) (void)hipFree(c->d_scratch);
+        c->d_scratch = nullptr;
+        c->scratch_cap = 0;
+        hipError_t e = hipMalloc((void**)&c->d_scratch, bytes);
+        if (e == hipSuccess) c->scratch_cap = bytes;
+        return e;
+    }
+    template <class T>
+    T* take(size_t n) {
+        off = align(off);
+        T* p = (T*)(c->d_scratch + off);
+        off += std::max<size_t>(n, 1) * sizeof(T);
+        return p;
+    }
+};
+
+// A host call's device arena and its pinned host mirror (Ctx::h_mstage): regions are laid out once
+// with add(), inputs are written into the mirror at the device offsets, one DMA takes the input span up
+// and one brings the output span back (per-call latency: a pageable copy per array cost ~10 us each).
+struct Stage {
+    Ctx* c;
+    size_t off = 0;
+    size_t add(size_t bytes) {
+        off = Arena::align(off);
+        const size_t o = off;
+        off += std::max<size_t>(bytes, 1);
+        return o;
+    }
+    int alloc() {
+        const size_t need = Arena::align(off) + 4096;
+        Arena a{c};
+        hipError_t e = a.reserve(need);
+        if (e != hipSuccess) return set_error("matcher scratch", e), ORB_ERR_NOMEM;
+        if (need > c->mstage_cap || !c->h_mstage) {
+            if (c->h_mstage) (void)hipHostFree(c->h_mstage);
+            c->h_mstage = nullptr;
+            c->mstage_cap = 0;
+            const size_t cap = std::max<size_t>(need, 1 << 20);
+            if ((e = hipHostMalloc((void**)&c->h_mstage, cap, hipHostMallocDefault)) != hipSuccess)
+                return set_error("matcher pinned staging", e), ORB_ERR_NOMEM;
+            c->mstage_cap = cap;
+        }
+        return ORB_OK;
+    }
+    template <class T>
+    T* h(size_t o) const { return reinterpret_cast<T*>(c->h_mstage + o); }
+    template <class T>
+    T* d(size_t o) const { return reinterpret_cast<T*>(c->d_scratch + o); }
+    hipError_t up(size_t from, size_t to) const {
+        return to > from ? hipMemcpyAsync(c->d_scratch + from, c->h_mstage + from, to - from, hipMemcpyHostToDevice,
+                                          c->stream)
+                         : hipSuccess;
+    }
+    hipError_t down(size_t from, size_t to) const {
+        return to > from ? hipMemcpyAsync(c->h_mstage + from, c->d_scratch + from, to - from, hipMemcpyDeviceToHost,
+                                          c->stream)
+                         : hipSuccess;
+    }
 };
 
 }  // namespace orbgpu

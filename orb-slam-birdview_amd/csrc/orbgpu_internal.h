@@ -152,6 +152,16 @@ int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: 
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
                                      int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream);
 
+// Window candidates from the Frame grid (orb_window_match_grid): per item the query feature, its
+// window centre and the grid geometry; ranks (dist, grid slot) like k_topk ranks (dist, list position).
+struct WinGrid {
+    float min_x, min_y, inv_w, inv_h, r;
+};
+hipError_t launch_window_topk(const uint8_t* d_q, const int* d_item_q, const float2* d_centre, int nitems,
+                              const orb_keypoint* d_kps1, const uint8_t* d_t, const orb_keypoint* d_kps2,
+                              const int* d_cell_off, const int* d_cell_idx, const WinGrid& wg, const int* d_thr,
+                              int k, int* d_dist, int* d_idx, int* d_nvalid, hipStream_t stream);
+
 struct TriParams {
     float F[9];
     float ex, ey;

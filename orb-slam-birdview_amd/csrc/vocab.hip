@@ -28,8 +28,6 @@ struct orb_vocab {
     uint8_t* d_cdesc = nullptr;   // per child slot: 32-byte descriptor
     int* d_word = nullptr;        // per node: word id (-1 for internal nodes)
     float* d_weight = nullptr;    // per node: weight (stored as float in the file)
-    int* d_scratch = nullptr;     // host-path staging
-    size_t scratch_cap = 0;
 };
 
 namespace orbgpu {
@@ -93,7 +91,7 @@ using namespace orbgpu;
 static void vocab_free(orb_vocab* v) {
     if (!v) return;
     (void)hipSetDevice(v->device);
-    void* bufs[] = {v->d_cbeg, v->d_ccnt, v->d_child, v->d_cdesc, v->d_word, v->d_weight, v->d_scratch};
+    void* bufs[] = {v->d_cbeg, v->d_ccnt, v->d_child, v->d_cdesc, v->d_word, v->d_weight};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     delete v;
@@ -210,31 +208,24 @@ int orb_vocab_transform(orb_ctx* h, const orb_vocab* v, const uint8_t* desc, int
     if (!v || v->device != c->device || n < 0 || (n && (!desc || !word_id || !weight || !node_id)))
         return set_error("orb_vocab_transform: bad arguments", hipSuccess), ORB_ERR_ARG;
     if (n == 0) return ORB_OK;
-    const size_t bytes = (size_t)n * (32 + 4 + 4 + 4) + 1024;
-    hipError_t e;
-    orb_vocab* mv = const_cast<orb_vocab*>(v);
-    if (bytes > mv->scratch_cap) {
-        if (mv->d_scratch) (void)hipFree(mv->d_scratch);
-        mv->d_scratch = nullptr;
-        mv->scratch_cap = 0;
-        if ((e = hipMalloc((void**)&mv->d_scratch, bytes)) != hipSuccess) return set_error("vocab scratch", e), ORB_ERR_NOMEM;
-        mv->scratch_cap = bytes;
-    }
-    uint8_t* d_desc = reinterpret_cast<uint8_t*>(mv->d_scratch);
-    int* d_w = reinterpret_cast<int*>(d_desc + (((size_t)n * 32 + 255) & ~(size_t)255));
-    float* d_wt = reinterpret_cast<float*>(d_w + n);
-    uint32_t* d_nd = reinterpret_cast<uint32_t*>(d_wt + n);
-    if ((e = hipMemcpyAsync(d_desc, desc, (size_t)n * 32, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-        return set_error("vocab upload", e), ORB_ERR_HIP;
+    // one DMA up (descriptors), one down ([word | weight | node]) through the context's pinned staging
+    Stage st{c};
+    const size_t o_desc = st.add((size_t)n * 32), o_w = st.add((size_t)n * 4), o_wt = st.add((size_t)n * 4),
+                 o_nd = st.add((size_t)n * 4), o_end = st.off;
+    const int r = st.alloc();
+    if (r != ORB_OK) return r;
+    std::memcpy(st.h<uint8_t>(o_desc), desc, (size_t)n * 32);
+    hipError_t e = st.up(o_desc, o_w);
+    if (e != hipSuccess) return set_error("vocab upload", e), ORB_ERR_HIP;
     hipLaunchKernelGGL(k_vocab_transform, dim3((n + 255) / 256, 1), dim3(256), 0, c->stream, v->d_cbeg, v->d_ccnt,
-                       v->d_child, v->d_cdesc, v->d_word, v->d_weight, d_desc, nullptr, n, 0, v->L - levelsup, d_w,
-                       d_wt, d_nd);
+                       v->d_child, v->d_cdesc, v->d_word, v->d_weight, st.d<uint8_t>(o_desc), nullptr, n, 0,
+                       v->L - levelsup, st.d<int>(o_w), st.d<float>(o_wt), st.d<uint32_t>(o_nd));
     if ((e = hipGetLastError()) != hipSuccess) return set_error("vocab kernel", e), ORB_ERR_HIP;
-    if ((e = hipMemcpyAsync(word_id, d_w, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(weight, d_wt, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(node_id, d_nd, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    if ((e = st.down(o_w, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return set_error("vocab download", e), ORB_ERR_HIP;
+    std::memcpy(word_id, st.h<int>(o_w), (size_t)n * 4);
+    std::memcpy(weight, st.h<float>(o_wt), (size_t)n * 4);
+    std::memcpy(node_id, st.h<uint32_t>(o_nd), (size_t)n * 4);
     return ORB_OK;
 }
 
@@ -261,53 +252,60 @@ int orb_vocab_bow(const orb_vocab* v, int n, const int* word_id, const float* we
     if (!v || n < 0 || !nbow || !nfv || !fv_off || (n && (!word_id || !weight || !node_id || !bow_words ||
                                                           !bow_values || !fv_nodes || !fv_idx)))
         return ORB_ERR_ARG;
-    // TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup) (:1139-1210)
-    std::map<int, double> bow;
-    std::map<uint32_t, std::vector<int>> fv;
+    // TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup) (:1139-1210).
+    // std::map order = ascending word / node id, and within a word / node the features in input order:
+    // sorting (id, feature) keys gives the same order and the same summation order as the map inserts.
     const bool tf = v->weighting == 0 || v->weighting == 1;   // TF_IDF, TF: addWeight; IDF, BINARY: addIfNotExist
     const bool must = v->scoring != 5;                        // DotProductScoring does not normalise
     const bool l1 = v->scoring != 1;                          // L2Scoring normalises with L2
+    int b = 0, j = 0, o = 0;
+    fv_off[0] = 0;
     if (v->nwords > 0) {   // if(empty()) return; (:1146-1149)
-        for (int i = 0; i < n; i++) {
-            const double w = (double)weight[i];
-            if (w > 0) {   // not stopped
-                if (tf)
-                    bow[word_id[i]] += w;
-                else if (!bow.count(word_id[i]))
-                    bow[word_id[i]] = w;
-                fv[node_id[i]].push_back(i);   // FeatureVector::addFeature (FeatureVector.cpp:31-45)
+        std::vector<unsigned long long> kw, kn;
+        kw.reserve(n);
+        kn.reserve(n);
+        for (int i = 0; i < n; i++)
+            if ((double)weight[i] > 0) {   // not stopped
+                kw.push_back(((unsigned long long)(uint32_t)word_id[i] << 32) | (uint32_t)i);
+                kn.push_back(((unsigned long long)node_id[i] << 32) | (uint32_t)i);
             }
+        std::sort(kw.begin(), kw.end());
+        std::sort(kn.begin(), kn.end());
+        for (size_t a = 0; a < kw.size();) {
+            const uint32_t w = (uint32_t)(kw[a] >> 32);
+            double acc = (double)weight[(uint32_t)kw[a]];
+            size_t e = a + 1;
+            for (; e < kw.size() && (uint32_t)(kw[e] >> 32) == w; e++)
+                if (tf) acc += (double)weight[(uint32_t)kw[e]];   // bow[word] += w, in feature order
+            bow_words[b] = (int)w;
+            bow_values[b] = acc;
+            b++;
+            a = e;
         }
-        if (tf && !bow.empty() && !must) {
-            const double nd = (double)bow.size();
-            for (auto& e : bow) e.second /= nd;
-        }
-        if (must) {   // BowVector::normalize (BowVector.cpp:61-86)
+        if (tf && b > 0 && !must)
+            for (int i = 0; i < b; i++) bow_values[i] /= (double)b;
+        if (must) {   // BowVector::normalize (BowVector.cpp:61-86), in map order
             double norm = 0.0;
             if (l1) {
-                for (auto& e : bow) norm += std::fabs(e.second);
+                for (int i = 0; i < b; i++) norm += std::fabs(bow_values[i]);
             } else {
-                for (auto& e : bow) norm += e.second * e.second;
+                for (int i = 0; i < b; i++) norm += bow_values[i] * bow_values[i];
                 norm = std::sqrt(norm);
             }
             if (norm > 0.0)
-                for (auto& e : bow) e.second /= norm;
+                for (int i = 0; i < b; i++) bow_values[i] /= norm;
         }
-    }
-    int b = 0;
-    for (auto& e : bow) {
-        bow_words[b] = e.first;
-        bow_values[b] = e.second;
-        b++;
+        for (size_t a = 0; a < kn.size(); a++) {   // FeatureVector::addFeature (FeatureVector.cpp:31-45)
+            const uint32_t nd = (uint32_t)(kn[a] >> 32);
+            if (a == 0 || (uint32_t)(kn[a - 1] >> 32) != nd) {
+                if (a) fv_off[++j] = o;
+                fv_nodes[j] = nd;
+            }
+            fv_idx[o++] = (int)(uint32_t)kn[a];
+        }
+        if (!kn.empty()) fv_off[++j] = o;
     }
     *nbow = b;
-    int j = 0, o = 0;
-    fv_off[0] = 0;
-    for (auto& e : fv) {
-        fv_nodes[j] = e.first;
-        for (int i : e.second) fv_idx[o++] = i;
-        fv_off[++j] = o;
-    }
     *nfv = j;
     return ORB_OK;
 }

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 
 from ._lib import (VARIANT_BLUR_HALFUP, VARIANT_DEFAULT, VARIANT_NO_FMA, VARIANT_RESIZE_GENERIC,
-                   VARIANT_TIE_REVERSE, OrbBirdParams, OrbError, OrbFeatVec, OrbParams, check, lib)
+                   VARIANT_TIE_REVERSE, OrbBirdParams, OrbError, OrbFeatVec, OrbFrameGrid, OrbParams, check, lib)
 
 __all__ = ["ORBextractor", "ORBmatcher", "BatchExtractor", "KP_DTYPE", "OrbError", "device_count",
            "features_in_area", "compute_stereo_matches", "ORBVocabulary", "BirdORB", "cornerSubPix",
@@ -271,6 +271,26 @@ def features_in_area(kps_un, min_x, max_x, min_y, max_y, x, y, r, min_level=-1, 
     return out[:n]
 
 
+def frame_grid(kps_un, min_x, max_x, min_y, max_y):
+    """Frame::AssignFeaturesToGrid (Frame.cc:378-393, PosInGrid :549-559) as the C-ABI's orb_frame_grid
+    CSR: cell (ix, iy) holds its keypoint indices in order at cell_idx[cell_off[ix*48+iy] ..].  Returns
+    (inv_w, inv_h, cell_off, cell_idx) with the float32 arithmetic of the reference."""
+    k = np.asarray(kps_un, KP_DTYPE)
+    f32 = np.float32
+    inv_w = f32(64) / (f32(max_x) - f32(min_x))
+    inv_h = f32(48) / (f32(max_y) - f32(min_y))
+    vx = ((k["x"].astype(f32) - f32(min_x)) * inv_w).astype(np.float64)
+    vy = ((k["y"].astype(f32) - f32(min_y)) * inv_h).astype(np.float64)
+    px = (np.sign(vx) * np.floor(np.abs(vx) + 0.5)).astype(np.int64)   # std::round: half away from zero
+    py = (np.sign(vy) * np.floor(np.abs(vy) + 0.5)).astype(np.int64)
+    ok = (px >= 0) & (px < 64) & (py >= 0) & (py < 48)
+    cell = np.where(ok, px * 48 + py, -1)
+    order = np.argsort(np.where(ok, cell, 1 << 30), kind="stable")[: int(ok.sum())]
+    off = np.zeros(64 * 48 + 1, np.int32)
+    np.add.at(off, cell[ok] + 1, 1)
+    return float(inv_w), float(inv_h), np.cumsum(off).astype(np.int32), order.astype(np.int32)
+
+
 class ORBmatcher:
     """ORB_SLAM2::ORBmatcher's descriptor matchers (ORBmatcher.cc) on the GPU."""
 
@@ -364,6 +384,21 @@ class ORBmatcher:
                                      len(a[0]), _p(a[0]), _p(a[1]), len(a[2]), _p(a[2]), _p(a[3]), _p(a[4]),
                                      _p(a[5]), _p(out), ctypes.byref(nm)), "window match")
         return nm.value, out
+
+    def window_match_grid(self, level0_only, desc1, kps1, desc2, kps2, grid, window, centres=None, min_xy=(0.0, 0.0)):
+        """orb_window_match_grid: the window searches with GetFeaturesInArea on the device over F2's grid
+        (frame_grid(...)); centres: (n1, 2) float32 window centres or None = kps1 positions."""
+        inv_w, inv_h, off, idx = grid
+        a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(kps1, KP_DTYPE), desc2, np.asarray(kps2, KP_DTYPE))]
+        cen = None if centres is None else np.ascontiguousarray(centres, np.float32).reshape(-1, 2)
+        idx = idx if len(idx) else np.zeros(1, np.int32)
+        g = OrbFrameGrid(float(min_xy[0]), float(min_xy[1]), inv_w, inv_h, off.ctypes.data, idx.ctypes.data)
+        out = np.full(max(len(a[0]), 1), -1, np.int32)
+        nm = ctypes.c_int()
+        check(lib().orb_window_match_grid(self._ctx.h, self.mfNNratio, int(self.mbCheckOrientation), int(level0_only),
+                                          len(a[0]), _p(a[0]), _p(a[1]), _p(cen), float(window), len(a[2]), _p(a[2]),
+                                          _p(a[3]), g, _p(out), ctypes.byref(nm)), "window match (grid)")
+        return nm.value, out[:len(a[0])]
 
     def SearchForInitialization(self, desc1, kps1, desc2, kps2, cand_off, cand_idx):
         """SearchForInitialization (ORBmatcher.cc:405-520); candidates = F2.GetFeaturesInArea per query.

@@ -36,6 +36,10 @@ class OrbFeatVec(ctypes.Structure):
     _fields_ = [("nnodes", ci), ("node_ids", vp), ("offsets", vp), ("indices", vp)]
 
 
+class OrbFrameGrid(ctypes.Structure):
+    _fields_ = [("min_x", cf), ("min_y", cf), ("inv_w", cf), ("inv_h", cf), ("cell_off", vp), ("cell_idx", vp)]
+
+
 # name -> (restype, argtypes); mirrors include/orbgpu.h
 SIGNATURES = {
     "orb_abi_version": (ci, []),
@@ -73,6 +77,8 @@ SIGNATURES = {
     "orb_search_for_triangulation": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, vp,
                                           OrbFeatVec, vp, cf, cf, vp, vp, ci, vp, ci, ctypes.POINTER(ci)]),
     "orb_window_match": (ci, [vp, cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, ctypes.POINTER(ci)]),
+    "orb_window_match_grid": (ci, [vp, cf, ci, ci, ci, vp, vp, vp, cf, ci, vp, vp, OrbFrameGrid, vp,
+                                   ctypes.POINTER(ci)]),
     "orb_features_in_area": (ci, [ci, vp, cf, cf, cf, cf, cf, cf, cf, ci, ci, vp, ci]),
     "orb_compute_stereo_matches": (ci, [vp, vp, ci, vp, vp, ci, vp, vp, cf, cf, vp, vp, ctypes.POINTER(ci)]),
     "orb_stereo_batch_device": (ci, [vp, ci, cf, cf, vp, vp, vp]),

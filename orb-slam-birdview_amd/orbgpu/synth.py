@@ -163,3 +163,35 @@ def write_synth_vocab(path, k=10, L=3, seed=0, scoring=0, weighting=0, stop_frac
                 w = 0.0 if rng.random() < stop_frac else float(rng.uniform(0.1, 3.0))
             f.write(struct.pack("<i", parent[i]) + desc[i].tobytes() + struct.pack("<f", w) + bytes([1 if leaf else 0]))
     return nb_nodes, nwords
+
+
+def write_synth_vocab_large(path, k=10, L=6, seed=0, stop_frac=0.05):
+    """write_synth_vocab's tree and file format, generated level by level with numpy: for the
+    ORBvoc.bin-sized k = 10, L = 6 tree (1,111,111 nodes, 10^6 words) the per-node loop would take
+    minutes.  Each child = its parent with every bit flipped with probability 1/4 (the AND of two
+    random bytes per byte); TF-IDF weighting, L1 scoring (ORBvoc.bin's own).  Returns (nb_nodes, nwords)."""
+    import struct
+    rng = np.random.default_rng(seed)
+    rec = np.dtype([("parent", "<i4"), ("desc", "u1", 32), ("weight", "<f4"), ("leaf", "u1")])
+    nb_nodes = 1 + sum(k ** lv for lv in range(1, L + 1))
+    nwords = k ** L
+    with open(path, "wb") as f:
+        f.write(struct.pack("<6i", nb_nodes, 4 + 32 + 4 + 1, k, L, 0, 0))
+        parent_desc = rng.integers(0, 256, (1, 32), dtype=np.uint8)   # root (not stored)
+        first_id = 0                                                   # id of the first node of the parent level
+        for lv in range(1, L + 1):
+            n = k ** lv
+            pd = np.repeat(parent_desc, k, axis=0)
+            flip = rng.integers(0, 256, (n, 32), dtype=np.uint8) & rng.integers(0, 256, (n, 32), dtype=np.uint8)
+            r = np.zeros(n, rec)
+            r["parent"] = first_id + np.arange(n) // k
+            r["desc"] = pd ^ flip
+            if lv == L:
+                w = rng.uniform(0.1, 3.0, n).astype(np.float32)
+                w[rng.random(n) < stop_frac] = 0.0
+                r["weight"] = w
+                r["leaf"] = 1
+            f.write(r.tobytes())
+            first_id = 1 + sum(k ** j for j in range(1, lv))   # ids of this level: children numbered breadth-first
+            parent_desc = r["desc"]
+    return nb_nodes, nwords

@@ -21,6 +21,7 @@
 #include <utility>
 #include <vector>
 
+#include "../../oracle/orb_oracle.h"
 #include "ORBmatcher.h"   // tests/cpp/slam_api (the reference's header, modelled)
 
 using namespace ORB_SLAM2;
@@ -171,6 +172,8 @@ int main(int argc, char** argv) {
         F1.mDescriptorsBird = A.desc;
         F1.birdW = (float)w;
         F1.birdH = (float)h;
+        F.AssignFeaturesToGrid();   // the Frame constructor's grid (Frame.cc:141)
+        F1.AssignFeaturesToGrid();
 
         // ---- SearchByBoW(KeyFrame*, Frame&): Tracking::TrackReferenceKeyFrame (ORBmatcher(0.7,true),
         // Tracking.cc:1029-1032) and Relocalization (0.75, :1918-1938)

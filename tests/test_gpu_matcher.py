@@ -216,6 +216,49 @@ def test_window_match(orbgpu_mod, oracle_mod, frames, level0_only, window):
         assert n > 20
 
 
+@pytest.mark.parametrize("level0_only,window,centred", [(True, 100, True), (True, 15, False), (False, 15, False),
+                                                         (False, 40, True)])
+def test_window_match_grid(orbgpu_mod, oracle_mod, frames, level0_only, window, centred):
+    """orb_window_match_grid (GetFeaturesInArea on the device over F2's grid) against the oracle with
+    candidates from the oracle's own GetFeaturesInArea restatement, around moved centres (vbPrevMatched)
+    or each query's own keypoint; the frame's grid bounds are not the image's (mnMinX > 0)."""
+    ka, da, kb, db = frames
+    bounds = (3.5, 636.0, 1.0, 470.5)
+    rng = np.random.default_rng(7)
+    cen = np.stack([ka["x"], ka["y"]], 1).astype(np.float32)
+    if centred:
+        cen = (cen + rng.uniform(-6, 6, cen.shape)).astype(np.float32)
+    offs, idxs = [0], []
+    for i, k in enumerate(ka):
+        if not (level0_only and k["octave"] > 0):
+            lv = int(k["octave"])
+            c = oracle_mod.features_in_area(kb, *bounds, float(cen[i, 0]), float(cen[i, 1]), float(window), lv, lv)
+            idxs.extend(c.tolist())
+        offs.append(len(idxs))
+    off = np.array(offs, np.int32)
+    cand = np.array(idxs or [0], np.int32)
+    grid = orbgpu_mod.frame_grid(kb, *bounds)
+    for ratio in (0.9, 0.99):
+        m = orbgpu_mod.ORBmatcher(ratio, True)
+        n, mm = m.window_match_grid(level0_only, da, ka, db, kb, grid, window, cen if centred else None,
+                                    (bounds[0], bounds[2]))
+        on, om = oracle_mod.window_match(ratio, True, level0_only, da, ka, db, kb, off, cand)
+        assert n == on and np.array_equal(mm, om)
+        assert n > 20
+
+
+def test_frame_grid_matches_oracle_lookup(orbgpu_mod, oracle_mod, frames):
+    """frame_grid's CSR is the reference grid: a lookup over it equals oracle_features_in_area."""
+    ka, da, kb, db = frames
+    inv_w, inv_h, off, idx = orbgpu_mod.frame_grid(kb, 0, 640, 0, 480)
+    assert off[-1] == len(kb) and sorted(idx.tolist()) == list(range(len(kb)))
+    for k in kb[::37]:
+        px = int(np.floor(float(np.float32(k["x"]) * np.float32(inv_w)) + 0.5))
+        py = int(np.floor(float(np.float32(k["y"]) * np.float32(inv_h)) + 0.5))
+        cell = idx[off[px * 48 + py]:off[px * 48 + py + 1]]
+        assert np.all(np.diff(cell) > 0)
+
+
 @pytest.mark.parametrize("nt", [0, 1, 40, 700])
 def test_top2_device_small_train_sets(orbgpu_mod, nt):
     """Edge sizes of the batched kernel: one train, a single slice, and a query count that is not a

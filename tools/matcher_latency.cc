@@ -1,0 +1,336 @@
+// Per-call latency of the ORBmatcher drop-ins at the reference's call granularity (bench.py `matcher`
+// leg): one call per frame / keyframe pair, as Tracking / LocalMapping / LoopClosing make them.
+//
+//   SearchByBoW(KeyFrame*, Frame&)       ORBmatcher(0.7, true)   Tracking::TrackReferenceKeyFrame, Tracking.cc:1029-1032
+//   SearchByBoW(KeyFrame*, KeyFrame*)    ORBmatcher(0.75, true)  LoopClosing::ComputeSim3, LoopClosing.cc:265
+//   SearchForTriangulation               ORBmatcher(0.6, false)  LocalMapping::CreateNewMapPoints, LocalMapping.cc:225,278
+//   SearchForInitialization (window 100) ORBmatcher(0.9, true)   Tracking::MonocularInitialization, Tracking.cc:738-739
+//   Frame::ComputeBoW (transform, levelsup 4)                    Frame.cc:562-569
+//
+// GPU side: the reference-signature adapter (adapter/ORBmatcher_gpu.cc) on Frame / KeyFrame objects
+// (tests/cpp/slam_api models; their grid lookups are the caller's CPU code, Frame.cc:378-547), and the
+// host-mirror ORBVocabulary.  Features: the GPU ORBextractor on two C3 frames (the second a shifted
+// copy of the first), FeatureVectors from the GPU vocabulary transform of a synthetic k = 10, L = 6
+// vocabulary in ORBvoc.bin's format.  CPU side (the baseline, single thread): the oracle's restatement
+// of each reference body (oracle/orb_oracle.cpp) on the same inputs -- for SearchForInitialization
+// including the per-keypoint GetFeaturesInArea queries on the frame's grid, as the reference loop
+// makes them.  Every GPU output is checked equal to the oracle's before anything is timed.
+//
+// usage: matcher_latency <frames.raw> <w> <h> <nfeatures> <vocab.bin> <reps> [cpu_reps]
+// Prints one JSON line.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../oracle/orb_oracle.h"
+#include "../orb-slam-birdview_amd/host/ORBVocabulary.h"
+#include "../orb-slam-birdview_amd/host/ORBextractor.h"
+#include "ORBmatcher.h"   // tests/cpp/slam_api: the reference's declaration, modelled
+
+using namespace ORB_SLAM2;
+
+template <class F>
+static double median_us(F f, int reps) {
+    f();   // warm: context creation, scratch growth
+    std::vector<double> t;
+    for (int i = 0; i < reps; i++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        f();
+        t.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+struct Feat {
+    std::vector<cv::KeyPoint> kps;
+    cv::Mat desc;
+    DBoW2::FeatureVector fv;
+};
+
+struct OFv {   // oracle CSR of a FeatureVector
+    std::vector<uint32_t> ids;
+    std::vector<int> off, idx;
+    OracleFeatVec fv;
+    explicit OFv(const DBoW2::FeatureVector& f) {
+        off.push_back(0);
+        for (auto it = f.begin(); it != f.end(); ++it) {
+            ids.push_back(it->first);
+            for (unsigned v : it->second) idx.push_back((int)v);
+            off.push_back((int)idx.size());
+        }
+        if (idx.empty()) idx.push_back(0);
+        fv.nnodes = (int)ids.size();
+        fv.node_ids = ids.data();
+        fv.offsets = off.data();
+        fv.indices = idx.data();
+    }
+};
+
+static uint32_t lcg(uint32_t& s) { return s = s * 1664525u + 1013904223u; }
+
+static std::vector<float> angles(const std::vector<cv::KeyPoint>& k) {
+    std::vector<float> a(k.size() + 1, 0.f);
+    for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
+    return a;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 7) {
+        fprintf(stderr, "usage: %s frames.raw w h nfeatures vocab.bin reps [cpu_reps]\n", argv[0]);
+        return 2;
+    }
+    const int w = atoi(argv[2]), h = atoi(argv[3]), nfeat = atoi(argv[4]), reps = atoi(argv[6]);
+    const int cpu_reps = argc > 7 ? atoi(argv[7]) : std::max(3, reps / 5);
+    std::vector<uint8_t> frames((size_t)w * h * 2);
+    FILE* fp = fopen(argv[1], "rb");
+    if (!fp || fread(frames.data(), 1, frames.size(), fp) != frames.size()) {
+        fprintf(stderr, "cannot read %s\n", argv[1]);
+        return 2;
+    }
+    fclose(fp);
+
+    // ---- features: GPU extractor + GPU vocabulary (the product)
+    ORBextractor ex(nfeat, 1.2f, 8, 20, 7, 0);
+    ORBVocabulary voc(0);
+    if (!voc.loadFromBinaryFile(argv[5])) {
+        fprintf(stderr, "cannot load %s\n", argv[5]);
+        return 2;
+    }
+    Feat fe[2];
+    std::vector<ORB_SLAM2::KeyPoint> hk;
+    DescriptorMat hd;
+    DescriptorMat descs[2];
+    for (int f = 0; f < 2; f++) {
+        ex(ImageView(frames.data() + (size_t)f * w * h, w, h), ImageView(), hk, hd);
+        fe[f].kps.resize(hk.size());
+        memcpy((void*)fe[f].kps.data(), hk.data(), hk.size() * sizeof(orb_keypoint));
+        fe[f].desc = cv::Mat((int)hk.size(), 32, CV_8U);
+        memcpy(fe[f].desc.data, hd.buf.data(), hk.size() * 32);
+        descs[f] = hd;
+        BowVector bv;
+        BowFeatureVector bfv;
+        voc.transform(hd, bv, bfv, 4);
+        for (auto& kv : bfv) fe[f].fv[kv.first] = kv.second;
+    }
+    const int nA = (int)fe[0].kps.size(), nB = (int)fe[1].kps.size();
+    std::vector<float> scale(8), sigma2(8);
+    {
+        std::vector<float> s = ex.GetScaleFactors(), s2 = ex.GetScaleSigmaSquares();
+        for (int l = 0; l < 8; l++) scale[l] = s[l], sigma2[l] = s2[l];
+    }
+
+    // ---- the SLAM objects (as make_kf in tests/cpp/test_matcher_adapter.cc)
+    std::vector<MapPoint*> pool;
+    KeyFrame KF[2];
+    const float I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const float tw[2][3] = {{0, 0, 0}, {-0.35f, 0.f, 0.02f}};
+    for (int f = 0; f < 2; f++) {
+        KeyFrame& kf = KF[f];
+        kf.N = (int)fe[f].kps.size();
+        kf.mvKeysUn = fe[f].kps;
+        kf.mDescriptors = fe[f].desc;
+        kf.mFeatVec = fe[f].fv;
+        kf.mvScaleFactors = scale;
+        kf.mvLevelSigma2 = sigma2;
+        kf.fx = kf.fy = 700.f;
+        kf.cx = w * 0.5f;
+        kf.cy = h * 0.5f;
+        kf.SetPose(I, tw[f]);
+        kf.mvpMapPoints.assign(kf.N, nullptr);
+        kf.mvuRight.assign(kf.N, -1.f);
+        uint32_t s = 11u + 18u * f;
+        for (int i = 0; i < kf.N; i++) {
+            if (lcg(s) % 10 < 7) {
+                pool.push_back(new MapPoint(lcg(s) % 10 == 0));
+                kf.mvpMapPoints[i] = pool.back();
+            }
+            if (lcg(s) % 10 < 3) kf.mvuRight[i] = fe[f].kps[i].pt.x - 5.f;
+        }
+    }
+    Frame F[2];
+    for (int f = 0; f < 2; f++) {
+        F[f].N = (int)fe[f].kps.size();
+        F[f].mvKeys = F[f].mvKeysUn = fe[f].kps;
+        F[f].mDescriptors = fe[f].desc;
+        F[f].mFeatVec = fe[f].fv;
+        F[f].mnMinX = 0;
+        F[f].mnMaxX = (float)w;
+        F[f].mnMinY = 0;
+        F[f].mnMaxY = (float)h;
+        F[f].AssignFeaturesToGrid();   // Frame constructor (Frame.cc:141)
+    }
+    const std::vector<float> aA = angles(fe[0].kps), aB = angles(fe[1].kps);
+    const OFv fvA(fe[0].fv), fvB(fe[1].fv);
+    std::vector<uint8_t> mpA(nA + 1, 0), mpB(nB + 1, 0);
+    for (int i = 0; i < nA; i++) mpA[i] = KF[0].mvpMapPoints[i] && !KF[0].mvpMapPoints[i]->isBad();
+    for (int i = 0; i < nB; i++) mpB[i] = KF[1].mvpMapPoints[i] && !KF[1].mvpMapPoints[i]->isBad();
+    const OracleKeyPoint* okA = reinterpret_cast<const OracleKeyPoint*>(fe[0].kps.data());
+    const OracleKeyPoint* okB = reinterpret_cast<const OracleKeyPoint*>(fe[1].kps.data());
+
+    std::string out = "{";
+    bool all_ok = true;
+    char buf[512];
+    auto emit = [&](const char* name, double gpu, double cpu, int nm, int onm, bool ok) {
+        all_ok = all_ok && ok;
+        snprintf(buf, sizeof buf, "%s\"%s\": {\"gpu_us\": %.1f, \"cpu_us\": %.1f, \"speedup\": %.2f, \"matches\": %d, "
+                 "\"oracle_matches\": %d, \"equal\": %s}", out.size() > 1 ? ", " : "", name, gpu, cpu, cpu / gpu, nm, onm,
+                 ok ? "true" : "false");
+        out += buf;
+    };
+
+    // ---- SearchByBoW(KF, F)
+    {
+        ORBmatcher m(0.7f, true);
+        std::vector<MapPoint*> v;
+        const int nm = m.SearchByBoW(&KF[0], F[1], v);
+        std::vector<int> om(nB + 1, -1);
+        const int onm = oracle_search_by_bow_kf_f(0.7f, 1, nA, fe[0].desc.data, aA.data(), mpA.data(), fvA.fv, nB,
+                                                  fe[1].desc.data, aB.data(), fvB.fv, om.data());
+        bool ok = nm == onm && (int)v.size() == nB;
+        for (int i = 0; ok && i < nB; i++) ok = v[i] == (om[i] >= 0 ? KF[0].mvpMapPoints[om[i]] : nullptr);
+        const double g = median_us([&] { m.SearchByBoW(&KF[0], F[1], v); }, reps);
+        const double c = median_us([&] {
+            oracle_search_by_bow_kf_f(0.7f, 1, nA, fe[0].desc.data, aA.data(), mpA.data(), fvA.fv, nB, fe[1].desc.data,
+                                      aB.data(), fvB.fv, om.data());
+        }, cpu_reps);
+        emit("SearchByBoW_KF_F", g, c, nm, onm, ok);
+    }
+    // ---- SearchByBoW(KF, KF)
+    {
+        ORBmatcher m(0.75f, true);
+        std::vector<MapPoint*> v;
+        const int nm = m.SearchByBoW(&KF[0], &KF[1], v);
+        std::vector<int> om(nA + 1, -1);
+        const int onm = oracle_search_by_bow_kf_kf(0.75f, 1, nA, fe[0].desc.data, aA.data(), mpA.data(), fvA.fv, nB,
+                                                   fe[1].desc.data, aB.data(), mpB.data(), fvB.fv, om.data());
+        bool ok = nm == onm && (int)v.size() == nA;
+        for (int i = 0; ok && i < nA; i++) ok = v[i] == (om[i] >= 0 ? KF[1].mvpMapPoints[om[i]] : nullptr);
+        const double g = median_us([&] { m.SearchByBoW(&KF[0], &KF[1], v); }, reps);
+        const double c = median_us([&] {
+            oracle_search_by_bow_kf_kf(0.75f, 1, nA, fe[0].desc.data, aA.data(), mpA.data(), fvA.fv, nB,
+                                       fe[1].desc.data, aB.data(), mpB.data(), fvB.fv, om.data());
+        }, cpu_reps);
+        emit("SearchByBoW_KF_KF", g, c, nm, onm, ok);
+    }
+    // ---- SearchForTriangulation (R = I, F12 = K^-T [t12]x K^-1, LocalMapping::ComputeF12's form)
+    {
+        const double t12[3] = {tw[0][0] - tw[1][0], tw[0][1] - tw[1][1], tw[0][2] - tw[1][2]};
+        const double fx = 700, cx = w * 0.5, cy = h * 0.5;
+        const double Kinv[3][3] = {{1 / fx, 0, -cx / fx}, {0, 1 / fx, -cy / fx}, {0, 0, 1}};
+        const double tx[3][3] = {{0, -t12[2], t12[1]}, {t12[2], 0, -t12[0]}, {-t12[1], t12[0], 0}};
+        double M[3][3], Fd[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                M[i][j] = 0;
+                for (int k = 0; k < 3; k++) M[i][j] += tx[i][k] * Kinv[k][j];
+            }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                Fd[i][j] = 0;
+                for (int k = 0; k < 3; k++) Fd[i][j] += Kinv[k][i] * M[k][j];
+            }
+        cv::Mat F12(3, 3, CV_32F);
+        float Fv[9];
+        for (int i = 0; i < 9; i++) Fv[i] = F12.at<float>(i / 3, i % 3) = (float)Fd[i / 3][i % 3];
+        ORBmatcher m(0.6f, false);
+        std::vector<std::pair<size_t, size_t> > v;
+        const int nm = m.SearchForTriangulation(&KF[0], &KF[1], F12, v, false);
+        cv::Mat Cw = KF[0].GetCameraCenter(), R2w = KF[1].GetRotation(), t2w = KF[1].GetTranslation();
+        cv::Mat C2 = R2w * Cw + t2w;
+        const float invz = 1.0f / C2.at<float>(2);
+        const float ex_ = KF[1].fx * C2.at<float>(0) * invz + KF[1].cx, ey_ = KF[1].fy * C2.at<float>(1) * invz + KF[1].cy;
+        std::vector<uint8_t> h1(nA + 1, 0), h2(nB + 1, 0);
+        for (int i = 0; i < nA; i++) h1[i] = KF[0].mvpMapPoints[i] != nullptr;
+        for (int i = 0; i < nB; i++) h2[i] = KF[1].mvpMapPoints[i] != nullptr;
+        std::vector<int> pairs(2 * (nA + 1));
+        const int onp = oracle_search_for_triangulation(0, 0, nA, fe[0].desc.data, okA, h1.data(), KF[0].mvuRight.data(),
+                                                        fvA.fv, nB, fe[1].desc.data, okB, h2.data(), KF[1].mvuRight.data(),
+                                                        fvB.fv, Fv, ex_, ey_, scale.data(), sigma2.data(), pairs.data(),
+                                                        nA + 1);
+        bool ok = nm == onp && (int)v.size() == onp;
+        for (int i = 0; ok && i < onp; i++)
+            ok = v[i].first == (size_t)pairs[2 * i] && v[i].second == (size_t)pairs[2 * i + 1];
+        const double g = median_us([&] { m.SearchForTriangulation(&KF[0], &KF[1], F12, v, false); }, reps);
+        const double c = median_us([&] {
+            oracle_search_for_triangulation(0, 0, nA, fe[0].desc.data, okA, h1.data(), KF[0].mvuRight.data(), fvA.fv, nB,
+                                            fe[1].desc.data, okB, h2.data(), KF[1].mvuRight.data(), fvB.fv, Fv, ex_, ey_,
+                                            scale.data(), sigma2.data(), pairs.data(), nA + 1);
+        }, cpu_reps);
+        emit("SearchForTriangulation", g, c, nm, onp, ok);
+    }
+    // ---- SearchForInitialization (window 100; vbPrevMatched = the first frame's keypoints)
+    {
+        ORBmatcher m(0.9f, true);
+        std::vector<cv::Point2f> prev0(nA);
+        for (int i = 0; i < nA; i++) prev0[i] = fe[0].kps[i].pt;
+        std::vector<cv::Point2f> prev = prev0;
+        std::vector<int> v;
+        const int nm = m.SearchForInitialization(F[0], F[1], prev, v, 100);
+        // the CPU loop: the reference's per-keypoint grid query (level 0 only, :421-426) + the restated body
+        std::vector<int> off(nA + 1, 0), cand, om(nA + 1, -1);
+        auto cpu = [&]() {
+            cand.clear();
+            for (int i = 0; i < nA; i++) {
+                if (fe[0].kps[i].octave == 0) {
+                    const std::vector<size_t> c = F[1].GetFeaturesInArea(prev0[i].x, prev0[i].y, 100.f, 0, 0);
+                    for (size_t j : c) cand.push_back((int)j);
+                }
+                off[i + 1] = (int)cand.size();
+            }
+            if (cand.empty()) cand.push_back(0);
+            return oracle_window_match(0.9f, 1, 1, nA, fe[0].desc.data, okA, nB, fe[1].desc.data, okB, off.data(),
+                                       cand.data(), om.data());
+        };
+        const int onm = cpu();
+        bool ok = nm == onm && (int)v.size() == nA;
+        for (int i = 0; ok && i < nA; i++) ok = v[i] == om[i];
+        const double g = median_us([&] {
+            std::vector<cv::Point2f> p = prev0;
+            m.SearchForInitialization(F[0], F[1], p, v, 100);
+        }, reps);
+        const double c = median_us([&] { cpu(); }, cpu_reps);
+        emit("SearchForInitialization", g, c, nm, onm, ok);
+    }
+    // ---- Frame::ComputeBoW: vocabulary transform of one frame's descriptors, levelsup 4
+    {
+        void* ov = oracle_vocab_load(argv[5]);
+        int k = 0, L = 0, sc = 0, wt = 0, nn = 0, nw = 0;
+        oracle_vocab_info(ov, &k, &L, &sc, &wt, &nn, &nw);
+        std::vector<int> bw(nB + 1), fo(nB + 2), fi(nB + 1);
+        std::vector<uint32_t> fn(nB + 1);
+        std::vector<double> bv(nB + 1);
+        int nb = 0, nf = 0;
+        BowVector gbv;
+        BowFeatureVector gfv;
+        voc.transform(descs[1], gbv, gfv, 4);
+        oracle_vocab_transform(ov, fe[1].desc.data, nB, 4, bw.data(), bv.data(), &nb, fn.data(), fo.data(),
+                               fi.data(), &nf);
+        bool ok = (int)gbv.size() == nb && (int)gfv.size() == nf;
+        int j = 0;
+        for (auto it = gfv.begin(); ok && it != gfv.end(); ++it, ++j)
+            ok = it->first == fn[j] && (int)it->second.size() == fo[j + 1] - fo[j];
+        const double g = median_us([&] { voc.transform(descs[1], gbv, gfv, 4); }, reps);
+        const double c = median_us([&] {
+            oracle_vocab_transform(ov, fe[1].desc.data, nB, 4, bw.data(), bv.data(), &nb, fn.data(),
+                                   fo.data(), fi.data(), &nf);
+        }, cpu_reps);
+        oracle_vocab_destroy(ov);
+        emit("ComputeBoW", g, c, (int)gfv.size(), nf, ok);
+        snprintf(buf, sizeof buf, ", \"vocabulary\": {\"k\": %d, \"L\": %d, \"nodes\": %d, \"words\": %d, \"levelsup\": 4, "
+                 "\"featvec_nodes\": [%d, %d]}", k, L, nn, nw, (int)fe[0].fv.size(), (int)fe[1].fv.size());
+        out += buf;
+    }
+    snprintf(buf, sizeof buf, ", \"keypoints\": [%d, %d], \"gpu_reps\": %d, \"cpu_reps\": %d, \"all_equal\": %s}", nA, nB,
+             reps, cpu_reps, all_ok ? "true" : "false");
+    out += buf;
+    printf("%s\n", out.c_str());
+    for (MapPoint* p : pool) delete p;
+    return all_ok ? 0 : 1;
+}
