@@ -12,6 +12,7 @@
 #include "pattern31_data.inc"
 
 #include <algorithm>
+#include <cstring>
 
 namespace orbgpu {
 
@@ -299,6 +300,158 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
             packed |= v << (8 * i);
         }
         __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
+    }
+}
+
+/* Few-launch pyramid for small batches (the host path's single frame, C5's per-GPU frame): the levels
+ * in segments of up to kChainSeg, ONE launch per segment instead of one per level.  A workgroup owns
+ * an output tile of one level and recomputes, in LDS, the chain of regions it depends on from the
+ * segment's base level up (ChainJob; the same fixed-point arithmetic as k_resize_tiled, so every value
+ * is the per-level launch's), writing only its own tile.  The recomputation is redundant work, but a
+ * single frame leaves most of the chip idle, and each dependent launch costs ~5 us of latency. */
+template <bool GENERIC>
+__global__ __launch_bounds__(256) void k_pyramid_chain(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef,
+                                                       const ChainJob* __restrict__ jobs, ChainSegment sg,
+                                                       RcoefOff roff, const uint8_t* __restrict__ frames,
+                                                       long long framePitch, int rowStride, uint8_t* __restrict__ pyr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    __shared__ int4 sreg[ORBGPU_MAX_LEVELS];
+    const int f = blockIdx.y;
+    const int tid = threadIdx.x;
+    const ChainJob* J = jobs + sg.job0 + blockIdx.x;
+    const int l = J->level, b = J->base;
+    if (tid <= l) sreg[tid] = J->reg[tid];
+    uint8_t* buf0 = sm;
+    uint8_t* buf1 = sm + sg.buf_bytes;
+    int4* sc = reinterpret_cast<int4*>(sm + 2 * sg.buf_bytes);
+    uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
+    __syncthreads();
+    // coefficients of every stage, relative to its source region in LDS: columns (o0, o1, c0, c1), rows
+    // (byte offsets of the two source rows, vertical weights as rs_row_entry) -- all loads in flight at once
+    {
+        int e0 = 0;
+        for (int k = b + 1; k <= l; k++) {
+            const int4 R = sreg[k], S = sreg[k - 1];
+            const int nx = R.y - R.x, ny = R.w - R.z;
+            const int sp = (S.y - S.x + 3) & ~3;   // source region pitch
+            const ResizeCoef* cx = coef + roff.o[k];
+            const int wk = g->L[k].w;
+            for (int e = tid; e < nx + ny; e += 256) {
+                int4 v;
+                if (e < nx) {
+                    const ResizeCoef c = cx[min(R.x + e, wk - 1)];
+                    v = make_int4(c.s0 - S.x, c.s1 - S.x, c.c0, c.c1);
+                } else {
+                    const ResizeCoef c = cx[wk + R.z + (e - nx)];
+                    v = rs_row_entry<GENERIC>(c, S.z);
+                    v.x = (c.s0 - S.z) * sp;
+                    v.y = (c.s1 - S.z) * sp;
+                }
+                sc[e0 + e] = v;
+            }
+            e0 += nx + ny;
+        }
+    }
+    // the base level's region: dwords where the rows allow, bytes at the right edge
+    {
+        const int4 R = sreg[b];
+        const int p0 = (R.y - R.x + 3) & ~3, nq = p0 >> 2, ny = R.w - R.z, wb = g->L[b].w;
+        const uint8_t* src = b == 0 ? frames + (long long)f * framePitch : fp + g->L[b].pyr_off;
+        const int stride = b == 0 ? rowStride : g->L[b].pitch;
+        const bool al = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)stride) & 3) == 0;
+        const int QW = nq <= 16 ? 16 : nq <= 32 ? 32 : 64, RP = 256 / QW;
+        for (int qb = 0; qb < nq; qb += QW)
+            for (int r = tid / QW; r < ny; r += RP) {
+                const int q = qb + (tid & (QW - 1));
+                if (q >= nq) continue;
+                const int col = R.x + 4 * q;
+                const uint8_t* rp = src + (long long)(R.z + r) * stride;
+                uint32_t v;
+                if (al && col + 3 < wb) {
+                    v = *reinterpret_cast<const uint32_t*>(rp + col);
+                } else {
+                    v = 0;
+                    for (int t = 0; t < 4; t++)
+                        if (col + t < wb) v |= (uint32_t)rp[col + t] << (8 * t);
+                }
+                *reinterpret_cast<uint32_t*>(buf0 + r * p0 + 4 * q) = v;
+            }
+    }
+    __syncthreads();
+    int e0 = 0;
+    for (int k = b + 1; k <= l; k++) {
+        const int4 R = sreg[k];
+        const int nx = R.y - R.x, ny = R.w - R.z, nq = nx >> 2;
+        const uint8_t* src = ((k - b) & 1) ? buf0 : buf1;
+        uint8_t* dst = ((k - b) & 1) ? buf1 : buf0;
+        const int4* cxs = sc + e0;
+        const int4* cys = sc + e0 + nx;
+        const bool last = k == l;
+        uint8_t* gl = fp + g->L[k].pyr_off;
+        const int gpitch = g->L[k].pitch, wk = g->L[k].w;
+        const int QW = nq <= 16 ? 16 : nq <= 32 ? 32 : 64, RP = 256 / QW;
+        for (int qb = 0; qb < nq; qb += QW) {
+            const int q = qb + (tid & (QW - 1));
+            const bool qon = q < nq;
+            // the dword group's 4 pixels: source byte offsets, weights; their bytes lie within 8 from bo
+            // when the scale factor is <= ~1.6 (then 3 dwords + v_perm + v_dot2 per row, else bytes)
+            int o0[4], o1[4];
+            unsigned c0[4], c1[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int4 cx = cxs[qon ? 4 * q + t : 0];
+                o0[t] = cx.x;
+                o1[t] = cx.y;
+                c0[t] = cx.z;
+                c1[t] = cx.w;
+            }
+            const int bo = o0[0], bw = bo >> 2, bsh = bo & 3;
+            const bool packed_ok = o1[3] - bo <= 7;
+            unsigned sel[4];
+            uint32_t cc[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                sel[t] = (unsigned)(o0[t] - bo) | 0x0C00u | ((unsigned)(o1[t] - bo) << 16) | 0x0C000000u;
+                cc[t] = c0[t] | (c1[t] << 16);
+            }
+            for (int r = tid / QW; r < ny; r += RP) {
+                if (!qon) continue;
+                const int4 cy = cys[r];
+                uint32_t packed = 0;
+                if (packed_ok) {
+                    // a row's 3 dwords from the aligned one, realigned to bo (as k_resize_tiled)
+                    const uint32_t* q0 = reinterpret_cast<const uint32_t*>(src + cy.x) + bw;
+                    const uint32_t* q1 = reinterpret_cast<const uint32_t*>(src + cy.y) + bw;
+                    const uint32_t u0 = q0[0], u1 = q0[1], u2 = q0[2], w0 = q1[0], w1 = q1[1], w2 = q1[2];
+                    const uint32_t a0 = __builtin_amdgcn_alignbyte(u1, u0, bsh), a1 = __builtin_amdgcn_alignbyte(u2, u1, bsh);
+                    const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, bsh), d1 = __builtin_amdgcn_alignbyte(w2, w1, bsh);
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        const unsigned h0 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cc[t]),
+                                                                   __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(a1, a0, sel[t])), 0u, false);
+                        const unsigned h1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cc[t]),
+                                                                   __builtin_bit_cast(ushort2_t, __builtin_amdgcn_perm(d1, d0, sel[t])), 0u, false);
+                        packed |= rs_vpass<GENERIC>((unsigned)cy.z, (unsigned)cy.w, h0, h1) << (8 * t);
+                    }
+                } else {
+                    const uint8_t* r0 = src + cy.x;
+                    const uint8_t* r1 = src + cy.y;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        const unsigned h0 = __umul24(r0[o0[t]], c0[t]) + __umul24(r0[o1[t]], c1[t]);
+                        const unsigned h1 = __umul24(r1[o0[t]], c0[t]) + __umul24(r1[o1[t]], c1[t]);
+                        packed |= rs_vpass<GENERIC>((unsigned)cy.z, (unsigned)cy.w, h0, h1) << (8 * t);
+                    }
+                }
+                if (!last) {
+                    *reinterpret_cast<uint32_t*>(dst + r * nx + 4 * q) = packed;
+                } else if (R.x + 4 * q < wk) {   // the pitch is a multiple of 64: the dword never leaves the row
+                    *reinterpret_cast<uint32_t*>(gl + (long long)(R.z + r) * gpitch + R.x + 4 * q) = packed;
+                }
+            }
+        }
+        e0 += nx + ny;
+        if (!last) __syncthreads();
     }
 }
 
@@ -942,6 +1095,43 @@ __device__ __forceinline__ int quad_mask(const int* qd) {
     return (qd[0] > 0) | ((qd[1] > 0) << 1) | ((qd[2] > 0) << 2) | ((qd[3] > 0) << 3);
 }
 
+/* Phase-1 fast-forward.  Phase 1 (:594-672) divides every node with > 1 key in every round, so the
+ * node set after round r is a function of the quadtree alone: the non-empty depth-r cells whose parent
+ * holds >= 2 keys, plus the one-key cells of every shallower depth (bNoMore).  Its list order follows
+ * from push_front (:617-652) and the in-order sweep: round r puts the children of the last-divided node
+ * first, n4..n1 each, ahead of the undivided nodes in their old order, so
+ *     L_r = [depth-r nodes in order_r] [one-key depth-(r-1) nodes in order_(r-1)] ... [one-key roots],
+ * where order_0 sorts roots ascending and order_r = (parent's order_(r-1) reversed, quadrant descending):
+ * a node's rank is its path code with the root reversed when r is odd and quadrant k reversed when
+ * r - k is even (XOR 3), i.e. code ^ 0x3333... on the quadrant bits.  Creation order within round r is
+ * the reverse of order_r (the next round's phase-2 tie key, :684).  So the list after R rounds is built
+ * in one pass: per-key path codes to depth F, cell counts in dense per-depth tables (LDS), per-depth
+ * node counts, the stop / phase-2 tests of :669-673 evaluated on those counts, and one scan over the
+ * tables of depths R..0 in rank order.  The round loop then continues from round R (phase 2, or phase
+ * 1 past depth F) exactly as before. */
+constexpr int kFfMaxDepth = 6;
+
+// depth F of the tables: one past the first depth whose cells can hold N nodes (the round where phase 1
+// usually ends), at most what fits in `room` ints with codes in 16 bits; 0 = no fast-forward
+__device__ __forceinline__ int ff_depth(int nIni, int N, int room) {
+    int F = 0, tot = 0, want = kFfMaxDepth;
+    for (int d = 1; d <= kFfMaxDepth; d++)
+        if ((nIni << (2 * d)) >= N) {
+            want = d + 1;
+            break;
+        }
+    for (int d = 1; d <= want && d <= kFfMaxDepth; d++) {
+        const int sz = nIni << (2 * d);
+        if (sz > 65536 || tot + sz > room) break;
+        tot += sz;
+        F = d;
+    }
+    return F;
+}
+
+// table offset of depth d (1..F) inside the tables area
+__device__ __forceinline__ int ff_base(int nIni, int d) { return nIni * (((1 << (2 * d)) - 4) / 3); }
+
 // One (frame, level) of DistributeOctTree once the candidate count C is known.  KeysInLds selects
 // whether keys / knode live in LDS (after the node tables) or in the per-level global scratch; the
 // two instantiations let the compiler use ds_* or global_* accesses instead of flat ones.
@@ -1042,46 +1232,211 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         if (tid == 0) { atomicOr(err, 1); lvlCount[f * g->nlevels + l] = 0; }
         return;
     }
-    for (int t = tid; t < nIni; t += NT) cntB[t] = 0;
-    __syncthreads();
-    for (int i0 = 0; i0 < C; i0 += NT) {   // uniform trip count: the ballots need the whole wave
-        const int i = i0 + tid;
-        const bool ok = i < C;
-        int r = 0;
-        if (ok) {
-            const int x = keys[i] & 0xFFF;
-            r = min((int)((float)x / hX), nIni - 1);
-            knode[i] = (uint16_t)r;
+    int S = 0, nextSeq = 0, phase = 1, round0 = 0;
+    bool ffDone = false;
+    const int F = C < (1 << 20) ? ff_depth(nIni, N, 8 * NC) : 0;
+    if (F > 0) {
+        // ---- phase-1 fast-forward (see above).  Tables: depth 0 = root counts in cntB, depths 1..F in
+        // the quad..nchr area (8 NC ints); entries cnt | pos << 20 once the node is placed.
+        int* T = quad;
+        int* ffc = reinterpret_cast<int*>(rxB);   // per depth d: [2d] nodes, [2d + 1] nodes with > 1 key
+        const int szF = nIni << (2 * F);
+        const int bF = ff_base(nIni, F);
+        for (int t = tid; t < szF; t += NT) T[bF + t] = 0;
+        for (int t = tid; t < 2 * (kFfMaxDepth + 1); t += NT) ffc[t] = 0;
+        __syncthreads();
+        OCT_STAMP(12);
+        // A. every key's path code down to depth F (the quadrants the rounds would send it to,
+        // DivideNode :477-535: children split at ceil(w / 2), x and y independently), counted at F
+        for (int i = tid; i < C; i += NT) {
+            const uint32_t k = keys[i];
+            const int x = k & 0xFFF, y = (k >> 12) & 0xFFF;
+            const int t = min((int)((float)x / hX), nIni - 1);
+            int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1)), y0 = 0, y1 = Hn;
+            int code = t;
+            for (int d = 1; d <= F; d++) {
+                const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
+                const bool bx = x >= xm, by = y >= ym;
+                x0 = bx ? xm : x0;
+                x1 = bx ? x1 : xm;
+                y0 = by ? ym : y0;
+                y1 = by ? y1 : ym;
+                code = code * 4 + ((int)bx | ((int)by << 1));
+            }
+            knode[i] = (uint16_t)code;
+            atomicAdd(&T[bF + code], 1);
         }
-        wave_agg_add(cntB, ok, r);   // the roots are few: a wave's keys usually share one or two
-    }
-    __syncthreads();
-    int S = 0;
-    for (int t0 = 0; t0 < nIni; t0 += NT) {   // keep the non-empty roots in order
-        const int t = t0 + tid;
-        const int n = t < nIni ? cntB[t] : 0;
-        int tot;
-        const int pos = S + oct_scan<NT>(n > 0 ? 1 : 0, sc, par, tot);
-        if (n > 0) {
-            const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
-            rxA[pos] = (uint32_t)x0 | ((uint32_t)x1 << 16);
-            ryA[pos] = (uint32_t)Hn << 16;
-            cntA[pos] = n;
-            seqA[pos] = -1 - t;
+        __syncthreads();
+        OCT_STAMP(13);
+        // B. the shallower depths' counts (sums of four children), and per depth the node counts: a
+        // non-empty cell whose parent holds >= 2 keys is a node (and divisible if it holds >= 2)
+        for (int d = F - 1; d >= 0; d--) {
+            const int sz = d == 0 ? nIni : nIni << (2 * d);
+            int* td = d == 0 ? cntB : T + ff_base(nIni, d);
+            const int* tc = T + ff_base(nIni, d + 1);
+            int dn = 0, en = 0, d0 = 0, e0 = 0;
+            for (int c = tid; c < sz; c += NT) {
+                const int4 ch = *reinterpret_cast<const int4*>(&tc[4 * c]);
+                const int pc = ch.x + ch.y + ch.z + ch.w;
+                td[c] = pc;
+                if (pc >= 2) {
+                    dn += (ch.x > 0) + (ch.y > 0) + (ch.z > 0) + (ch.w > 0);
+                    en += (ch.x > 1) + (ch.y > 1) + (ch.z > 1) + (ch.w > 1);
+                }
+                d0 += pc > 0;
+                e0 += pc > 1;
+            }
+            dn = wave_sum(dn);
+            en = wave_sum(en);
+            if ((threadIdx.x & 63) == 0 && (dn | en)) {
+                atomicAdd(&ffc[2 * (d + 1)], dn);
+                atomicAdd(&ffc[2 * (d + 1) + 1], en);
+            }
+            if (d == 0) {   // the roots themselves (erased when empty, :577-588)
+                d0 = wave_sum(d0);
+                e0 = wave_sum(e0);
+                if ((threadIdx.x & 63) == 0 && (d0 | e0)) {
+                    atomicAdd(&ffc[0], d0);
+                    atomicAdd(&ffc[1], e0);
+                }
+            }
+            __syncthreads();
         }
-        if (t < nIni) info[t] = pos;
-        S += tot;
+        OCT_STAMP(14);
+        // C. the rounds' size bookkeeping on the counts (:600, :669-673), identical in every thread
+        int Sr = ffc[0], Eprev = ffc[1], R = 0, base = 0, nseq = 0;
+        bool fin = false, ph2 = false, over = false;
+        for (int r = 1; r <= F; r++) {
+            const int Dr = ffc[2 * r], Er = ffc[2 * r + 1];
+            const int prev = Sr;
+            Sr = Sr - Eprev + Dr;
+            base = nseq;
+            nseq += Dr;
+            R = r;
+            if (Sr > NC) { over = true; break; }
+            if (Sr >= N || Sr == prev) { fin = true; break; }
+            if (Sr + Er * 3 > N) { ph2 = true; break; }
+            Eprev = Er;
+        }
+        if (over) {
+            if (tid == 0) { atomicOr(err, 2); lvlCount[f * g->nlevels + l] = 0; }
+            return;
+        }
+        const int DR = ffc[2 * R];
+        // D. the list after round R: one scan over the tables [depth R] [depth R-1] ... [roots], each
+        // in rank order, flagging depth R's nodes and the shallower one-key nodes
+        int V = 0;
+        for (int d = R; d >= 0; d--) V += d == 0 ? nIni : nIni << (2 * d);
+        OCT_STAMP(15);
+        int run = 0;
+        for (int v0 = 0; v0 < V; v0 += NT) {   // uniform trip count (the scan)
+            const int v = v0 + tid;
+            int c = 0, n = 0, d = 0;
+            bool on = false;
+            int* td = cntB;
+            if (v < V) {
+                int off = 0;
+                d = R;
+                for (;;) {
+                    const int sz = d == 0 ? nIni : nIni << (2 * d);
+                    if (v < off + sz) break;
+                    off += sz;
+                    d--;
+                }
+                const int p = v - off;
+                const int lowMask = (1 << (2 * d)) - 1;
+                const int rt = p >> (2 * d);
+                // rank -> cell: root reversed for odd d, quadrant k reversed where d - k is even
+                c = (((d & 1) ? nIni - 1 - rt : rt) << (2 * d)) | ((p & lowMask) ^ (0x33333333 & lowMask));
+                td = d == 0 ? cntB : T + ff_base(nIni, d);
+                n = td[c] & 0xFFFFF;
+                const int* ptab = d == 1 ? cntB : T + ff_base(nIni, d > 1 ? d - 1 : 1);
+                const bool node = n > 0 && (d == 0 || (ptab[c >> 2] & 0xFFFFF) >= 2);
+                on = node && (d == R || n == 1);
+            }
+            int tot;
+            const int pos = run + oct_scan<NT>(on ? 1 : 0, sc, par, tot);
+            if (on) {
+                const int t = c >> (2 * d);
+                int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1)), y0 = 0, y1 = Hn;
+                for (int k2 = d - 1; k2 >= 0; k2--) {
+                    const int q = (c >> (2 * k2)) & 3;
+                    const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
+                    x0 = (q & 1) ? xm : x0;
+                    x1 = (q & 1) ? x1 : xm;
+                    y0 = (q & 2) ? ym : y0;
+                    y1 = (q & 2) ? y1 : ym;
+                }
+                rxA[pos] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+                ryA[pos] = (uint32_t)y0 | ((uint32_t)y1 << 16);
+                cntA[pos] = n;
+                // creation order in round R is the reverse of the rank (phase 2's tie key, :684); the
+                // one-key nodes are never divided and their seq is never read
+                seqA[pos] = d == 0 ? -1 - t : d == R ? base + DR - 1 - pos : base;
+                td[c] = n | (pos << 20);
+            }
+            run += tot;
+        }
+        __syncthreads();
+        OCT_STAMP(16);
+        // E. each key's node: its first one-key ancestor, else its depth-R cell
+        for (int i = tid; i < C; i += NT) {
+            const int code = knode[i];
+            int node = 0;
+            for (int d = 0; d <= R; d++) {
+                const int c = code >> (2 * (F - d));
+                const int e = d == 0 ? cntB[c] : T[ff_base(nIni, d) + c];
+                if (d == R || (e & 0xFFFFF) == 1) {
+                    node = e >> 20;
+                    break;
+                }
+            }
+            knode[i] = (uint16_t)node;
+        }
+        S = run;
+        nextSeq = nseq;
+        round0 = R;
+        ffDone = fin;
+        if (ph2) phase = 2;
+    } else {
+        for (int t = tid; t < nIni; t += NT) cntB[t] = 0;
+        __syncthreads();
+        for (int i0 = 0; i0 < C; i0 += NT) {   // uniform trip count: the ballots need the whole wave
+            const int i = i0 + tid;
+            const bool ok = i < C;
+            int r = 0;
+            if (ok) {
+                const int x = keys[i] & 0xFFF;
+                r = min((int)((float)x / hX), nIni - 1);
+                knode[i] = (uint16_t)r;
+            }
+            wave_agg_add(cntB, ok, r);   // the roots are few: a wave's keys usually share one or two
+        }
+        __syncthreads();
+        for (int t0 = 0; t0 < nIni; t0 += NT) {   // keep the non-empty roots in order
+            const int t = t0 + tid;
+            const int n = t < nIni ? cntB[t] : 0;
+            int tot;
+            const int pos = S + oct_scan<NT>(n > 0 ? 1 : 0, sc, par, tot);
+            if (n > 0) {
+                const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
+                rxA[pos] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+                ryA[pos] = (uint32_t)Hn << 16;
+                cntA[pos] = n;
+                seqA[pos] = -1 - t;
+            }
+            if (t < nIni) info[t] = pos;
+            S += tot;
+        }
+        __syncthreads();
+        for (int i = tid; i < C; i += NT) knode[i] = (uint16_t)info[knode[i]];
     }
-    __syncthreads();
-    for (int i = tid; i < C; i += NT) knode[i] = (uint16_t)info[knode[i]];
     if (tid == 0) sv[3] = 0;
-    int nextSeq = 0;
-    int phase = 1;
     __syncthreads();
     OCT_STAMP(2);
 
     int p2seen = 0;
-    for (int round = 0; round < 4 * NC + 64; round++) {
+    for (int round = round0; round < 4 * NC + 64 && !ffDone; round++) {
         const int prevSize = S;
         // sub-step stamps of round 0 (slots 12..16) and of the first phase-2 round (20..28)
         [[maybe_unused]] const int subBase = round == 0 ? 12 : (phase == 2 && !p2seen) ? 20 : -1;
@@ -1890,7 +2245,19 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     };
     int* zero = b.zero_err ? b.d_err : nullptr;
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);
-    for (int l = 1; l < g.nlevels; l++) resize(l, stream);
+    if (b.chain.nseg && nframes <= kChainMaxFrames) {   // the few-launch pyramid (k_pyramid_chain)
+        RcoefOff ro;
+        std::memcpy(ro.o, b.rcoef_off, sizeof ro.o);
+        const bool gen = (g.variant & ORB_VARIANT_RESIZE_GENERIC) != 0;
+        for (int sgi = 0; sgi < b.chain.nseg; sgi++) {
+            const ChainSegment& sg = b.chain.seg[sgi];
+            hipLaunchKernelGGL(gen ? k_pyramid_chain<true> : k_pyramid_chain<false>, dim3(sg.njobs, nframes), dim3(256),
+                               (size_t)sg.lds_bytes, stream, b.d_geom, b.d_rcoef, b.d_chain, sg, ro, d_frames, frame_pitch,
+                               row_stride, b.d_pyr);
+        }
+    } else {
+        for (int l = 1; l < g.nlevels; l++) resize(l, stream);
+    }
     if (marker) marker(user, ORB_K_RESIZE, 0, stream);
     if (marker) marker(user, ORB_K_FAST, 1, stream);
     fast(0, g.ncells, stream, zero);

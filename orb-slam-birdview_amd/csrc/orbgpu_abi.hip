@@ -200,6 +200,66 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
     return e;
 }
 
+/* The few-launch pyramid's plan (k_pyramid_chain): the levels in segments of up to kChainSeg, one
+ * launch each, every level of a segment computed from the segment's base level (the frame, or the
+ * previous segment's last level).  Per level l output tiles of 64 x 32 (32 x 16 for the third and later
+ * levels of a segment, so a tile's recomputed chain stays short), and for each tile the region of every
+ * level base .. l-1 its pixels depend on, walked back through the resize coefficient tables (monotone:
+ * a region's span is its end columns' / rows' source indices).  Regions above the base start at a
+ * multiple of 4 and span a multiple of 4 columns; the base region is clipped to the level. */
+static void build_chain(const Geom& g, const std::vector<ResizeCoef>& coefs, const int* off, std::vector<ChainJob>& jobs,
+                        ChainPlan& plan) {
+    jobs.clear();
+    plan = ChainPlan{};
+    const int nl = g.nlevels;
+    if (nl < 2) return;
+    auto r4 = [](int x) { return (x + 3) & ~3; };
+    for (int base = 0; base < nl - 1; base += kChainSeg) {
+        const int top = std::min(base + kChainSeg, nl - 1);
+        ChainSegment sg;
+        sg.job0 = (int)jobs.size();
+        int bufb = 0, coefe = 0;
+        for (int l = base + 1; l <= top; l++) {
+            const int TW = l - base <= 2 ? 64 : 32, TH = l - base <= 2 ? 32 : 16;
+            const int wl = g.L[l].w, hl = g.L[l].h;
+            for (int y0 = 0; y0 < hl; y0 += TH)
+                for (int x0 = 0; x0 < wl; x0 += TW) {
+                    ChainJob J;
+                    std::memset(&J, 0, sizeof J);
+                    J.level = l;
+                    J.base = base;
+                    J.reg[l] = make_int4(x0, r4(std::min(x0 + TW, wl)), y0, std::min(y0 + TH, hl));
+                    int ce = 0;
+                    for (int k = l; k > base; k--) {
+                        const int4 R = J.reg[k];
+                        const ResizeCoef* cx = &coefs[off[k]];
+                        const ResizeCoef* cy = cx + g.L[k].w;
+                        const int sx0 = cx[R.x].s0, sx1 = cx[std::min(R.y, g.L[k].w) - 1].s1 + 1;
+                        const int sy0 = cy[R.z].s0, sy1 = cy[R.w - 1].s1 + 1;
+                        J.reg[k - 1] = make_int4(sx0 & ~3, k - 1 > base ? r4(sx1) : std::min(sx1, g.L[k - 1].w), sy0, sy1);
+                        ce += (R.y - R.x) + (R.w - R.z);
+                    }
+                    for (int k = base; k < l; k++) {
+                        const int4 R = J.reg[k];
+                        bufb = std::max(bufb, r4(R.y - R.x) * (R.w - R.z));
+                    }
+                    coefe = std::max(coefe, ce);
+                    jobs.push_back(J);
+                }
+        }
+        sg.njobs = (int)jobs.size() - sg.job0;
+        sg.buf_bytes = (bufb + 15) & ~15;
+        sg.coef_entries = coefe;
+        sg.lds_bytes = 2 * sg.buf_bytes + 16 * coefe;
+        if (sg.lds_bytes > 64 * 1024) {   // wide images keep the per-level launches
+            jobs.clear();
+            plan = ChainPlan{};
+            return;
+        }
+        plan.seg[plan.nseg++] = sg;
+    }
+}
+
 int Ctx::ensure_geometry(int W, int H) {
     if (have_geom && geom.W == W && geom.H == H) return ORB_OK;
     Geom g;
@@ -224,8 +284,18 @@ int Ctx::ensure_geometry(int W, int H) {
     if ((e = hipMemcpyAsync(d_rcoef, coefs.data(), coefs.size() * sizeof(ResizeCoef), hipMemcpyHostToDevice,
                             stream)) != hipSuccess)
         return set_error("upload coefs", e), ORB_ERR_HIP;
+    std::vector<ChainJob> cjobs;
+    ChainPlan cplan;
+    build_chain(g, coefs, off, cjobs, cplan);
+    if (cplan.nseg) {
+        if ((e = grow(d_chain, chain_cap, cjobs.size())) != hipSuccess) return set_error("hipMalloc chain", e), ORB_ERR_NOMEM;
+        if ((e = hipMemcpyAsync(d_chain, cjobs.data(), cjobs.size() * sizeof(ChainJob), hipMemcpyHostToDevice, stream)) !=
+            hipSuccess)
+            return set_error("upload chain", e), ORB_ERR_HIP;
+    }
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
     geom = g;
+    chain = cplan;
     std::memcpy(rcoef_off, off, sizeof off);
     have_geom = true;
     ++geom_serial;
@@ -263,6 +333,9 @@ ExtractBuffers Ctx::buffers() const {
     b.d_rcoef = d_rcoef;
     b.d_cells = d_cells;
     std::memcpy(b.rcoef_off, rcoef_off, sizeof rcoef_off);
+    b.d_chain = d_chain;
+    b.chain = chain;
+    if (no_chain) b.chain.nseg = 0;
     b.d_pyr = d_pyr;
     b.d_cands = d_cands;
     b.d_cellCount = d_cellCount;
@@ -287,10 +360,13 @@ void Ctx::marker(void* user, int id, int begin, hipStream_t s) {
 }
 
 int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
-                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err) {
+                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err, bool latency) {
     hipError_t e;
     ExtractBuffers bufs = buffers();
     if (err) bufs.d_err = err;
+    // the few-launch pyramid trades redundant work for fewer dependent launches: it pays for one frame
+    // in flight (the host path), not when several batches share the GPU (measured)
+    if (!latency) bufs.chain.nseg = 0;
     if (use_graph && !prof_on && !fast_stamps) {
         // HIP graph replay: one submission per batch instead of 10 launches; captured on the first batch
         // with a given set of buffers / arguments and re-instantiated when any of them changes
@@ -299,7 +375,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)d_desc, (uintptr_t)d_counts, (uintptr_t)kp_cap, (uintptr_t)geom.W, (uintptr_t)geom.H,
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
-            (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream, 0};
+            (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream, (uintptr_t)bufs.chain.nseg};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -397,6 +473,8 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     // diagnostics only (tests/test_gpu_extract.py checks both leave the results unchanged):
     // ORBGPU_FAST_STAMPS=1 records kernel phase timestamps, ORBGPU_GRAPH=0 launches without graph replay
     if (const char* e = std::getenv("ORBGPU_FAST_STAMPS")) c->fast_stamps = e[0] == '1';
+    // ORBGPU_NO_CHAIN=1: small batches take the per-level pyramid launches (A/B diagnostic; same results)
+    if (const char* e = std::getenv("ORBGPU_NO_CHAIN")) c->no_chain = e[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
     // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
@@ -433,7 +511,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.b);
         (void)hipEventDestroy(pr.e);
     }
-    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
+    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_pyr, c->d_cands, c->d_cellCount, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_hout,
                     c->d_scratch, c->d_peer};
     for (void* b : bufs)
@@ -527,7 +605,8 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     // ms per C3 frame end to end, tools/host_latency)
     if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return set_error("upload image", e), ORB_ERR_HIP;
-    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, d_k, d_d, d_cnt, kcap, d_cnt + 1)) != ORB_OK)
+    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, d_k, d_d, d_cnt, kcap, d_cnt + 1, true)) !=
+        ORB_OK)
         return st;
     if (need > c->pinned_cap) {
         if (c->h_pinned) (void)hipHostFree(c->h_pinned);

@@ -22,7 +22,8 @@ struct Ctx {
     int device = 0;
     int num_cu = 256;
     bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: the kernels record phase timestamps (diagnostic)
-    bool stereo_stage = false;    // ORBGPU_STEREO_STAGE=1: stereo stages the right side as for a peer GPU (test)
+    bool stereo_stage = false;
+    bool no_chain = false;        // ORBGPU_NO_CHAIN=1: no one-launch pyramid for small batches (A/B diagnostic)    // ORBGPU_STEREO_STAGE=1: stereo stages the right side as for a peer GPU (test)
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
@@ -43,6 +44,9 @@ struct Ctx {
     size_t geom_cap = 0;
     ResizeCoef* d_rcoef = nullptr;
     size_t rcoef_cap = 0;
+    ChainJob* d_chain = nullptr;   // the one-launch pyramid's jobs (small batches)
+    size_t chain_cap = 0;
+    ChainPlan chain{};
     CellDesc* d_cells = nullptr;
     size_t cells_cap = 0;
 
@@ -116,7 +120,7 @@ struct Ctx {
     // err: the overflow flag the kernels raise (default d_err; orb_extract passes a word of its output
     // block so that one download brings it back)
     int run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
-                    uint8_t* d_desc, int* d_counts, int kp_cap, int* err = nullptr);
+                    uint8_t* d_desc, int* d_counts, int kp_cap, int* err = nullptr, bool latency = false);
     static void marker(void* user, int id, int begin, hipStream_t s);
 };
 

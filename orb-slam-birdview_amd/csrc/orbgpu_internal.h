@@ -95,12 +95,39 @@ struct ResizeCoef {
     int c0, c1;          // 11-bit fixed-point weights (saturate_cast<short>(w*2048))
 };
 
+// One workgroup of k_pyramid_chain (the few-launch pyramid of small batches): an output tile of
+// `level`, computed from level `base` (the frame, or a level an earlier launch wrote) through the
+// region reg[k] = (x0, x1, y0, y1) of every level k = base .. level - 1 its pixels depend on (levels
+// above base: x0 and x1 - x0 multiples of 4, so every stage writes dwords).
+struct ChainJob {
+    int level, base, pad0, pad1;
+    int4 reg[ORBGPU_MAX_LEVELS];
+};
+// Plan of k_pyramid_chain, host-built once per image size (orbgpu_abi.hip build_chain): the levels in
+// segments of up to kChainSeg, one launch each; a segment's jobs are contiguous, in level order.  LDS
+// carve per launch = two region buffers (ping-pong) + the stages' coefficient slots.
+constexpr int kChainSeg = 4;
+struct ChainSegment {
+    int job0 = 0, njobs = 0;
+    int buf_bytes = 0, coef_entries = 0, lds_bytes = 0;
+};
+struct ChainPlan {
+    int nseg = 0;           // 0: the plan does not fit (per-level launches only)
+    ChainSegment seg[ORBGPU_MAX_LEVELS];
+};
+constexpr int kChainMaxFrames = 2;
+struct RcoefOff {   // per-level offsets into the coefficient table (a kernel argument)
+    int o[ORBGPU_MAX_LEVELS];
+};   // batches up to this many frames take the one-launch pyramid
+
 // Kernel launchers (extract_kernels.hip / hamming_kernels.hip).
 struct ExtractBuffers {
     const Geom* d_geom;
     const ResizeCoef* d_rcoef;     // per level: w_l x-coefs then h_l y-coefs, at rcoef_off[l]
     const CellDesc* d_cells;       // ncells FAST cell descriptors
     int rcoef_off[ORBGPU_MAX_LEVELS];
+    const ChainJob* d_chain;       // k_pyramid_chain jobs (chain.njobs per frame)
+    ChainPlan chain;
     uint8_t* d_pyr;                // nframes * pyr_bytes
     uint32_t* d_cands;             // nframes * ncand
     int* d_cellCount;              // nframes * ncells
