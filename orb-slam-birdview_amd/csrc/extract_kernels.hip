@@ -1856,11 +1856,13 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         const uint32_t idx = __umul24(xb, (unsigned)kRtPitch) + (yb & 0xFFFFu);
         const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + ((idx & ~1u) << 1));
         const uint32_t sh = idx << 4;   // v_alignbit reads bits 4:0: 16 for an odd element, realigning the u16 pairs
-        const uint32_t d0 = rp[0], d1 = rp[1], d2 = rp[2], d3 = rp[3], d4 = rp[4];
+        // 7 taps from 4 dwords: the last pair's high element has weight 0 (K60), so whatever alignbit
+        // shifts into it (d3 again for an odd element) drops out -- no fifth dword
+        const uint32_t d0 = rp[0], d1 = rp[1], d2 = rp[2], d3 = rp[3];
         uint32_t S = __builtin_amdgcn_udot2(K01, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d1, d0, sh)), 0u, false);
         S = __builtin_amdgcn_udot2(K23, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d2, d1, sh)), S, false);
         S = __builtin_amdgcn_udot2(K45, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d3, d2, sh)), S, false);
-        S = __builtin_amdgcn_udot2(K60, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d4, d3, sh)), S, false);
+        S = __builtin_amdgcn_udot2(K60, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d3, d3, sh)), S, false);
         // round(S / 65536): half-to-even = (S + 32767 + q&1) >> 16, half-up = (S + 32768) >> 16
         if (ALLEVEN) return S + 32767u + ((S >> 16) & 1u);
         return S + (colBase + (int)xb < xsimd ? 32767u + ((S >> 16) & 1u) : 32768u);
