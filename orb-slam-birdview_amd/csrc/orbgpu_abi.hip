@@ -360,7 +360,8 @@ void Ctx::marker(void* user, int id, int begin, hipStream_t s) {
 }
 
 int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
-                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err, bool latency) {
+                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err, bool latency, void* tail_dst,
+                     const void* tail_src, size_t tail_bytes) {
     hipError_t e;
     ExtractBuffers bufs = buffers();
     if (err) bufs.d_err = err;
@@ -375,7 +376,8 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)d_desc, (uintptr_t)d_counts, (uintptr_t)kp_cap, (uintptr_t)geom.W, (uintptr_t)geom.H,
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
-            (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream, (uintptr_t)bufs.chain.nseg};
+            (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream,
+            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)tail_dst << 4) ^ ((uintptr_t)tail_bytes << 40)};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -384,8 +386,12 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             if ((e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal)) != hipSuccess)
                 return set_error("graph capture", e), ORB_ERR_HIP;
             // the overflow flag is zeroed by the FAST kernel (no separate memset node)
-            const hipError_t le = launch_extract(geom, bufs, d_frames, frame_pitch, row_stride, nframes, d_kps,
-                                                 d_desc, d_counts, kp_cap, stream, nullptr, nullptr);
+            hipError_t le = launch_extract(geom, bufs, d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc,
+                                           d_counts, kp_cap, stream, nullptr, nullptr);
+            // the host path's result download as the graph's last node: it starts as the last kernel ends
+            // instead of waiting for the host to submit it after the graph launch returns
+            if (le == hipSuccess && tail_dst)
+                le = hipMemcpyAsync(tail_dst, tail_src, tail_bytes, hipMemcpyDeviceToHost, stream);
             hipGraph_t gr = nullptr;
             e = hipStreamEndCapture(stream, &gr);
             if (le != hipSuccess || e != hipSuccess) {
@@ -405,6 +411,8 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
         e = launch_extract(geom, bufs, d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
                            stream, &Ctx::marker, this);
         if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
+        if (tail_dst && (e = hipMemcpyAsync(tail_dst, tail_src, tail_bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return set_error("download", e), ORB_ERR_HIP;
     }
     last_frames = d_frames;
     last_frame_pitch = frame_pitch;
@@ -605,9 +613,6 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     // ms per C3 frame end to end, tools/host_latency)
     if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return set_error("upload image", e), ORB_ERR_HIP;
-    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, d_k, d_d, d_cnt, kcap, d_cnt + 1, true)) !=
-        ORB_OK)
-        return st;
     if (need > c->pinned_cap) {
         if (c->h_pinned) (void)hipHostFree(c->h_pinned);
         c->h_pinned = nullptr;
@@ -620,9 +625,11 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     const int* hcnt = reinterpret_cast<const int*>(hp);
     const orb_keypoint* hk = reinterpret_cast<const orb_keypoint*>(hp + 16);
     const uint8_t* hd = hp + 16 + kbytes;
-    if ((e = hipMemcpyAsync(hp, c->d_hout, need, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return set_error("download keypoints", e), ORB_ERR_HIP;
+    // kernels + the output block's download in one submission (the copy is the graph's last node)
+    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, d_k, d_d, d_cnt, kcap, d_cnt + 1, true, hp,
+                             c->d_hout, need)) != ORB_OK)
+        return st;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("download keypoints", e), ORB_ERR_HIP;
     if (hcnt[1]) {
         set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
         return ORB_ERR_INTERNAL;

@@ -120,7 +120,8 @@ struct Ctx {
     // err: the overflow flag the kernels raise (default d_err; orb_extract passes a word of its output
     // block so that one download brings it back)
     int run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
-                    uint8_t* d_desc, int* d_counts, int kp_cap, int* err = nullptr, bool latency = false);
+                    uint8_t* d_desc, int* d_counts, int kp_cap, int* err = nullptr, bool latency = false,
+                    void* tail_dst = nullptr, const void* tail_src = nullptr, size_t tail_bytes = 0);
     static void marker(void* user, int id, int begin, hipStream_t s);
 };
 

@@ -29,7 +29,7 @@ def main():
     if dirty:
         commit += "+dirty"
     main_line = None
-    for name in ("bench", "bench_c2", "bench_c5"):
+    for name in ("bench", "bench_c2", "bench_c5", "bench_c5b1"):
         p = os.path.join(OUT, name + ".log")
         if not os.path.exists(p):
             continue
@@ -56,6 +56,29 @@ def main():
         for path in (os.path.join(prof, f"{tag}_pmc.json"), os.path.join(ROOT, "profiles", "pmc_traffic.json")):
             with open(path, "w") as f:
                 json.dump(d, f, indent=1)
+    # roofline.frac reproduced from the committed serial trace: the dominant kernel's mean duration over
+    # the timed launches only (the trace also holds the warm-up launches, whose clocks are still ramping)
+    tr = os.path.join(OUT, "prof_serial", "run_kernel_trace.csv")
+    if os.path.exists(tr) and main_line and main_line.get("roofline"):
+        import csv
+        rl = main_line["roofline"]
+        kname = {"fast": "k_fast_wave", "describe": "k_describe", "resize": "k_resize", "octree": "k_octree"}[rl["kernel"]]
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                for r in sorted(csv.DictReader(open(tr)), key=lambda r: int(r["Start_Timestamp"]))
+                if kname in r["Kernel_Name"]]
+        warm = int(os.environ.get("SERIAL_WARMUP", "20"))
+        timed = durs[warm:] if len(durs) > warm else durs
+        mean_us = sum(timed) / len(timed) / 1e3
+        ach = rl["algorithmic_bytes_per_launch"] / (mean_us * 1e-6) / 1e9
+        chk = {"kernel": kname, "trace": f"{tag}_kernel_stats_serial.csv / run_kernel_trace.csv (prof_serial)",
+               "launches": len(durs), "warmup_launches_dropped": len(durs) - len(timed),
+               "mean_us_timed": round(mean_us, 2), "mean_us_all": round(sum(durs) / len(durs) / 1e3, 2),
+               "algorithmic_bytes_per_launch": rl["algorithmic_bytes_per_launch"],
+               "achieved_GBs_from_trace": round(ach, 1), "frac_from_trace": round(ach / rl["peak"], 4),
+               "bench_line": {"kernel_avg_launch_us": rl["kernel_avg_launch_us"], "frac": rl["frac"]}}
+        with open(os.path.join(prof, f"{tag}_roofline_check.json"), "w") as f:
+            json.dump(chk, f, indent=1)
+        shutil.copy(tr, os.path.join(prof, f"{tag}_kernel_trace_serial.csv"))
     print("collected", rnd, tag, "commit", commit)
 
 

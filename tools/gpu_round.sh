@@ -21,8 +21,10 @@ fi
 step bench 600 python bench.py || exit 1
 step bench_c2 300 python bench.py --config c2 --no-cpu --no-c4 --no-bird || exit 1
 step bench_c5 300 python bench.py --config c5 --steps 50 --warmup 5 --no-cpu --no-c4 --no-bird --no-stereo || exit 1
+# what one GPU does at N = 8 in C5 (one frame per step, four in flight)
+step bench_c5b1 300 python bench.py --config c5 --batch 1 --pipelines 4 --steps 400 --warmup 40 --only-extract || exit 1
 # the timed loop as the bench runs it (two batches in flight: kernel durations of the two streams overlap)
 step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --only-extract --no-profile-pass --steps 20 --warmup 3 || exit 1
 # the same loop one batch at a time: per-launch durations comparable with the bench's HIP-event roofline pass
-step rocprof_serial 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_serial -o run -- python3 bench.py --only-extract --no-profile-pass --pipelines 1 --steps 20 --warmup 3 || exit 1
+step rocprof_serial 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_serial -o run -- python3 bench.py --only-extract --no-profile-pass --pipelines 1 --steps 100 --warmup 20 || exit 1
 exit 0
