@@ -368,7 +368,9 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     // the few-launch pyramid trades redundant work for fewer dependent launches: it pays for one frame
     // in flight (the host path), not when several batches share the GPU (measured)
     if (!latency) bufs.chain.nseg = 0;
-    if (use_graph && !prof_on && !fast_stamps) {
+    // one frame in flight (the host path): direct launches measured faster than a graph replay (the first
+    // kernel is dispatched as soon as it is launched, while the host submits the rest)
+    if (use_graph && !prof_on && !fast_stamps && !latency) {
         // HIP graph replay: one submission per batch instead of 10 launches; captured on the first batch
         // with a given set of buffers / arguments and re-instantiated when any of them changes
         const std::array<uintptr_t, 24> key = {
