@@ -1137,8 +1137,7 @@ __device__ __forceinline__ int ff_base(int nIni, int d) { return nIni * (((1 << 
 // two instantiations let the compiler use ds_* or global_* accesses instead of flat ones.
 template <bool KeysInLds, int NT>
 __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const LevelGeom& L, int f, int l, int* smem,
-                                             int C, const int* __restrict__ cc, const uint32_t* __restrict__ cs,
-                                             uint32_t* keys, uint16_t* knode, uint32_t* __restrict__ lvlKps,
+                                             int C, uint32_t* keys, uint16_t* knode, uint32_t* __restrict__ lvlKps,
                                              int* __restrict__ lvlCount, int* __restrict__ err, int par,
                                              unsigned long long* __restrict__ ost) {
     const int NC = g->node_cap;
@@ -1169,56 +1168,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
 #define OCT_STAMP(k)
 #endif
 
-    // 1. gather candidates in cell order (vToDistributeKeys, :818-825)
-    const int ncl = L.nCols * L.nRows;
-    if (ncl + 1 <= 8 * NC) {
-        // cell offsets in LDS, then a flat copy: key i lives in the last cell whose offset is <= i
-        // (binary search), so each lane's loads are independent and issued together
-        int* coff = quad;   // holds the cell counts (staged by k_octree), scanned in place
-        int base = 0;
-        for (int c0 = 0; c0 < ncl; c0 += NT) {
-            const int c = c0 + tid;
-            const int n = c < ncl ? coff[c] : 0;
-            int tot;
-            const int off = oct_scan<NT>(n, sc, par, tot);
-            if (c < ncl) coff[c] = base + off;
-            base += tot;
-        }
-        if (tid == 0) coff[ncl] = base;
-        __syncthreads();
-        constexpr int U = 4;
-        for (int i0 = 0; i0 < C; i0 += U * NT) {
-            uint32_t v[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int i = i0 + u * NT + tid;
-                v[u] = 0;
-                if (i < C) {
-                    int lo = 0, hi = ncl;   // coff[lo] <= i < coff[hi]
-                    while (hi - lo > 1) {
-                        const int mid = (lo + hi) >> 1;
-                        if (coff[mid] <= i) lo = mid; else hi = mid;
-                    }
-                    v[u] = cs[__umul24((unsigned)lo, (unsigned)L.cell_cap) + (unsigned)(i - coff[lo])];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int i = i0 + u * NT + tid;
-                if (i < C) keys[i] = v[u];
-            }
-        }
-    } else {
-        int base = 0;
-        for (int c0 = 0; c0 < ncl; c0 += NT) {
-            const int c = c0 + tid;
-            const int n = c < ncl ? cc[c] : 0;
-            int tot;
-            const int off = oct_scan<NT>(n, sc, par, tot);
-            for (int k = 0; k < n; k++) keys[base + off + k] = cs[(long long)c * L.cell_cap + k];
-            base += tot;
-        }
-    }
+    // 1. the keys (vToDistributeKeys order) are in place: k_octree gathered them
     __syncthreads();
     OCT_STAMP(1);
     if (ost && tid == 0) ost[29] = (unsigned long long)C;
@@ -1233,7 +1183,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         return;
     }
     int S = 0, nextSeq = 0, phase = 1, round0 = 0;
-    bool ffDone = false;
+    bool ffDone = false, quadReady = false;
     const int F = C < (1 << 20) ? ff_depth(nIni, N, 8 * NC) : 0;
     if (F > 0) {
         // ---- phase-1 fast-forward (see above).  Tables: depth 0 = root counts in cntB, depths 1..F in
@@ -1374,6 +1324,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 // one-key nodes are never divided and their seq is never read
                 seqA[pos] = d == 0 ? -1 - t : d == R ? base + DR - 1 - pos : base;
                 td[c] = n | (pos << 20);
+                if (d == R) ryB[pos] = (uint32_t)c;   // the node's depth-R cell (phase 2's quadrant counts)
             }
             run += tot;
         }
@@ -1392,6 +1343,27 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 }
             }
             knode[i] = (uint16_t)node;
+        }
+        // phase 2 starts at round R + 1 and divides depth-R nodes: their quadrant counts are the depth-(R+1)
+        // table's, so its first round needs no pass over the keys (read here, written once every read of
+        // the tables is done: quad aliases them)
+        if (ph2 && R + 1 <= F) {
+            constexpr int kMaxPer = 8;   // node_cap <= 8 * NT (host: octree_lds_bytes <= 160 KiB)
+            int4 qv[kMaxPer];
+            const int* tq = T + ff_base(nIni, R + 1);
+#pragma unroll
+            for (int j = 0; j < kMaxPer; j++) {
+                const int pos = tid + j * NT;
+                qv[j] = make_int4(0, 0, 0, 0);
+                if (pos < run && pos < DR && cntA[pos] >= 2) qv[j] = *reinterpret_cast<const int4*>(&tq[4 * (int)ryB[pos]]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kMaxPer; j++) {
+                const int pos = tid + j * NT;
+                if (pos < run) *reinterpret_cast<int4*>(&quad[4 * pos]) = qv[j];
+            }
+            quadReady = true;
         }
         S = run;
         nextSeq = nseq;
@@ -1447,11 +1419,11 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
 #else
 #define OCT_SUB(k)
 #endif
-        for (int t = tid; t < 4 * S; t += NT) quad[t] = 0;
+        if (!quadReady) for (int t = tid; t < 4 * S; t += NT) quad[t] = 0;
         for (int t = tid; t < S; t += NT) rank[t] = -1;
         __syncthreads();
         OCT_SUB(0);
-        for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread, branch-free reads (clamped)
+        for (int i0 = 0; i0 < (quadReady ? 0 : C); i0 += 4 * NT) {   // 4 keys per thread, branch-free reads (clamped)
             int tt[4], tg[4];
             uint32_t kk[4];
             bool inc[4];
@@ -1473,6 +1445,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         }
         __syncthreads();
         OCT_SUB(1);
+        quadReady = false;
         int CH = 0, ndiv = 0;   // children created / nodes divided this round
         if (phase == 1) {
             // every node with > 1 key, in list order: one scan of (divided, #children) packed 16:16;
@@ -1708,8 +1681,6 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
     // frames along x so that every frame's level-0 block (the longest) is dispatched first
     const int f = blockIdx.x, l = lbase + (int)blockIdx.y;
     const LevelGeom& L = g->L[l];
-    int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
-    int* sv = sc + 32;
     // optional timestamps (ORBGPU_FAST_STAMPS=1): 32 per (frame, level): 0 start, 1 gathered, 2 roots,
     // 3.. end of round r (up to 9), 12.. / 20.. sub-steps of round 0 / the first phase-2 round,
     // 29 = C, 30 = phase-2 start round, 31 done
@@ -1717,29 +1688,78 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
 #if ORBGPU_KERNEL_STAMPS
     if (ost && tid == 0) ost[0] = __builtin_amdgcn_s_memtime();
 #endif
+    // 1. gather the candidates in cell order (vToDistributeKeys, :818-825) in one global round trip: a
+    // thread per cell loads its count and, speculatively, its first kFirst slots together; one block scan
+    // gives the cells' offsets; the rare cell with more keys loads the rest after it.  Keys go to LDS after
+    // the node tables when they fit (every pass re-reads them), else to the per-level global scratch.
+    constexpr int kFirst = 4;
     const int ncl = L.nCols * L.nRows;
     const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
     const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
-    int mine = 0;
-    int* cstage = smem + 8 * NC;   // octree_level's quad area: cell counts for its gather
-    const bool stage = ncl + 1 <= 8 * NC;
-    for (int c = tid; c < ncl; c += NT) {
-        const int n = cc[c];
-        mine += n;
-        if (stage) cstage[c] = n;
+    int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
+    int* sv = sc + 32;
+    uint32_t* keysL = reinterpret_cast<uint32_t*>(sv + 8);
+    const long long o = ((long long)f * g->nlevels + l) * g->max_level_cand;
+    int par = 0;
+    // the common case: every cell in one chunk of NT, first slots + offsets staged in the node tables' area
+    const bool staged = ncl <= NT && (kFirst + 1) * ncl <= 16 * NC;
+    int C = 0;
+    {
+        int base = 0;
+        for (int c0 = 0; c0 < ncl; c0 += NT) {
+            const int c = c0 + tid;
+            int n = 0;
+            uint32_t v[kFirst] = {};
+            if (c < ncl) {
+                n = cc[c];
+                if (staged) {
+#pragma unroll
+                    for (int k = 0; k < kFirst; k++) v[k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+                }
+            }
+            int tot;
+            const int off = base + oct_scan<NT>(n, sc, par, tot);
+            // the keys' home is only known once C is: stage the first slots and the offsets in the node
+            // tables' area (free until octree_level)
+            if (staged && c < ncl) {
+                uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
+#pragma unroll
+                for (int k = 0; k < kFirst; k++) stage[kFirst * c + k] = v[k];
+                reinterpret_cast<int*>(stage + kFirst * ncl)[c] = off;
+            }
+            base += tot;
+        }
+        C = base;
     }
-    int par = 0, C = 0;
-    (void)oct_scan<NT>(mine, sc, par, C);
-    // keys and their node indices live in LDS after the node tables when they fit (every round
-    // re-reads them), else in the per-level global scratch
-    if (C <= lds_keys) {
-        uint32_t* keys = reinterpret_cast<uint32_t*>(sv + 8);
-        octree_level<true, NT>(g, L, f, l, smem, C, cc, cs, keys, reinterpret_cast<uint16_t*>(keys + lds_keys), lvlKps,
-                           lvlCount, err, par, ost);
-    } else {
-        const long long o = ((long long)f * g->nlevels + l) * g->max_level_cand;
-        octree_level<false, NT>(g, L, f, l, smem, C, cc, cs, keysAll + o, knodeAll + o, lvlKps, lvlCount, err, par, ost);
+    __syncthreads();
+    const bool inLds = C <= lds_keys;
+    uint32_t* keys = inLds ? keysL : keysAll + o;
+    if (staged) {
+        const uint32_t* stage = reinterpret_cast<const uint32_t*>(smem);
+        const int c = tid;
+        if (c < ncl) {
+            const int n = cc[c], off = reinterpret_cast<const int*>(stage + kFirst * ncl)[c];
+#pragma unroll
+            for (int k = 0; k < kFirst; k++)
+                if (k < n) keys[off + k] = stage[kFirst * c + k];
+            for (int k = kFirst; k < n; k++) keys[off + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+        }
+    } else {   // many cells (large images / fine grids): one chunk of NT cells at a time
+        int base = 0;
+        for (int c0 = 0; c0 < ncl; c0 += NT) {
+            const int c = c0 + tid;
+            const int n = c < ncl ? cc[c] : 0;
+            int tot;
+            const int off = base + oct_scan<NT>(n, sc, par, tot);
+            for (int k = 0; k < n; k++) keys[off + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+            base += tot;
+        }
     }
+    if (inLds)
+        octree_level<true, NT>(g, L, f, l, smem, C, keys, reinterpret_cast<uint16_t*>(keysL + lds_keys), lvlKps, lvlCount,
+                               err, par, ost);
+    else
+        octree_level<false, NT>(g, L, f, l, smem, C, keys, knodeAll + o, lvlKps, lvlCount, err, par, ost);
 }
 
 /* ------------------------------------------------------------------------------------------------
