@@ -1111,13 +1111,14 @@ __device__ __forceinline__ int quad_mask(const int* qd) {
  * 1 past depth F) exactly as before. */
 constexpr int kFfMaxDepth = 6;
 
-// depth F of the tables: one past the first depth whose cells can hold N nodes (the round where phase 1
-// usually ends), at most what fits in `room` ints with codes in 16 bits; 0 = no fast-forward
+// depth F of the tables: the first depth whose cells can hold N nodes (phase 1 usually switches to phase 2
+// the round before, so phase 2's first round still finds its quadrant counts in the table), at most what
+// fits in `room` ints with codes in 16 bits; 0 = no fast-forward
 __device__ __forceinline__ int ff_depth(int nIni, int N, int room) {
     int F = 0, tot = 0, want = kFfMaxDepth;
     for (int d = 1; d <= kFfMaxDepth; d++)
         if ((nIni << (2 * d)) >= N) {
-            want = d + 1;
+            want = d;
             break;
         }
     for (int d = 1; d <= want && d <= kFfMaxDepth; d++) {

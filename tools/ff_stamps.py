@@ -25,7 +25,11 @@ orbgpu._lib.lib().orb_debug_fast_stamps(bx.h, st.ctypes.data, cap)
 o = st[B * NCELLS * 8:].reshape(B, NL, 32).astype(np.int64)
 for lv in range(NL):
     s = o[:, lv]
-    seq = [0, 1, 12, 13, 14, 15, 16, 2, 31]
+    seq = [0, 1, 12, 13, 14, 15, 16, 2]
     d = [np.mean(s[:, b] - s[:, a]) for a, b in zip(seq, seq[1:])]
+    # rounds after the fast-forward: stamps 3 + round at each round's end (round0 = R); the last one set
+    ends = [max(int(np.max(np.nonzero(r[3:12])[0])) if np.any(r[3:12]) else -1, -1) for r in s]
+    last = np.array([r[3 + e] if e >= 0 else r[2] for r, e in zip(s, ends)])
     print(f"level {lv}: C {s[:, 29].mean():6.0f} total {np.mean(s[:, 31] - s[:, 0]):7.0f}  gather {d[0]:6.0f} zero {d[1]:5.0f} "
-          f"A {d[2]:5.0f} B {d[3]:5.0f} C {d[4]:5.0f} D {d[5]:5.0f} E {d[6]:5.0f} rest {d[7]:6.0f}")
+          f"A {d[2]:5.0f} B {d[3]:5.0f} C {d[4]:5.0f} D {d[5]:5.0f} E+prep {d[6]:5.0f} rounds {np.mean(last - s[:, 2]):6.0f} "
+          f"best {np.mean(s[:, 31] - last):6.0f}")
