@@ -853,7 +853,7 @@ __device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int r
 template <int TQ>
 __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane,
                                                uint16_t* tile, uint16_t* sList,
-                                               uint32_t* __restrict__ cands,
+                                               uint32_t* __restrict__ cands, uint32_t* __restrict__ candFirst,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
     constexpr int PX = 16, TB = 2 * TQ;   // PX: pixels per lane and row round; TB: tile row pitch in bytes
     const int dw = c.dw, dh = c.dh;
@@ -932,8 +932,14 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 k = m > max(max(n0, n1), n2);
                 packed = (uint32_t)((p & 63) + c.xo) | ((uint32_t)((p >> 6) + c.yo) << 12) | ((uint32_t)s << 24);
             }
+            // a cell's first kCandFirst corners go to its dense record (the octree reads most cells' corners
+            // with one coalesced 16-byte load), the rest to its slots
             const unsigned long long km = __ballot(k);
-            if (k) cands[(long long)c.f * g->ncand + c.out_off + kept + lanes_below(km)] = packed;
+            const int slot = kept + lanes_below(km);
+            if (k) {
+                if (slot < kCandFirst) candFirst[((long long)c.f * g->ncells + c.cell) * kCandFirst + slot] = packed;
+                else cands[(long long)c.f * g->ncand + c.out_off + slot] = packed;
+            }
             kept += __popcll(km);
         }
         if (kept > 0 || th == g->minTh) break;
@@ -955,7 +961,8 @@ template <int TQ>
 __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, const CellDesc* __restrict__ cells,
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
-                                                   uint32_t* __restrict__ cands, int* __restrict__ cellCount, int total,
+                                                   uint32_t* __restrict__ cands, uint32_t* __restrict__ candFirst,
+                                                   int* __restrict__ cellCount, int total,
                                                    int cbeg, int cnum, unsigned long long* __restrict__ stamps,
                                                    int* __restrict__ err, int ipw) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
@@ -996,7 +1003,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         if (lane == 0) *cntOut = (int)tile[lane] & 0;
         continue;
 #endif
-        fast_cell_body<TQ>(g, c, lane, tile, sList, cands, cntOut, stamps, item);
+        fast_cell_body<TQ>(g, c, lane, tile, sList, cands, candFirst, cntOut, stamps, item);
     }
 }
 
@@ -1670,6 +1677,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
 template <int NT>   // block size: kOctreeThreads for batches, 1024 for one frame (the host path's latency)
 __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
                                                            const uint32_t* __restrict__ cands,
+                                                           const uint32_t* __restrict__ candFirst,
                                                            const int* __restrict__ cellCount,
                                                            uint32_t* __restrict__ keysAll,
                                                            uint16_t* __restrict__ knodeAll,
@@ -1690,69 +1698,91 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
     if (ost && tid == 0) ost[0] = __builtin_amdgcn_s_memtime();
 #endif
     // 1. gather the candidates in cell order (vToDistributeKeys, :818-825) in one global round trip: a
-    // thread per cell loads its count and, speculatively, its first kFirst slots together; one block scan
-    // gives the cells' offsets; the rare cell with more keys loads the rest after it.  Keys go to LDS after
+    // thread per cell loads its count and its dense record of the first kFirst corners together (two
+    // 16-byte loads: 36 B per cell instead of a line per cell); block scans give the cells'
+    // offsets; a cell with more corners loads the rest from its slots after them.  Keys go to LDS after
     // the node tables when they fit (every pass re-reads them), else to the per-level global scratch.
-    constexpr int kFirst = 4;
+    constexpr int kFirst = kCandFirst;
     const int ncl = L.nCols * L.nRows;
     const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
     const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
+    const uint4* cf = reinterpret_cast<const uint4*>(candFirst) + ((long long)f * g->ncells + L.cell_base) * 2;
+    static_assert(kCandFirst == 8, "two uint4 per cell record");
     int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
     int* sv = sc + 32;
     uint32_t* keysL = reinterpret_cast<uint32_t*>(sv + 8);
     const long long o = ((long long)f * g->nlevels + l) * g->max_level_cand;
     int par = 0;
-    // the common case: every cell in one chunk of NT, first slots + offsets staged in the node tables' area
-    const bool staged = ncl <= NT && (kFirst + 1) * ncl <= 16 * NC;
+    // the common case: at most kMaxChunks chunks of NT cells, every load issued before the first scan and
+    // the values held in registers until the keys' home (LDS or scratch, known once C is) is decided
+    constexpr int kMaxChunks = 4;
+    const int nch = (ncl + NT - 1) / NT;
     int C = 0;
-    {
-        int base = 0;
-        for (int c0 = 0; c0 < ncl; c0 += NT) {
-            const int c = c0 + tid;
-            int n = 0;
-            uint32_t v[kFirst] = {};
-            if (c < ncl) {
-                n = cc[c];
-                if (staged) {
+    bool inLds;
+    uint32_t* keys;
+    if (nch <= kMaxChunks) {
+        int n[kMaxChunks], off[kMaxChunks];
+        uint32_t v[kMaxChunks][kFirst];
 #pragma unroll
-                    for (int k = 0; k < kFirst; k++) v[k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
-                }
+        for (int j = 0; j < kMaxChunks; j++) {
+            n[j] = 0;
+#pragma unroll
+            for (int k = 0; k < kFirst; k++) v[j][k] = 0;
+            const int c = j * NT + tid;
+            if (j < nch && c < ncl) {
+                n[j] = cc[c];
+                const uint4 r0 = cf[2 * c], r1 = cf[2 * c + 1];
+                v[j][0] = r0.x;
+                v[j][1] = r0.y;
+                v[j][2] = r0.z;
+                v[j][3] = r0.w;
+                v[j][4] = r1.x;
+                v[j][5] = r1.y;
+                v[j][6] = r1.z;
+                v[j][7] = r1.w;
             }
-            int tot;
-            const int off = base + oct_scan<NT>(n, sc, par, tot);
-            // the keys' home is only known once C is: stage the first slots and the offsets in the node
-            // tables' area (free until octree_level)
-            if (staged && c < ncl) {
-                uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
+        }
 #pragma unroll
-                for (int k = 0; k < kFirst; k++) stage[kFirst * c + k] = v[k];
-                reinterpret_cast<int*>(stage + kFirst * ncl)[c] = off;
+        for (int j = 0; j < kMaxChunks; j++) {
+            if (j < nch) {   // uniform
+                int tot;
+                off[j] = C + oct_scan<NT>(n[j], sc, par, tot);
+                C += tot;
             }
-            base += tot;
         }
-        C = base;
-    }
-    __syncthreads();
-    const bool inLds = C <= lds_keys;
-    uint32_t* keys = inLds ? keysL : keysAll + o;
-    if (staged) {
-        const uint32_t* stage = reinterpret_cast<const uint32_t*>(smem);
-        const int c = tid;
-        if (c < ncl) {
-            const int n = cc[c], off = reinterpret_cast<const int*>(stage + kFirst * ncl)[c];
+        inLds = C <= lds_keys;
+        keys = inLds ? keysL : keysAll + o;
 #pragma unroll
-            for (int k = 0; k < kFirst; k++)
-                if (k < n) keys[off + k] = stage[kFirst * c + k];
-            for (int k = kFirst; k < n; k++) keys[off + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+        for (int j = 0; j < kMaxChunks; j++) {
+            const int c = j * NT + tid;
+            if (j < nch && c < ncl) {
+#pragma unroll
+                for (int k = 0; k < kFirst; k++)
+                    if (k < n[j]) keys[off[j] + k] = v[j][k];
+                for (int k = kFirst; k < n[j]; k++) keys[off[j] + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+            }
         }
-    } else {   // many cells (large images / fine grids): one chunk of NT cells at a time
+    } else {   // many cells (large images / fine grids): two passes, a chunk of NT cells at a time
         int base = 0;
         for (int c0 = 0; c0 < ncl; c0 += NT) {
             const int c = c0 + tid;
             const int n = c < ncl ? cc[c] : 0;
             int tot;
+            (void)oct_scan<NT>(n, sc, par, tot);
+            base += tot;
+        }
+        C = base;
+        inLds = C <= lds_keys;
+        keys = inLds ? keysL : keysAll + o;
+        base = 0;
+        for (int c0 = 0; c0 < ncl; c0 += NT) {
+            const int c = c0 + tid;
+            const int n = c < ncl ? cc[c] : 0;
+            int tot;
             const int off = base + oct_scan<NT>(n, sc, par, tot);
-            for (int k = 0; k < n; k++) keys[off + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+            for (int k = 0; k < n; k++)
+                keys[off + k] = k < kFirst ? candFirst[((long long)f * g->ncells + L.cell_base + c) * kFirst + k]
+                                           : cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
             base += tot;
         }
     }
@@ -2245,7 +2275,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         // a single frame (the host path's latency) takes one cell per wave: twice the waves, half each one's chain
         const int ipw = nframes == 1 ? 1 : 2;
         hipLaunchKernelGGL(kern, dim3(cdiv(items, ipw)), dim3(64), (size_t)g.fast_wave_bytes, s, b.d_geom, b.d_cells,
-                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_cellCount, items, cbeg, cnum,
+                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_candFirst, b.d_cellCount, items, cbeg, cnum,
                            b.d_stamps, zero, ipw);
     };
     auto octree = [&](int lbase, int nl, hipStream_t s) {
@@ -2255,7 +2285,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         // 512 (three blocks per CU)
         const bool one = nframes * nl <= 256;
         hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
-                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_cellCount,
+                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_candFirst, b.d_cellCount,
                            b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
                            b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
     };

@@ -57,6 +57,8 @@ struct Ctx {
     size_t cands_cap = 0;
     int* d_cellCount = nullptr;
     size_t cellc_cap = 0;
+    uint32_t* d_candFirst = nullptr;
+    size_t candfirst_cap = 0;
     uint32_t* d_keys = nullptr;
     size_t keys_cap = 0;
     uint16_t* d_knode = nullptr;
