@@ -43,7 +43,10 @@ typedef enum {
     ORB_ERR_ARG = -1,        /* bad argument / NULL pointer                                     */
     ORB_ERR_HIP = -2,        /* HIP runtime error (message via orb_last_error)                   */
     ORB_ERR_CAPACITY = -3,   /* caller buffer too small; *n receives the required count          */
-    ORB_ERR_GEOMETRY = -4,   /* image too small for the pyramid (reference: division by zero UB) */
+    ORB_ERR_GEOMETRY = -4,   /* image too small for the pyramid (reference: division by zero UB), a side
+                                above 4096 pixels (candidates pack 12-bit coordinates), or a level whose
+                                octree node tables exceed one CU's LDS (N per level above ~2,550, i.e.
+                                nfeatures above ~11,700 at scale 1.2 / 8 levels) */
     ORB_ERR_NOMEM = -5,      /* device allocation failed                                         */
     ORB_ERR_INTERNAL = -6    /* a kernel reported an overflow of an internal bound               */
 } orb_status;

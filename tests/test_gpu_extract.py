@@ -335,3 +335,39 @@ def test_c2_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
             assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
     for e in exs:
         e.close()
+
+
+@pytest.mark.parametrize("w,h,nf,kind,batch", [
+    (3840, 2160, 8000, "scene", False),   # level 0 has >4 chunks of cells: the octree's two-pass gather
+    (4096, 4096, 8000, "noise", False),   # kMaxDim: 12-bit candidate coordinates at their limit
+    (3840, 2160, 8000, "scene", True),    # the batch (graph) path at the same size
+])
+def test_maximum_sizes_bit_exact(orbgpu_mod, oracle_mod, w, h, nf, kind, batch):
+    from orbgpu.synth import synth_frame
+    img = synth_frame(w, h, 1, kind)
+    ok, od = oracle_mod.OracleExtractor(nf)(img)
+    if batch:
+        e = orbgpu_mod.BatchExtractor(nf, w, h, 2)
+        e.upload(np.stack([img, img]))
+        e.launch()
+        e.sync()
+        for f in range(2):
+            gk, gd = e.results(f)
+            assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), f
+        e.close()
+    else:
+        g = orbgpu_mod.ORBextractor(nf, 1.2, 8, 20, 7)
+        gk, gd = g(img)
+        assert len(gk) == len(ok) and gk.tobytes() == ok.tobytes() and np.array_equal(gd, od)
+
+
+def test_geometry_limits_are_errors(orbgpu_mod):
+    """The documented limits (include/orbgpu.h): a side above 4096 pixels, and a level whose
+    octree node tables would not fit one CU's LDS (level-0 N above ~2,550: nfeatures > ~11,700 at 1.2/8)."""
+    from orbgpu._lib import OrbError
+    g = orbgpu_mod.ORBextractor(1000, 1.2, 8, 20, 7)
+    with pytest.raises(OrbError):
+        g(np.zeros((480, 4097), np.uint8))
+    g = orbgpu_mod.ORBextractor(12000, 1.2, 8, 20, 7)
+    with pytest.raises(OrbError):
+        g(np.zeros((2160, 3840), np.uint8))
