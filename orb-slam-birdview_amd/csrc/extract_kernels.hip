@@ -470,41 +470,55 @@ __global__ __launch_bounds__(256) void k_pyramid_chain(const Geom* __restrict__ 
 // low bytes: CS = 2).  On the raw circle values p: the dark strength max over arcs of min (v - p) is
 // v - X with X = min over arcs of max p, the bright one Y - v with Y = max over arcs of min p, so
 // M = max(v - X, Y - v, 0) needs no per-pixel differences.
+// Both sides run in one packed chain: each circle value is held as the f16 pair (p, -p) (bit patterns;
+// p < 256 is a positive f16 denormal, -p its negation, and f16 order on them is integer order, denormals
+// preserved: float_denorm_mode_16_64 = 3), so one v_pk_maximum3_f16 takes the max of p over a 3-run in
+// the low half and the max of -p = -(min p) in the high half: the 9-arc extrema of both sides are 16 + 16
+// pk_maximum3, their min over the 16 arcs 8 pk_minimum3 (the -p negation folds into neg_hi modifiers).
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ half2_t circle_pair(int p) {   // (p, -p)
+    half2_t q = __builtin_bit_cast(half2_t, (uint32_t)p * 0x10001u);
+    q.y = -q.y;
+    return q;
+}
+__device__ __forceinline__ half2_t pk_max3h(half2_t a, half2_t b, half2_t c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+__device__ __forceinline__ half2_t pk_min3h(half2_t a, half2_t b, half2_t c) {
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+
 template <int P, int CS>
 __device__ __forceinline__ int fast_arc_strength(const uint8_t* c) {
     const int v = c[0];
-    int p[16];
-    p[0] = c[0 * CS + 3 * P];
-    p[1] = c[1 * CS + 3 * P];
-    p[2] = c[2 * CS + 2 * P];
-    p[3] = c[3 * CS + 1 * P];
-    p[4] = c[3 * CS + 0 * P];
-    p[5] = c[3 * CS + -1 * P];
-    p[6] = c[2 * CS + -2 * P];
-    p[7] = c[1 * CS + -3 * P];
-    p[8] = c[0 * CS + -3 * P];
-    p[9] = c[-1 * CS + -3 * P];
-    p[10] = c[-2 * CS + -2 * P];
-    p[11] = c[-3 * CS + -1 * P];
-    p[12] = c[-3 * CS + 0 * P];
-    p[13] = c[-3 * CS + 1 * P];
-    p[14] = c[-2 * CS + 2 * P];
-    p[15] = c[-1 * CS + 3 * P];
-    // 9-arc [k, k+8] = three 3-runs: v_min3/v_max3 over runs, then over the arcs
-    int m3[16], x3[16];
+    half2_t q[16];
+    q[0] = circle_pair(c[0 * CS + 3 * P]);
+    q[1] = circle_pair(c[1 * CS + 3 * P]);
+    q[2] = circle_pair(c[2 * CS + 2 * P]);
+    q[3] = circle_pair(c[3 * CS + 1 * P]);
+    q[4] = circle_pair(c[3 * CS + 0 * P]);
+    q[5] = circle_pair(c[3 * CS + -1 * P]);
+    q[6] = circle_pair(c[2 * CS + -2 * P]);
+    q[7] = circle_pair(c[1 * CS + -3 * P]);
+    q[8] = circle_pair(c[0 * CS + -3 * P]);
+    q[9] = circle_pair(c[-1 * CS + -3 * P]);
+    q[10] = circle_pair(c[-2 * CS + -2 * P]);
+    q[11] = circle_pair(c[-3 * CS + -1 * P]);
+    q[12] = circle_pair(c[-3 * CS + 0 * P]);
+    q[13] = circle_pair(c[-3 * CS + 1 * P]);
+    q[14] = circle_pair(c[-2 * CS + 2 * P]);
+    q[15] = circle_pair(c[-1 * CS + 3 * P]);
+    // 9-arc [k, k+8] = three 3-runs
+    half2_t x3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m3[k] = min(min(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
-        x3[k] = max(max(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
-    }
-    int X = 255, Y = 0;
+    for (int k = 0; k < 16; k++) x3[k] = pk_max3h(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
+    half2_t a = pk_max3h(x3[0], x3[3], x3[6]);
 #pragma unroll
-    for (int k = 0; k < 16; k += 2) {   // two arcs per v_min3 / v_max3
-        X = min(min(X, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15])),
-                max(max(x3[k + 1], x3[(k + 4) & 15]), x3[(k + 7) & 15]));   // dark arcs:   max p
-        Y = max(max(Y, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15])),
-                min(min(m3[k + 1], m3[(k + 4) & 15]), m3[(k + 7) & 15]));   // bright arcs: min p
-    }
+    for (int k = 1; k < 16; k += 2)   // two arcs per v_pk_minimum3
+        a = pk_min3h(a, pk_max3h(x3[k], x3[(k + 3) & 15], x3[(k + 6) & 15]),
+                     k + 1 < 16 ? pk_max3h(x3[k + 1], x3[(k + 4) & 15], x3[(k + 7) & 15]) : a);
+    const uint32_t u = __builtin_bit_cast(uint32_t, a);   // low: X = min over arcs of max p; high: -Y
+    const int X = (int)(u & 0xFFu), Y = (int)((u >> 16) & 0xFFu);
     return max(max(v - X, Y - v), 0);
 }
 
