@@ -1909,17 +1909,36 @@ template <bool ALLEVEN, bool FMA>
 __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float b, const float (&pf)[4][4], int colBase,
                                               int xsimd, ushort2_t K01, ushort2_t K23, ushort2_t K45, ushort2_t K60,
                                               int lane, unsigned long long* __restrict__ dst) {
-    const uint8_t* base = reinterpret_cast<const uint8_t*>(rt);
+    // RT's LDS byte address, biased by -2C (see below): sample addresses are 32-bit LDS offsets
+    typedef const uint32_t __attribute__((address_space(3))) lds_u32;
+    const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u32*)reinterpret_cast<const uint32_t*>(rt) - 0xAC000000u;
+    // the scalar-tail test colBase + xb < xsimd on the raw x bits (xbits = 0x4B400000 + xb)
+    const uint32_t xlim = (uint32_t)(xsimd - colBase) + 0x4B400000u;
+    const uint32_t bias = sgpr_const(32767u);
     // S + rounding bias of the blurred pixel at offset (cvRound(fx), cvRound(fy)) from the centre;
     // the blurred value is the high half
-    auto sample = [&](float fx, float fy) -> uint32_t {
+    typedef float f32x2_t __attribute__((ext_vector_type(2)));
+    const f32x2_t ab = {a, b}, nba = {-b, a}, cr = {12582930.0f, 12582930.0f};
+    // the sample offsets as the reference's -O3 -march=native build contracts them (:119-120;
+    // tools/ref_flags_probe.cpp): x = fma(px, a, -(py*b)), y = fma(px, b, py*a), both coordinates in
+    // packed f32 ops (ORB_VARIANT_NO_FMA: px * a - py * b and px * b + py * a, each product rounded; the
+    // kernels build with -ffp-contract=off)
+    auto sample = [&](f32x2_t pp) -> uint32_t {   // pp = (px, py)
+        const f32x2_t pyv = __builtin_shufflevector(pp, pp, 1, 1), pxv = __builtin_shufflevector(pp, pp, 0, 0);
+        const f32x2_t t = pyv * nba;
+        const f32x2_t r = (FMA ? __builtin_elementwise_fma(pxv, ab, t) : pxv * ab + t) + cr;
+        const float fx = r.x, fy = r.y;
         // cvRound (half-to-even) as one add: v + 1.5*2^23 rounds to an integer for |v| < 2^22, and the
-        // +18 centre offset is folded into the constant (it is even, so ties still go to even)
-        const uint32_t xb = __builtin_bit_cast(uint32_t, fx + 12582930.0f) & 0xFFFFu;
-        const uint32_t yb = __builtin_bit_cast(uint32_t, fy + 12582930.0f);
-        // RT element (xb, yb); the pitch is odd, so an element's dword parity depends on both
-        const uint32_t idx = __umul24(xb, (unsigned)kRtPitch) + (yb & 0xFFFFu);
-        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + ((idx & ~1u) << 1));
+        // +18 centre offset is folded into the constant (it is even, so ties still go to even).  The sum's
+        // bits are 0x4B400000 + xb: v_mad_u32_u24 on the raw bits (its 24-bit operand keeps 0x400000 + xb)
+        // gives RT element xb * 43 + yb plus C = 43 * 0x400000 + 0x4B400000 = 0x56000000, even, so it
+        // keeps the element's parity and cancels against lbase's -2C in the 32-bit LDS address
+        const uint32_t xbits = __builtin_bit_cast(uint32_t, fx);
+        const uint32_t ybits = __builtin_bit_cast(uint32_t, fy);
+        const uint32_t idx = __umul24(xbits, (unsigned)kRtPitch) + ybits;
+        uint32_t ie = idx & ~1u;
+        asm("" : "+v"(ie));   // keeps and + v_lshl_add (the compiler would re-form shl, and, add)
+        lds_u32* rp = (lds_u32*)(uintptr_t)(lbase + (ie << 1));
         const uint32_t sh = idx << 4;   // v_alignbit reads bits 4:0: 16 for an odd element, realigning the u16 pairs
         // 7 taps from 4 dwords: the last pair's high element has weight 0 (K60), so whatever alignbit
         // shifts into it (d3 again for an odd element) drops out -- no fifth dword
@@ -1929,21 +1948,14 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         S = __builtin_amdgcn_udot2(K45, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d3, d2, sh)), S, false);
         S = __builtin_amdgcn_udot2(K60, __builtin_bit_cast(ushort2_t, __builtin_amdgcn_alignbit(d3, d3, sh)), S, false);
         // round(S / 65536): half-to-even = (S + 32767 + q&1) >> 16, half-up = (S + 32768) >> 16
-        if (ALLEVEN) return S + 32767u + ((S >> 16) & 1u);
-        return S + (colBase + (int)xb < xsimd ? 32767u + ((S >> 16) & 1u) : 32768u);
+        if (ALLEVEN) return S + bias + ((S >> 16) & 1u);
+        return S + (xbits < xlim ? bias + ((S >> 16) & 1u) : 32768u);
     };
     unsigned long long mq[4];
 #pragma unroll
     for (int gq = 0; gq < 4; gq++) {   // test pair lane + 64 gq: (x0, y0, x1, y1) = pf[gq]
-        const float px0 = pf[gq][0], py0 = pf[gq][1], px1 = pf[gq][2], py1 = pf[gq][3];
-        // the sample offsets as the reference's -O3 -march=native build contracts them (:119-120;
-        // tools/ref_flags_probe.cpp): x = fma(px, a, -(py*b)), y = fma(px, b, py*a)
-        // (ORB_VARIANT_NO_FMA: px * a - py * b and px * b + py * a, each product rounded; the kernels build
-        // with -ffp-contract=off)
-        const uint32_t r0 = FMA ? sample(__builtin_fmaf(px0, a, -(py0 * b)), __builtin_fmaf(px0, b, py0 * a))
-                                : sample(px0 * a - py0 * b, px0 * b + py0 * a);
-        const uint32_t r1 = FMA ? sample(__builtin_fmaf(px1, a, -(py1 * b)), __builtin_fmaf(px1, b, py1 * a))
-                                : sample(px1 * a - py1 * b, px1 * b + py1 * a);
+        const uint32_t r0 = sample(f32x2_t{pf[gq][0], pf[gq][1]});
+        const uint32_t r1 = sample(f32x2_t{pf[gq][2], pf[gq][3]});
         // saturate_cast<uchar>: only the right-hand side needs the clamp (t0 = 256 compares as 255 would)
         mq[gq] = __ballot((r0 >> 16) < min(r1 >> 16, 255u));
     }
