@@ -851,9 +851,10 @@ __device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int r
         const int cnt = __popc(pm);
         const int incl = wave_incl_scan(cnt);
         int pos = nlist + incl - cnt;
-        const int base = dy * 64 + x0;
+        // entries are the pixels' byte offsets in the tile from domain pixel (0, 0): dy * 2TQ + 2x
+        const int base = dy * (2 * TQ) + 2 * x0;
         // one iteration per set bit (survivors are sparse: the wave runs max-popcount iterations)
-        for (uint32_t b = (uint32_t)pm; b; b &= b - 1) sList[pos++] = (uint16_t)(base + __builtin_ctz(b));
+        for (uint32_t b = (uint32_t)pm; b; b &= b - 1) sList[pos++] = (uint16_t)(base + 2 * __builtin_ctz(b));
         nlist += __builtin_amdgcn_readlane(incl, 63);
     }
     return nlist;
@@ -870,6 +871,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                                                uint32_t* __restrict__ cands, uint32_t* __restrict__ candFirst,
                                                int* cntOut, unsigned long long* __restrict__ stamps, int item) {
     constexpr int PX = 16, TB = 2 * TQ;   // PX: pixels per lane and row round; TB: tile row pitch in bytes
+    constexpr unsigned kRecipTB = (1u << 20) / TB + 1;
     const int dw = c.dw, dh = c.dh;
     ORBGPU_STAMP(1);
     // lane -> (run of PX = 16 pixels, row) of the prefilter, fixed for the cell (rows advance by 64 / nruns)
@@ -908,7 +910,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             int p = 0, m = 0;
             if (i < nlist) {
                 p = sList[i];
-                uint8_t* e = t0 + (p >> 6) * TB + 2 * (p & 63);
+                uint8_t* e = t0 + p;
                 m = fast_arc_strength<TB, 2>(e);
                 e[1] = (uint8_t)m;
             }
@@ -934,7 +936,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             uint32_t packed = 0;
             if (i < ncorner) {
                 const int p = sList[i];
-                const uint8_t* q = t0 + (p >> 6) * TB + 2 * (p & 63) + 1;
+                const uint8_t* q = t0 + p + 1;
                 const int m = q[0];
                 const int s = m - 1;
                 // the reference keeps score s = M - 1 iff s > sn for every neighbour, sn = Mn - 1 for a
@@ -944,7 +946,10 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const int n1 = max(max((int)q[-2], (int)q[2]), 1);
                 const int n2 = max(max((int)q[TB - 2], (int)q[TB]), (int)q[TB + 2]);
                 k = m > max(max(n0, n1), n2);
-                packed = (uint32_t)((p & 63) + c.xo) | ((uint32_t)((p >> 6) + c.yo) << 12) | ((uint32_t)s << 24);
+                // (x, y) from the byte offset: y = p / TB by a 20-bit reciprocal (exact for even p < 2^15 at
+                // TB = 96 or 160; a tile holds hCell + 6 rows, about 40), x = (p - y TB) / 2
+                const int py = (int)(__umul24((unsigned)p, kRecipTB) >> 20), px = (p - py * TB) >> 1;
+                packed = (uint32_t)(px + c.xo) | ((uint32_t)(py + c.yo) << 12) | ((uint32_t)s << 24);
             }
             // a cell's first kCandFirst corners go to its dense record (the octree reads most cells' corners
             // with one coalesced 16-byte load), the rest to its slots

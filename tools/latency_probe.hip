@@ -7,6 +7,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <cstring>
 #include <chrono>
 #include <vector>
 
@@ -78,6 +79,98 @@ int main() {
                    hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256), dim3(256), 0, s, h_in, d_out, n);
                    (void)hipStreamSynchronize(s);
                }));
+    }
+    // a C3 host image (1280 x 720 u8) as ORBextractor::operator() receives it: pageable caller memory
+    {
+        const size_t W = 1280, H = 720, bytes = W * H;
+        std::vector<uint8_t> img(bytes, 7);
+        uint8_t *d_img, *h_stage;
+        CK(hipMalloc(&d_img, bytes));
+        CK(hipHostMalloc(&h_stage, bytes, hipHostMallocDefault));
+        printf(", \"img_pageable_1d_us\": %.1f", med([&] {
+                   (void)hipMemcpyAsync(d_img, img.data(), bytes, hipMemcpyHostToDevice, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        printf(", \"img_pageable_2d_us\": %.1f", med([&] {
+                   (void)hipMemcpy2DAsync(d_img, W, img.data(), W, W, H, hipMemcpyHostToDevice, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        printf(", \"img_pageable_1d_then_kernel_us\": %.1f", med([&] {
+                   (void)hipMemcpyAsync(d_img, img.data(), bytes, hipMemcpyHostToDevice, s);
+                   hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        printf(", \"img_pageable_2d_then_kernel_us\": %.1f", med([&] {
+                   (void)hipMemcpy2DAsync(d_img, W, img.data(), W, W, H, hipMemcpyHostToDevice, s);
+                   hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        printf(", \"img_host_memcpy_to_pinned_us\": %.1f", med([&] { std::memcpy(h_stage, img.data(), bytes); }));
+        printf(", \"img_memcpy_pinned_dma_us\": %.1f", med([&] {
+                   std::memcpy(h_stage, img.data(), bytes);
+                   (void)hipMemcpyAsync(d_img, h_stage, bytes, hipMemcpyHostToDevice, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        printf(", \"img_pinned_dma_us\": %.1f", med([&] {
+                   (void)hipMemcpyAsync(d_img, h_stage, bytes, hipMemcpyHostToDevice, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        printf(", \"img_register_dma_unregister_us\": %.1f", med([&] {
+                   (void)hipHostRegister(img.data(), bytes, hipHostRegisterDefault);
+                   void* dp = nullptr;
+                   (void)hipHostGetDevicePointer(&dp, img.data(), 0);
+                   (void)hipMemcpyAsync(d_img, img.data(), bytes, hipMemcpyHostToDevice, s);
+                   (void)hipStreamSynchronize(s);
+                   (void)hipHostUnregister(img.data());
+               }));
+        printf(", \"img_memcpy_pinned_dma_then_kernel_us\": %.1f", med([&] {
+                   std::memcpy(h_stage, img.data(), bytes);
+                   (void)hipMemcpyAsync(d_img, h_stage, bytes, hipMemcpyHostToDevice, s);
+                   hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                   (void)hipStreamSynchronize(s);
+               }));
+        hipStream_t s2[4];
+        hipEvent_t ev[4];
+        for (int i = 0; i < 4; i++) {
+            CK(hipStreamCreateWithFlags(&s2[i], hipStreamNonBlocking));
+            CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+        }
+        for (int parts : {2, 4}) {
+            const size_t pb = bytes / parts;
+            printf(", \"img_pinned_dma_%dstreams_then_kernel_us\": %.1f", parts, med([&] {
+                       for (int i = 0; i < parts; i++) {
+                           (void)hipMemcpyAsync(d_img + i * pb, h_stage + i * pb, pb, hipMemcpyHostToDevice, s2[i]);
+                           (void)hipEventRecord(ev[i], s2[i]);
+                           (void)hipStreamWaitEvent(s, ev[i], 0);
+                       }
+                       hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                       (void)hipStreamSynchronize(s);
+                   }));
+            printf(", \"img_memcpy_pinned_dma_%dstreams_then_kernel_us\": %.1f", parts, med([&] {
+                       for (int i = 0; i < parts; i++) {
+                           std::memcpy(h_stage + i * pb, img.data() + i * pb, pb);
+                           (void)hipMemcpyAsync(d_img + i * pb, h_stage + i * pb, pb, hipMemcpyHostToDevice, s2[i]);
+                           (void)hipEventRecord(ev[i], s2[i]);
+                           (void)hipStreamWaitEvent(s, ev[i], 0);
+                       }
+                       hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                       (void)hipStreamSynchronize(s);
+                   }));
+            printf(", \"img_memcpy_pinned_dma_%dchunks_1stream_then_kernel_us\": %.1f", parts, med([&] {
+                       for (int i = 0; i < parts; i++) {
+                           std::memcpy(h_stage + i * pb, img.data() + i * pb, pb);
+                           (void)hipMemcpyAsync(d_img + i * pb, h_stage + i * pb, pb, hipMemcpyHostToDevice, s);
+                       }
+                       hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                       (void)hipStreamSynchronize(s);
+                   }));
+        }
+        printf(", \"img_kernel_reads_pinned_us\": %.1f", med([&] {
+                   hipLaunchKernelGGL(k_touch, dim3((int)(bytes / 4 + 255) / 256), dim3(256), 0, s, (const int*)h_stage, (int*)d_img, (int)(bytes / 4));
+                   (void)hipStreamSynchronize(s);
+               }));
+        (void)hipFree(d_img);
+        (void)hipHostFree(h_stage);
     }
     printf("}\n");
     return 0;
