@@ -797,7 +797,7 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef const u32x2_t __attribute__((address_space(3))) lds_cu32x2;
 typedef const uint32x4_t __attribute__((address_space(3))) lds_cu32x4;
 
-template <int TQ, bool CLEAN>   // CLEAN: drop the high bytes (a pass-0 arc strength may sit there)
+template <int TQ>   // the tile's high bytes are 0 here (pass 1 clears pass 0's arc strengths first)
 __device__ __forceinline__ uint32_t prefilter16(lds_cu32* w, uint32_t tt) {   // w: element dy * TQ + x0
     static_assert(TQ % 8 == 0, "tile rows must keep 16-byte alignment");
     const uint32x4_t c0 = *(lds_cu32x4*)(w + 3 * TQ / 2), c1 = *(lds_cu32x4*)(w + 3 * TQ / 2 + 4);
@@ -807,15 +807,6 @@ __device__ __forceinline__ uint32_t prefilter16(lds_cu32* w, uint32_t tt) {   //
     const u32x2_t m0 = *(volatile lds_cu32x2*)(w + 2), m1 = *(volatile lds_cu32x2*)(w + 4);
     uint32_t D[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
     uint32_t P[4] = {p0[0], p0[1], p1[0], p1[1]}, M[4] = {m0[0], m0[1], m1[0], m1[1]};
-    if (CLEAN) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) D[j] &= 0x00FF00FFu;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            P[j] &= 0x00FF00FFu;
-            M[j] &= 0x00FF00FFu;
-        }
-    }
     uint32_t r[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -835,7 +826,7 @@ __device__ __forceinline__ uint32_t prefilter16(lds_cu32* w, uint32_t tt) {   //
 // Stage 1 of a cell at threshold tt: the prefilter over every domain row, survivors compacted into
 // sList in raster order (one wave prefix sum of the per-lane counts per row round, then each lane
 // writes its entries at its offset).  Returns the list length.
-template <int TQ, bool CLEAN>
+template <int TQ>
 __device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int rpi, int lrow, bool lane_on, int x0,
                                               uint32_t xvalid, uint32_t tt, uint16_t* sList) {
     int nlist = 0;
@@ -846,7 +837,7 @@ __device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int r
             // one VGPR address per row round (the asm keeps the compiler from re-deriving it per load)
             lds_cu32* w = (lds_cu32*)(t32 + r0 * (TQ / 2));
             asm volatile("" : "+v"(w));
-            pm = (int)((prefilter16<TQ, CLEAN>(w, tt) | (prefilter16<TQ, CLEAN>(w + 4, tt) << 8)) & xvalid);
+            pm = (int)((prefilter16<TQ>(w, tt) | (prefilter16<TQ>(w + 4, tt) << 8)) & xvalid);
         }
         const int cnt = __popc(pm);
         const int incl = wave_incl_scan(cnt);
@@ -885,17 +876,16 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
     uint8_t* t0 = reinterpret_cast<uint8_t*>(&tile[3 * TQ + 4]);   // domain pixel (0, 0), low byte
     // Pass 0 runs the whole cell at iniThFAST; only a cell left with no keypoint (:812-816) runs pass 1
     // at minThFAST.  The prefilter is a necessary condition for M > th at the pass threshold, so a
-    // pass only scores the pixels that can matter at its threshold: everything else reads 0 in the map
-    // (M <= th counts 0 in the NMS), and pass 1's survivors are a superset that overwrites pass 0's
-    // (pass 1's prefilter masks the high bytes pass 0 wrote).
+    // pass only scores the pixels that can matter at its threshold, and only its corners (M > th) are
+    // written to the map: everything else reads 0 (M <= th counts 0 in the NMS).  Before pass 1 the
+    // pass-0 corners (the list NMS ran over) are cleared, so its prefilter reads clean pixel pairs.
     int th = g->iniTh;
     int kept = 0;
     for (int pass = 0; pass < 2; pass++) {
         // ---- stage 1: compass prefilter at th, 8 pixels per lane as 16-bit pixel pairs, survivors
         // compacted into sList by one wave scan
         const uint32_t tt = (uint32_t)th | ((uint32_t)th << 16);
-        const int nlist = pass == 0 ? prefilter_cell<TQ, false>(t32, dh, rpi, lrow, lane_on, x0, xvalid, tt, sList)
-                                    : prefilter_cell<TQ, true>(t32, dh, rpi, lrow, lane_on, x0, xvalid, tt, sList);
+        const int nlist = prefilter_cell<TQ>(t32, dh, rpi, lrow, lane_on, x0, xvalid, tt, sList);
         wave_lds_sync();
         ORBGPU_STAMP(2);
 #if defined(ORBGPU_FAST_CUT) && ORBGPU_FAST_CUT == 2
@@ -910,13 +900,14 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             int p = 0, m = 0;
             if (i < nlist) {
                 p = sList[i];
-                uint8_t* e = t0 + p;
-                m = fast_arc_strength<TB, 2>(e);
-                e[1] = (uint8_t)m;
+                m = fast_arc_strength<TB, 2>(t0 + p);
             }
             const bool corner = m > th;
             const unsigned long long cm = __ballot(corner);
-            if (corner) sList[ncorner + lanes_below(cm)] = (uint16_t)p;
+            if (corner) {
+                t0[p + 1] = (uint8_t)m;
+                sList[ncorner + lanes_below(cm)] = (uint16_t)p;
+            }
             ncorner += __popcll(cm);
         }
         wave_lds_sync();
@@ -963,6 +954,7 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         }
         if (kept > 0 || th == g->minTh) break;
         th = g->minTh;   // nothing kept: nothing was emitted
+        for (int i = lane; i < ncorner; i += 64) t0[sList[i] + 1] = 0;   // pass 0's map entries
         wave_lds_sync();
     }
     ORBGPU_STAMP(4);
