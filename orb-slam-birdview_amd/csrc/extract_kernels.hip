@@ -1990,13 +1990,18 @@ __device__ __forceinline__ GaussShift gauss_shift(const int* gk) {
 
 // k_describe row pass, 8 rounds of one lane: RT[4gq + o][wy] = sum_t k_t * window[wy][SH + 4gq + o + t]
 // (the window row starts SH bytes into its first dword)
+// RT and the window share the wave's LDS (kDescWinOff): every RT store lands in window rows 0..5, which
+// round 0 reads.  So round 0 reads through rw0 (ordered before the stores), rounds 1..7 through the
+// restrict rw1 (nothing stored aliases them: their loads may be scheduled past earlier rounds' stores).
+// full: the lane's four columns are all stored (column group 9 keeps only column 36: BRIEF reads 0..36).
 template <int SH>
-__device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, const GaussShift& K, bool last) {
+__device__ __forceinline__ void desc_row_pass(const uint32_t* rw0, const uint32_t* __restrict__ rw1, uint16_t* rq,
+                                              const GaussShift& K, bool last, bool full) {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         uint32_t w[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) w[i] = rw[72 * r + i];
+        for (int i = 0; i < 4; i++) w[i] = r == 0 ? rw0[i] : rw1[72 * r + i];
         // the four outputs' dot4 chains interleaved level by level (independent neighbours, no dependent
         // back-to-back v_dot4 that needs wait states)
         uint32_t acc[4];
@@ -2009,7 +2014,8 @@ __device__ __forceinline__ void desc_row_pass(const uint32_t* rw, uint16_t* rq, 
             if (((SH + o) & 3) >= 2) acc[o] = __builtin_amdgcn_udot4(w[((SH + o) >> 2) + 2], K.kc[(SH + o) & 3], acc[o], false);
         if (r < 7 || last) {   // round 7: only row 42 (RT rows stop at 42: pitch 43)
 #pragma unroll
-            for (int o = 0; o < 4; o++) rq[o * kRtPitch + 6 * r] = (uint16_t)acc[o];
+            for (int o = 0; o < 4; o++)
+                if (o == 0 || full) rq[o * kRtPitch + 6 * r] = (uint16_t)acc[o];
         }
     }
 }
@@ -2116,10 +2122,10 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
         const uint32_t* rw = w32 + wy0 * 12 + gq;
         uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy0;   // RT[4gq + j][wy]
         switch (sh) {
-            case 0: desc_row_pass<0>(rw, rq, K, wy0 == 0); break;
-            case 1: desc_row_pass<1>(rw, rq, K, wy0 == 0); break;
-            case 2: desc_row_pass<2>(rw, rq, K, wy0 == 0); break;
-            default: desc_row_pass<3>(rw, rq, K, wy0 == 0); break;
+            case 0: desc_row_pass<0>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
+            case 1: desc_row_pass<1>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
+            case 2: desc_row_pass<2>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
+            default: desc_row_pass<3>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
         }
     }
     wave_lds_sync();
@@ -2182,6 +2188,16 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 /* Fused IC angle + 7x7 blur + rBRIEF, one wavefront per keypoint slot; a wavefront owns two consecutive
  * slots and issues the second interior window's loads before processing the first. */
 constexpr int kDescWaves = 4, kDescSlotsPerWave = 2;
+// Per-wave LDS: RT (kDescRtCols columns of kRtPitch u16) from offset 0, the 43 x 48 window from kDescWinOff,
+// overlapping RT's tail by less than six window rows: every RT store lands in window rows 0..5, which only
+// round 0 of the row pass reads (before any store; IC_Angle reads rows 6..36), checked below.  4,960 B per
+// wave instead of 5,520: 8 workgroups (32 waves) per CU instead of 7.
+constexpr int kDescRtCols = 37, kDescWinOff = 2896, kDescWaveBytes = kDescWinOff + kDescWin * kDescWinPitch;
+constexpr bool desc_overlap_ok() {
+    return 2 * kRtPitch * kDescRtCols <= kDescWinOff + 6 * kDescWinPitch && kDescWinOff % 16 == 0 &&
+           kDescWaveBytes % 16 == 0 && kDescWaves * kDescWaveBytes + 256 <= 160 * 1024 / 8;
+}
+static_assert(desc_overlap_ok(), "k_describe LDS overlap");
 template <bool FMA>   // false: ORB_VARIANT_NO_FMA
 __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
@@ -2189,10 +2205,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
                                                   unsigned long long* __restrict__ dstamps, int spw) {
-    // per wave: 43x48 window (+16 B pad) and the transposed row-pass sums RT[rx][wy] (u16, 40 x kRtPitch;
-    // an odd pitch spreads the transposed stores of the 10 column groups over distinct banks)
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[kDescWaves][kDescWin * kDescWinPitch + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t s_rt[kDescWaves][40 * kRtPitch];
+    // per wave: the transposed row-pass sums RT[rx][wy] (u16, 37 x kRtPitch; an odd pitch spreads the
+    // transposed stores of the 10 column groups over distinct banks) and the 43x48 window overlapping RT's
+    // tail (kDescWinOff); 256 B past the last wave for the row pass's reads of rows 43..47
+    __shared__ __attribute__((aligned(16))) uint8_t s_desc[kDescWaves * kDescWaveBytes + 256];
+    uint8_t* const s_wave = s_desc + (size_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kDescWaveBytes;
     // 1-D grid, blocks dealt round-robin over the 8 XCDs: XCD x takes a contiguous run of the (frame,
     // slot-block) sequence, so a frame's windows are fetched into one L2 (PMC: 0.71 GB per 256 C3
     // frames against 1.96 GB with the frames spread over every XCD)
@@ -2227,11 +2244,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, co
     if (d0.ok && d0.interior) desc_issue(d0, lane, v0);
     if (d1.ok && d1.interior) desc_issue(d1, lane, v1);
     write_n();   // (after the window loads are issued)
-    if (d0.ok) desc_body<FMA>(g, d0, f, lane, v0, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
+    if (d0.ok) desc_body<FMA>(g, d0, f, lane, v0, s_wave + kDescWinOff, reinterpret_cast<uint16_t*>(s_wave), outK, outD, kpCap, dstamps);
     if (d1.ok) {
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();   // the first keypoint's LDS reads precede these window stores
-        desc_body<FMA>(g, d1, f, lane, v1, s_win[wv], s_rt[wv], outK, outD, kpCap, dstamps);
+        desc_body<FMA>(g, d1, f, lane, v1, s_wave + kDescWinOff, reinterpret_cast<uint16_t*>(s_wave), outK, outD, kpCap, dstamps);
     }
 }
 
