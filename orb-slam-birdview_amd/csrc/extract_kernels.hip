@@ -1837,6 +1837,17 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {   // cv::fastAta
 
 
 
+// Per-wave LDS: RT (kDescRtCols columns of kRtPitch u16) from offset 0, the 43 x 48 window from kDescWinOff,
+// overlapping RT's tail by less than six window rows: every RT store lands in window rows 0..5, which only
+// the row pass's first row tile reads (before any store; IC_Angle reads rows 6..36), checked below.  5,040 B
+// per wave instead of 5,520: 8 workgroups (32 waves) per CU instead of 7.
+constexpr int kDescRtCols = 37, kDescWinOff = 2976, kDescWaveBytes = kDescWinOff + kDescWin * kDescWinPitch;
+constexpr bool desc_overlap_ok() {
+    return 2 * kRtPitch * kDescRtCols <= kDescWinOff + 6 * kDescWinPitch && kDescWinOff % 16 == 0 &&
+           kDescWaveBytes % 16 == 0 && 4 * kDescWaveBytes + 256 <= 160 * 1024 / 8;
+}
+static_assert(desc_overlap_ok(), "k_describe LDS overlap");
+
 // One keypoint slot of k_describe: decoded from the octree output (level, coordinates, output index).
 struct DescSlot {
     bool ok, interior;   // a keypoint; its 48-byte aligned window rows stay inside the level (dword loads)
@@ -1906,9 +1917,11 @@ template <bool ALLEVEN, bool FMA>
 __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float b, const float (&pf)[4][4], int colBase,
                                               int xsimd, ushort2_t K01, ushort2_t K23, ushort2_t K45, ushort2_t K60,
                                               int lane, unsigned long long* __restrict__ dst) {
-    // RT's LDS byte address, biased by -2C (see below): sample addresses are 32-bit LDS offsets
+    // RT's LDS byte address, biased by -2kC (see below): sample addresses are 32-bit LDS offsets
     typedef const uint32_t __attribute__((address_space(3))) lds_u32;
-    const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u32*)reinterpret_cast<const uint32_t*>(rt) - 0xAC000000u;
+    constexpr uint32_t kC = (uint32_t)kRtPitch * 0x400000u + 0x4B400000u;   // even (see below)
+    static_assert((kC & 1u) == 0, "the element bias must keep the parity");
+    const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u32*)reinterpret_cast<const uint32_t*>(rt) - 2u * kC;
     // the scalar-tail test colBase + xb < xsimd on the raw x bits (xbits = 0x4B400000 + xb)
     const uint32_t xlim = (uint32_t)(xsimd - colBase) + 0x4B400000u;
     const uint32_t bias = sgpr_const(32767u);
@@ -1928,7 +1941,7 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
         // cvRound (half-to-even) as one add: v + 1.5*2^23 rounds to an integer for |v| < 2^22, and the
         // +18 centre offset is folded into the constant (it is even, so ties still go to even).  The sum's
         // bits are 0x4B400000 + xb: v_mad_u32_u24 on the raw bits (its 24-bit operand keeps 0x400000 + xb)
-        // gives RT element xb * 43 + yb plus C = 43 * 0x400000 + 0x4B400000 = 0x56000000, even, so it
+        // gives RT element xb * kRtPitch + yb plus kC = kRtPitch * 0x400000 + 0x4B400000, even, so it
         // keeps the element's parity and cancels against lbase's -2C in the 32-bit LDS address
         const uint32_t xbits = __builtin_bit_cast(uint32_t, fx);
         const uint32_t ybits = __builtin_bit_cast(uint32_t, fy);
@@ -2108,24 +2121,44 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
     return;
 #endif
 
-    // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass: item = (row wy, 4 outputs
-    // rx = 4g..4g+3) over window bytes 4g..4g+9; output o = v_dot4(bytes o..o+3, k0..k3) +
-    // v_dot4(bytes o+4..o+7, k4 k5 k6 0) (the 8-bit taps sum to 257, so every sum fits 16 bits).
-    const GaussShift K = gauss_shift(g->gk);
-    // lane = (row wy0 = lane / 10, group gq = lane % 10), round r takes row wy0 + 6r: the read and store
-    // addresses are the lane's base plus immediate offsets.  8 rounds cover rows 0..47; rows 43..47 are
-    // computed (from reads past the window, inside the workgroup's LDS) but not stored: RT's pitch is 43.
-    // The window shift sh is wave-uniform: one instantiation per value, so output
-    // o's byte runs start at the compile-time offset sh + o (aligned runs need no v_alignbyte).
-    if (lane < 60) {
-        const int wy0 = (int)(__umul24((unsigned)lane, 205u) >> 11), gq = lane - wy0 * 10;   // lane / 10, lane < 60
-        const uint32_t* rw = w32 + wy0 * 12 + gq;
-        uint16_t* rq = rt + __umul24((unsigned)gq, 4u * kRtPitch) + wy0;   // RT[4gq + j][wy]
-        switch (sh) {
-            case 0: desc_row_pass<0>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
-            case 1: desc_row_pass<1>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
-            case 2: desc_row_pass<2>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
-            default: desc_row_pass<3>(rw, rw, rq, K, wy0 == 0, gq < 9); break;
+    // ---- GaussianBlur 7x7 sigma 2 (:1085-1086), exact integer row pass on the matrix cores: RT[c][y] =
+    // sum_t k_t * window[y][sh + c + t] is D = W T with W the window (43 x 64 bytes: row y's 48 loaded bytes,
+    // the rest of the K range meets zero taps) and T the banded tap matrix (Geom::desc_taps, per sh).  Nine
+    // v_mfma_i32_16x16x64_i8 (y and c in tiles of 16); the window bytes are signed by ^ 0x80 (i8 operands)
+    // and the accumulator starts at 128 * sum(k) = 128 * 257, which restores the unsigned sums exactly
+    // (every sum < 2^16).  Lane l holds W[y = 16 ty + (l & 15)][16 (l >> 4) .. + 15] (one 16-byte LDS read)
+    // and, of D, column c = 16 tc + (l & 15) at rows 4 (l >> 4) .. + 3: four u16 of RT's column c, one
+    // 8-byte store (kRtPitch even).
+    {
+        typedef int v4i_t __attribute__((ext_vector_type(4)));
+        const int4* tp = g->desc_taps + sh * kDescTapTiles * 64 + lane;
+        v4i_t bt[kDescTapTiles];
+#pragma unroll
+        for (int tc = 0; tc < kDescTapTiles; tc++) {
+            const int4 q = tp[tc * 64];
+            bt[tc] = v4i_t{q.x, q.y, q.z, q.w};
+        }
+        const int yl = lane & 15, kq = lane >> 4;
+        const int bias = 128 * (g->gk[0] + g->gk[1] + g->gk[2] + g->gk[3] + g->gk[4] + g->gk[5] + g->gk[6]);
+#pragma unroll
+        for (int ty = 0; ty < 3; ty++) {
+            const int y = min(16 * ty + yl, kDescWin - 1);   // rows 43..47 repeat row 42 (not stored)
+            const uint4 w = *reinterpret_cast<const uint4*>(wbase + y * kDescWinPitch + 16 * kq);
+            const v4i_t a = v4i_t{(int)(w.x ^ 0x80808080u), (int)(w.y ^ 0x80808080u), (int)(w.z ^ 0x80808080u),
+                                  (int)(w.w ^ 0x80808080u)};
+            const int y0 = 16 * ty + 4 * kq;   // this lane's first D row
+#pragma unroll
+            for (int tc = 0; tc < kDescTapTiles; tc++) {
+                v4i_t d = v4i_t{bias, bias, bias, bias};
+                d = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bt[tc], d, 0, 0, 0);
+                const int c = 16 * tc + yl;
+                if (y0 < kDescWin && c < kDescRtCols) {   // (row 43 of the last group lands in the column's pad)
+                    uint2 pk;
+                    pk.x = (uint32_t)(d[0] & 0xFFFF) | ((uint32_t)d[1] << 16);
+                    pk.y = (uint32_t)(d[2] & 0xFFFF) | ((uint32_t)d[3] << 16);
+                    *reinterpret_cast<uint2*>(rt + c * kRtPitch + y0) = pk;
+                }
+            }
         }
     }
     wave_lds_sync();
@@ -2188,18 +2221,8 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
 /* Fused IC angle + 7x7 blur + rBRIEF, one wavefront per keypoint slot; a wavefront owns two consecutive
  * slots and issues the second interior window's loads before processing the first. */
 constexpr int kDescWaves = 4, kDescSlotsPerWave = 2;
-// Per-wave LDS: RT (kDescRtCols columns of kRtPitch u16) from offset 0, the 43 x 48 window from kDescWinOff,
-// overlapping RT's tail by less than six window rows: every RT store lands in window rows 0..5, which only
-// round 0 of the row pass reads (before any store; IC_Angle reads rows 6..36), checked below.  4,960 B per
-// wave instead of 5,520: 8 workgroups (32 waves) per CU instead of 7.
-constexpr int kDescRtCols = 37, kDescWinOff = 2896, kDescWaveBytes = kDescWinOff + kDescWin * kDescWinPitch;
-constexpr bool desc_overlap_ok() {
-    return 2 * kRtPitch * kDescRtCols <= kDescWinOff + 6 * kDescWinPitch && kDescWinOff % 16 == 0 &&
-           kDescWaveBytes % 16 == 0 && kDescWaves * kDescWaveBytes + 256 <= 160 * 1024 / 8;
-}
-static_assert(desc_overlap_ok(), "k_describe LDS overlap");
 template <bool FMA>   // false: ORB_VARIANT_NO_FMA
-__global__ __launch_bounds__(256) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_describe(const Geom* __restrict__ g, const uint8_t* __restrict__ frames,
                                                   long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,

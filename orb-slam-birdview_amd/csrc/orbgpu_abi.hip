@@ -109,6 +109,16 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
     g.variant = c->p.variant;
     for (int i = 0; i < 16; i++) g.umax[i] = c->umax[i];
     for (int i = 0; i < 7; i++) g.gk[i] = c->gk[i];
+    for (int sh = 0; sh < 4; sh++)   // k_describe's MFMA tap fragments (Geom::desc_taps)
+        for (int tc = 0; tc < kDescTapTiles; tc++)
+            for (int l = 0; l < 64; l++) {
+                uint8_t b[16];
+                for (int e = 0; e < 16; e++) {
+                    const int t = 16 * (l >> 4) + e - sh - (16 * tc + (l & 15));
+                    b[e] = (uint8_t)(t >= 0 && t <= 6 ? c->gk[t] : 0);
+                }
+                std::memcpy(&g.desc_taps[(sh * kDescTapTiles + tc) * 64 + l], b, 16);
+            }
     long long pyr = 0;
     int cells = 0, cand = 0, kpc = 0, maxN = 0, maxNini = 0, maxLevelCand = 0;
     coefs.clear();

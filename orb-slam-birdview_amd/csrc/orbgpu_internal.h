@@ -22,8 +22,9 @@ constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3
 constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as aligned dwords
 constexpr int kDescBlur = 37;         // blurred window: radius 18
 constexpr int kDescBlurPitch = 40;
-constexpr int kRtPitch = 43;          // k_describe row-pass sums, u16 per transposed row (43 rows, odd: the row
-                                      // pass's transposed u16 stores of 10 column groups hit distinct banks)
+constexpr int kRtPitch = 44;          // k_describe row-pass sums RT[column][row], u16, 43 rows + 1 (even: the
+                                      // MFMA row pass stores four rows of a column as one 8-byte write)
+constexpr int kDescTapTiles = 3;      // k_describe MFMA row pass: 16-column tiles of RT (37 columns used)
 constexpr int kRsTileW = 128;         // k_resize_tiled<TH>: output tile 128 x TH, 4 px per thread
 constexpr int kRsPitch = 272;         // LDS source tile: up to 272 bytes (from a 16-B aligned column) x (2*TH + 8) rows
 constexpr int rs_rows(int th) { return 2 * th + 8; }
@@ -67,6 +68,10 @@ struct Geom {
     int umax[16];        // ORBextractor.cc:454-469
     int gk[8];           // 7-tap Gaussian, sigma 2, 8-bit fixed point (getGaussianKernel x 256)
     LevelGeom L[ORBGPU_MAX_LEVELS];
+    // k_describe's row pass as int8 MFMA (v_mfma_i32_16x16x64_i8): the B fragments of the banded tap matrix
+    // T[k][c] = gk[k - sh - c] (0 <= k - sh - c <= 6, else 0) for window shift sh, column tile tc and lane l:
+    // bytes e = 0..15 of desc_taps[(sh * kDescTapTiles + tc) * 64 + l] are T[16 (l >> 4) + e][16 tc + (l & 15)]
+    int4 desc_taps[4 * kDescTapTiles * 64];
 };
 
 // Per-cell descriptor of the FAST grid (host-built once per image size; k_fast_wave reads one per
