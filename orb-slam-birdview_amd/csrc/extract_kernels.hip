@@ -2153,9 +2153,9 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
                 d = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bt[tc], d, 0, 0, 0);
                 const int c = 16 * tc + yl;
                 if (y0 < kDescWin && c < kDescRtCols) {   // (row 43 of the last group lands in the column's pad)
-                    uint2 pk;
-                    pk.x = (uint32_t)(d[0] & 0xFFFF) | ((uint32_t)d[1] << 16);
-                    pk.y = (uint32_t)(d[2] & 0xFFFF) | ((uint32_t)d[3] << 16);
+                    uint2 pk;   // the low halves of two results per dword: one v_perm each
+                    pk.x = __builtin_amdgcn_perm((uint32_t)d[1], (uint32_t)d[0], 0x05040100u);
+                    pk.y = __builtin_amdgcn_perm((uint32_t)d[3], (uint32_t)d[2], 0x05040100u);
                     *reinterpret_cast<uint2*>(rt + c * kRtPitch + y0) = pk;
                 }
             }
