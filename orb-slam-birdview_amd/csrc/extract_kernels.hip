@@ -942,12 +942,12 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
                 const int py = (int)(__umul24((unsigned)p, kRecipTB) >> 20), px = (p - py * TB) >> 1;
                 packed = (uint32_t)(px + c.xo) | ((uint32_t)(py + c.yo) << 12) | ((uint32_t)s << 24);
             }
-            // a cell's first kCandFirst corners go to its dense record (the octree reads most cells' corners
-            // with one coalesced 16-byte load), the rest to its slots
+            // a cell's first kCandFirst corners go to its dense record after the count (the octree reads most
+            // cells' count and corners with two coalesced 16-byte loads), the rest to its slots
             const unsigned long long km = __ballot(k);
             const int slot = kept + lanes_below(km);
             if (k) {
-                if (slot < kCandFirst) candFirst[((long long)c.f * g->ncells + c.cell) * kCandFirst + slot] = packed;
+                if (slot < kCandFirst) candFirst[((long long)c.f * g->ncells + c.cell) * kCandRec + 1 + slot] = packed;
                 else cands[(long long)c.f * g->ncand + c.out_off + slot] = packed;
             }
             kept += __popcll(km);
@@ -973,7 +973,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
                                                    const uint8_t* __restrict__ frames,
                                                    long long framePitch, int rowStride, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ cands, uint32_t* __restrict__ candFirst,
-                                                   int* __restrict__ cellCount, int total,
+                                                   int total,
                                                    int cbeg, int cnum, unsigned long long* __restrict__ stamps,
                                                    int* __restrict__ err, int ipw) {
     extern __shared__ __attribute__((aligned(16))) int smem_fast[];
@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
         if (k == 1 && !has1) break;
         const FastCellT& c = k == 0 ? c0 : c1;
         const int item = item0 + k;
-        int* cntOut = cellCount + (long long)c.f * g->ncells + c.cell;
+        int* cntOut = reinterpret_cast<int*>(candFirst + ((long long)c.f * g->ncells + c.cell) * kCandRec);   // record[0]
         if (!c.valid) {
             if (lane == 0) *cntOut = 0;
             continue;
@@ -1689,7 +1689,6 @@ template <int NT>   // block size: kOctreeThreads for batches, 1024 for one fram
 __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
                                                            const uint32_t* __restrict__ cands,
                                                            const uint32_t* __restrict__ candFirst,
-                                                           const int* __restrict__ cellCount,
                                                            uint32_t* __restrict__ keysAll,
                                                            uint16_t* __restrict__ knodeAll,
                                                            uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
@@ -1709,16 +1708,16 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
     if (ost && tid == 0) ost[0] = __builtin_amdgcn_s_memtime();
 #endif
     // 1. gather the candidates in cell order (vToDistributeKeys, :818-825) in one global round trip: a
-    // thread per cell loads its count and its dense record of the first kFirst corners together (two
-    // 16-byte loads: 36 B per cell instead of a line per cell); block scans give the cells'
-    // offsets; a cell with more corners loads the rest from its slots after them.  Keys go to LDS after
-    // the node tables when they fit (every pass re-reads them), else to the per-level global scratch.
+    // thread per cell loads its record, the corner count and the first kFirst corners (two 16-byte loads:
+    // 32 B per cell instead of a line per cell); block scans give the cells' offsets; a cell
+    // with more corners loads the rest from its slots after them.  Keys go to LDS after the node tables
+    // when they fit (every pass re-reads them), else to the per-level global scratch.
     constexpr int kFirst = kCandFirst;
     const int ncl = L.nCols * L.nRows;
-    const int* cc = cellCount + (long long)f * g->ncells + L.cell_base;
     const uint32_t* cs = cands + (long long)f * g->ncand + L.cand_base;
     const uint4* cf = reinterpret_cast<const uint4*>(candFirst) + ((long long)f * g->ncells + L.cell_base) * 2;
-    static_assert(kCandFirst == 8, "two uint4 per cell record");
+    const uint32_t* cr = candFirst + ((long long)f * g->ncells + L.cell_base) * kCandRec;
+    static_assert(kCandRec == 8, "two uint4 per cell record");
     int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
     int* sv = sc + 32;
     uint32_t* keysL = reinterpret_cast<uint32_t*>(sv + 8);
@@ -1741,16 +1740,15 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
             for (int k = 0; k < kFirst; k++) v[j][k] = 0;
             const int c = j * NT + tid;
             if (j < nch && c < ncl) {
-                n[j] = cc[c];
                 const uint4 r0 = cf[2 * c], r1 = cf[2 * c + 1];
-                v[j][0] = r0.x;
-                v[j][1] = r0.y;
-                v[j][2] = r0.z;
-                v[j][3] = r0.w;
-                v[j][4] = r1.x;
-                v[j][5] = r1.y;
-                v[j][6] = r1.z;
-                v[j][7] = r1.w;
+                n[j] = (int)r0.x;
+                v[j][0] = r0.y;
+                v[j][1] = r0.z;
+                v[j][2] = r0.w;
+                v[j][3] = r1.x;
+                v[j][4] = r1.y;
+                v[j][5] = r1.z;
+                v[j][6] = r1.w;
             }
         }
 #pragma unroll
@@ -1777,7 +1775,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
         int base = 0;
         for (int c0 = 0; c0 < ncl; c0 += NT) {
             const int c = c0 + tid;
-            const int n = c < ncl ? cc[c] : 0;
+            const int n = c < ncl ? (int)cr[(long long)c * kCandRec] : 0;
             int tot;
             (void)oct_scan<NT>(n, sc, par, tot);
             base += tot;
@@ -1788,11 +1786,11 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
         base = 0;
         for (int c0 = 0; c0 < ncl; c0 += NT) {
             const int c = c0 + tid;
-            const int n = c < ncl ? cc[c] : 0;
+            const int n = c < ncl ? (int)cr[(long long)c * kCandRec] : 0;
             int tot;
             const int off = base + oct_scan<NT>(n, sc, par, tot);
             for (int k = 0; k < n; k++)
-                keys[off + k] = k < kFirst ? candFirst[((long long)f * g->ncells + L.cell_base + c) * kFirst + k]
+                keys[off + k] = k < kFirst ? cr[(long long)c * kCandRec + 1 + k]
                                            : cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
             base += tot;
         }
@@ -2338,7 +2336,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         // a single frame (the host path's latency) takes one cell per wave: twice the waves, half each one's chain
         const int ipw = nframes == 1 ? 1 : 2;
         hipLaunchKernelGGL(kern, dim3(cdiv(items, ipw)), dim3(64), (size_t)g.fast_wave_bytes, s, b.d_geom, b.d_cells,
-                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_candFirst, b.d_cellCount, items, cbeg, cnum,
+                           d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_candFirst, items, cbeg, cnum,
                            b.d_stamps, zero, ipw);
     };
     auto octree = [&](int lbase, int nl, hipStream_t s) {
@@ -2348,7 +2346,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         // 512 (three blocks per CU)
         const bool one = nframes * nl <= 256;
         hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
-                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_candFirst, b.d_cellCount,
+                           octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_candFirst,
                            b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
                            b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
     };

@@ -319,8 +319,7 @@ int Ctx::ensure_frames(int nframes) {
     const size_t nl = g.nlevels;
     if ((e = grow(d_pyr, pyr_cap, (size_t)nframes * g.pyr_bytes)) != hipSuccess ||
         (e = grow(d_cands, cands_cap, (size_t)nframes * g.ncand)) != hipSuccess ||
-        (e = grow(d_cellCount, cellc_cap, (size_t)nframes * g.ncells)) != hipSuccess ||
-        (e = grow(d_candFirst, candfirst_cap, (size_t)nframes * g.ncells * kCandFirst)) != hipSuccess ||
+        (e = grow(d_candFirst, candfirst_cap, (size_t)nframes * g.ncells * kCandRec)) != hipSuccess ||
         (e = grow(d_keys, keys_cap, (size_t)nframes * nl * g.max_level_cand)) != hipSuccess ||
         (e = grow(d_knode, knode_cap, (size_t)nframes * nl * g.max_level_cand)) != hipSuccess ||
         (e = grow(d_lvlKps, lvlkps_cap, (size_t)nframes * g.nkpcap)) != hipSuccess ||
@@ -349,7 +348,6 @@ ExtractBuffers Ctx::buffers() const {
     if (no_chain) b.chain.nseg = 0;
     b.d_pyr = d_pyr;
     b.d_cands = d_cands;
-    b.d_cellCount = d_cellCount;
     b.d_candFirst = d_candFirst;
     b.d_keys = d_keys;
     b.d_knode = d_knode;
@@ -389,7 +387,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)d_frames, (uintptr_t)nframes, (uintptr_t)frame_pitch, (uintptr_t)row_stride, (uintptr_t)d_kps,
             (uintptr_t)d_desc, (uintptr_t)d_counts, (uintptr_t)kp_cap, (uintptr_t)geom.W, (uintptr_t)geom.H,
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
-            (uintptr_t)d_cands ^ ((uintptr_t)d_candFirst << 1), (uintptr_t)d_cellCount, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
+            (uintptr_t)d_cands, (uintptr_t)d_candFirst, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
             (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream,
             (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)tail_dst << 4) ^ ((uintptr_t)tail_bytes << 40)};
         if (!gexec || key != gkey) {
@@ -533,7 +531,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.b);
         (void)hipEventDestroy(pr.e);
     }
-    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_pyr, c->d_cands, c->d_cellCount, c->d_candFirst, c->d_keys, c->d_knode,
+    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_hout,
                     c->d_scratch, c->d_peer};
     for (void* b : bufs)
@@ -739,21 +737,18 @@ int orb_debug_candidates(orb_ctx* h, int frame, int level, int* out, int cap) {
         return ORB_ERR_ARG;
     const LevelGeom& L = c->geom.L[level];
     const int ncl = L.nCols * L.nRows;
-    std::vector<int> cnt(ncl);
-    std::vector<uint32_t> slots((size_t)L.cand_cap), first((size_t)ncl * kCandFirst);
+    std::vector<uint32_t> slots((size_t)L.cand_cap), rec((size_t)ncl * kCandRec);   // [count | first corners]
     hipError_t e;
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess ||
-        (e = hipMemcpy(cnt.data(), c->d_cellCount + (size_t)frame * c->geom.ncells + L.cell_base, ncl * sizeof(int),
-                       hipMemcpyDeviceToHost)) != hipSuccess ||
-        (e = hipMemcpy(first.data(), c->d_candFirst + ((size_t)frame * c->geom.ncells + L.cell_base) * kCandFirst,
-                       first.size() * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(rec.data(), c->d_candFirst + ((size_t)frame * c->geom.ncells + L.cell_base) * kCandRec,
+                       rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
         (e = hipMemcpy(slots.data(), c->d_cands + (size_t)frame * c->geom.ncand + L.cand_base,
                        slots.size() * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess)
         return set_error("download candidates", e), ORB_ERR_HIP;
     int n = 0;
     for (int i = 0; i < ncl; i++)
-        for (int k = 0; k < cnt[i]; k++) {
-            const uint32_t v = k < kCandFirst ? first[(size_t)i * kCandFirst + k] : slots[(size_t)i * L.cell_cap + k];
+        for (int k = 0; k < (int)rec[(size_t)i * kCandRec]; k++) {
+            const uint32_t v = k < kCandFirst ? rec[(size_t)i * kCandRec + 1 + k] : slots[(size_t)i * L.cell_cap + k];
             if (n < cap && out) {
                 out[3 * n] = v & 0xFFF;
                 out[3 * n + 1] = (v >> 12) & 0xFFF;

@@ -55,8 +55,6 @@ struct Ctx {
     size_t pyr_cap = 0;
     uint32_t* d_cands = nullptr;
     size_t cands_cap = 0;
-    int* d_cellCount = nullptr;
-    size_t cellc_cap = 0;
     uint32_t* d_candFirst = nullptr;
     size_t candfirst_cap = 0;
     uint32_t* d_keys = nullptr;

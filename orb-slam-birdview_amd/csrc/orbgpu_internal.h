@@ -17,7 +17,8 @@ constexpr int kMaxDim = 4096;         // candidate coordinates are packed in 12 
 constexpr int kFastTilePitch = 80;    // 16-bit elements per FAST tile row (ROI <= 66 px, prefilter window <= 74)
 constexpr int kFastMaxRoi = 66;
 constexpr int kOctreeThreads = 512;
-constexpr int kCandFirst = 8;         // corners per cell in the dense d_candFirst records (32 B)
+constexpr int kCandRec = 8;           // dwords per cell in d_candFirst: [corner count | first kCandFirst corners]
+constexpr int kCandFirst = kCandRec - 1;
 constexpr int kDescWin = 43;          // unblurred window: radius 18 (BRIEF) + 3 (blur taps)
 constexpr int kDescWinPitch = 48;       // 12 dwords: window rows are loaded as aligned dwords
 constexpr int kDescBlur = 37;         // blurred window: radius 18
@@ -136,9 +137,8 @@ struct ExtractBuffers {
     ChainPlan chain;
     uint8_t* d_pyr;                // nframes * pyr_bytes
     uint32_t* d_cands;             // nframes * ncand: a cell's corners from the (kCandFirst+1)th on, at its slots
-    uint32_t* d_candFirst;         // nframes * ncells * kCandFirst: a cell's first corners, densely (32 B per
+    uint32_t* d_candFirst;         // nframes * ncells * kCandRec: a cell's corner count and first corners (32 B per
                                    // cell: the octree reads most cells' corners with two coalesced loads)
-    int* d_cellCount;              // nframes * ncells
     uint32_t* d_keys;              // nframes * nlevels * max_level_cand
     uint16_t* d_knode;             // same
     uint32_t* d_lvlKps;            // nframes * nkpcap
