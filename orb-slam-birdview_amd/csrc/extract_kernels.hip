@@ -2303,6 +2303,12 @@ static int octree_lds_keys(int node_cap) {
     const long long room = 52 * 1024 - (long long)octree_lds_bytes(node_cap);
     return room > 0 ? (int)((room / 6) & ~7LL) : 0;
 }
+// one block per CU (small batches): the keys of the largest level, within the CU's 160 KiB
+static int octree_lds_keys_whole_cu(const Geom& g) {
+    const long long room = 160 * 1024 - (long long)octree_lds_bytes(g.node_cap);
+    const long long want = ((long long)g.max_level_cand + 7) & ~7LL;
+    return room > 0 ? (int)std::min(want, (room / 6) & ~7LL) : 0;
+}
 
 hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
@@ -2340,11 +2346,12 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                            b.d_stamps, zero, ipw);
     };
     auto octree = [&](int lbase, int nl, hipStream_t s) {
-        const int lk = octree_lds_keys(g.node_cap);
         // a small batch (the host path's single frame, C5's 8-frame step) has fewer blocks than CUs, so the
-        // level-0 blocks are the whole latency: 1024 threads halve their per-key steps; larger batches keep
-        // 512 (three blocks per CU)
+        // level-0 blocks are the whole latency: 1024 threads halve their per-key steps, and the keys get all
+        // the LDS a CU has (no global key scratch: at 4,000 features the node tables alone pass the 52 KiB
+        // of the batch layout); larger batches keep 512 threads and 52 KiB (three blocks per CU)
         const bool one = nframes * nl <= 256;
+        const int lk = one ? octree_lds_keys_whole_cu(g) : octree_lds_keys(g.node_cap);
         hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
                            octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_candFirst,
                            b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
