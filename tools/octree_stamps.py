@@ -18,7 +18,8 @@ from orbgpu.synth import synth_batch  # noqa: E402
 
 def main():
     B, NL, NCELLS = int(sys.argv[1]) if len(sys.argv) > 1 else 64, 8, 2656
-    bx = orbgpu.BatchExtractor(2000, 1280, 720, B)
+    NF = int(sys.argv[2]) if len(sys.argv) > 2 else 2000   # features (C5: 4000)
+    bx = orbgpu.BatchExtractor(NF, 1280, 720, B)
     bx.upload(synth_batch(1280, 720, B))
     for _ in range(3):
         bx.launch()
