@@ -1971,66 +1971,6 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
     if (lane < 4) dst[lane] = lane == 0 ? mq[0] : lane == 1 ? mq[1] : lane == 2 ? mq[2] : mq[3];
 }
 
-// The 7-tap Gaussian as byte weights shifted to each of the four byte alignments of an output's
-// 7-byte run within aligned window dwords: alignment r uses dwords a, a+1 (and a+2 for r >= 2) with
-// KA[r], KB[r] (, KC[r]), so no byte run is ever realigned (10 v_dot4 per 4 outputs instead of 8 v_dot4
-// and 6 v_alignbyte).
-struct GaussShift {
-    uint32_t ka[4], kb[4], kc[4];
-};
-
-__device__ __forceinline__ GaussShift gauss_shift(const int* gk) {
-    auto b4 = [](int x0, int x1, int x2, int x3) {
-        return (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)x2 << 16) | ((uint32_t)x3 << 24);
-    };
-    GaussShift k;
-    k.ka[0] = b4(gk[0], gk[1], gk[2], gk[3]);
-    k.kb[0] = b4(gk[4], gk[5], gk[6], 0);
-    k.kc[0] = 0;
-    k.ka[1] = b4(0, gk[0], gk[1], gk[2]);
-    k.kb[1] = b4(gk[3], gk[4], gk[5], gk[6]);
-    k.kc[1] = 0;
-    k.ka[2] = b4(0, 0, gk[0], gk[1]);
-    k.kb[2] = b4(gk[2], gk[3], gk[4], gk[5]);
-    k.kc[2] = b4(gk[6], 0, 0, 0);
-    k.ka[3] = b4(0, 0, 0, gk[0]);
-    k.kb[3] = b4(gk[1], gk[2], gk[3], gk[4]);
-    k.kc[3] = b4(gk[5], gk[6], 0, 0);
-    return k;
-}
-
-// k_describe row pass, 8 rounds of one lane: RT[4gq + o][wy] = sum_t k_t * window[wy][SH + 4gq + o + t]
-// (the window row starts SH bytes into its first dword)
-// RT and the window share the wave's LDS (kDescWinOff): every RT store lands in window rows 0..5, which
-// round 0 reads.  So round 0 reads through rw0 (ordered before the stores), rounds 1..7 through the
-// restrict rw1 (nothing stored aliases them: their loads may be scheduled past earlier rounds' stores).
-// full: the lane's four columns are all stored (column group 9 keeps only column 36: BRIEF reads 0..36).
-template <int SH>
-__device__ __forceinline__ void desc_row_pass(const uint32_t* rw0, const uint32_t* __restrict__ rw1, uint16_t* rq,
-                                              const GaussShift& K, bool last, bool full) {
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) w[i] = r == 0 ? rw0[i] : rw1[72 * r + i];
-        // the four outputs' dot4 chains interleaved level by level (independent neighbours, no dependent
-        // back-to-back v_dot4 that needs wait states)
-        uint32_t acc[4];
-#pragma unroll
-        for (int o = 0; o < 4; o++) acc[o] = __builtin_amdgcn_udot4(w[(SH + o) >> 2], K.ka[(SH + o) & 3], 0u, false);
-#pragma unroll
-        for (int o = 0; o < 4; o++) acc[o] = __builtin_amdgcn_udot4(w[((SH + o) >> 2) + 1], K.kb[(SH + o) & 3], acc[o], false);
-#pragma unroll
-        for (int o = 0; o < 4; o++)
-            if (((SH + o) & 3) >= 2) acc[o] = __builtin_amdgcn_udot4(w[((SH + o) >> 2) + 2], K.kc[(SH + o) & 3], acc[o], false);
-        if (r < 7 || last) {   // round 7: only row 42 (RT rows stop at 42: pitch 43)
-#pragma unroll
-            for (int o = 0; o < 4; o++)
-                if (o == 0 || full) rq[o * kRtPitch + 6 * r] = (uint16_t)acc[o];
-        }
-    }
-}
-
 template <bool FMA>
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
                                           const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt,
