@@ -445,56 +445,51 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
  * (:140-157, float with the final comparison in double).  The reference keeps the LAST candidate
  * reaching the running minimum ('dist > bestDist' skips only strictly larger), so the key is
  * dist << 32 | ~pos. */
-__global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict__ desc1,
-                                                       const orb_keypoint* __restrict__ kps1,
-                                                       const float* __restrict__ ur1,
-                                                       const uint8_t* __restrict__ desc2,
-                                                       const orb_keypoint* __restrict__ kps2,
-                                                       const uint8_t* __restrict__ mp2, const float* __restrict__ ur2,
-                                                       const int* __restrict__ item_q, const int2* __restrict__ ranges,
-                                                       const int* __restrict__ cand_idx, int nitems, TriParams tp,
-                                                       int* __restrict__ best_out) {
+__global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict__ qdesc,
+                                                       const float4* __restrict__ qinfo,
+                                                       const uint8_t* __restrict__ tdesc,
+                                                       const float4* __restrict__ tinfo,
+                                                       const int2* __restrict__ ranges, const int* __restrict__ cand,
+                                                       int nitems, TriParams tp, int* __restrict__ best_out) {
     const int it = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (it >= nitems) return;
-    const int idx1 = item_q[it];
-    const uint4* qp = reinterpret_cast<const uint4*>(desc1 + (long long)idx1 * 32);
+    const uint4* qp = reinterpret_cast<const uint4*>(qdesc + (long long)it * 32);
     const uint4 qa = qp[0], qb = qp[1];
-    const orb_keypoint kp1 = kps1[idx1];
-    const bool st1 = ur1[idx1] >= 0;
+    const float4 q = qinfo[it];   // x, y, stereo (1 / 0)
+    const bool st1 = q.z != 0.f;
     const float* F = tp.F;
     // CheckDistEpipolarLine's float expressions with the contractions the reference's -O3 -march=native
     // build applies (tools/ref_flags_probe.cpp fixes each form)
-    const float la = __builtin_fmaf(kp1.x, F[0], kp1.y * F[3]) + F[6];
-    const float lb = __builtin_fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
-    const float lc = __builtin_fmaf(kp1.y, F[5], kp1.x * F[2]) + F[8];
+    const float la = __builtin_fmaf(q.x, F[0], q.y * F[3]) + F[6];
+    const float lb = __builtin_fmaf(q.x, F[1], q.y * F[4]) + F[7];
+    const float lc = __builtin_fmaf(q.y, F[5], q.x * F[2]) + F[8];
     const float den = __builtin_fmaf(la, la, lb * lb);
     unsigned long long bestKey = ~0ull;
     const int c0 = ranges[it].x, c1 = ranges[it].y;
     for (int pos = c0 + lane; pos < c1; pos += 64) {
-        const int idx2 = cand_idx[pos];
-        if (mp2[idx2]) continue;
-        const bool st2 = ur2[idx2] >= 0;
-        if (tp.only_stereo && !st2) continue;
-        const uint4* tq = reinterpret_cast<const uint4*>(desc2 + (long long)idx2 * 32);
+        const int j = cand[pos];   // (no map point, stereo if asked: filtered on the host, :725-733)
+        const uint4* tq = reinterpret_cast<const uint4*>(tdesc + (long long)j * 32);
         const int dist = hamming256(qa, qb, tq[0], tq[1]);
         if (dist > 50) continue;
-        const orb_keypoint kp2 = kps2[idx2];
+        const float4 t = tinfo[j];   // x, y, octave, stereo
+        const int oct = (int)t.z;
+        const bool st2 = t.w != 0.f;
         if (!st1 && !st2) {
-            const float dex = tp.ex - kp2.x, dey = tp.ey - kp2.y;
-            if (__builtin_fmaf(dex, dex, dey * dey) < 100 * tp.scale2[kp2.octave]) continue;
+            const float dex = tp.ex - t.x, dey = tp.ey - t.y;
+            if (__builtin_fmaf(dex, dex, dey * dey) < 100 * tp.scale2[oct]) continue;
         }
         if (den == 0) continue;
-        const float num = __builtin_fmaf(lb, kp2.y, la * kp2.x) + lc;
+        const float num = __builtin_fmaf(lb, t.y, la * t.x) + lc;
         const float dsqr = num * num / den;
-        if (!((double)dsqr < 3.84 * (double)tp.sigma2[kp2.octave])) continue;
+        if (!((double)dsqr < 3.84 * (double)tp.sigma2[oct])) continue;
         const unsigned long long key = ((unsigned long long)dist << 32) | (unsigned)(0x7FFFFFFF - (pos - c0));
         bestKey = key < bestKey ? key : bestKey;
     }
     bestKey = wave_min_u64(bestKey);
     if (lane == 0) {
         int r = -1;
-        if (bestKey != ~0ull) r = cand_idx[c0 + (0x7FFFFFFF - (int)(bestKey & 0xFFFFFFFFu))];
+        if (bestKey != ~0ull) r = cand[c0 + (0x7FFFFFFF - (int)(bestKey & 0xFFFFFFFFu))];
         best_out[it] = r;
     }
 }
@@ -520,13 +515,12 @@ hipError_t launch_window_topk(const uint8_t* d_q, const int* d_item_q, const flo
     return hipGetLastError();
 }
 
-hipError_t launch_triangulation(const uint8_t* d_desc1, const orb_keypoint* d_kps1, const float* d_ur1,
-                                const uint8_t* d_desc2, const orb_keypoint* d_kps2, const uint8_t* d_mp2,
-                                const float* d_ur2, const int* d_item_q, const int2* d_ranges, const int* d_cand_idx,
-                                int nitems, const TriParams& tp, int* d_best, hipStream_t stream) {
+hipError_t launch_triangulation(const uint8_t* d_qdesc, const float4* d_qinfo, const uint8_t* d_tdesc,
+                                const float4* d_tinfo, const int2* d_ranges, const int* d_cand, int nitems,
+                                const TriParams& tp, int* d_best, hipStream_t stream) {
     if (nitems <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_triangulation, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_desc1, d_kps1, d_ur1, d_desc2,
-                       d_kps2, d_mp2, d_ur2, d_item_q, d_ranges, d_cand_idx, nitems, tp, d_best);
+    hipLaunchKernelGGL(k_triangulation, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_qdesc, d_qinfo, d_tdesc, d_tinfo,
+                       d_ranges, d_cand, nitems, tp, d_best);
     return hipGetLastError();
 }
 

@@ -471,42 +471,59 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
     if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
-    std::vector<int> item_q;
+    // Compact inputs (the upload is the call's cost): queries in item order, and per common
+    // node its candidates without a map point (and stereo ones only if asked, :725-733) as compact train
+    // indices, in the node's order (the reference keeps the last candidate reaching the minimum)
+    std::vector<int> item_q, cand, train_of;           // item -> idx1; candidates; compact train -> idx2
     std::vector<int2> rng;
+    std::vector<int> tmap(n2 > 0 ? n2 : 1, -1);       // idx2 -> compact train
     for_common_nodes(fv1, fv2, [&](int a, int b) {
+        const int cb = (int)cand.size();
+        for (int i = fv2.offsets[b]; i < fv2.offsets[b + 1]; i++) {
+            const int idx2 = fv2.indices[i];
+            if (has_mp2[idx2]) continue;
+            if (only_stereo && !(uright2[idx2] >= 0)) continue;
+            if (tmap[idx2] < 0) {
+                tmap[idx2] = (int)train_of.size();
+                train_of.push_back(idx2);
+            }
+            cand.push_back(tmap[idx2]);
+        }
+        const int ce = (int)cand.size();
         for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
             const int idx1 = fv1.indices[i];
             if (has_mp1[idx1]) continue;                              // :694-696
             if (only_stereo && !(uright1[idx1] >= 0)) continue;       // :698-702
             item_q.push_back(idx1);
-            rng.push_back(make_int2(fv2.offsets[b], fv2.offsets[b + 1]));
+            rng.push_back(make_int2(cb, ce));
         }
     });
-    const int nitems = (int)item_q.size();
-    const int ncand = fv2.nnodes ? fv2.offsets[fv2.nnodes] : 0;
+    const int nitems = (int)item_q.size(), nt = (int)train_of.size(), ncand = (int)cand.size();
     std::vector<int> best(nitems, -1);
     if (nitems) {
         Stage st{c};
-        const size_t o_d1 = st.add((size_t)n1 * 32), o_k1 = st.add((size_t)n1 * sizeof(orb_keypoint)),
-                     o_u1 = st.add((size_t)n1 * 4), o_d2 = st.add((size_t)n2 * 32),
-                     o_k2 = st.add((size_t)n2 * sizeof(orb_keypoint)), o_m2 = st.add(n2), o_u2 = st.add((size_t)n2 * 4),
-                     o_q = st.add((size_t)nitems * 4), o_r = st.add((size_t)nitems * 8), o_c = st.add((size_t)ncand * 4);
+        const size_t o_qd = st.add((size_t)nitems * 32), o_qi = st.add((size_t)nitems * 16),
+                     o_td = st.add((size_t)nt * 32), o_ti = st.add((size_t)nt * 16), o_r = st.add((size_t)nitems * 8),
+                     o_c = st.add((size_t)ncand * 4);
         const size_t o_in_end = st.off, o_b = st.add((size_t)nitems * 4), o_end = st.off;
         int r = st.alloc();
         if (r != ORB_OK) return r;
-        auto put = [&](size_t o, const void* src, size_t bytes) {
-            if (bytes) std::memcpy(c->h_mstage + o, src, bytes);
-        };
-        put(o_d1, desc1, (size_t)n1 * 32);
-        put(o_k1, kps1, (size_t)n1 * sizeof(orb_keypoint));
-        put(o_u1, uright1, (size_t)n1 * 4);
-        put(o_d2, desc2, (size_t)n2 * 32);
-        put(o_k2, kps2, (size_t)n2 * sizeof(orb_keypoint));
-        put(o_m2, has_mp2, n2);
-        put(o_u2, uright2, (size_t)n2 * 4);
-        put(o_q, item_q.data(), (size_t)nitems * 4);
-        put(o_r, rng.data(), (size_t)nitems * 8);
-        put(o_c, fv2.indices, (size_t)ncand * 4);
+        uint8_t* qd = st.h<uint8_t>(o_qd);
+        float4* qi = st.h<float4>(o_qi);
+        for (int i = 0; i < nitems; i++) {
+            const int idx1 = item_q[i];
+            std::memcpy(qd + (size_t)i * 32, desc1 + (size_t)idx1 * 32, 32);
+            qi[i] = make_float4(kps1[idx1].x, kps1[idx1].y, uright1[idx1] >= 0 ? 1.f : 0.f, 0.f);
+        }
+        uint8_t* td = st.h<uint8_t>(o_td);
+        float4* ti = st.h<float4>(o_ti);
+        for (int j = 0; j < nt; j++) {
+            const int idx2 = train_of[j];
+            std::memcpy(td + (size_t)j * 32, desc2 + (size_t)idx2 * 32, 32);
+            ti[j] = make_float4(kps2[idx2].x, kps2[idx2].y, (float)kps2[idx2].octave, uright2[idx2] >= 0 ? 1.f : 0.f);
+        }
+        if (nitems) std::memcpy(st.h<int2>(o_r), rng.data(), (size_t)nitems * 8);
+        if (ncand) std::memcpy(st.h<int>(o_c), cand.data(), (size_t)ncand * 4);
         hipError_t e = st.up(0, o_in_end);
         if (e != hipSuccess) return set_error("upload", e), ORB_ERR_HIP;
         TriParams tp;
@@ -520,14 +537,14 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         }
         tp.only_stereo = only_stereo;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-        e = launch_triangulation(st.d<uint8_t>(o_d1), st.d<orb_keypoint>(o_k1), st.d<float>(o_u1), st.d<uint8_t>(o_d2),
-                                 st.d<orb_keypoint>(o_k2), st.d<uint8_t>(o_m2), st.d<float>(o_u2), st.d<int>(o_q),
+        e = launch_triangulation(st.d<uint8_t>(o_qd), st.d<float4>(o_qi), st.d<uint8_t>(o_td), st.d<float4>(o_ti),
                                  st.d<int2>(o_r), st.d<int>(o_c), nitems, tp, st.d<int>(o_b), c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
         if ((e = st.down(o_b, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return set_error("download", e), ORB_ERR_HIP;
-        std::memcpy(best.data(), st.h<int>(o_b), (size_t)nitems * 4);
+        const int* hb = st.h<int>(o_b);
+        for (int i = 0; i < nitems; i++) best[i] = hb[i] >= 0 ? train_of[hb[i]] : -1;
     }
     std::vector<int> vMatches12(n1, -1);
     std::vector<int> rotHist[HISTO_LENGTH];

@@ -204,12 +204,12 @@ struct TriParams {
     float sigma2[ORBGPU_MAX_LEVELS];
     int only_stereo;
 };
-// One work item per (query idx1, candidate range): returns best idx2 (or -1) per item.
-hipError_t launch_triangulation(const uint8_t* d_desc1, const orb_keypoint* d_kps1, const float* d_ur1,
-                                const uint8_t* d_desc2, const orb_keypoint* d_kps2, const uint8_t* d_mp2,
-                                const float* d_ur2, const int* d_item_q, const int2* d_ranges,
-                                const int* d_cand_idx, int nitems, const TriParams& tp, int* d_best,
-                                hipStream_t stream);
+// One work item per query (compacted on the host: descriptor, (x, y, stereo) in item order), its
+// candidates a [begin, end) range of d_cand (compact train indices: the trains without a map point, and
+// stereo ones only if asked, in the reference's per-node order); returns the best compact train (or -1).
+hipError_t launch_triangulation(const uint8_t* d_qdesc, const float4* d_qinfo, const uint8_t* d_tdesc,
+                                const float4* d_tinfo, const int2* d_ranges, const int* d_cand, int nitems,
+                                const TriParams& tp, int* d_best, hipStream_t stream);
 
 // Frame::ComputeStereoMatches (stereo.hip).  One side of a rectified pair: its pyramid (level 0 in
 // `frames`, levels >= 1 in `pyr`) and extraction outputs, for pair p at frame frame0 + p*frame_step.
