@@ -178,17 +178,18 @@ struct TopkSession {
             e = launch_window_topk(st.d<uint8_t>(o_q), st.d<int>(o_item) + from, cen ? st.d<float2>(o_cen) : nullptr, n,
                                    st.d<orb_keypoint>(o_k1), st.d<uint8_t>(o_t), st.d<orb_keypoint>(o_k2),
                                    st.d<int>(o_coff), st.d<int>(o_cidx), wg, thr ? st.d<int>(o_thr) : nullptr, K,
-                                   st.d<int>(o_dist) + (size_t)from * K, st.d<int>(o_idx) + (size_t)from * K,
-                                   st.d<int>(o_nv) + from, c->stream);
+                                   st.h<int>(o_dist) + (size_t)from * K, st.h<int>(o_idx) + (size_t)from * K,
+                                   st.h<int>(o_nv) + from, c->stream);
         else
             e = launch_hamming_topk(st.d<uint8_t>(o_q) + (size_t)from * 32, n, st.d<uint8_t>(o_t), nt,
                                     st.d<int2>(o_rng) + from, st.d<int>(o_cand), thr ? st.d<int>(o_thr) : nullptr, K,
-                                    st.d<int>(o_dist) + (size_t)from * K, st.d<int>(o_idx) + (size_t)from * K,
-                                    st.d<int>(o_nv) + from, c->stream);
+                                    st.h<int>(o_dist) + (size_t)from * K, st.h<int>(o_idx) + (size_t)from * K,
+                                    st.h<int>(o_nv) + from, c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("hamming kernel", e), ORB_ERR_HIP;
-        // the output span in one DMA (items before `from` come back unchanged)
-        if ((e = st.down(o_dist, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        // the kernel writes the lists straight into the pinned mirror (host-coherent memory; items before
+        // `from` keep their values): no D2H command, one synchronisation
+        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return set_error("download top-k", e), ORB_ERR_HIP;
         return ORB_OK;
     }
@@ -538,10 +539,12 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         tp.only_stereo = only_stereo;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
         e = launch_triangulation(st.d<uint8_t>(o_qd), st.d<float4>(o_qi), st.d<uint8_t>(o_td), st.d<float4>(o_ti),
-                                 st.d<int2>(o_r), st.d<int>(o_c), nitems, tp, st.d<int>(o_b), c->stream);
+                                 st.d<int2>(o_r), st.d<int>(o_c), nitems, tp, st.h<int>(o_b), c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
-        if ((e = st.down(o_b, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        // the kernel writes its results straight into the pinned mirror (host-coherent memory): no D2H command
+        (void)o_end;
+        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return set_error("download", e), ORB_ERR_HIP;
         const int* hb = st.h<int>(o_b);
         for (int i = 0; i < nitems; i++) best[i] = hb[i] >= 0 ? train_of[hb[i]] : -1;

@@ -208,7 +208,8 @@ int orb_vocab_transform(orb_ctx* h, const orb_vocab* v, const uint8_t* desc, int
     if (!v || v->device != c->device || n < 0 || (n && (!desc || !word_id || !weight || !node_id)))
         return set_error("orb_vocab_transform: bad arguments", hipSuccess), ORB_ERR_ARG;
     if (n == 0) return ORB_OK;
-    // one DMA up (descriptors), one down ([word | weight | node]) through the context's pinned staging
+    // one DMA up (descriptors) through the context's pinned staging; the results come back by the kernel's
+    // own stores to it
     Stage st{c};
     const size_t o_desc = st.add((size_t)n * 32), o_w = st.add((size_t)n * 4), o_wt = st.add((size_t)n * 4),
                  o_nd = st.add((size_t)n * 4), o_end = st.off;
@@ -219,10 +220,11 @@ int orb_vocab_transform(orb_ctx* h, const orb_vocab* v, const uint8_t* desc, int
     if (e != hipSuccess) return set_error("vocab upload", e), ORB_ERR_HIP;
     hipLaunchKernelGGL(k_vocab_transform, dim3((n + 255) / 256, 1), dim3(256), 0, c->stream, v->d_cbeg, v->d_ccnt,
                        v->d_child, v->d_cdesc, v->d_word, v->d_weight, st.d<uint8_t>(o_desc), nullptr, n, 0,
-                       v->L - levelsup, st.d<int>(o_w), st.d<float>(o_wt), st.d<uint32_t>(o_nd));
+                       v->L - levelsup, st.h<int>(o_w), st.h<float>(o_wt), st.h<uint32_t>(o_nd));
     if ((e = hipGetLastError()) != hipSuccess) return set_error("vocab kernel", e), ORB_ERR_HIP;
-    if ((e = st.down(o_w, o_end)) != hipSuccess || (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return set_error("vocab download", e), ORB_ERR_HIP;
+    // the kernel writes [word | weight | node] straight into the pinned mirror: no D2H command
+    (void)o_end;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("vocab sync", e), ORB_ERR_HIP;
     std::memcpy(word_id, st.h<int>(o_w), (size_t)n * 4);
     std::memcpy(weight, st.h<float>(o_wt), (size_t)n * 4);
     std::memcpy(node_id, st.h<uint32_t>(o_nd), (size_t)n * 4);
