@@ -2165,7 +2165,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                                                   const uint32_t* __restrict__ lvlKps,
                                                   const int* __restrict__ lvlCount, orb_keypoint* __restrict__ outK,
                                                   uint8_t* __restrict__ outD, int* __restrict__ outN, int kpCap,
-                                                  unsigned long long* __restrict__ dstamps, int spw) {
+                                                  unsigned long long* __restrict__ dstamps, int spw,
+                                                  const int* __restrict__ err, int* __restrict__ errHost) {
     // per wave: the transposed row-pass sums RT[rx][wy] (u16, 37 x kRtPitch; an odd pitch spreads the
     // transposed stores of the 10 column groups over distinct banks) and the 43x48 window overlapping RT's
     // tail (kDescWinOff); 256 B past the last wave for the row pass's reads of rows 43..47
@@ -2188,6 +2189,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             int tot = 0;
             for (int i = 0; i < nl; i++) tot += cnts[i];
             outN[f] = tot;
+            if (errHost && f == 0) *errHost = *err;   // the octree's overflow flag, for the host path
         }
     };
     if (s0 >= g->nkpcap) {
@@ -2302,7 +2304,8 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         const int spw = nframes == 1 ? 1 : kDescSlotsPerWave;   // a single frame: one keypoint per wave
         const unsigned gx = cdiv(g.nkpcap, kDescWaves * spw);
         hipLaunchKernelGGL((g.variant & ORB_VARIANT_NO_FMA) ? k_describe<false> : k_describe<true>, dim3(gx * nframes), dim3(64 * kDescWaves), 0, s, b.d_geom, d_frames, frame_pitch,
-                           row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap, dst, spw);
+                           row_stride, b.d_pyr, b.d_lvlKps, b.d_lvlCount, d_kps, d_desc, d_counts, kp_cap, dst, spw,
+                           b.d_err, b.err_host);
     };
     int* zero = b.zero_err ? b.d_err : nullptr;
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);

@@ -355,6 +355,7 @@ ExtractBuffers Ctx::buffers() const {
     b.d_lvlCount = d_lvlCount;
     b.d_err = d_err;
     b.zero_err = 1;
+    b.err_host = nullptr;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
     return b;
 }
@@ -370,11 +371,11 @@ void Ctx::marker(void* user, int id, int begin, hipStream_t s) {
 }
 
 int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
-                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err, bool latency, void* tail_dst,
-                     const void* tail_src, size_t tail_bytes) {
+                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err, bool latency, int* err_host) {
     hipError_t e;
     ExtractBuffers bufs = buffers();
     if (err) bufs.d_err = err;
+    bufs.err_host = err_host;
     // the few-launch pyramid trades redundant work for fewer dependent launches: it pays for one frame
     // in flight (the host path), not when several batches share the GPU (measured)
     if (!latency) bufs.chain.nseg = 0;
@@ -389,7 +390,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_candFirst, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
             (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream,
-            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)tail_dst << 4) ^ ((uintptr_t)tail_bytes << 40)};
+            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)err_host << 4)};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -400,10 +401,6 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             // the overflow flag is zeroed by the FAST kernel (no separate memset node)
             hipError_t le = launch_extract(geom, bufs, d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc,
                                            d_counts, kp_cap, stream, nullptr, nullptr);
-            // the host path's result download as the graph's last node: it starts as the last kernel ends
-            // instead of waiting for the host to submit it after the graph launch returns
-            if (le == hipSuccess && tail_dst)
-                le = hipMemcpyAsync(tail_dst, tail_src, tail_bytes, hipMemcpyDeviceToHost, stream);
             hipGraph_t gr = nullptr;
             e = hipStreamEndCapture(stream, &gr);
             if (le != hipSuccess || e != hipSuccess) {
@@ -423,8 +420,6 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
         e = launch_extract(geom, bufs, d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap,
                            stream, &Ctx::marker, this);
         if (e != hipSuccess) return set_error("kernel launch", e), ORB_ERR_HIP;
-        if (tail_dst && (e = hipMemcpyAsync(tail_dst, tail_src, tail_bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-            return set_error("download", e), ORB_ERR_HIP;
     }
     last_frames = d_frames;
     last_frame_pitch = frame_pitch;
@@ -532,7 +527,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.e);
     }
     void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
-                    c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in, c->d_hout,
+                    c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in,
                     c->d_scratch, c->d_peer};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -615,14 +610,9 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     const int kcap = c->geom.nkpcap;
     const size_t kbytes = ((size_t)kcap * sizeof(orb_keypoint) + 63) & ~(size_t)63;   // descriptors 64-B aligned
     const size_t need = 16 + kbytes + (size_t)kcap * 32;
-    if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess || (e = grow(c->d_hout, c->hout_cap, need)) != hipSuccess)
-        return set_error("device allocation", e), ORB_ERR_NOMEM;
-    // output block [count | overflow flag | 8 B pad | keypoints | descriptors]: one download
-    int* d_cnt = reinterpret_cast<int*>(c->d_hout);
-    orb_keypoint* d_k = reinterpret_cast<orb_keypoint*>(c->d_hout + 16);
-    uint8_t* d_d = c->d_hout + 16 + kbytes;
+    if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess) return set_error("device allocation", e), ORB_ERR_NOMEM;
     // pageable 2-D upload (measured faster than a host copy into pinned staging + one DMA: 0.149 vs 0.168
-    // ms per C3 frame end to end, tools/host_latency)
+    // ms per C3 frame end to end, tools/host_latency; profiles/r03/latency_probe_upload.json)
     if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return set_error("upload image", e), ORB_ERR_HIP;
     if (need > c->pinned_cap) {
@@ -633,15 +623,17 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
             return set_error("pinned staging", e), ORB_ERR_NOMEM;
         c->pinned_cap = need;
     }
+    // output block [count | overflow flag | 8 B pad | keypoints | descriptors] in pinned, host-coherent
+    // memory: k_describe writes the keypoints, descriptors and count straight into it (and copies the
+    // octree's overflow flag), so no download follows the kernels
     uint8_t* hp = static_cast<uint8_t*>(c->h_pinned);
-    const int* hcnt = reinterpret_cast<const int*>(hp);
-    const orb_keypoint* hk = reinterpret_cast<const orb_keypoint*>(hp + 16);
-    const uint8_t* hd = hp + 16 + kbytes;
-    // kernels + the output block's download in one submission (the copy is the graph's last node)
-    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, d_k, d_d, d_cnt, kcap, d_cnt + 1, true, hp,
-                             c->d_hout, need)) != ORB_OK)
+    int* hcnt = reinterpret_cast<int*>(hp);
+    orb_keypoint* hk = reinterpret_cast<orb_keypoint*>(hp + 16);
+    uint8_t* hd = hp + 16 + kbytes;
+    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, hk, hd, hcnt, kcap, nullptr, true,
+                             hcnt + 1)) != ORB_OK)
         return st;
-    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("download keypoints", e), ORB_ERR_HIP;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("extract", e), ORB_ERR_HIP;
     if (hcnt[1]) {
         set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
         return ORB_ERR_INTERNAL;

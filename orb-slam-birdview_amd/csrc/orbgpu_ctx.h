@@ -71,11 +71,9 @@ struct Ctx {
     // host-image path (orb_extract)
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
-    // host-path outputs in one allocation, [count | 12 B pad | keypoints | descriptors], so that one
-    // download brings all of them back
-    uint8_t* d_hout = nullptr;
-    size_t hout_cap = 0;
-    void* h_pinned = nullptr;     // pinned staging for orb_extract's single download (count, flag, keypoints, descriptors)
+    // orb_extract's outputs [count | flag | pad | keypoints | descriptors]: host-coherent pinned memory the
+    // kernels write directly (no download)
+    void* h_pinned = nullptr;
     size_t pinned_cap = 0;
 
     std::vector<int> pairs_upload_host;   // staging for orb_hamming_top2_frames_device pair lists / slots
@@ -117,11 +115,11 @@ struct Ctx {
     int ensure_geometry(int W, int H);
     int ensure_frames(int nframes);
     ExtractBuffers buffers() const;
-    // err: the overflow flag the kernels raise (default d_err; orb_extract passes a word of its output
-    // block so that one download brings it back)
+    // err: the overflow flag the kernels raise (default d_err); err_host: a host-coherent word k_describe
+    // copies it to (orb_extract, whose kernels write their outputs straight into pinned memory)
     int run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch, int row_stride, orb_keypoint* d_kps,
                     uint8_t* d_desc, int* d_counts, int kp_cap, int* err = nullptr, bool latency = false,
-                    void* tail_dst = nullptr, const void* tail_src = nullptr, size_t tail_bytes = 0);
+                    int* err_host = nullptr);
     static void marker(void* user, int id, int begin, hipStream_t s);
 };
 

@@ -144,6 +144,7 @@ struct ExtractBuffers {
     uint32_t* d_lvlKps;            // nframes * nkpcap
     int* d_lvlCount;               // nframes * nlevels
     int* d_err;                    // 1 int: internal overflow flag
+    int* err_host;                 // host-coherent copy of it written by k_describe (the host path), or NULL
     int zero_err;                  // FAST zeroes d_err (0: the caller did)
     unsigned long long* d_stamps;  // phase timestamps (ORBGPU_FAST_STAMPS=1 diagnostic): 8 per (frame, cell),
                                    // 32 per (frame, level), 8 per keypoint slot
