@@ -96,6 +96,22 @@ def test_level_counts(orbgpu_mod, oracle_mod, w, h, params):
     assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), params
 
 
+def test_host_path_frame_sequence(orbgpu_mod, oracle_mod):
+    """One extractor (the host path: few-launch pyramid, direct launches, outputs written into pinned
+    memory) over a run of frames with image-size changes in between (the geometry, coefficient tables and
+    chain plan are rebuilt, the buffers regrown): every frame equal to the oracle (Frame.cc:414-420 calls
+    one ORBextractor per camera for the whole sequence)."""
+    from orbgpu.synth import synth_frame
+    g = orbgpu_mod.ORBextractor(2000, 1.2, 8, 20, 7)
+    o = oracle_mod.OracleExtractor(2000)
+    seq = [(1280, 720)] * 6 + [(640, 480)] * 3 + [(1280, 720)] * 3 + [(641, 479)] * 2
+    for i, (w, h) in enumerate(seq):
+        img = synth_frame(w, h, 30 + i)
+        ok, od = o(img)
+        gk, gd = g(img)
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), (i, w, h)
+
+
 def test_threshold_edges(orbgpu_mod, oracle_mod):
     # iniThFAST / minThFAST of 0 and 1 on a low-contrast frame, where arc strengths M of 1 and 2 decide
     # corners and the NMS (k_fast_wave keeps a corner iff M > max(neighbour M, 1): score M - 1 > 0 at
@@ -248,13 +264,15 @@ def test_device_sincosf_matches_glibc_restatement(orbgpu_mod, oracle_mod):
 @pytest.mark.parametrize("env", [{"ORBGPU_GRAPH": "0"}, {"ORBGPU_FAST_STAMPS": "1"}])
 def test_diagnostic_switches_leave_results_unchanged(orbgpu_mod, oracle_mod, monkeypatch, env):
     """The two environment switches liborbgpu still reads are diagnostics: direct launches instead of
-    graph replay, and kernel phase timestamps.  Both must give the default path's bytes."""
+    graph replay, and kernel phase timestamps.  Both must give the default path's bytes (three frames,
+    launched twice)."""
     from orbgpu.synth import synth_batch
     frames = synth_batch(1280, 720, 3, first=50)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     b = orbgpu_mod.BatchExtractor(2000, 1280, 720, 3)
     b.upload(frames)
+    b.launch()
     b.launch()
     b.sync()
     o = oracle_mod.OracleExtractor(2000)
