@@ -142,6 +142,12 @@ def level_sizes(w, h, nl=8, sf=1.2):
             for x in s]
 
 
+def fast_cells(w, h):
+    """FAST cells per frame: the reference's grid per level, nCols x nRows with nCols = (w_l - 32) / 30
+    (ORBextractor.cc:773-787: minBorder 16, W = 30)."""
+    return sum(((a - 32) // 30) * ((b - 32) // 30) for a, b in level_sizes(w, h))
+
+
 def algorithmic_bytes(w, h, kps_per_frame, cands_per_frame):
     """Per-frame compulsory bytes by kernel."""
     lv = level_sizes(w, h)
@@ -167,14 +173,17 @@ VALU_INT_CYCLES = 4.33
 VALU_INT_CEIL = 256 * 4 * 2.4e9 / VALU_INT_CYCLES   # wave64 instructions per second, whole chip
 
 
-def read_pmc(kernel, batch):
+def read_pmc(kernel, batch, workload):
     """(HBM bytes per launch, VALU instructions per launch, source) of `kernel` from the rocprofv3 PMC
-    summary (tools/pmc.sh -> profiles/pmc_traffic.json), scaled to `batch` frames per launch, or Nones."""
+    summary (tools/pmc.sh -> profiles/pmc_traffic.json), scaled to `batch` frames per launch, or Nones
+    when the summary was collected on another configuration (its "workload", C3 when absent)."""
     path = os.environ.get("ORBGPU_PMC_JSON") or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except Exception:
+        return None, None, None
+    if d.get("workload", "c3") != workload:
         return None, None, None
     k = batch / float(d.get("batch_frames_per_launch", batch) or batch)
     sq = d.get("sq_per_launch", {}).get(kernel, {})
@@ -568,7 +577,7 @@ def main():
         dom_s = ms_per_step_k[dom] / 1e3
         achieved = dom_bytes / dom_s / 1e9
         launches_per_step = klaunch[KNAMES.index(dom)] / steps
-        traffic, valu_insts, pmc_src = read_pmc(dom, B)
+        traffic, valu_insts, pmc_src = read_pmc(dom, B, args.config)
         sum_k_s = sum(ms_per_step_k.values()) / 1e3
         launch_s = dom_s / launches_per_step
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -585,7 +594,10 @@ def main():
                               "ceiling": "measured: 4.33 cycles per wave64 integer VOP3/VOP3P instruction per SIMD "
                                          "(tools/valu_rate.hip, profiles/r02/valu_rate.txt)",
                               "dual_rate_frac": round(valu_insts * 64 / launch_s / PEAK_VALU_LANE_OPS, 4),
-                              "valu_insts_per_launch": valu_insts, "pmc_source": pmc_src}
+                              "valu_insts_per_launch": valu_insts,
+                              "valu_insts_per_cell": (round(valu_insts / (fast_cells(w, h) * B / launches_per_step), 1)
+                                                      if dom == "fast" else None),
+                              "pmc_source": pmc_src}
                              if valu_insts else None),
                     "pipeline": {"bytes_per_frame": int(ab["pipeline"]),
                                  "achieved": round(ab["pipeline"] * B / sum_k_s / 1e9, 2),
@@ -673,8 +685,9 @@ def main():
         host_path = {"frames_per_s": round(1e3 / ms, 1), "features_per_s": round(per_frame_kps * 1e3 / ms, 1),
                      "ms_per_frame": round(ms, 4), "caller": "C++ mirror (tools/host_latency)" if cpp else "python",
                      "cpp": cpp, "python_ms_per_frame": round(py_ms, 4),
-                     "note": "ORBextractor::operator() per host frame: upload + graph replay + one download, one "
-                             "frame in flight, median of 200"}
+                     "note": "ORBextractor::operator() per host frame: pageable upload, direct launches (two-launch "
+                             "pyramid), outputs written by the kernels into pinned memory, one frame in flight, "
+                             "median of 200"}
 
     # ---- the ORBmatcher drop-ins per call (SURVEY 8(a) rows a9-a13 at the reference's granularity: one call
     # per frame / keyframe pair) and Frame::ComputeBoW, through the reference-signature adapter, against

@@ -53,6 +53,9 @@ def main():
     calib_read = 512 << 20
     calib_write = 256 << 20
     out = {"unit_note": "counters in KiB -> bytes x1024; per launch = mean over dispatches",
+           # the bench configuration the passes ran (tools/pmc.sh: C3 unless BENCH_ARGS names another); bench.py
+           # attaches the figures only to a line of the same configuration
+           "workload": os.environ.get("PMC_WORKLOAD", "c3"),
            "calibration": {}, "raw_bytes_per_launch": {}, "per_launch_bytes": {}}
     fr, ffiles = load(os.path.join(root, "calib_FETCH_SIZE"), "FETCH_SIZE")
     wr, wfiles = load(os.path.join(root, "calib_WRITE_SIZE"), "WRITE_SIZE")
