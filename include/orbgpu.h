@@ -218,6 +218,11 @@ int orb_hamming_top2_frames_device(orb_ctx* ctx, const uint8_t* d_desc, const in
                                    const int* q_frames, const int* t_frames, int* d_best, int* d_best_idx,
                                    int* d_second);
 
+/* Train slices one top-2 launch splits each pair into for these sizes (orb_hamming_top2_device passes
+ * npairs = 1; the frames form passes kp_cap for both maxima).  1 = the MFMA kernel writes best / index /
+ * second itself; more = per-slice partial results merged by a second kernel.  Host only (test / tuning). */
+int orb_hamming_top2_slices(int npairs, int max_nq, int max_nt);
+
 /* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21) as CSR. */
 typedef struct {
     int nnodes;

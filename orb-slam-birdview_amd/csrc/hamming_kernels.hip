@@ -410,19 +410,30 @@ int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     return std::max(ns, 1);
 }
 
+// Train slice length of one launch: >= 2048 workgroups, slices of whole 32-train tiles, at most
+// top2_batch_slices of them (the partial buffer is sized for that many).  (max_nt == 0: one empty slice of
+// one tile width, so that nothing divides by zero.)
+static int top2_slice_len(int npairs, int max_nq, int max_nt) {
+    const int ns = top2_batch_slices(npairs, max_nq, max_nt);
+    const int qb = (max_nq + kMfQ - 1) / kMfQ;
+    int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
+    want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
+    return std::max(((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr, kMfTr);
+}
+
+int top2_launch_slices(int npairs, int max_nq, int max_nt) {
+    if (npairs <= 0 || max_nq <= 0 || max_nt < 0) return 0;
+    return std::max(1, (max_nt + top2_slice_len(npairs, max_nq, max_nt) - 1) / top2_slice_len(npairs, max_nq, max_nt));
+}
+
 hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq, int max_nt, int* d_best,
                                      int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream) {
     if (npairs <= 0 || max_nq <= 0) return hipSuccess;
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
-    const int ns = top2_batch_slices(npairs, max_nq, max_nt);   // the partial buffer is sized for this many
-    // matrix-core form: >= 2048 workgroups, slices of whole 32-train tiles
     const int qb = (max_nq + kMfQ - 1) / kMfQ;
-    int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
-    want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
-    // (max_nt == 0: one empty slice of one tile width, so that nothing below divides by zero)
-    a.slice = std::max(((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr, kMfTr);
-    const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);
+    a.slice = top2_slice_len(npairs, max_nq, max_nt);
+    const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);   // 1: k_top2_mfma writes the outputs itself
     // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
     // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels
     if (a.tx && max_nt > 0) {

@@ -241,6 +241,10 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {   // ORBmatche
     return d;
 }
 
+int orb_hamming_top2_slices(int npairs, int max_nq, int max_nt) {
+    return orbgpu::top2_launch_slices(npairs, max_nq, max_nt);
+}
+
 int orb_hamming_topk(orb_ctx* h, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_off,
                      const int* cand_idx, const int* train_thr, int k, int* out_dist, int* out_idx, int* out_nvalid) {
     Ctx* c = reinterpret_cast<Ctx*>(h);

@@ -185,6 +185,7 @@ struct Top2Batch {
     int n_tx_frames;
 };
 int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
+int top2_launch_slices(int npairs, int max_nq, int max_nt);   // slices one launch uses (1 = direct write)
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
                                      int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream);
 

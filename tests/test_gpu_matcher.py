@@ -358,6 +358,57 @@ def test_top2_frames_batch_vs_numpy(orbgpu_mod):
     bx.close()
 
 
+def _top2_numpy(dq, dt):
+    """(best, first argmin, second) of the 256-bit Hamming distances, DescriptorDistance
+    (ORBmatcher.cc:1647-1663) as a popcount of the XOR of four u64 words."""
+    a = np.ascontiguousarray(dq).view(np.uint64)
+    b = np.ascontiguousarray(dt).view(np.uint64)
+    D = np.zeros((len(a), len(b)), np.int32)
+    for w in range(4):
+        D += np.bitwise_count(a[:, w, None] ^ b[None, :, w]).astype(np.int32)
+    srt = np.partition(D, 1, axis=1) if D.shape[1] > 1 else D
+    return D.min(1), D.argmin(1), srt[:, 1] if D.shape[1] > 1 else np.full(len(a), 257)
+
+
+def test_top2_frames_bench_shape(orbgpu_mod):
+    """The Hamming half of the headline metric exactly as bench.py times it: B = 256 C3 frames
+    (1280x720, 2000 features, bench_frames), the 255 consecutive pairs f -> f+1 in ONE
+    orb_hamming_top2_frames_device launch.  At this shape top2_batch_slices gives one train slice, so
+    k_top2_mfma writes best / index / second directly (hamming_kernels.hip, gridDim.y == 1 branch; no
+    k_top2b_merge).  Pairs 0, 127 and 254 against numpy on the downloaded descriptors: best distance,
+    first index on ties (SearchByBoW's strict '<', ORBmatcher.cc:216-225) and the second distance."""
+    from orbgpu import _lib
+    from orbgpu.synth import bench_frames
+    B = 256
+    bx = orbgpu_mod.BatchExtractor(2000, 1280, 720, B)
+    bx.upload(bench_frames(1280, 720, B))
+    bx.launch()
+    bx.sync()
+    cap = bx.kp_cap
+    counts = bx.counts()
+    assert counts.min() > 1900
+    L = _lib.lib()
+    assert L.orb_hamming_top2_slices(B - 1, cap, cap) == 1   # the direct-write branch
+    qf, tf = list(range(B - 1)), list(range(1, B))
+    out = [bx._alloc((B - 1) * cap * 4) for _ in range(3)]
+    bx.hamming_top2_frames(qf, tf, *out)
+    bx.sync()
+    for p in (0, 127, 254):
+        res = [np.zeros(cap, np.int32) for _ in range(3)]
+        for r, d in zip(res, out):
+            L.orb_memcpy_d2h(bx.h, r.ctypes.data, d + p * cap * 4, r.nbytes)
+        _, dq = bx.results(p)
+        _, dt = bx.results(p + 1)
+        best, idx, second = _top2_numpy(dq, dt)
+        n = len(dq)
+        assert np.array_equal(res[0][:n], best), p
+        assert np.array_equal(res[1][:n], idx), p
+        assert np.array_equal(res[2][:n], second), p
+    for d in out:
+        L.orb_device_free(bx.h, d)
+    bx.close()
+
+
 def test_distinctive_descriptors_vs_oracle(orbgpu_mod, oracle_mod):
     """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307), batched over map points with
     1..300 observations (noisy copies of a prototype: realistic ties in the medians), plus empty."""
