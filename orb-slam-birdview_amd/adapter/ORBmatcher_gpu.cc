@@ -248,6 +248,11 @@ int window_match(float nnratio, bool checkOri, bool level0_only, const std::vect
                  const std::vector<cv::Point2f>* centres, int windowSize, std::vector<int>& vnMatches12) {
     static_assert(sizeof(cv::Point2f) == 8, "cv::Point2f must be two floats");
     const int n1 = (int)k1.size(), n2 = (int)k2.size();
+    // the reference reads vbPrevMatched[i1] / vPrevMatched[i1] for every query i1 (:429, :1690): one centre
+    // per F1 keypoint, or none (the own-position form)
+    if (centres && !centres->empty() && centres->size() != k1.size())
+        throw std::invalid_argument("window match: " + std::to_string(centres->size()) + " window centres for " +
+                                    std::to_string(n1) + " keypoints");
     std::vector<uint8_t> t1, t2;
     std::vector<int> out(n1 > 0 ? n1 : 1, -1);
     int nmatches = 0;

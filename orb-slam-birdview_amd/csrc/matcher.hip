@@ -327,8 +327,7 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
             return set_error("orb_hamming_top2_frames_device: negative frame index", hipSuccess), ORB_ERR_ARG;
     // each distinct train frame is expanded to +-1 once (consecutive-frame pairs share their frames), so the
     // expansion scratch grows with the distinct frames, not with the pairs
-    // host staging in the context (it outlives the asynchronous upload): [pairs (q, t) | slot per pair |
-    // train frame per slot], one upload
+    // [pairs (q, t) | slot per pair | train frame per slot], assembled on the host, one upload from a pinned slot
     std::vector<int>& up = c->pairs_upload_host;
     up.assign((size_t)npairs * 3, 0);
     {
@@ -357,8 +356,28 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     int* d_up = a.take<int>(up.size());
     uint2* part = a.take<uint2>((size_t)npairs * ns * kp_cap);
     uint8_t* tx = a.take<uint8_t>((size_t)nslots * kp_cap * 256);   // each distinct train frame expanded once
-    if ((e = hipMemcpyAsync(d_up, up.data(), up.size() * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-        return set_error("upload pairs", e), ORB_ERR_HIP;
+    {   // the pinned slot this call uploads from: its previous upload (two calls ago) must have been read
+        const int sl = c->pairs_slot;
+        c->pairs_slot ^= 1;
+        if (c->pairs_ev[sl] && (e = hipEventSynchronize(c->pairs_ev[sl])) != hipSuccess)
+            return set_error("pairs staging event", e), ORB_ERR_HIP;
+        if (!c->pairs_ev[sl] && (e = hipEventCreateWithFlags(&c->pairs_ev[sl], hipEventDisableTiming)) != hipSuccess)
+            return set_error("pairs staging event", e), ORB_ERR_HIP;
+        if (up.size() * 4 > c->pairs_cap[sl]) {
+            if (c->h_pairs[sl]) (void)hipHostFree(c->h_pairs[sl]);
+            c->h_pairs[sl] = nullptr;
+            c->pairs_cap[sl] = 0;
+            const size_t cap = std::max<size_t>(up.size() * 4, 4096);
+            if ((e = hipHostMalloc((void**)&c->h_pairs[sl], cap, hipHostMallocDefault)) != hipSuccess)
+                return set_error("pairs pinned staging", e), ORB_ERR_NOMEM;
+            c->pairs_cap[sl] = cap;
+        }
+        std::memcpy(c->h_pairs[sl], up.data(), up.size() * 4);
+        if ((e = hipMemcpyAsync(d_up, c->h_pairs[sl], up.size() * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return set_error("upload pairs", e), ORB_ERR_HIP;
+        if ((e = hipEventRecord(c->pairs_ev[sl], c->stream)) != hipSuccess)
+            return set_error("pairs staging event", e), ORB_ERR_HIP;
+    }
     const int2* d_frames = reinterpret_cast<const int2*>(d_up);
     Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap, tx, kp_cap,
                  d_up + 2 * npairs, d_up + 3 * npairs, nslots};
@@ -655,14 +674,21 @@ int orb_window_match_grid(orb_ctx* h, float nnratio, int check_ori, int level0_o
                           const orb_keypoint* kps1, const float* centres, float window, int n2,
                           const uint8_t* desc2, const orb_keypoint* kps2, orb_frame_grid grid2, int* match12,
                           int* nmatches_out) {
-    Ctx* c = reinterpret_cast<Ctx*>(h);
-    CTX_GUARD(c);
+    // the arguments are checked before the context: k_window_topk reads cell_idx[cell_off[..]] for every
+    // rectangle column, so a malformed CSR would be an out-of-bounds device read
     if (n1 < 0 || n2 < 0 || !match12 || (n1 && (!desc1 || !kps1)) || (n2 && (!desc2 || !kps2)) ||
         !grid2.cell_off || (grid2.cell_off[64 * 48] && !grid2.cell_idx))
         return set_error("orb_window_match_grid: bad arguments", hipSuccess), ORB_ERR_ARG;
+    if (grid2.cell_off[0] != 0)
+        return set_error("orb_window_match_grid: grid cell_off[0] != 0", hipSuccess), ORB_ERR_ARG;
+    for (int i = 0; i < 64 * 48; i++)   // offsets non-decreasing, so every run lies in [0, cell_off[3072])
+        if (grid2.cell_off[i + 1] < grid2.cell_off[i])
+            return set_error("orb_window_match_grid: grid cell_off decreases", hipSuccess), ORB_ERR_ARG;
     for (int i = 0, nslots = grid2.cell_off[64 * 48]; i < nslots; i++)   // the device indexes kps2 by these
         if (grid2.cell_idx[i] < 0 || grid2.cell_idx[i] >= n2)
             return set_error("orb_window_match_grid: grid index out of range", hipSuccess), ORB_ERR_ARG;
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
     TopkSession s{c};
     for (int i1 = 0; i1 < n1; i1++) {
         if (level0_only && kps1[i1].octave > 0) continue;   // :420-423 (a query without candidates ranks nothing)

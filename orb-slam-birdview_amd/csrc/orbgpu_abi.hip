@@ -533,6 +533,10 @@ void orb_destroy(orb_ctx* h) {
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_mstage) (void)hipHostFree(c->h_mstage);
+    for (int i = 0; i < 2; i++) {
+        if (c->h_pairs[i]) (void)hipHostFree(c->h_pairs[i]);
+        if (c->pairs_ev[i]) (void)hipEventDestroy(c->pairs_ev[i]);
+    }
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -619,7 +623,9 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
         if (c->h_pinned) (void)hipHostFree(c->h_pinned);
         c->h_pinned = nullptr;
         c->pinned_cap = 0;
-        if ((e = hipHostMalloc(&c->h_pinned, need, hipHostMallocDefault)) != hipSuccess)
+        // mapped + coherent (fine-grained) explicitly: k_describe stores the outputs straight into this block and
+        // the host reads them after hipStreamSynchronize, with no D2H copy in between
+        if ((e = hipHostMalloc(&c->h_pinned, need, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return set_error("pinned staging", e), ORB_ERR_NOMEM;
         c->pinned_cap = need;
     }

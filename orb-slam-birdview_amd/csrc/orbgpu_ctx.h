@@ -22,8 +22,8 @@ struct Ctx {
     int device = 0;
     int num_cu = 256;
     bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: the kernels record phase timestamps (diagnostic)
-    bool stereo_stage = false;
-    bool no_chain = false;        // ORBGPU_NO_CHAIN=1: no one-launch pyramid for small batches (A/B diagnostic)    // ORBGPU_STEREO_STAGE=1: stereo stages the right side as for a peer GPU (test)
+    bool stereo_stage = false;    // ORBGPU_STEREO_STAGE=1: stereo stages the right side as for a peer GPU (test)
+    bool no_chain = false;        // ORBGPU_NO_CHAIN=1: no one-launch pyramid for small batches (A/B diagnostic)
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
@@ -76,7 +76,13 @@ struct Ctx {
     void* h_pinned = nullptr;
     size_t pinned_cap = 0;
 
-    std::vector<int> pairs_upload_host;   // staging for orb_hamming_top2_frames_device pair lists / slots
+    std::vector<int> pairs_upload_host;   // orb_hamming_top2_frames_device: pair lists / slots assembled here
+    // ... and staged through two pinned slots used in turn: a slot is rewritten only after the event recorded
+    // behind its previous upload has completed (the call returns before its copy runs)
+    int* h_pairs[2] = {nullptr, nullptr};
+    size_t pairs_cap[2] = {0, 0};
+    hipEvent_t pairs_ev[2] = {nullptr, nullptr};
+    int pairs_slot = 0;
     // matcher scratch arena (bytes)
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;
@@ -168,7 +174,10 @@ struct Stage {
             c->h_mstage = nullptr;
             c->mstage_cap = 0;
             const size_t cap = std::max<size_t>(need, 1 << 20);
-            if ((e = hipHostMalloc((void**)&c->h_mstage, cap, hipHostMallocDefault)) != hipSuccess)
+            // mapped + coherent explicitly: the matcher kernels store their results straight into this mirror
+            // and the host reads them after the stream synchronisation, with no D2H copy
+            if ((e = hipHostMalloc((void**)&c->h_mstage, cap, hipHostMallocMapped | hipHostMallocCoherent)) !=
+                hipSuccess)
                 return set_error("matcher pinned staging", e), ORB_ERR_NOMEM;
             c->mstage_cap = cap;
         }

@@ -87,3 +87,37 @@ def test_features_in_area_host_helper(orbgpu_mod, oracle_mod):
         a = orbgpu_mod.features_in_area(k, 0, 640, 0, 480, x, y, r, lv, lv)
         b = oracle_mod.features_in_area(k, 0, 640, 0, 480, x, y, r, lv, lv)
         assert a.tolist() == b.tolist()
+
+
+def test_window_match_grid_rejects_malformed_csr(orbgpu_mod):
+    """orb_window_match_grid validates F2's grid CSR before it touches the context (k_window_topk reads
+    cell_idx[cell_off[..]], so a malformed CSR would be an out-of-bounds device read): cell_off[0] != 0,
+    a decreasing offset and an index past n2 are ORB_ERR_ARG, each with its own message.  The context
+    is NULL here (no GPU), so a well-formed grid gets as far as the NULL-context error."""
+    from orbgpu import _lib
+    L = _lib.lib()
+    n2 = 10
+    desc = np.zeros((n2, 32), np.uint8)
+    k = np.zeros(n2, orbgpu_mod.KP_DTYPE)
+    match = np.zeros(n2, np.int32)
+    nm = ctypes.c_int(0)
+
+    def call(off, idx):
+        g = _lib.OrbFrameGrid(0.0, 0.0, 0.1, 0.1, off.ctypes.data, idx.ctypes.data)
+        st = L.orb_window_match_grid(None, 0.9, 1, 1, n2, desc.ctypes.data, k.ctypes.data, None, 100.0, n2,
+                                     desc.ctypes.data, k.ctypes.data, g, match.ctypes.data, ctypes.byref(nm))
+        return st, L.orb_last_error().decode()
+
+    good = np.zeros(64 * 48 + 1, np.int32)
+    good[5:] = n2   # cell 4 holds all ten keypoints
+    idx = np.arange(n2, dtype=np.int32)
+    assert call(good, idx) == (-1, "NULL context")
+    bad = good.copy()
+    bad[0] = 1
+    assert call(bad, idx) == (-1, "orb_window_match_grid: grid cell_off[0] != 0")
+    bad = good.copy()
+    bad[100] = 3   # 10 -> 3 -> 10: a run that would start past its end
+    assert call(bad, idx) == (-1, "orb_window_match_grid: grid cell_off decreases")
+    bad_idx = idx.copy()
+    bad_idx[7] = n2
+    assert call(good, bad_idx) == (-1, "orb_window_match_grid: grid index out of range")
