@@ -231,7 +231,7 @@ constexpr int kMfQ = 128;      // queries per workgroup
 
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {   // v_med3_u32
     unsigned r;
-    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));   // (not volatile: schedulable)
     return r;
 }
 
@@ -285,12 +285,21 @@ template <bool PRE>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx)
 __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
                                                    int* __restrict__ idx_o, int* __restrict__ second_o) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[2][kMfTr * kMfPitch];
-    const int p = blockIdx.z, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    // 1-D grid of (pair, slice, query block), query block fastest.  Blocks are dealt round-robin over the 8
+    // XCDs (b and b + 8 share one), so XCD x takes a contiguous run of that sequence: the query blocks of a
+    // pair, which all stream the same expanded trains, then share one L2 (dealt round-robin, every pair's
+    // 512 KB of C3 trains was fetched into all eight L2s: PMC 1.14 GB per 255-pair launch,
+    // profiles/r04/v1_hamming.json)
+    const int nb = gridDim.x, xq = nb >> 3, xr = nb & 7, xcd = blockIdx.x & 7, xj = blockIdx.x >> 3;
+    const int lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xj;
+    const int qbi = lb % a.qblocks, rest = lb / a.qblocks;
+    const int sli = rest % a.nslices, p = rest / a.nslices;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
     const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
-    const int qblk = blockIdx.x * kMfQ;
+    const int qblk = qbi * kMfQ;
     if (qblk >= nq) return;   // whole workgroup
-    const int t0 = blockIdx.y * a.slice, t1 = min(nt, t0 + a.slice);
+    const int t0 = sli * a.slice, t1 = min(nt, t0 + a.slice);
     const int h = lane >> 5, c = lane & 31;
     const int qi = qblk + wv * 32 + c;
     // B operand: K-step s = descriptor dword s, lane half h = its bits 16h .. 16h+15
@@ -393,12 +402,12 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
     b = min(b, ob);
     if (h != 0 || qi >= nq) return;
     const long long o = (long long)p * a.out_stride + qi;
-    if (gridDim.y == 1) {
+    if (a.nslices == 1) {
         best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
         idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
         second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
     } else {
-        part[((long long)p * gridDim.y + blockIdx.y) * a.out_stride + qi] = make_uint2(b, s2);
+        part[((long long)p * a.nslices + sli) * a.out_stride + qi] = make_uint2(b, s2);
     }
 }
 
@@ -434,15 +443,18 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     const int qb = (max_nq + kMfQ - 1) / kMfQ;
     a.slice = top2_slice_len(npairs, max_nq, max_nt);
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);   // 1: k_top2_mfma writes the outputs itself
+    a.qblocks = qb;
+    a.nslices = nsu;
+    const dim3 grid((unsigned)((long long)qb * nsu * npairs));
     // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
     // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels
     if (a.tx && max_nt > 0) {
         const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
         hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, nslots), dim3(256), 0, stream, a, max_nt);
-        hipLaunchKernelGGL(k_top2_mfma<true>, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
+        hipLaunchKernelGGL(k_top2_mfma<true>, grid, dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
                            d_second);
     } else {
-        hipLaunchKernelGGL(k_top2_mfma<false>, dim3(qb, nsu, npairs), dim3(256), 0, stream, a, d_part, d_best,
+        hipLaunchKernelGGL(k_top2_mfma<false>, grid, dim3(256), 0, stream, a, d_part, d_best,
                            d_best_idx, d_second);
     }
     if (nsu > 1)

@@ -183,6 +183,8 @@ struct Top2Batch {
     const int* tx_slot;
     const int* tx_frames;
     int n_tx_frames;
+    // set by launch_hamming_top2_batch: query blocks per pair and train slices per pair of the 1-D grid
+    int qblocks, nslices;
 };
 int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
 int top2_launch_slices(int npairs, int max_nq, int max_nt);   // slices one launch uses (1 = direct write)
