@@ -227,7 +227,6 @@ typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 constexpr int kMfTr = 32;      // trains per tile (MFMA rows)
 constexpr int kMfPitch = 272;  // LDS bytes per expanded train (256 + 16)
-constexpr int kMfQ = 128;      // queries per workgroup
 
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {   // v_med3_u32
     unsigned r;
@@ -249,22 +248,6 @@ __device__ __forceinline__ v4i_t pm1x16(uint32_t w) {   // bits 0..15 of w -> 16
     r.w = pm1x4(w >> 12);
     return r;
 }
-// 4 query bits -> 4 bytes: -16 (0xF0) where the bit is set, +16 (0x10) where it is clear.  Against +-1
-// trains the MFMA then sums -16 * dot, and from an initial 4096 + row each result is its tile-local key.
-__device__ __forceinline__ int pm16x4(uint32_t n) {
-    const uint32_t s = __umul24(n & 15u, 0x00204081u) & 0x01010101u;
-    const uint32_t m = (s << 8) - s;                                    // 0xFF in the set bytes
-    return (int)(0x10101010u ^ (m & 0xE0E0E0E0u));
-}
-__device__ __forceinline__ v4i_t pm16x16(uint32_t w) {
-    v4i_t r;
-    r.x = pm16x4(w);
-    r.y = pm16x4(w >> 4);
-    r.z = pm16x4(w >> 8);
-    r.w = pm16x4(w >> 12);
-    return r;
-}
-
 /* The pairs' train descriptors expanded to +-1 int8 once per launch (thread = one descriptor dword ->
  * 32 bytes), so k_top2_mfma's train tiles are plain copies: without it every query workgroup of a pair
  * re-expands every train tile (~40 VALU per thread and tile, more than the tile's top-2 updates). */
@@ -281,10 +264,32 @@ __global__ __launch_bounds__(256) void k_expand_pm1(Top2Batch a, int max_nt) {
     d[1] = pm1x16(w >> 16);
 }
 
-template <bool PRE>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx)
-__global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
-                                                   int* __restrict__ idx_o, int* __restrict__ second_o) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_t[2][kMfTr * kMfPitch];
+// 4 query bits -> 4 bytes of +-S (S = 16 or 32): -S where the bit is set, +S where it is clear
+template <int S>
+__device__ __forceinline__ int pmSx4(uint32_t n) {
+    const uint32_t s = __umul24(n & 15u, 0x00204081u) & 0x01010101u;
+    const uint32_t m = (s << 8) - s;                                    // 0xFF in the set bytes
+    return (int)((uint32_t)S * 0x01010101u ^ (m & ((uint32_t)(256 - 2 * S) * 0x01010101u)));
+}
+template <int S>
+__device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
+    return v4i_t{pmSx4<S>(w), pmSx4<S>(w >> 4), pmSx4<S>(w >> 8), pmSx4<S>(w >> 12)};
+}
+
+/* NS 32-train subtiles per stage (one accumulator chain each).  With the queries scaled to -S / +S,
+ * S = 16 NS, and the accumulators seeded with 128 S + subtile * 32 + row, every result is the stage-local key
+ * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
+ * pass and is merged into the running keys once per stage (NS = 2: one merge per 64 trains instead of
+ * two). */
+template <bool PRE, int NW, int NS>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW waves of 32 queries
+__global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
+                                                       int* __restrict__ idx_o, int* __restrict__ second_o) {
+    constexpr int NT = NW * 64, QB = NW * 32, TR = NS * kMfTr;   // threads, queries, trains per stage
+    constexpr int CH = 16 * TR / NT;   // 16-byte chunks of the stage's expanded trains each thread stages
+    constexpr int SC = 16 * NS;        // query scale
+    constexpr int KB = 5 + (NS == 2);  // stage-local key: dist << KB | stage row
+    static_assert(CH >= 1 && CH <= 4, "staging chunks");
+    __shared__ __attribute__((aligned(16))) uint8_t s_t[2][TR * kMfPitch];
     // 1-D grid of (pair, slice, query block), query block fastest.  Blocks are dealt round-robin over the 8
     // XCDs (b and b + 8 share one), so XCD x takes a contiguous run of that sequence: the query blocks of a
     // pair, which all stream the same expanded trains, then share one L2 (dealt round-robin, every pair's
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
     const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
-    const int qblk = qbi * kMfQ;
+    const int qblk = qbi * QB;
     if (qblk >= nq) return;   // whole workgroup
     const int t0 = sli * a.slice, t1 = min(nt, t0 + a.slice);
     const int h = lane >> 5, c = lane & 31;
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
         }
         const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-        for (int s = 0; s < 8; s++) qf[s] = pm16x16(qd[s] >> (16 * h));
+        for (int s = 0; s < 8; s++) qf[s] = pmSx16<SC>(qd[s] >> (16 * h));
     }
     const uint32_t* __restrict__ T = reinterpret_cast<const uint32_t*>(a.t + (long long)fr.y * a.t_stride * 32);
     // PRE: this pair's expanded trains through a buffer descriptor (SGPRs), 32-bit offsets
@@ -323,74 +328,87 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
         reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(txb >> 32)) << 32) |
                                 (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)txb)),
         0, 0x7FFFFFFF, 0x00020000);
-    const int er = tid >> 3, es = tid & 7;   // staging: thread -> (train row, descriptor dword = 32 expanded bytes)
+    // staging: thread -> stage row er, chunks ec .. ec + CH - 1 (16 expanded bytes = 16 descriptor bits each)
+    const int er = (tid * CH) >> 4, ec = (tid * CH) & 15;
     struct Chunk {
-        uint32_t w;    // !PRE: the descriptor dword
-        v4i_t x0, x1;  // PRE: its 32 expanded bytes
+        uint32_t w[(CH + 1) / 2];   // !PRE: the descriptor dwords holding the chunks' bits
+        v4i_t x[CH];                // PRE: the expanded bytes
     };
     auto fetch = [&](int row) -> Chunk {
         Chunk k;
         if (PRE) {
-            const int o = row * 256 + 32 * es;
-            k.x0 = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, o, 0, 0));
-            k.x1 = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, o + 16, 0, 0));
+#pragma unroll
+            for (int i = 0; i < CH; i++)
+                k.x[i] = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, row * 256 + 16 * (ec + i), 0, 0));
         } else {
-            k.w = T[(long long)row * 8 + es];
+#pragma unroll
+            for (int i = 0; i < (CH + 1) / 2; i++) k.w[i] = T[(long long)row * 8 + (ec >> 1) + i];
         }
         return k;
     };
     auto stage = [&](int buf, const Chunk& k) {
-        v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * kMfPitch + es * 32]);
-        d[0] = PRE ? k.x0 : pm1x16(k.w);
-        d[1] = PRE ? k.x1 : pm1x16(k.w >> 16);
+        v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * kMfPitch + ec * 16]);
+#pragma unroll
+        for (int i = 0; i < CH; i++) d[i] = PRE ? k.x[i] : pm1x16(k.w[i >> 1] >> (16 * ((ec + i) & 1)));
     };
     unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-    // the MFMA's initial accumulator: 4096 + row, so that with the queries scaled to -16 / +16 every result
-    // is already its tile-local key 4096 - 16 dot + row = dist * 32 + row (dist = (256 - dot) / 2)
-    v16i_t kc;
+    // the MFMA's initial accumulators: 128 SC + subtile * 32 + row, so that every result is already its
+    // stage-local key 128 SC - SC dot + (subtile * 32 + row) = dist << KB | stage row (dist = (256 - dot) / 2)
+    v16i_t kc[NS];
 #pragma unroll
-    for (int r = 0; r < 16; r++) kc[r] = 4096 + (r & 3) + 8 * (r >> 2);
-    const int ntile = t1 > t0 ? (t1 - t0 + kMfTr - 1) / kMfTr : 0;   // uniform
-    if (ntile > 0) {
+    for (int u = 0; u < NS; u++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) kc[u][r] = 128 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
+    if (nst > 0) {
         // rows past the slice load the slice's last row (their keys are masked): no zeroing, no branch
         stage(0, fetch(min(t0 + er, t1 - 1)));
         __syncthreads();
-        for (int j = 0; j < ntile; j++) {
-            const int tb = t0 + kMfTr * j;
-            const bool more = j + 1 < ntile;
+        for (int j = 0; j < nst; j++) {
+            const int tb = t0 + TR * j;
+            const bool more = j + 1 < nst;
             Chunk wn;
-            if (more) wn = fetch(min(tb + kMfTr + er, t1 - 1));
-            const uint8_t* A = &s_t[j & 1][c * kMfPitch + 16 * h];
-            v16i_t acc = kc;
+            if (more) wn = fetch(min(tb + TR + er, t1 - 1));
+            v16i_t acc[NS];
 #pragma unroll
-            for (int s = 0; s < 8; s++)   // one chain: the other waves on the SIMD hide its latency
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s], acc, 0, 0, 0);
-            // the results are tile-local keys dist * 32 + row (row = (r&3) + 8(r>>2) < 32; dist = (256 - dot)
-            // / 2, see kc): the tile's top-2 by med3 / min (2 ops per distance), then merged
-            // into the running keys dist << 16 | train index once per tile
-            unsigned lb = 0xFFFFFFFFu, ls = 0xFFFFFFFFu;
-            if (tb + kMfTr <= t1) {
+            for (int u = 0; u < NS; u++) {
+                const uint8_t* A = &s_t[j & 1][(32 * u + c) * kMfPitch + 16 * h];
+                acc[u] = kc[u];
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const unsigned key = (unsigned)acc[r];
-                    ls = umed3(lb, key, ls);
-                    lb = min(lb, key);
-                }
-            } else {   // the slice's last, partial tile
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int tr = tb + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const unsigned key = tr < t1 ? (unsigned)acc[r] : 0xFFFFFFFFu;
-                    ls = umed3(lb, key, ls);
-                    lb = min(lb, key);
-                }
+                for (int s = 0; s < 8; s++)   // one chain per subtile: the other waves on the SIMD hide its latency
+                    acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s],
+                                                                   acc[u], 0, 0, 0);
             }
-            if (lb != 0xFFFFFFFFu) {   // (only a partial tile leaves a lane without keys)
-                const unsigned gb = ((lb << 11) & 0xFFFF0000u) + (lb & 31u) + (unsigned)(tb + 4 * h);
+            // the stage's top-2 by med3 / min (2 ops per distance), then merged into the running keys
+            // dist << 16 | train index once per stage
+            unsigned lbt = 0xFFFFFFFFu, lst = 0xFFFFFFFFu;
+            if (tb + TR <= t1) {
+#pragma unroll
+                for (int u = 0; u < NS; u++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const unsigned key = (unsigned)acc[u][r];
+                        lst = umed3(lbt, key, lst);
+                        lbt = min(lbt, key);
+                    }
+            } else {   // the slice's last, partial stage
+#pragma unroll
+                for (int u = 0; u < NS; u++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int tr = tb + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        const unsigned key = tr < t1 ? (unsigned)acc[u][r] : 0xFFFFFFFFu;
+                        lst = umed3(lbt, key, lst);
+                        lbt = min(lbt, key);
+                    }
+            }
+            if (lbt != 0xFFFFFFFFu) {   // (only a partial stage leaves a lane without keys)
+                constexpr unsigned RM = (1u << KB) - 1;
+                const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
                 s2 = umed3(b, gb, s2);
                 b = min(b, gb);
                 // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
-                if (ls != 0xFFFFFFFFu) s2 = min(s2, (ls << 11) | 0xFFFFu);
+                if (lst != 0xFFFFFFFFu) s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
             }
             if (more) stage((j + 1) & 1, wn);
             __syncthreads();
@@ -411,6 +429,23 @@ __global__ __launch_bounds__(256) void k_top2_mfma(Top2Batch a, uint2* __restric
     }
 }
 
+// waves per k_top2_mfma workgroup and subtiles per stage (ORBGPU_TOP2=<waves><subtiles>, e.g. 82; an A/B
+// switch, default 82)
+static int top2_waves() {
+    static const int w = [] {
+        const char* e = std::getenv("ORBGPU_TOP2");
+        return (e && e[0] == '4') ? 4 : 8;
+    }();
+    return w;
+}
+static int top2_stage() {
+    static const int v = [] {
+        const char* e = std::getenv("ORBGPU_TOP2");
+        return (e && e[0] && e[1] == '1') ? 1 : 2;
+    }();
+    return v;
+}
+
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     npairs = std::max(npairs, 1);
     const int qwaves = std::max(1, (max_nq + 63) / 64);
@@ -419,13 +454,14 @@ int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     return std::max(ns, 1);
 }
 
-// Train slice length of one launch: >= 2048 workgroups, slices of whole 32-train tiles, at most
+// Train slice length of one launch: >= 8192 waves, slices of whole 32-train tiles, at most
 // top2_batch_slices of them (the partial buffer is sized for that many).  (max_nt == 0: one empty slice of
 // one tile width, so that nothing divides by zero.)
 static int top2_slice_len(int npairs, int max_nq, int max_nt) {
     const int ns = top2_batch_slices(npairs, max_nq, max_nt);
-    const int qb = (max_nq + kMfQ - 1) / kMfQ;
-    int want = std::max(1, (2048 + qb * npairs - 1) / (qb * npairs));
+    const int nw = top2_waves(), qb = (max_nq + 32 * nw - 1) / (32 * nw);
+    const int wg = 8192 / nw;
+    int want = std::max(1, (wg + qb * npairs - 1) / (qb * npairs));
     want = std::min({want, ns, std::max(1, (max_nt + kMfTr - 1) / kMfTr)});
     return std::max(((max_nt + want - 1) / want + kMfTr - 1) / kMfTr * kMfTr, kMfTr);
 }
@@ -440,7 +476,8 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (npairs <= 0 || max_nq <= 0) return hipSuccess;
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
-    const int qb = (max_nq + kMfQ - 1) / kMfQ;
+    const int nw = top2_waves(), ns = top2_stage();
+    const int qb = (max_nq + 32 * nw - 1) / (32 * nw);
     a.slice = top2_slice_len(npairs, max_nq, max_nt);
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);   // 1: k_top2_mfma writes the outputs itself
     a.qblocks = qb;
@@ -451,11 +488,13 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (a.tx && max_nt > 0) {
         const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
         hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, nslots), dim3(256), 0, stream, a, max_nt);
-        hipLaunchKernelGGL(k_top2_mfma<true>, grid, dim3(256), 0, stream, a, d_part, d_best, d_best_idx,
-                           d_second);
+        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<true, 8, 2> : k_top2_mfma<true, 8, 1>)
+                            : (ns == 2 ? k_top2_mfma<true, 4, 2> : k_top2_mfma<true, 4, 1>);
+        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second);
     } else {
-        hipLaunchKernelGGL(k_top2_mfma<false>, grid, dim3(256), 0, stream, a, d_part, d_best,
-                           d_best_idx, d_second);
+        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2> : k_top2_mfma<false, 8, 1>)
+                            : (ns == 2 ? k_top2_mfma<false, 4, 2> : k_top2_mfma<false, 4, 1>);
+        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second);
     }
     if (nsu > 1)
         hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,

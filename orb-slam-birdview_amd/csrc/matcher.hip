@@ -106,11 +106,11 @@ struct TopkSession {
         o_end = st.off;
         const int r = st.alloc();
         if (r != ORB_OK) return r;
-        uint8_t* hq = st.h<uint8_t>(o_q);
+        uint8_t* hq = st.hi<uint8_t>(o_q);
         for (int i = 0; i < nitems; i++) std::memcpy(hq + (size_t)i * 32, qdesc + (size_t)item_q[i] * 32, 32);
-        if (nt) std::memcpy(st.h<uint8_t>(o_t), tdesc, (size_t)nt * 32);
-        std::memcpy(st.h<int2>(o_rng), item_rng.data(), (size_t)nitems * 8);
-        if (ncand) std::memcpy(st.h<int>(o_cand), cand, (size_t)ncand * 4);
+        if (nt) std::memcpy(st.hi<uint8_t>(o_t), tdesc, (size_t)nt * 32);
+        std::memcpy(st.hi<int2>(o_rng), item_rng.data(), (size_t)nitems * 8);
+        if (ncand) std::memcpy(st.hi<int>(o_cand), cand, (size_t)ncand * 4);
         dist = st.h<int>(o_dist);
         idx = st.h<int>(o_idx);
         nvalid = st.h<int>(o_nv);
@@ -145,7 +145,7 @@ struct TopkSession {
         const int rr = st.alloc();
         if (rr != ORB_OK) return rr;
         auto put = [&](size_t o, const void* src, size_t bytes) {
-            if (bytes) std::memcpy(c->h_mstage + o, src, bytes);
+            if (bytes) std::memcpy(st.hi<uint8_t>(o), src, bytes);
         };
         put(o_q, desc1, (size_t)n1 * 32);
         put(o_item, item_q.data(), (size_t)nitems * 4);
@@ -168,21 +168,21 @@ struct TopkSession {
         const int n = nitems - from;
         if (n <= 0) return ORB_OK;
         hipError_t e;
-        if (thr) std::memcpy(st.h<int>(o_thr), thr, (size_t)nt * 4);
+        if (thr) std::memcpy(st.hi<int>(o_thr), thr, (size_t)nt * 4);
         // first call: the whole input span in one DMA; a re-rank: the thresholds only
         if ((e = uploaded ? (thr ? st.up(o_thr, o_thr + (size_t)nt * 4) : hipSuccess) : st.up(0, o_in_end)) != hipSuccess)
             return set_error("upload", e), ORB_ERR_HIP;
         uploaded = true;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
         if (grid)
-            e = launch_window_topk(st.d<uint8_t>(o_q), st.d<int>(o_item) + from, cen ? st.d<float2>(o_cen) : nullptr, n,
-                                   st.d<orb_keypoint>(o_k1), st.d<uint8_t>(o_t), st.d<orb_keypoint>(o_k2),
-                                   st.d<int>(o_coff), st.d<int>(o_cidx), wg, thr ? st.d<int>(o_thr) : nullptr, K,
+            e = launch_window_topk(st.di<uint8_t>(o_q), st.di<int>(o_item) + from, cen ? st.di<float2>(o_cen) : nullptr, n,
+                                   st.di<orb_keypoint>(o_k1), st.di<uint8_t>(o_t), st.di<orb_keypoint>(o_k2),
+                                   st.di<int>(o_coff), st.di<int>(o_cidx), wg, thr ? st.di<int>(o_thr) : nullptr, K,
                                    st.h<int>(o_dist) + (size_t)from * K, st.h<int>(o_idx) + (size_t)from * K,
                                    st.h<int>(o_nv) + from, c->stream);
         else
-            e = launch_hamming_topk(st.d<uint8_t>(o_q) + (size_t)from * 32, n, st.d<uint8_t>(o_t), nt,
-                                    st.d<int2>(o_rng) + from, st.d<int>(o_cand), thr ? st.d<int>(o_thr) : nullptr, K,
+            e = launch_hamming_topk(st.di<uint8_t>(o_q) + (size_t)from * 32, n, st.di<uint8_t>(o_t), nt,
+                                    st.di<int2>(o_rng) + from, st.di<int>(o_cand), thr ? st.di<int>(o_thr) : nullptr, K,
                                     st.h<int>(o_dist) + (size_t)from * K, st.h<int>(o_idx) + (size_t)from * K,
                                     st.h<int>(o_nv) + from, c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
@@ -532,22 +532,22 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         const size_t o_in_end = st.off, o_b = st.add((size_t)nitems * 4), o_end = st.off;
         int r = st.alloc();
         if (r != ORB_OK) return r;
-        uint8_t* qd = st.h<uint8_t>(o_qd);
-        float4* qi = st.h<float4>(o_qi);
+        uint8_t* qd = st.hi<uint8_t>(o_qd);
+        float4* qi = st.hi<float4>(o_qi);
         for (int i = 0; i < nitems; i++) {
             const int idx1 = item_q[i];
             std::memcpy(qd + (size_t)i * 32, desc1 + (size_t)idx1 * 32, 32);
             qi[i] = make_float4(kps1[idx1].x, kps1[idx1].y, uright1[idx1] >= 0 ? 1.f : 0.f, 0.f);
         }
-        uint8_t* td = st.h<uint8_t>(o_td);
-        float4* ti = st.h<float4>(o_ti);
+        uint8_t* td = st.hi<uint8_t>(o_td);
+        float4* ti = st.hi<float4>(o_ti);
         for (int j = 0; j < nt; j++) {
             const int idx2 = train_of[j];
             std::memcpy(td + (size_t)j * 32, desc2 + (size_t)idx2 * 32, 32);
             ti[j] = make_float4(kps2[idx2].x, kps2[idx2].y, (float)kps2[idx2].octave, uright2[idx2] >= 0 ? 1.f : 0.f);
         }
-        if (nitems) std::memcpy(st.h<int2>(o_r), rng.data(), (size_t)nitems * 8);
-        if (ncand) std::memcpy(st.h<int>(o_c), cand.data(), (size_t)ncand * 4);
+        if (nitems) std::memcpy(st.hi<int2>(o_r), rng.data(), (size_t)nitems * 8);
+        if (ncand) std::memcpy(st.hi<int>(o_c), cand.data(), (size_t)ncand * 4);
         hipError_t e = st.up(0, o_in_end);
         if (e != hipSuccess) return set_error("upload", e), ORB_ERR_HIP;
         TriParams tp;
@@ -561,8 +561,8 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         }
         tp.only_stereo = only_stereo;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-        e = launch_triangulation(st.d<uint8_t>(o_qd), st.d<float4>(o_qi), st.d<uint8_t>(o_td), st.d<float4>(o_ti),
-                                 st.d<int2>(o_r), st.d<int>(o_c), nitems, tp, st.h<int>(o_b), c->stream);
+        e = launch_triangulation(st.di<uint8_t>(o_qd), st.di<float4>(o_qi), st.di<uint8_t>(o_td), st.di<float4>(o_ti),
+                                 st.di<int2>(o_r), st.di<int>(o_c), nitems, tp, st.h<int>(o_b), c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
         // the kernel writes its results straight into the pinned mirror (host-coherent memory): no D2H command

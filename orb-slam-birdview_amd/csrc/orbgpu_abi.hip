@@ -493,6 +493,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
     // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
+    if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);
@@ -533,6 +534,7 @@ void orb_destroy(orb_ctx* h) {
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_mstage) (void)hipHostFree(c->h_mstage);
+    if (c->h_min) (void)hipHostFree(c->h_min);
     for (int i = 0; i < 2; i++) {
         if (c->h_pairs[i]) (void)hipHostFree(c->h_pairs[i]);
         if (c->pairs_ev[i]) (void)hipEventDestroy(c->pairs_ev[i]);

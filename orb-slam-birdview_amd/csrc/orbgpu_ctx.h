@@ -90,6 +90,12 @@ struct Ctx {
     // in one DMA, its outputs come back in one (matcher.hip Stage)
     uint8_t* h_mstage = nullptr;
     size_t mstage_cap = 0;
+    // ORBGPU_MATCH_ZC (A/B switch, default 0): 0 = a call's inputs go up in one DMA into d_scratch; 1 = the
+    // kernels read them straight from the (coherent) pinned mirror, no DMA; 2 = the same from a second,
+    // non-coherent (GPU-cacheable) pinned mirror h_min.  Outputs are always stored into h_mstage.
+    int match_zc = 0;
+    uint8_t* h_min = nullptr;
+    size_t min_cap = 0;
     // the right extractor's frame + pyramid when it runs on another GPU (orb_compute_stereo_matches)
     uint8_t* d_peer = nullptr;
     size_t peer_cap = 0;
@@ -181,13 +187,31 @@ struct Stage {
                 return set_error("matcher pinned staging", e), ORB_ERR_NOMEM;
             c->mstage_cap = cap;
         }
+        if (c->match_zc == 2 && (need > c->min_cap || !c->h_min)) {
+            if (c->h_min) (void)hipHostFree(c->h_min);
+            c->h_min = nullptr;
+            c->min_cap = 0;
+            const size_t cap = std::max<size_t>(need, 1 << 20);
+            if ((e = hipHostMalloc((void**)&c->h_min, cap, hipHostMallocMapped | hipHostMallocNonCoherent)) !=
+                hipSuccess)
+                return set_error("matcher pinned input mirror", e), ORB_ERR_NOMEM;
+            c->min_cap = cap;
+        }
         return ORB_OK;
     }
     template <class T>
-    T* h(size_t o) const { return reinterpret_cast<T*>(c->h_mstage + o); }
+    T* h(size_t o) const { return reinterpret_cast<T*>(c->h_mstage + o); }   // outputs (host view)
     template <class T>
     T* d(size_t o) const { return reinterpret_cast<T*>(c->d_scratch + o); }
+    uint8_t* in_base() const { return c->match_zc == 2 ? c->h_min : c->h_mstage; }
+    template <class T>
+    T* hi(size_t o) const { return reinterpret_cast<T*>(in_base() + o); }   // inputs, written by the host
+    template <class T>
+    T* di(size_t o) const {   // inputs, as the kernels read them
+        return c->match_zc ? reinterpret_cast<T*>(in_base() + o) : d<T>(o);
+    }
     hipError_t up(size_t from, size_t to) const {
+        if (c->match_zc) return hipSuccess;   // the kernels read the pinned mirror itself
         return to > from ? hipMemcpyAsync(c->d_scratch + from, c->h_mstage + from, to - from, hipMemcpyHostToDevice,
                                           c->stream)
                          : hipSuccess;

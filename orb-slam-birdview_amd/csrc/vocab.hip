@@ -215,11 +215,11 @@ int orb_vocab_transform(orb_ctx* h, const orb_vocab* v, const uint8_t* desc, int
                  o_nd = st.add((size_t)n * 4), o_end = st.off;
     const int r = st.alloc();
     if (r != ORB_OK) return r;
-    std::memcpy(st.h<uint8_t>(o_desc), desc, (size_t)n * 32);
+    std::memcpy(st.hi<uint8_t>(o_desc), desc, (size_t)n * 32);
     hipError_t e = st.up(o_desc, o_w);
     if (e != hipSuccess) return set_error("vocab upload", e), ORB_ERR_HIP;
     hipLaunchKernelGGL(k_vocab_transform, dim3((n + 255) / 256, 1), dim3(256), 0, c->stream, v->d_cbeg, v->d_ccnt,
-                       v->d_child, v->d_cdesc, v->d_word, v->d_weight, st.d<uint8_t>(o_desc), nullptr, n, 0,
+                       v->d_child, v->d_cdesc, v->d_word, v->d_weight, st.di<uint8_t>(o_desc), nullptr, n, 0,
                        v->L - levelsup, st.h<int>(o_w), st.h<float>(o_wt), st.h<uint32_t>(o_nd));
     if ((e = hipGetLastError()) != hipSuccess) return set_error("vocab kernel", e), ORB_ERR_HIP;
     // the kernel writes [word | weight | node] straight into the pinned mirror: no D2H command
