@@ -277,7 +277,7 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
 }
 
 /* NS 32-train subtiles per stage (one accumulator chain each).  With the queries scaled to -S / +S,
- * S = 16 NS, and the accumulators seeded with 128 S + subtile * 32 + row, every result is the stage-local key
+ * S = 16 NS, and the accumulators seeded with 256 S + subtile * 32 + row, every result is the stage-local key
  * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
  * pass and is merged into the running keys once per stage (NS = 2: one merge per 64 trains instead of
  * two). */
@@ -352,13 +352,14 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         for (int i = 0; i < CH; i++) d[i] = PRE ? k.x[i] : pm1x16(k.w[i >> 1] >> (16 * ((ec + i) & 1)));
     };
     unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-    // the MFMA's initial accumulators: 128 SC + subtile * 32 + row, so that every result is already its
-    // stage-local key 128 SC - SC dot + (subtile * 32 + row) = dist << KB | stage row (dist = (256 - dot) / 2)
+    // the MFMA's initial accumulators: 256 SC + subtile * 32 + row, so that every result is already its
+    // stage-local key 256 SC - SC dot + (subtile * 32 + row) = dist << KB | stage row (dot = 256 - 2 dist: the
+    // sum over the 256 bits of (+-1 train bit) x (-+1 query bit))
     v16i_t kc[NS];
 #pragma unroll
     for (int u = 0; u < NS; u++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) kc[u][r] = 128 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+        for (int r = 0; r < 16; r++) kc[u][r] = 256 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
     if (nst > 0) {
         // rows past the slice load the slice's last row (their keys are masked): no zeroing, no branch
