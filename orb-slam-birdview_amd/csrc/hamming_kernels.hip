@@ -281,13 +281,15 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
  * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
  * pass and is merged into the running keys once per stage (NS = 2: one merge per 64 trains instead of
  * two). */
-template <bool PRE, int NW, int NS>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW waves of 32 queries
+template <bool PRE, int NW, int NS, bool PIPE>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW waves of 32
+                                                 // queries; PIPE: stage j's MFMAs beside stage j-1's top-2
 __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
                                                        int* __restrict__ idx_o, int* __restrict__ second_o) {
     constexpr int NT = NW * 64, QB = NW * 32, TR = NS * kMfTr;   // threads, queries, trains per stage
     constexpr int CH = 16 * TR / NT;   // 16-byte chunks of the stage's expanded trains each thread stages
     constexpr int SC = 16 * NS;        // query scale
     constexpr int KB = 5 + (NS == 2);  // stage-local key: dist << KB | stage row
+    constexpr int VG = NS == 2 ? 5 : 6; // VALU issued after each MFMA of the pipelined stage
     static_assert(CH >= 1 && CH <= 4, "staging chunks");
     __shared__ __attribute__((aligned(16))) uint8_t s_t[2][TR * kMfPitch];
     // 1-D grid of (pair, slice, query block), query block fastest.  Blocks are dealt round-robin over the 8
@@ -352,67 +354,126 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         for (int i = 0; i < CH; i++) d[i] = PRE ? k.x[i] : pm1x16(k.w[i >> 1] >> (16 * ((ec + i) & 1)));
     };
     unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-    // the MFMA's initial accumulators: 256 SC + subtile * 32 + row, so that every result is already its
-    // stage-local key 256 SC - SC dot + (subtile * 32 + row) = dist << KB | stage row (dot = 256 - 2 dist: the
-    // sum over the 256 bits of (+-1 train bit) x (-+1 query bit))
+    // the MFMA's initial accumulators: 2^23 + 256 SC + subtile * 32 + row, so that every result is already its
+    // stage-local key 2^23 + (256 SC - SC dot + subtile * 32 + row) = 2^23 + (dist << KB | stage row) (dot =
+    // 256 - 2 dist: the sum over the 256 bits of (+-1 train bit) x (-+1 query bit)).  The 2^23 makes every key
+    // a positive normal f32 bit pattern, ordered like the integer: the top-2 runs in v_med3_f32 /
+    // v_minimum3_f32 (compiler builtins the scheduler can interleave with the MFMAs; the integer v_med3_u32
+    // exists only as inline asm), and the merge's shifts drop bit 23 past bit 31.
     v16i_t kc[NS];
 #pragma unroll
     for (int u = 0; u < NS; u++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) kc[u][r] = 256 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+        for (int r = 0; r < 16; r++) kc[u][r] = 0x800000 + 256 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
+    auto mfma_stage = [&](int buf, v16i_t (&acc)[NS]) {
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            const uint8_t* A = &s_t[buf][(32 * u + c) * kMfPitch + 16 * h];
+            acc[u] = kc[u];
+#pragma unroll
+            for (int s = 0; s < 8; s++)   // one chain per subtile: the other waves on the SIMD hide its latency
+                acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s],
+                                                               acc[u], 0, 0, 0);
+        }
+    };
+    // a stage's top-2 by med3 / min (2 ops per distance), merged into the running keys dist << 16 | train
+    // index once per stage.  A full stage gives every lane 16 NS keys: no tests.
+    constexpr unsigned RM = (1u << KB) - 1;
+    auto top2f = [&](const v16i_t (&acc)[NS], unsigned& lbu, unsigned& lsu, auto keep) {
+        float lbf = __builtin_inff(), lsf = __builtin_inff();
+#pragma unroll
+        for (int u = 0; u < NS; u++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                // (via an int: clang's __builtin_bit_cast of an ext_vector element reads element 0)
+                const int ki = acc[u][r];
+                const float key = keep(u, r) ? __builtin_bit_cast(float, ki) : __builtin_inff();
+                lsf = __builtin_amdgcn_fmed3f(lbf, key, lsf);
+                lbf = __builtin_elementwise_minimum(lbf, key);
+            }
+        lbu = __builtin_bit_cast(uint32_t, lbf);
+        lsu = __builtin_bit_cast(uint32_t, lsf);
+    };
+    auto reduce_full = [&](const v16i_t (&acc)[NS], int tb) {
+        unsigned lbt, lst;
+        top2f(acc, lbt, lst, [](int, int) { return true; });
+        const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
+        s2 = umed3(b, gb, s2);
+        b = min(b, gb);
+        // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
+        s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
+    };
+    auto reduce_any = [&](const v16i_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
+        if (tb + TR <= t1) {
+            reduce_full(acc, tb);
+            return;
+        }
+        unsigned lbt, lst;
+        top2f(acc, lbt, lst, [&](int u, int r) { return tb + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
+        constexpr unsigned kInf = 0x7F800000u;
+        if (lbt != kInf) {   // (only a partial stage leaves a lane without keys)
+            const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
+            s2 = umed3(b, gb, s2);
+            b = min(b, gb);
+            if (lst != kInf) s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
+        }
+    };
     if (nst > 0) {
         // rows past the slice load the slice's last row (their keys are masked): no zeroing, no branch
         stage(0, fetch(min(t0 + er, t1 - 1)));
         __syncthreads();
-        for (int j = 0; j < nst; j++) {
-            const int tb = t0 + TR * j;
-            const bool more = j + 1 < nst;
-            Chunk wn;
-            if (more) wn = fetch(min(tb + TR + er, t1 - 1));
-            v16i_t acc[NS];
-#pragma unroll
-            for (int u = 0; u < NS; u++) {
-                const uint8_t* A = &s_t[j & 1][(32 * u + c) * kMfPitch + 16 * h];
-                acc[u] = kc[u];
-#pragma unroll
-                for (int s = 0; s < 8; s++)   // one chain per subtile: the other waves on the SIMD hide its latency
-                    acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s],
-                                                                   acc[u], 0, 0, 0);
+        if (!PIPE) {
+            for (int j = 0; j < nst; j++) {
+                const int tb = t0 + TR * j;
+                const bool more = j + 1 < nst;
+                Chunk wn;
+                if (more) wn = fetch(min(tb + TR + er, t1 - 1));
+                v16i_t acc[NS];
+                mfma_stage(j & 1, acc);
+                reduce_any(acc, tb);
+                if (more) stage((j + 1) & 1, wn);
+                __syncthreads();
             }
-            // the stage's top-2 by med3 / min (2 ops per distance), then merged into the running keys
-            // dist << 16 | train index once per stage
-            unsigned lbt = 0xFFFFFFFFu, lst = 0xFFFFFFFFu;
-            if (tb + TR <= t1) {
+        } else {
+            // software-pipelined: stage j's MFMA chains are issued beside stage j-1's top-2, so one wave keeps
+            // the matrix pipe and the VALU busy together (every stage but the last is full)
+            v16i_t accA[NS], accB[NS];
+            auto step = [&](int j, v16i_t (&accNew)[NS], const v16i_t (&accOld)[NS]) {
+                const bool more = j + 1 < nst;
+                Chunk wn;
+                if (more) wn = fetch(min(t0 + TR * (j + 1) + er, t1 - 1));
+                mfma_stage(j & 1, accNew);
+                reduce_full(accOld, t0 + TR * (j - 1));
+                // interleave: the A-fragment reads ahead, then each MFMA followed by a share of the top-2
 #pragma unroll
-                for (int u = 0; u < NS; u++)
-#pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const unsigned key = (unsigned)acc[u][r];
-                        lst = umed3(lbt, key, lst);
-                        lbt = min(lbt, key);
-                    }
-            } else {   // the slice's last, partial stage
-#pragma unroll
-                for (int u = 0; u < NS; u++)
-#pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const int tr = tb + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        const unsigned key = tr < t1 ? (unsigned)acc[u][r] : 0xFFFFFFFFu;
-                        lst = umed3(lbt, key, lst);
-                        lbt = min(lbt, key);
-                    }
+                for (int i = 0; i < 8 * NS; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, VG, 0);  // VG VALU
+                }
+                if (more) stage((j + 1) & 1, wn);
+                __syncthreads();
+            };
+            {
+                const bool more = 1 < nst;
+                Chunk wn;
+                if (more) wn = fetch(min(t0 + TR + er, t1 - 1));
+                mfma_stage(0, accA);
+                if (more) stage(1, wn);
+                __syncthreads();
             }
-            if (lbt != 0xFFFFFFFFu) {   // (only a partial stage leaves a lane without keys)
-                constexpr unsigned RM = (1u << KB) - 1;
-                const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
-                s2 = umed3(b, gb, s2);
-                b = min(b, gb);
-                // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
-                if (lst != 0xFFFFFFFFu) s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
+            int j = 1;
+            for (; j + 1 < nst; j += 2) {
+                step(j, accB, accA);
+                step(j + 1, accA, accB);
             }
-            if (more) stage((j + 1) & 1, wn);
-            __syncthreads();
+            if (j < nst) {
+                step(j, accB, accA);
+                reduce_any(accB, t0 + TR * (nst - 1));
+            } else {
+                reduce_any(accA, t0 + TR * (nst - 1));
+            }
         }
     }
     // the two lane halves hold different train rows of the same query
@@ -430,14 +491,21 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     }
 }
 
-// waves per k_top2_mfma workgroup and subtiles per stage (ORBGPU_TOP2=<waves><subtiles>, e.g. 82; an A/B
-// switch, default 82)
+// waves per k_top2_mfma workgroup, subtiles per stage and software pipelining (ORBGPU_TOP2=<waves><subtiles>
+// [p], e.g. 82p; an A/B switch)
 static int top2_waves() {
     static const int w = [] {
         const char* e = std::getenv("ORBGPU_TOP2");
         return (e && e[0] == '4') ? 4 : 8;
     }();
     return w;
+}
+static bool top2_pipe() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_TOP2");
+        return e && e[0] && e[1] && e[2] == 'p';
+    }();
+    return v;
 }
 static int top2_stage() {
     static const int v = [] {
@@ -489,12 +557,15 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (a.tx && max_nt > 0) {
         const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
         hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, nslots), dim3(256), 0, stream, a, max_nt);
-        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<true, 8, 2> : k_top2_mfma<true, 8, 1>)
-                            : (ns == 2 ? k_top2_mfma<true, 4, 2> : k_top2_mfma<true, 4, 1>);
+        const bool pp = top2_pipe();
+        auto kern = nw == 8 ? (ns == 2 ? (pp ? k_top2_mfma<true, 8, 2, true> : k_top2_mfma<true, 8, 2, false>)
+                                       : (pp ? k_top2_mfma<true, 8, 1, true> : k_top2_mfma<true, 8, 1, false>))
+                            : (ns == 2 ? (pp ? k_top2_mfma<true, 4, 2, true> : k_top2_mfma<true, 4, 2, false>)
+                                       : (pp ? k_top2_mfma<true, 4, 1, true> : k_top2_mfma<true, 4, 1, false>));
         hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second);
     } else {
-        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2> : k_top2_mfma<false, 8, 1>)
-                            : (ns == 2 ? k_top2_mfma<false, 4, 2> : k_top2_mfma<false, 4, 1>);
+        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
+                            : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
         hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second);
     }
     if (nsu > 1)
