@@ -195,3 +195,22 @@ def write_synth_vocab_large(path, k=10, L=6, seed=0, stop_frac=0.05):
             first_id = 1 + sum(k ** j for j in range(1, lv))   # ids of this level: children numbered breadth-first
             parent_desc = r["desc"]
     return nb_nodes, nwords
+
+
+def fisheye_driver_frame(keep_mask, idx=0):
+    """The mono_fisheye driver's image path (Examples/Monocular/mono_fisheye.cc:102-116) over a seeded
+    synthetic frame of the camera's size: applyMask (:202-212, pixels whose mask pixel has G > 250 set to 0;
+    `keep_mask` is the (1208, 1920) bool array of pixels that stay), crop Rect(0, 0, 1900, 800) (:111-113),
+    then cv::resize(..., Size(0, 0), 0.5, 0.5) (:116).  For an exact 2x2 downscale OpenCV's INTER_LINEAR
+    switches to the INTER_AREA fast path, the rounded mean (a + b + c + d + 2) >> 2.  The frame is
+    synthesised gray (the driver's colour image is converted to gray later, in Tracking), so only the
+    geometry and the mask are the driver's.  Returns (950x400 image, 950x400 keep mask as 0 / 255: a
+    pixel stays when at least two of its four source pixels stay)."""
+    h, w = keep_mask.shape
+    img = synth_frame(w, h, idx)
+    img = np.where(keep_mask, img, 0).astype(np.uint8)
+    img = img[:800, :1900].astype(np.int32)
+    km = keep_mask[:800, :1900].astype(np.int32)
+    out = (img[0::2, 0::2] + img[0::2, 1::2] + img[1::2, 0::2] + img[1::2, 1::2] + 2) >> 2
+    kq = km[0::2, 0::2] + km[0::2, 1::2] + km[1::2, 0::2] + km[1::2, 1::2]
+    return np.ascontiguousarray(out.astype(np.uint8)), np.where(kq >= 2, 255, 0).astype(np.uint8)

@@ -1,0 +1,14 @@
+# new GPU tests (mask fixture, vocab -> BoW chain), the matcher tests under each zero-copy mode, then the
+# per-call matcher leg under each mode
+set -o pipefail
+mkdir -p gpurun_out/zc; export TMPDIR=/tmp
+T="timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread"
+$T tests/test_mask_fixture.py tests/test_gpu_bow_chain.py > gpurun_out/zc/pytest_new.log 2>&1; rc=$?; tail -3 gpurun_out/zc/pytest_new.log; [ $rc -eq 0 ] || exit 1
+for zc in 1 2; do
+  ORBGPU_MATCH_ZC=$zc $T tests/test_gpu_matcher.py tests/test_gpu_bow_chain.py tests/test_matcher_adapter.py tests/test_gpu_vocab.py > gpurun_out/zc/pytest_zc$zc.log 2>&1; rc=$?; echo "zc=$zc"; tail -2 gpurun_out/zc/pytest_zc$zc.log; [ $rc -eq 0 ] || exit 1
+done
+ARGS="--steps 5 --warmup 2 --no-cpu --no-hamming --no-stereo --no-host-path --no-bird --no-c4 --no-profile-pass"
+for zc in 0 1 2 0 1 2; do
+  ORBGPU_MATCH_ZC=$zc timeout -k 10 200 python3 bench.py $ARGS > gpurun_out/zc/bench_zc$zc.log 2>&1 || { echo "bench zc $zc failed"; tail -5 gpurun_out/zc/bench_zc$zc.log; exit 1; }
+  python3 -c "import json; d=json.loads([l for l in open('gpurun_out/zc/bench_zc$zc.log') if l.startswith('{')][-1])['matcher']; print('zc=$zc', json.dumps({k: v for k, v in d.items() if k != 'note'}))"
+done
