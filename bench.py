@@ -384,10 +384,12 @@ def matcher_leg(img, w, h, nf, device):
     tmp = tempfile.mkdtemp(prefix="orbgpu_matcher_")
     raw, voc = os.path.join(tmp, "frames.raw"), os.path.join(tmp, "voc.bin")
     try:
+        from orbgpu.synth import synth_stereo_right
         a = np.ascontiguousarray(img)
         b = np.ascontiguousarray(np.roll(a, (2, 3), axis=(0, 1)))
+        sr = np.ascontiguousarray(synth_stereo_right(a, 0))   # a rectified right view of `a` (ComputeStereoMatches)
         with open(raw, "wb") as f:
-            f.write(a.tobytes() + b.tobytes())
+            f.write(a.tobytes() + b.tobytes() + a.tobytes() + sr.tobytes())
         write_synth_vocab_large(voc, 10, 6)
         r = subprocess.run([exe, raw, str(w), str(h), str(nf), voc, "50", "10"], capture_output=True, text=True,
                            timeout=300, env=dict(os.environ, ORBGPU_DEVICE=str(device)))
@@ -395,7 +397,7 @@ def matcher_leg(img, w, h, nf, device):
             return {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
         out = json.loads(r.stdout.strip().splitlines()[-1])
         out["note"] = ("median us per call, one call per frame / keyframe pair as Tracking.cc:1029-1032, "
-                       "LoopClosing.cc:265, LocalMapping.cc:278, Tracking.cc:738-739 and Frame.cc:562-569 make them; "
+                       "LoopClosing.cc:265, LocalMapping.cc:278, Tracking.cc:738-739, Frame.cc:562-569 and Frame.cc:141 make them; "
                        "GPU = adapter/ORBmatcher_gpu.cc (host inputs, upload + kernels + host replay), CPU = the "
                        "oracle's restatement of each body, single thread, same inputs; outputs compared equal")
         return out

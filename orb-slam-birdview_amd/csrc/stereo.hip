@@ -373,41 +373,36 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     hipError_t e;
     if ((e = hipStreamSynchronize(cr->stream)) != hipSuccess) return set_error("sync right", e), ORB_ERR_HIP;
     const int cap = std::max(nL, 1);
-    const size_t A = 256;
-    auto al = [&](size_t x) { return (x + A - 1) & ~(A - 1); };
     const int scap = std::max(cap, nR);   // slots: sad (left) and sorted right indices share one stride
-    const size_t need = al((size_t)nL * 28) + al((size_t)nL * 32) + al((size_t)std::max(nR, 1) * 28) +
-                        al((size_t)std::max(nR, 1) * 32) + al(16) + 2 * al((size_t)cap * 4) +
-                        al(stereo_scratch_ints(cl->geom, 1, scap) * 4) + al(4) + A;
-    if (need > cl->scratch_cap || !cl->d_scratch) {
-        if (cl->d_scratch) (void)hipFree(cl->d_scratch);
-        cl->d_scratch = nullptr;
-        cl->scratch_cap = 0;
-        if ((e = hipMalloc((void**)&cl->d_scratch, need)) != hipSuccess) return set_error("stereo scratch", e), ORB_ERR_NOMEM;
-        cl->scratch_cap = need;
+    // the call's device arena with its pinned host mirror (orbgpu_ctx.h Stage, as the matcher calls): the
+    // inputs are packed into the mirror and go up in one DMA, the kernels store mvuRight / mvDepth and the
+    // match count straight into the mirror (host-coherent), one synchronisation
+    Stage st{cl};
+    const size_t o_kL = st.add((size_t)nL * 28), o_dL = st.add((size_t)nL * 32);
+    const size_t o_kR = st.add((size_t)std::max(nR, 1) * 28), o_dR = st.add((size_t)std::max(nR, 1) * 32);
+    const size_t o_cnt = st.add(16);
+    const size_t o_in_end = st.off;
+    const size_t o_u = st.add((size_t)cap * 4), o_d = st.add((size_t)cap * 4), o_nm = st.add(4);
+    const size_t o_s = st.add(stereo_scratch_ints(cl->geom, 1, scap) * 4);   // device-only working space
+    if (const int r = st.alloc(); r != ORB_OK) return r;
+    std::memcpy(st.hi<uint8_t>(o_kL), kpsL, (size_t)nL * 28);
+    std::memcpy(st.hi<uint8_t>(o_dL), descL, (size_t)nL * 32);
+    if (nR) {
+        std::memcpy(st.hi<uint8_t>(o_kR), kpsR, (size_t)nR * 28);
+        std::memcpy(st.hi<uint8_t>(o_dR), descR, (size_t)nR * 32);
     }
-    size_t off = 0;
-    auto take = [&](size_t bytes) {
-        uint8_t* q = cl->d_scratch + off;
-        off += al(bytes);
-        return q;
-    };
-    orb_keypoint* d_kL = (orb_keypoint*)take((size_t)nL * 28);
-    uint8_t* d_dL = take((size_t)nL * 32);
-    orb_keypoint* d_kR = (orb_keypoint*)take((size_t)std::max(nR, 1) * 28);
-    uint8_t* d_dR = take((size_t)std::max(nR, 1) * 32);
-    int* d_cnt = (int*)take(16);
-    float* d_u = (float*)take((size_t)cap * 4);
-    float* d_d = (float*)take((size_t)cap * 4);
-    int* d_s = (int*)take(stereo_scratch_ints(cl->geom, 1, scap) * 4);
-    int* d_nm = (int*)take(4);
-    const int cnt[2] = {nL, nR};
-    if ((e = hipMemcpyAsync(d_kL, kpsL, (size_t)nL * 28, hipMemcpyHostToDevice, cl->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(d_dL, descL, (size_t)nL * 32, hipMemcpyHostToDevice, cl->stream)) != hipSuccess ||
-        (nR && (e = hipMemcpyAsync(d_kR, kpsR, (size_t)nR * 28, hipMemcpyHostToDevice, cl->stream)) != hipSuccess) ||
-        (nR && (e = hipMemcpyAsync(d_dR, descR, (size_t)nR * 32, hipMemcpyHostToDevice, cl->stream)) != hipSuccess) ||
-        (e = hipMemcpyAsync(d_cnt, cnt, sizeof cnt, hipMemcpyHostToDevice, cl->stream)) != hipSuccess)
-        return set_error("stereo upload", e), ORB_ERR_HIP;
+    st.hi<int>(o_cnt)[0] = nL;
+    st.hi<int>(o_cnt)[1] = nR;
+    if ((e = st.up(0, o_in_end)) != hipSuccess) return set_error("stereo upload", e), ORB_ERR_HIP;
+    orb_keypoint* d_kL = st.di<orb_keypoint>(o_kL);
+    uint8_t* d_dL = st.di<uint8_t>(o_dL);
+    orb_keypoint* d_kR = st.di<orb_keypoint>(o_kR);
+    uint8_t* d_dR = st.di<uint8_t>(o_dR);
+    int* d_cnt = st.di<int>(o_cnt);
+    float* h_u = st.h<float>(o_u);
+    float* h_d = st.h<float>(o_d);
+    int* h_nm = st.h<int>(o_nm);
+    int* d_s = st.d<int>(o_s);
     StereoSide SL{cl->last_frames, cl->last_frame_pitch, cl->last_row_stride, cl->d_pyr, 0, 0, d_kL, d_dL, d_cnt, 0};
     StereoSide SR{cr->last_frames, cr->last_frame_pitch, cr->last_row_stride, cr->d_pyr, 0, 0, d_kR, d_dR, d_cnt + 1, 0};
     // Left and right extractors on different GPUs (one GPU per camera stream, BASELINE C4): the window
@@ -441,16 +436,13 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
         SR.pyr = sp;
     }
     if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 1, cl->stream);
-    e = launch_stereo(cl->d_geom, cl->geom, SL, SR, 1, mb, mbf, d_u, d_d, d_s, scap, d_nm, cl->stream);
+    e = launch_stereo(cl->d_geom, cl->geom, SL, SR, 1, mb, mbf, h_u, h_d, d_s, scap, h_nm, cl->stream);
     if (cl->prof_on) Ctx::marker(cl, ORB_K_STEREO, 0, cl->stream);
     if (e != hipSuccess) return set_error("stereo kernels", e), ORB_ERR_HIP;
-    int nm = 0;
-    if ((e = hipMemcpyAsync(uright, d_u, (size_t)nL * 4, hipMemcpyDeviceToHost, cl->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(depth, d_d, (size_t)nL * 4, hipMemcpyDeviceToHost, cl->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(&nm, d_nm, 4, hipMemcpyDeviceToHost, cl->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(cl->stream)) != hipSuccess)
-        return set_error("stereo download", e), ORB_ERR_HIP;
-    if (nmatched) *nmatched = nm;
+    if ((e = hipStreamSynchronize(cl->stream)) != hipSuccess) return set_error("stereo sync", e), ORB_ERR_HIP;
+    std::memcpy(uright, h_u, (size_t)nL * 4);
+    std::memcpy(depth, h_d, (size_t)nL * 4);
+    if (nmatched) *nmatched = *h_nm;
     return ORB_OK;
 }
 

@@ -6,6 +6,8 @@
 //   SearchForTriangulation               ORBmatcher(0.6, false)  LocalMapping::CreateNewMapPoints, LocalMapping.cc:225,278
 //   SearchForInitialization (window 100) ORBmatcher(0.9, true)   Tracking::MonocularInitialization, Tracking.cc:738-739
 //   Frame::ComputeBoW (transform, levelsup 4)                    Frame.cc:562-569
+//   Frame::ComputeStereoMatches (rectified pair, KITTI mb / mbf)  Frame.cc:662-836, from the stereo Frame ctor :141
+//     (only when frames.raw holds four frames: the last two are the left / right images)
 //
 // GPU side: the reference-signature adapter (adapter/ORBmatcher_gpu.cc) on Frame / KeyFrame objects
 // (tests/cpp/slam_api models; their grid lookups are the caller's CPU code, Frame.cc:378-547), and the
@@ -31,6 +33,7 @@
 #include "../oracle/orb_oracle.h"
 #include "../orb-slam-birdview_amd/host/ORBVocabulary.h"
 #include "../orb-slam-birdview_amd/host/ORBextractor.h"
+#include "../orb-slam-birdview_amd/host/Stereo.h"
 #include "ORBmatcher.h"   // tests/cpp/slam_api: the reference's declaration, modelled
 
 using namespace ORB_SLAM2;
@@ -88,13 +91,15 @@ int main(int argc, char** argv) {
     }
     const int w = atoi(argv[2]), h = atoi(argv[3]), nfeat = atoi(argv[4]), reps = atoi(argv[6]);
     const int cpu_reps = argc > 7 ? atoi(argv[7]) : std::max(3, reps / 5);
-    std::vector<uint8_t> frames((size_t)w * h * 2);
+    std::vector<uint8_t> frames((size_t)w * h * 4);
     FILE* fp = fopen(argv[1], "rb");
-    if (!fp || fread(frames.data(), 1, frames.size(), fp) != frames.size()) {
+    const size_t nread = fp ? fread(frames.data(), 1, frames.size(), fp) : 0;
+    if (!fp || (nread != frames.size() / 2 && nread != frames.size())) {
         fprintf(stderr, "cannot read %s\n", argv[1]);
         return 2;
     }
     fclose(fp);
+    const bool with_stereo = nread == frames.size();
 
     // ---- features: GPU extractor + GPU vocabulary (the product)
     ORBextractor ex(nfeat, 1.2f, 8, 20, 7, 0);
@@ -326,6 +331,39 @@ int main(int argc, char** argv) {
         snprintf(buf, sizeof buf, ", \"vocabulary\": {\"k\": %d, \"L\": %d, \"nodes\": %d, \"words\": %d, \"levelsup\": 4, "
                  "\"featvec_nodes\": [%d, %d]}", k, L, nn, nw, (int)fe[0].fv.size(), (int)fe[1].fv.size());
         out += buf;
+    }
+    // ---- Frame::ComputeStereoMatches on a rectified pair (frames 2 and 3): the two extractors ran on the left
+    // and right images (the stereo Frame ctor, Frame.cc:124-127), then the search (:141 -> :662-836)
+    if (with_stereo) {
+        ORBextractor exL(nfeat, 1.2f, 8, 20, 7, 0), exR(nfeat, 1.2f, 8, 20, 7, 0);
+        std::vector<ORB_SLAM2::KeyPoint> kL, kR;
+        DescriptorMat dL, dR;
+        const uint8_t* imL = frames.data() + (size_t)2 * w * h;
+        const uint8_t* imR = frames.data() + (size_t)3 * w * h;
+        exL(ImageView(imL, w, h), ImageView(), kL, dL);
+        exR(ImageView(imR, w, h), ImageView(), kR, dR);
+        const float mb = 0.54f, mbf = 0.54f * 721.5f;   // KITTI-like baseline / baseline x fx
+        std::vector<float> ur, dp;
+        const int nm = ComputeStereoMatches(exL, exR, kL, dL, kR, dR, mb, mbf, ur, dp);
+        void* oL = oracle_create(nfeat, 1.2f, 8, 20, 7, 0);
+        void* oR = oracle_create(nfeat, 1.2f, 8, 20, 7, 0);
+        oracle_run(oL, imL, w, h, w);
+        oracle_run(oR, imR, w, h, w);
+        const int nL = (int)kL.size(), nR = (int)kR.size();
+        std::vector<float> our(nL + 1), odp(nL + 1);
+        const OracleKeyPoint* okL = reinterpret_cast<const OracleKeyPoint*>(kL.data());
+        const OracleKeyPoint* okR = reinterpret_cast<const OracleKeyPoint*>(kR.data());
+        const int onm = oracle_stereo_matches(oL, oR, nL, okL, dL.buf.data(), nR, okR, dR.buf.data(), mb, mbf,
+                                              our.data(), odp.data());
+        bool ok = nm == onm && (int)ur.size() == nL && (int)dp.size() == nL;
+        for (int i = 0; ok && i < nL; i++) ok = memcmp(&ur[i], &our[i], 4) == 0 && memcmp(&dp[i], &odp[i], 4) == 0;
+        const double g = median_us([&] { ComputeStereoMatches(exL, exR, kL, dL, kR, dR, mb, mbf, ur, dp); }, reps);
+        const double c = median_us([&] {
+            oracle_stereo_matches(oL, oR, nL, okL, dL.buf.data(), nR, okR, dR.buf.data(), mb, mbf, our.data(), odp.data());
+        }, cpu_reps);
+        oracle_destroy(oL);
+        oracle_destroy(oR);
+        emit("ComputeStereoMatches", g, c, nm, onm, ok);
     }
     snprintf(buf, sizeof buf, ", \"keypoints\": [%d, %d], \"gpu_reps\": %d, \"cpu_reps\": %d, \"all_equal\": %s}", nA, nB,
              reps, cpu_reps, all_ok ? "true" : "false");

@@ -3,9 +3,9 @@
 set -o pipefail
 mkdir -p gpurun_out/zc; export TMPDIR=/tmp
 T="timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread"
-$T tests/test_mask_fixture.py tests/test_gpu_bow_chain.py > gpurun_out/zc/pytest_new.log 2>&1; rc=$?; tail -3 gpurun_out/zc/pytest_new.log; [ $rc -eq 0 ] || exit 1
+$T tests/test_mask_fixture.py tests/test_gpu_bow_chain.py tests/test_gpu_stereo.py > gpurun_out/zc/pytest_new.log 2>&1; rc=$?; tail -3 gpurun_out/zc/pytest_new.log; [ $rc -eq 0 ] || exit 1
 for zc in 1 2; do
-  ORBGPU_MATCH_ZC=$zc $T tests/test_gpu_matcher.py tests/test_gpu_bow_chain.py tests/test_matcher_adapter.py tests/test_gpu_vocab.py > gpurun_out/zc/pytest_zc$zc.log 2>&1; rc=$?; echo "zc=$zc"; tail -2 gpurun_out/zc/pytest_zc$zc.log; [ $rc -eq 0 ] || exit 1
+  ORBGPU_MATCH_ZC=$zc $T tests/test_gpu_matcher.py tests/test_gpu_bow_chain.py tests/test_matcher_adapter.py tests/test_gpu_vocab.py tests/test_gpu_stereo.py > gpurun_out/zc/pytest_zc$zc.log 2>&1; rc=$?; echo "zc=$zc"; tail -2 gpurun_out/zc/pytest_zc$zc.log; [ $rc -eq 0 ] || exit 1
 done
 ARGS="--steps 5 --warmup 2 --no-cpu --no-hamming --no-stereo --no-host-path --no-bird --no-c4 --no-profile-pass"
 for zc in 0 1 2 0 1 2; do
