@@ -994,7 +994,10 @@ __global__ __launch_bounds__(256) void k_fast_wave(const Geom* __restrict__ g, c
     uint32_t v0[8], v1[8];
     if (c0.valid && c0.aligned) fast_roi_issue(c0, lane, v0);
     if (has1 && c1.valid && c1.aligned) fast_roi_issue(c1, lane, v1);
-    if (err && blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // k_octree's overflow flag (set after this kernel)
+    if (err && blockIdx.x == 0 && threadIdx.x == 0) {   // k_octree's overflow flag (set after this kernel)
+        err[0] = 0;
+        if (cnum == g->ncells) err[1] = 0;   // a launch over every level also clears the forked branch's flag
+    }
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         if (k == 1 && !has1) break;
@@ -2189,7 +2192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             int tot = 0;
             for (int i = 0; i < nl; i++) tot += cnts[i];
             outN[f] = tot;
-            if (errHost && f == 0) *errHost = *err;   // the octree's overflow flag, for the host path
+            if (errHost && f == 0) *errHost = err[0] | err[1];   // the octrees' overflow flags, for the host path
         }
     };
     if (s0 >= g->nkpcap) {
@@ -2287,7 +2290,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                            d_frames, frame_pitch, row_stride, b.d_pyr, b.d_cands, b.d_candFirst, items, cbeg, cnum,
                            b.d_stamps, zero, ipw);
     };
-    auto octree = [&](int lbase, int nl, hipStream_t s) {
+    auto octree = [&](int lbase, int nl, hipStream_t s, int* err) {
         // a small batch (the host path's single frame, C5's 8-frame step) has fewer blocks than CUs, so the
         // level-0 blocks are the whole latency: 1024 threads halve their per-key steps, and the keys get all
         // the LDS a CU has (no global key scratch: at 4,000 features the node tables alone pass the 52 KiB
@@ -2296,7 +2299,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         const int lk = one ? octree_lds_keys_whole_cu(g) : octree_lds_keys(g.node_cap);
         hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
                            octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_candFirst,
-                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, b.d_err, lk,
+                           b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, err, lk,
                            b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
     };
     auto describe = [&](hipStream_t s) {
@@ -2308,6 +2311,18 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
                            b.d_err, b.err_host);
     };
     int* zero = b.zero_err ? b.d_err : nullptr;
+    hipError_t fe = hipSuccess;
+    const bool forked = b.fork_s2 != nullptr && g.nlevels > 1;
+    const int c0 = g.L[1].cell_base;   // level 0's cells
+    if (forked) {
+        // level 0's FAST -> octree reads only the input frame (ORBextractor.cc:1115, 1127): its own stream and
+        // overflow flag (d_err[1], zeroed by its FAST launch), joined before k_describe
+        if ((fe = hipEventRecord(b.ev_fork, stream)) != hipSuccess || (fe = hipStreamWaitEvent(b.fork_s2, b.ev_fork, 0)) != hipSuccess)
+            return fe;
+        fast(0, c0, b.fork_s2, b.d_err + 1);
+        octree(0, 1, b.fork_s2, b.d_err + 1);
+        if ((fe = hipEventRecord(b.ev_join, b.fork_s2)) != hipSuccess) return fe;
+    }
     if (marker) marker(user, ORB_K_RESIZE, 1, stream);
     if (b.chain.nseg && nframes <= kChainMaxFrames) {   // the few-launch pyramid (k_pyramid_chain)
         RcoefOff ro;
@@ -2324,11 +2339,14 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     }
     if (marker) marker(user, ORB_K_RESIZE, 0, stream);
     if (marker) marker(user, ORB_K_FAST, 1, stream);
-    fast(0, g.ncells, stream, zero);
+    if (forked) fast(c0, g.ncells - c0, stream, zero);
+    else fast(0, g.ncells, stream, zero);
     if (marker) marker(user, ORB_K_FAST, 0, stream);
     if (marker) marker(user, ORB_K_OCTREE, 1, stream);
-    octree(0, g.nlevels, stream);
+    if (forked) octree(1, g.nlevels - 1, stream, b.d_err);
+    else octree(0, g.nlevels, stream, b.d_err);
     if (marker) marker(user, ORB_K_OCTREE, 0, stream);
+    if (forked && (fe = hipStreamWaitEvent(stream, b.ev_join, 0)) != hipSuccess) return fe;
     if (marker) marker(user, ORB_K_DESCRIBE, 1, stream);
     describe(stream);
     if (marker) marker(user, ORB_K_DESCRIBE, 0, stream);

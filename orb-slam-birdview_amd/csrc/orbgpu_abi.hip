@@ -324,7 +324,7 @@ int Ctx::ensure_frames(int nframes) {
         (e = grow(d_knode, knode_cap, (size_t)nframes * nl * g.max_level_cand)) != hipSuccess ||
         (e = grow(d_lvlKps, lvlkps_cap, (size_t)nframes * g.nkpcap)) != hipSuccess ||
         (e = grow(d_lvlCount, lvlc_cap, (size_t)nframes * nl)) != hipSuccess ||
-        (e = grow(d_err, err_cap, 1)) != hipSuccess) {
+        (e = grow(d_err, err_cap, 2)) != hipSuccess) {
         set_error("device allocation for the extractor", e);
         return ORB_ERR_NOMEM;
     }
@@ -332,7 +332,7 @@ int Ctx::ensure_frames(int nframes) {
         return set_error("stamps", e), ORB_ERR_NOMEM;
     // the overflow flag is read by orb_sync even before the first extraction (every extraction zeroes
     // it in its first kernel)
-    if (fresh_err && (e = hipMemsetAsync(d_err, 0, sizeof(int), stream)) != hipSuccess)
+    if (fresh_err && (e = hipMemsetAsync(d_err, 0, 2 * sizeof(int), stream)) != hipSuccess)
         return set_error("memset", e), ORB_ERR_HIP;
     return ORB_OK;
 }
@@ -357,6 +357,8 @@ ExtractBuffers Ctx::buffers() const {
     b.zero_err = 1;
     b.err_host = nullptr;
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
+    b.fork_s2 = nullptr;
+    b.ev_fork = b.ev_join = nullptr;
     return b;
 }
 
@@ -379,6 +381,19 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     // the few-launch pyramid trades redundant work for fewer dependent launches: it pays for one frame
     // in flight (the host path), not when several batches share the GPU (measured)
     if (!latency) bufs.chain.nseg = 0;
+    // one frame in flight: level 0's FAST -> octree on a second stream beside the pyramid
+    if (latency && fork && !prof_on && !fast_stamps && geom.nlevels > 1 && nframes == 1) {
+        hipError_t fe = hipSuccess;
+        if (!stream2 && (fe = hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking)) != hipSuccess)
+            return set_error("second stream", fe), ORB_ERR_HIP;
+        if (!ev_fork && (fe = hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming)) != hipSuccess)
+            return set_error("fork event", fe), ORB_ERR_HIP;
+        if (!ev_join && (fe = hipEventCreateWithFlags(&ev_join, hipEventDisableTiming)) != hipSuccess)
+            return set_error("join event", fe), ORB_ERR_HIP;
+        bufs.fork_s2 = stream2;
+        bufs.ev_fork = ev_fork;
+        bufs.ev_join = ev_join;
+    }
     // one frame in flight (the host path): direct launches measured faster than a graph replay (the first
     // kernel is dispatched as soon as it is launched, while the host submits the rest)
     if (use_graph && !prof_on && !fast_stamps && !latency) {
@@ -493,6 +508,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
     // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
+    if (const char* ev = std::getenv("ORBGPU_FORK")) c->fork = ev[0] != '0';
     if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
@@ -542,6 +558,9 @@ void orb_destroy(orb_ctx* h) {
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -592,10 +611,10 @@ int orb_sync(orb_ctx* h) {
     CTX_GUARD(c);
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return set_error("hipStreamSynchronize", e), ORB_ERR_HIP;
-    int err = 0;
-    if (c->d_err && (e = hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess)
+    int err[2] = {0, 0};
+    if (c->d_err && (e = hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost)) != hipSuccess)
         return set_error("read error flag", e), ORB_ERR_HIP;
-    if (err) {
+    if (err[0] | err[1]) {
         set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
         return ORB_ERR_INTERNAL;
     }

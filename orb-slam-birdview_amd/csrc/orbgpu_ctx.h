@@ -27,6 +27,10 @@ struct Ctx {
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
+    // the host path's second stream and fork / join events (Ctx::run_extract latency mode; ORBGPU_FORK=0: off)
+    bool fork = true;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
     // ORBextractor tables (ORBextractor.cc:410-470)
     float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},

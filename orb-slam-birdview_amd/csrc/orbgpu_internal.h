@@ -143,11 +143,15 @@ struct ExtractBuffers {
     uint16_t* d_knode;             // same
     uint32_t* d_lvlKps;            // nframes * nkpcap
     int* d_lvlCount;               // nframes * nlevels
-    int* d_err;                    // 1 int: internal overflow flag
+    int* d_err;                    // 2 ints: internal overflow flags (the level-0 branch of a forked launch sets [1])
     int* err_host;                 // host-coherent copy of it written by k_describe (the host path), or NULL
     int zero_err;                  // FAST zeroes d_err (0: the caller did)
     unsigned long long* d_stamps;  // phase timestamps (ORBGPU_FAST_STAMPS=1 diagnostic): 8 per (frame, cell),
                                    // 32 per (frame, level), 8 per keypoint slot
+    // Forked launch (one frame in flight, the host path): level 0's FAST -> octree branch runs on fork_s2
+    // beside the pyramid and levels 1.. on the launch stream, joined before k_describe (NULL: one stream)
+    hipStream_t fork_s2;
+    hipEvent_t ev_fork, ev_join;
 };
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin, hipStream_t stream);

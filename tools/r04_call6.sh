@@ -12,3 +12,7 @@ for zc in 0 1 2 0 1 2; do
   ORBGPU_MATCH_ZC=$zc timeout -k 10 200 python3 bench.py $ARGS > gpurun_out/zc/bench_zc$zc.log 2>&1 || { echo "bench zc $zc failed"; tail -5 gpurun_out/zc/bench_zc$zc.log; exit 1; }
   python3 -c "import json; d=json.loads([l for l in open('gpurun_out/zc/bench_zc$zc.log') if l.startswith('{')][-1])['matcher']; print('zc=$zc', json.dumps({k: v for k, v in d.items() if k != 'note'}))"
 done
+# the forked host path: extraction / mirror tests (forked by default), then its latency A/B
+$T tests/test_gpu_extract.py tests/test_host_mirror.py tests/test_gpu_variants.py > gpurun_out/zc/pytest_fork.log 2>&1; rc=$?; tail -2 gpurun_out/zc/pytest_fork.log; [ $rc -eq 0 ] || exit 1
+bash tools/host_quick.sh ORBGPU_FORK=0 > gpurun_out/zc/host_fork.log 2>&1 || { tail -5 gpurun_out/zc/host_fork.log; exit 1; }
+cat gpurun_out/zc/host_fork.log | cut -c1-200
