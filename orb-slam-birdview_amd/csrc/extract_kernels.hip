@@ -1,7 +1,8 @@
 // gfx950 kernels of the ORB extractor: pyramid, per-cell FAST+NMS, DistributeOctTree, and the fused
-// IC-angle + 7x7 Gaussian + rBRIEF descriptor.  Integer/byte work: no MFMA in these kernels (the
-// all-pairs Hamming top-2 in hamming_kernels.hip is the one MFMA user); the bounds
-// are HBM bytes and VALU issue.
+// IC-angle + 7x7 Gaussian + rBRIEF descriptor.  Integer/byte work, bound by HBM bytes and VALU issue
+// (DESIGN.md §4); the one matrix-core use here is k_describe's blur row pass, an exact int8 product of the
+// keypoint window and the banded 7-tap matrix (v_mfma_i32_16x16x64_i8).  The all-pairs
+// Hamming top-2 (hamming_kernels.hip) is the other MFMA user.
 //
 // Compiled with -ffp-contract=off and correctly-rounded fp32 divide, so every float expression on the
 // path (root split hX, fastAtan2, BRIEF rotation, keypoint scaling) is evaluated exactly as written; the
