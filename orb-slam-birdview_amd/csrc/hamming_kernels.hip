@@ -9,6 +9,7 @@
 // (matcher.hip).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "orbgpu_internal.h"
 
@@ -284,7 +285,8 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
 template <bool PRE, int NW, int NS, bool PIPE>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW waves of 32
                                                  // queries; PIPE: stage j's MFMAs beside stage j-1's top-2
 __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
-                                                       int* __restrict__ idx_o, int* __restrict__ second_o) {
+                                                       int* __restrict__ idx_o, int* __restrict__ second_o,
+                                                       int vblocks) {
     constexpr int NT = NW * 64, QB = NW * 32, TR = NS * kMfTr;   // threads, queries, trains per stage
     constexpr int CH = 16 * TR / NT;   // 16-byte chunks of the stage's expanded trains each thread stages
     constexpr int SC = 16 * NS;        // query scale
@@ -297,7 +299,12 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     // pair, which all stream the same expanded trains, then share one L2 (dealt round-robin, every pair's
     // 512 KB of C3 trains was fetched into all eight L2s: PMC 1.14 GB per 255-pair launch,
     // profiles/r04/v1_hamming.json)
-    const int nb = gridDim.x, xq = nb >> 3, xr = nb & 7, xcd = blockIdx.x & 7, xj = blockIdx.x >> 3;
+    // Persistent form (vblocks > gridDim.x): workgroup w runs the virtual blocks w, w + G, w + 2G, ... of a
+    // vblocks-block grid (G = gridDim.x, a multiple of 8, so a virtual block keeps its XCD): no per-block launch
+    // and drain, one workgroup per slot for the whole launch.
+    for (int vb = blockIdx.x; vb < vblocks; vb += gridDim.x) {
+    __syncthreads();   // (a previous item's last LDS reads precede this item's staging)
+    const int nb = vblocks, xq = nb >> 3, xr = nb & 7, xcd = vb & 7, xj = vb >> 3;
     const int lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xj;
     const int qbi = lb % a.qblocks, rest = lb / a.qblocks;
     const int sli = rest % a.nslices, p = rest / a.nslices;
@@ -305,7 +312,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
     const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
     const int qblk = qbi * QB;
-    if (qblk >= nq) return;   // whole workgroup
+    if (qblk >= nq) continue;   // whole workgroup
     const int t0 = sli * a.slice, t1 = min(nt, t0 + a.slice);
     const int h = lane >> 5, c = lane & 31;
     const int qi = qblk + wv * 32 + c;
@@ -480,40 +487,39 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     const unsigned ob = __shfl_xor(b, 32), os = __shfl_xor(s2, 32);
     s2 = min(min(s2, os), max(b, ob));
     b = min(b, ob);
-    if (h != 0 || qi >= nq) return;
-    const long long o = (long long)p * a.out_stride + qi;
-    if (a.nslices == 1) {
-        best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
-        idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
-        second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
-    } else {
-        part[((long long)p * a.nslices + sli) * a.out_stride + qi] = make_uint2(b, s2);
+    if (h == 0 && qi < nq) {
+        const long long o = (long long)p * a.out_stride + qi;
+        if (a.nslices == 1) {
+            best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
+            idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
+            second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
+        } else {
+            part[((long long)p * a.nslices + sli) * a.out_stride + qi] = make_uint2(b, s2);
+        }
     }
+    }   // virtual blocks
 }
 
-// waves per k_top2_mfma workgroup, subtiles per stage and software pipelining (ORBGPU_TOP2=<waves><subtiles>
-// [p], e.g. 82p; an A/B switch)
-static int top2_waves() {
-    static const int w = [] {
+// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81pP"): '4' / '8' waves per workgroup,
+// '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot)
+struct Top2Cfg {
+    int waves = 8, stage = 1;
+    bool pipe = true, persist = true;
+};
+static const Top2Cfg& top2_cfg() {
+    static const Top2Cfg c = [] {
+        Top2Cfg t;
         const char* e = std::getenv("ORBGPU_TOP2");
-        return (e && e[0] == '4') ? 4 : 8;
+        if (!e || !*e) return t;
+        t.waves = std::strchr(e, '4') ? 4 : 8;
+        t.stage = std::strchr(e, '2') ? 2 : 1;
+        t.pipe = std::strchr(e, 'p') != nullptr;
+        t.persist = std::strchr(e, 'P') != nullptr;
+        return t;
     }();
-    return w;
+    return c;
 }
-static bool top2_pipe() {
-    static const bool v = [] {
-        const char* e = std::getenv("ORBGPU_TOP2");
-        return e && e[0] && e[1] && e[2] == 'p';
-    }();
-    return v;
-}
-static int top2_stage() {
-    static const int v = [] {
-        const char* e = std::getenv("ORBGPU_TOP2");
-        return (e && e[0] && e[1] == '1') ? 1 : 2;
-    }();
-    return v;
-}
+static int top2_waves() { return top2_cfg().waves; }
 
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     npairs = std::max(npairs, 1);
@@ -545,28 +551,38 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (npairs <= 0 || max_nq <= 0) return hipSuccess;
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
-    const int nw = top2_waves(), ns = top2_stage();
+    const Top2Cfg& cfg = top2_cfg();
+    const int nw = cfg.waves, ns = cfg.stage;
     const int qb = (max_nq + 32 * nw - 1) / (32 * nw);
     a.slice = top2_slice_len(npairs, max_nq, max_nt);
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);   // 1: k_top2_mfma writes the outputs itself
     a.qblocks = qb;
     a.nslices = nsu;
-    const dim3 grid((unsigned)((long long)qb * nsu * npairs));
+    const int vblocks = (int)((long long)qb * nsu * npairs);
+    dim3 grid((unsigned)vblocks);
     // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
     // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels
     if (a.tx && max_nt > 0) {
         const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
         hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, nslots), dim3(256), 0, stream, a, max_nt);
-        const bool pp = top2_pipe();
+        const bool pp = cfg.pipe;
         auto kern = nw == 8 ? (ns == 2 ? (pp ? k_top2_mfma<true, 8, 2, true> : k_top2_mfma<true, 8, 2, false>)
                                        : (pp ? k_top2_mfma<true, 8, 1, true> : k_top2_mfma<true, 8, 1, false>))
                             : (ns == 2 ? (pp ? k_top2_mfma<true, 4, 2, true> : k_top2_mfma<true, 4, 2, false>)
                                        : (pp ? k_top2_mfma<true, 4, 1, true> : k_top2_mfma<true, 4, 1, false>));
-        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second);
+        if (cfg.persist) {   // one workgroup per resident slot (a multiple of 8: virtual blocks keep their XCD)
+            int dev = 0, ncu = 256, per = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 64 * nw, 0) != hipSuccess || per < 1) per = 1;
+            const int slots = std::max(8, (per * ncu) & ~7);
+            if (vblocks > slots) grid = dim3((unsigned)slots);
+        }
+        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second, vblocks);
     } else {
         auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
                             : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
-        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second);
+        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second, vblocks);
     }
     if (nsu > 1)
         hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,
