@@ -252,9 +252,10 @@ __device__ __forceinline__ v4i_t pm1x16(uint32_t w) {   // bits 0..15 of w -> 16
 /* The pairs' train descriptors expanded to +-1 int8 once per launch (thread = one descriptor dword ->
  * 32 bytes), so k_top2_mfma's train tiles are plain copies: without it every query workgroup of a pair
  * re-expands every train tile (~40 VALU per thread and tile, more than the tile's top-2 updates). */
-__global__ __launch_bounds__(256) void k_expand_pm1(Top2Batch a, int max_nt) {
-    // blockIdx.y = expansion slot: one per distinct train frame (a.tx_frames) or, without that list, one per pair
-    const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void k_expand_pm1(Top2Batch a, int max_nt, int slot0) {
+    // slot0 + blockIdx.y = expansion slot: one per distinct train frame (a.tx_frames) or, without that list, one
+    // per pair
+    const int p = slot0 + blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
     const int row = i >> 3, s = i & 7;
     const int tf = a.tx_frames ? a.tx_frames[p] : (a.frames ? a.frames[p].y : 0);
     const int nt = a.counts ? a.counts[tf] : a.nt;
@@ -500,11 +501,12 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     }   // virtual blocks
 }
 
-// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81pP"): '4' / '8' waves per workgroup,
-// '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot)
+// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81pPo"): '4' / '8' waves per workgroup,
+// '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
+// expansion of chunk c + 1 overlapped with the top-2 of chunk c (Top2Overlap)
 struct Top2Cfg {
     int waves = 8, stage = 1;
-    bool pipe = true, persist = true;
+    bool pipe = true, persist = true, overlap = true;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {
@@ -515,11 +517,14 @@ static const Top2Cfg& top2_cfg() {
         t.stage = std::strchr(e, '2') ? 2 : 1;
         t.pipe = std::strchr(e, 'p') != nullptr;
         t.persist = std::strchr(e, 'P') != nullptr;
+        t.overlap = std::strchr(e, 'o') != nullptr;
         return t;
     }();
     return c;
 }
 static int top2_waves() { return top2_cfg().waves; }
+bool top2_overlap_enabled() { return top2_cfg().overlap; }
+int top2_queries_per_block() { return 32 * top2_cfg().waves; }
 
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     npairs = std::max(npairs, 1);
@@ -547,7 +552,8 @@ int top2_launch_slices(int npairs, int max_nq, int max_nt) {
 }
 
 hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq, int max_nt, int* d_best,
-                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream) {
+                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream,
+                                     const Top2Overlap* ov) {
     if (npairs <= 0 || max_nq <= 0) return hipSuccess;
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
@@ -559,30 +565,60 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     a.qblocks = qb;
     a.nslices = nsu;
     const int vblocks = (int)((long long)qb * nsu * npairs);
-    dim3 grid((unsigned)vblocks);
     // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
     // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels
-    if (a.tx && max_nt > 0) {
-        const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
-        hipLaunchKernelGGL(k_expand_pm1, dim3((max_nt * 8 + 255) / 256, nslots), dim3(256), 0, stream, a, max_nt);
+    if (!(a.tx && max_nt > 0)) {
+        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
+                            : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)vblocks), dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx,
+                           d_second, vblocks);
+    } else {
         const bool pp = cfg.pipe;
         auto kern = nw == 8 ? (ns == 2 ? (pp ? k_top2_mfma<true, 8, 2, true> : k_top2_mfma<true, 8, 2, false>)
                                        : (pp ? k_top2_mfma<true, 8, 1, true> : k_top2_mfma<true, 8, 1, false>))
                             : (ns == 2 ? (pp ? k_top2_mfma<true, 4, 2, true> : k_top2_mfma<true, 4, 2, false>)
                                        : (pp ? k_top2_mfma<true, 4, 1, true> : k_top2_mfma<true, 4, 1, false>));
-        if (cfg.persist) {   // one workgroup per resident slot (a multiple of 8: virtual blocks keep their XCD)
+        int slots = 1 << 30;   // persistent: one workgroup per resident slot (a multiple of 8: virtual blocks keep
+        if (cfg.persist) {     // their XCD)
             int dev = 0, ncu = 256, per = 0;
             (void)hipGetDevice(&dev);
             if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 64 * nw, 0) != hipSuccess || per < 1) per = 1;
-            const int slots = std::max(8, (per * ncu) & ~7);
-            if (vblocks > slots) grid = dim3((unsigned)slots);
+            slots = std::max(8, (per * ncu) & ~7);
         }
-        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second, vblocks);
-    } else {
-        auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
-                            : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
-        hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx, d_second, vblocks);
+        const int nslots = a.tx_frames ? a.n_tx_frames : npairs;
+        const int gx = (max_nt * 8 + 255) / 256;
+        if (ov && ov->nchunks > 1 && nsu == 1 && a.tx_frames && a.tx_slot) {
+            // chunk c's expansion (its pairs' train slots) on the side stream, chunk c's top-2 on the launch
+            // stream behind it: expansion c + 1 (HBM writes) runs beside top-2 c (matrix cores)
+            hipError_t e;
+            if ((e = hipEventRecord(ov->ev_fork, stream)) != hipSuccess ||
+                (e = hipStreamWaitEvent(ov->s2, ov->ev_fork, 0)) != hipSuccess)
+                return e;
+            int s0 = 0;
+            for (int cix = 0; cix < ov->nchunks; cix++) {
+                const int s1 = std::min(ov->slot_end[cix], nslots);
+                if (s1 > s0) hipLaunchKernelGGL(k_expand_pm1, dim3(gx, s1 - s0), dim3(256), 0, ov->s2, a, max_nt, s0);
+                s0 = std::max(s0, s1);
+                if ((e = hipEventRecord(ov->ev[cix], ov->s2)) != hipSuccess) return e;
+            }
+            for (int cix = 0; cix < ov->nchunks; cix++) {
+                const int pb = ov->pair_beg[cix], pe = ov->pair_beg[cix + 1];
+                if (pe <= pb) continue;
+                if ((e = hipStreamWaitEvent(stream, ov->ev[cix], 0)) != hipSuccess) return e;
+                Top2Batch ac = a;
+                ac.frames = a.frames + pb;
+                ac.tx_slot = a.tx_slot + pb;
+                const int vb = qb * (pe - pb);
+                const long long oo = (long long)pb * a.out_stride;
+                hipLaunchKernelGGL(kern, dim3((unsigned)std::min(vb, slots)), dim3(64 * nw), 0, stream, ac, d_part,
+                                   d_best + oo, d_best_idx + oo, d_second + oo, vb);
+            }
+            return hipGetLastError();
+        }
+        hipLaunchKernelGGL(k_expand_pm1, dim3(gx, nslots), dim3(256), 0, stream, a, max_nt, 0);
+        hipLaunchKernelGGL(kern, dim3((unsigned)std::min(vblocks, slots)), dim3(64 * nw), 0, stream, a, d_part, d_best,
+                           d_best_idx, d_second, vblocks);
     }
     if (nsu > 1)
         hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,

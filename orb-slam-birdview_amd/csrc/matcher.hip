@@ -381,8 +381,34 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     const int2* d_frames = reinterpret_cast<const int2*>(d_up);
     Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap, tx, kp_cap,
                  d_up + 2 * npairs, d_up + 3 * npairs, nslots};
+    // overlap plan: chunks of one persistent round of query blocks each (pairs' slots non-decreasing, one
+    // train slice), up to kTop2MaxChunks; chunk c's expansion runs on the second stream beside chunk c-1's top-2
+    Top2Overlap ov{};
+    const Top2Overlap* ovp = nullptr;
+    if (top2_overlap_enabled() && top2_launch_slices(npairs, kp_cap, kp_cap) == 1 && npairs >= 32) {
+        bool mono = true;
+        for (int p = 1; p < npairs && mono; p++) mono = up[(size_t)2 * npairs + p] >= up[(size_t)2 * npairs + p - 1];
+        const int per_chunk = std::max(1, 512 / std::max(1, (kp_cap + top2_queries_per_block() - 1) / top2_queries_per_block()));
+        const int nch = std::min(kTop2MaxChunks, (npairs + per_chunk - 1) / per_chunk);
+        if (mono && nch > 1) {
+            if (!c->stream2 && (e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess)
+                return set_error("second stream", e), ORB_ERR_HIP;
+            for (hipEvent_t& ev : c->ham_ev)
+                if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess)
+                    return set_error("top-2 events", e), ORB_ERR_HIP;
+            ov.s2 = c->stream2;
+            ov.ev_fork = c->ham_ev[kTop2MaxChunks];
+            ov.nchunks = nch;
+            for (int k = 0; k <= nch; k++) ov.pair_beg[k] = (int)((long long)npairs * k / nch);
+            for (int k = 0; k < nch; k++) {
+                ov.ev[k] = c->ham_ev[k];
+                ov.slot_end[k] = up[(size_t)2 * npairs + ov.pair_beg[k + 1] - 1] + 1;
+            }
+            ovp = &ov;
+        }
+    }
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-    e = launch_hamming_top2_batch(tb, npairs, kp_cap, kp_cap, d_best, d_best_idx, d_second, part, c->stream);
+    e = launch_hamming_top2_batch(tb, npairs, kp_cap, kp_cap, d_best, d_best_idx, d_second, part, c->stream, ovp);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
     return e == hipSuccess ? ORB_OK : (set_error("top2 kernel", e), ORB_ERR_HIP);
 }

@@ -561,6 +561,8 @@ void orb_destroy(orb_ctx* h) {
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    for (hipEvent_t ev : c->ham_ev)
+        if (ev) (void)hipEventDestroy(ev);
     delete c;
 }
 

@@ -31,6 +31,7 @@ struct Ctx {
     bool fork = true;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ham_ev[kTop2MaxChunks + 1] = {};   // the overlapped batched top-2: fork + one per chunk
 
     // ORBextractor tables (ORBextractor.cc:410-470)
     float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},

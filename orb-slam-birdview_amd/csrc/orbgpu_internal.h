@@ -192,8 +192,23 @@ struct Top2Batch {
 };
 int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
 int top2_launch_slices(int npairs, int max_nq, int max_nt);   // slices one launch uses (1 = direct write)
+// Overlapped form of the batched top-2: pairs [pair_beg[c], pair_beg[c + 1]) use expansion slots below
+// slot_end[c] (slots non-decreasing over the pairs); chunk c's slots are expanded on s2 (event ev[c]) while the
+// launch stream runs chunk c - 1's top-2.  Only with one train slice.
+constexpr int kTop2MaxChunks = 8;
+struct Top2Overlap {
+    hipStream_t s2;
+    hipEvent_t ev_fork;
+    hipEvent_t ev[kTop2MaxChunks];
+    int nchunks;
+    int pair_beg[kTop2MaxChunks + 1];
+    int slot_end[kTop2MaxChunks];
+};
+bool top2_overlap_enabled();
+int top2_queries_per_block();
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
-                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream);
+                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream,
+                                     const Top2Overlap* ov = nullptr);
 
 // Window candidates from the Frame grid (orb_window_match_grid): per item the query feature, its
 // window centre and the grid geometry; ranks (dist, grid slot) like k_topk ranks (dist, list position).
