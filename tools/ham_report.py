@@ -5,7 +5,9 @@ MFMA-i8 roofline fraction recomputed from the trace.
 
   ops per launch = 512 x sum over the 255 pairs of n_query x n_train    (one +-1 i8 32x32x32 MFMA tile
                    covers 32 x 32 pairs x 256 bits = 512 ops per pair; bench.py `hamming.mfma_i8`)
-  frac           = ops per launch / (mean k_expand_pm1 + mean k_top2_mfma duration) / PEAK_I8_OPS
+  frac           = ops per launch / (leg wall time in the trace: the launch's first kernel start to its last
+                   kernel end, expansion and top-2 chunks overlapping on two streams) / PEAK_I8_OPS
+Counter sections are per dispatch (one chunk); rocprofv3 serialises dispatches while it counts.
 
 FETCH_SIZE is doubled (gfx950 reports half of wide streaming reads, MI355X_MICROARCH.md §HBM); WRITE_SIZE
 is taken as is.  Usage: python3 tools/ham_report.py gpurun_out/ham > report.json
@@ -32,11 +34,21 @@ def kname(s):
 def trace(d):
     fn = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     dur = defaultdict(list)
+    spans = []
     for row in csv.DictReader(open(fn[0])):
         k = kname(row["Kernel_Name"])
         if k:
-            dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
-    return dur, fn[0]
+            t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+            dur[k].append((t1 - t0) / 1e3)
+            spans.append((t0, t1))
+    return dur, fn[0], sorted(spans)
+
+
+def leg_spans(spans, legs):
+    """Wall time (us) of each Hamming leg launch: its kernels (expansion chunks on the side stream, top-2 chunks
+    on the launch stream, which overlap) from the first start to the last end."""
+    per = len(spans) // legs
+    return [(max(e for _, e in spans[i * per:(i + 1) * per]) - spans[i * per][0]) / 1e3 for i in range(legs)]
 
 
 def counters(d):
@@ -63,27 +75,30 @@ def main(root):
     line = bench_line(os.path.join(root, "bench.log"))
     ham = line["hamming"]
     ops = ham["mfma_i8"]["achieved_ops_per_s"] * ham["kernel_avg_us"] * 1e-6   # 512 x evals per launch
-    dur, tfile = trace(os.path.join(root, "trace"))
-    # the leg's launches only: the first (warm) launch is in the trace too; take all, warm one dropped
-    mean = {k: sum(v[1:]) / max(1, len(v) - 1) for k, v in dur.items()}
-    t_launch = sum(mean.get(k, 0.0) for k in KERNELS)
+    dur, tfile, spans = trace(os.path.join(root, "trace"))
+    legs = int(os.environ.get("HAM_LEGS", "21"))   # bench.py's Hamming leg: one warm launch + max(2, steps) timed
+    ls = leg_spans(spans, legs)[1:]                # the warm launch dropped
+    t_launch = sum(ls) / len(ls)
+    mean = {k: sum(v) / len(v) for k, v in dur.items()}
     out = {"bench_line_hamming": ham, "ops_per_launch": ops, "trace_file": os.path.relpath(tfile, root),
-           "trace_launches": {k: len(v) for k, v in dur.items()},
-           "trace_mean_us": {k: round(v, 3) for k, v in mean.items()},
+           "trace_dispatches": {k: len(v) for k, v in dur.items()},
+           "trace_mean_us_per_dispatch": {k: round(v, 3) for k, v in mean.items()},
            "trace_leg_us": round(t_launch, 3),
+           "trace_leg_note": "per launch of orb_hamming_top2_frames_device: first kernel start to last kernel end "
+                             "(expansion chunks on the second stream overlap the top-2 chunks)",
            "frac_from_trace": round(ops / (t_launch * 1e-6) / PEAK_I8_OPS, 4),
            "frac_bench_line": ham["mfma_i8"]["frac"]}
     sq, n = counters(os.path.join(root, "sq"))
     sq2, _ = counters(os.path.join(root, "sq2"))
     for k in sq:
         sq[k].update(sq2.get(k, {}))
-    out["sq_per_launch"] = {k: {c: round(v) for c, v in sorted(cs.items())} for k, cs in sq.items()}
+    out["sq_per_dispatch"] = {k: {c: round(v) for c, v in sorted(cs.items())} for k, cs in sq.items()}
     out["sq_dispatches"] = n
     t = sq.get("k_top2_mfma")
     if t:
         # MFMA pipe cycles summed over SIMDs / (SIMDs x busy cycles of the kernel): the matrix cores' duty
         # cycle; GRBM_GUI_ACTIVE / 8 XCDs / wall = the effective clock
-        w = mean.get("k_top2_mfma", 0) * 1e-6
+        w = mean.get("k_top2_mfma", 0) * 1e-6 * len(dur.get("k_top2_mfma", [])) / max(1, n.get("k_top2_mfma", 1))
         out["top2_mfma"] = {
             "mfma_insts": t.get("SQ_INSTS_MFMA"), "valu_insts": t.get("SQ_INSTS_VALU"),
             "valu_per_mfma": round(t["SQ_INSTS_VALU"] / t["SQ_INSTS_MFMA"], 3) if t.get("SQ_INSTS_MFMA") else None,
@@ -93,7 +108,7 @@ def main(root):
         }
     fetch, _ = counters(os.path.join(root, "fetch"))
     write, _ = counters(os.path.join(root, "write"))
-    out["hbm_bytes_per_launch"] = {k: {"fetch_corrected": round(2 * fetch.get(k, {}).get("FETCH_SIZE", 0) * 1024),
+    out["hbm_bytes_per_dispatch"] = {k: {"fetch_corrected": round(2 * fetch.get(k, {}).get("FETCH_SIZE", 0) * 1024),
                                        "write": round(write.get(k, {}).get("WRITE_SIZE", 0) * 1024)}
                                    for k in set(fetch) | set(write)}
     print(json.dumps(out, indent=1))
