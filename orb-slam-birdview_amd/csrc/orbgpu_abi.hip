@@ -382,7 +382,8 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     // in flight (the host path), not when several batches share the GPU (measured)
     if (!latency) bufs.chain.nseg = 0;
     // one frame in flight: level 0's FAST -> octree on a second stream beside the pyramid
-    if (latency && fork && !prof_on && !fast_stamps && geom.nlevels > 1 && nframes == 1) {
+    // (ORBGPU_FORK_BATCH=1: also small batches, captured into the graph as two branches; an A/B switch)
+    if ((latency || (fork_batch && nframes <= 8)) && fork && !prof_on && !fast_stamps && geom.nlevels > 1) {
         hipError_t fe = hipSuccess;
         if (!stream2 && (fe = hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking)) != hipSuccess)
             return set_error("second stream", fe), ORB_ERR_HIP;
@@ -405,7 +406,7 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_candFirst, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
             (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream,
-            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)err_host << 4)};
+            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)err_host << 4) ^ ((uintptr_t)(bufs.fork_s2 != nullptr) << 3)};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -509,6 +510,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_FORK")) c->fork = ev[0] != '0';
+    if (const char* ev = std::getenv("ORBGPU_FORK_BATCH")) c->fork_batch = ev[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;

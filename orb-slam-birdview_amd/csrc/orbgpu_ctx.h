@@ -29,6 +29,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     // the host path's second stream and fork / join events (Ctx::run_extract latency mode; ORBGPU_FORK=0: off)
     bool fork = true;
+    bool fork_batch = false;   // ORBGPU_FORK_BATCH=1: batches of <= 8 frames fork too (graph branches)
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ham_ev[kTop2MaxChunks + 1] = {};   // the overlapped batched top-2: fork + one per chunk
