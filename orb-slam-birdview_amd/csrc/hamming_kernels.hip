@@ -362,17 +362,18 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         for (int i = 0; i < CH; i++) d[i] = PRE ? k.x[i] : pm1x16(k.w[i >> 1] >> (16 * ((ec + i) & 1)));
     };
     unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-    // the MFMA's initial accumulators: 2^23 + 256 SC + subtile * 32 + row, so that every result is already its
-    // stage-local key 2^23 + (256 SC - SC dot + subtile * 32 + row) = 2^23 + (dist << KB | stage row) (dot =
-    // 256 - 2 dist: the sum over the 256 bits of (+-1 train bit) x (-+1 query bit)).  The 2^23 makes every key
-    // a positive normal f32 bit pattern, ordered like the integer: the top-2 runs in v_med3_f32 /
-    // v_minimum3_f32 (compiler builtins the scheduler can interleave with the MFMAs; the integer v_med3_u32
-    // exists only as inline asm), and the merge's shifts drop bit 23 past bit 31.
+    // the MFMA's initial accumulators: 256 SC + subtile * 32 + row, so that every result is already its
+    // stage-local key 256 SC - SC dot + subtile * 32 + row = dist << KB | stage row (dot = 256 - 2 dist: the sum
+    // over the 256 bits of (+-1 train bit) x (-+1 query bit)).  A key is < 2^15, so its low half is a finite
+    // positive f16 bit pattern ordered like the integer (those below 0x400 are f16 denormals, which gfx950 keeps):
+    // the top-2 runs in v_med3_f16 + v_min_f16 (VOP2, full rate: 2.5 cycles per wave instruction against 4.3 for
+    // v_min_u32 / v_med3_u32, profiles/r02/valu_rate.txt; compiler builtins the scheduler can interleave with the
+    // MFMAs; the file builds with -fno-honor-nans so that v_min_f16 needs no canonicalising v_max_f16).
     v16i_t kc[NS];
 #pragma unroll
     for (int u = 0; u < NS; u++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) kc[u][r] = 0x800000 + 256 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+        for (int r = 0; r < 16; r++) kc[u][r] = 256 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
     auto mfma_stage = [&](int buf, v16i_t (&acc)[NS]) {
 #pragma unroll
@@ -389,19 +390,20 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     // index once per stage.  A full stage gives every lane 16 NS keys: no tests.
     constexpr unsigned RM = (1u << KB) - 1;
     auto top2f = [&](const v16i_t (&acc)[NS], unsigned& lbu, unsigned& lsu, auto keep) {
-        float lbf = __builtin_inff(), lsf = __builtin_inff();
+        const _Float16 inf = __builtin_bit_cast(_Float16, (unsigned short)0x7C00u);
+        _Float16 lbh = inf, lsh = inf;
 #pragma unroll
         for (int u = 0; u < NS; u++)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 // (via an int: clang's __builtin_bit_cast of an ext_vector element reads element 0)
                 const int ki = acc[u][r];
-                const float key = keep(u, r) ? __builtin_bit_cast(float, ki) : __builtin_inff();
-                lsf = __builtin_amdgcn_fmed3f(lbf, key, lsf);
-                lbf = __builtin_elementwise_minimum(lbf, key);
+                const _Float16 key = keep(u, r) ? __builtin_bit_cast(_Float16, (unsigned short)ki) : inf;
+                lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
+                lbh = __builtin_fminf16(lbh, key);
             }
-        lbu = __builtin_bit_cast(uint32_t, lbf);
-        lsu = __builtin_bit_cast(uint32_t, lsf);
+        lbu = __builtin_bit_cast(unsigned short, lbh);
+        lsu = __builtin_bit_cast(unsigned short, lsh);
     };
     auto reduce_full = [&](const v16i_t (&acc)[NS], int tb) {
         unsigned lbt, lst;
@@ -419,7 +421,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         }
         unsigned lbt, lst;
         top2f(acc, lbt, lst, [&](int u, int r) { return tb + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
-        constexpr unsigned kInf = 0x7F800000u;
+        constexpr unsigned kInf = 0x7C00u;   // f16 +inf: a lane without keys
         if (lbt != kInf) {   // (only a partial stage leaves a lane without keys)
             const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
             s2 = umed3(b, gb, s2);
