@@ -2219,6 +2219,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     }
 }
 
+/* The host path's image upload, streamed: the host copies the caller's image band by band into pinned,
+ * host-coherent memory and raises a per-band flag (the call's sequence number); this kernel is launched before
+ * the host copy starts, each workgroup waits for its band's flag (one lane polls with a system-scope load and
+ * s_sleep) and copies the band into HBM over PCIe.  So the PCIe transfer overlaps the host memcpy, and the
+ * extraction kernels, queued behind this one before the host copy, start as soon as the last band lands (a
+ * pageable hipMemcpy2DAsync returns only after its DMA, and the first kernel then starts ~18 us later,
+ * profiles/r03/v11_host_path_timeline.txt).  The poll is bounded: a band that never arrives sets the host-side
+ * failure flag *err and the workgroup exits (every wave reaches the end).  Band b = rows [b R, min(h, (b + 1) R)); blockIdx.y splits a band. */
+__global__ __launch_bounds__(256) void k_upload_stream(const uint8_t* __restrict__ h_img, const uint32_t* h_flags,
+                                                       uint32_t seq, uint8_t* __restrict__ d_img, int pitch, int h,
+                                                       int band_rows, uint32_t* __restrict__ err) {
+    __shared__ int s_ok;
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int ok = 0;
+        for (int it = 0; it < (1 << 22); it++) {   // >= 0.5 s: a safety bound, never reached while the host runs
+            if (__hip_atomic_load(h_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
+                ok = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) *err = 1;   // (vector store to the host flag; the extraction reads a stale image, the host fails the call)
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // (the band's bytes are read after the flag)
+    const int r0 = b * band_rows, r1 = min(h, r0 + band_rows);
+    const size_t n16 = (size_t)(r1 - r0) * pitch / 16;   // pitch is a multiple of 64
+    const uint4* src = reinterpret_cast<const uint4*>(h_img + (size_t)r0 * pitch);
+    uint4* dst = reinterpret_cast<uint4*>(d_img + (size_t)r0 * pitch);
+    for (size_t i = blockIdx.y * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.y * 256) dst[i] = src[i];
+}
+
+hipError_t launch_upload_stream(const uint8_t* h_img, const uint32_t* h_flags, uint32_t seq, uint8_t* d_img, int pitch,
+                                int h, int nbands, int band_rows, uint32_t* h_fail, hipStream_t stream) {
+    hipLaunchKernelGGL(k_upload_stream, dim3(nbands, 4), dim3(256), 0, stream, h_img, h_flags, seq, d_img, pitch, h,
+                       band_rows, h_fail);
+    return hipGetLastError();
+}
+
 /* glibc_sincosf over an array of angles (the C-ABI's orb_debug_sincosf: the GPU test pins the device
  * restatement against the oracle's and libm on the host) */
 __global__ __launch_bounds__(256) void k_debug_sincosf(const float* __restrict__ x, int n, float* __restrict__ s,

@@ -510,6 +510,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_FORK")) c->fork = ev[0] != '0';
+    if (const char* ev = std::getenv("ORBGPU_UPLOAD")) c->upload_stream = ev[0] != '0';
     if (const char* ev = std::getenv("ORBGPU_FORK_BATCH")) c->fork_batch = ev[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
@@ -553,6 +554,8 @@ void orb_destroy(orb_ctx* h) {
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_mstage) (void)hipHostFree(c->h_mstage);
     if (c->h_min) (void)hipHostFree(c->h_min);
+    if (c->h_img) (void)hipHostFree(c->h_img);
+    if (c->h_flags) (void)hipHostFree(c->h_flags);
     for (int i = 0; i < 2; i++) {
         if (c->h_pairs[i]) (void)hipHostFree(c->h_pairs[i]);
         if (c->pairs_ev[i]) (void)hipEventDestroy(c->pairs_ev[i]);
@@ -640,10 +643,8 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     const size_t kbytes = ((size_t)kcap * sizeof(orb_keypoint) + 63) & ~(size_t)63;   // descriptors 64-B aligned
     const size_t need = 16 + kbytes + (size_t)kcap * 32;
     if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess) return set_error("device allocation", e), ORB_ERR_NOMEM;
-    // pageable 2-D upload (measured faster than a host copy into pinned staging + one DMA: 0.149 vs 0.168
-    // ms per C3 frame end to end, tools/host_latency; profiles/r03/latency_probe_upload.json)
-    if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-        return set_error("upload image", e), ORB_ERR_HIP;
+    // every allocation before the first launch: with the streamed upload the kernels queued below wait for the
+    // host copy at the end, so nothing in between may block on the stream (hipHostFree / hipFree do)
     if (need > c->pinned_cap) {
         if (c->h_pinned) (void)hipHostFree(c->h_pinned);
         c->h_pinned = nullptr;
@@ -654,6 +655,34 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
             return set_error("pinned staging", e), ORB_ERR_NOMEM;
         c->pinned_cap = need;
     }
+    constexpr int kBands = 16;   // (h_flags[kBands .. 63]: [63] = the upload kernel's timeout flag)
+    const int band_rows = (hgt + kBands - 1) / kBands, nbands = (hgt + band_rows - 1) / band_rows;
+    if (c->upload_stream) {
+        if (pitch * hgt > c->himg_cap) {
+            if (c->h_img) (void)hipHostFree(c->h_img);
+            c->h_img = nullptr;
+            c->himg_cap = 0;
+            if ((e = hipHostMalloc((void**)&c->h_img, pitch * hgt, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+                return set_error("pinned image staging", e), ORB_ERR_NOMEM;
+            c->himg_cap = pitch * hgt;
+        }
+        if (!c->h_flags) {
+            if ((e = hipHostMalloc((void**)&c->h_flags, 64 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+                hipSuccess)
+                return set_error("pinned upload flags", e), ORB_ERR_NOMEM;
+            std::memset(c->h_flags, 0, 64 * sizeof(uint32_t));
+        }
+        if (++c->upload_seq == 0) c->upload_seq = 1;   // (flags start at 0)
+        // the upload kernel first, the extraction kernels behind it (below), then the host copy raising the flags
+        if ((e = launch_upload_stream(c->h_img, c->h_flags, c->upload_seq, c->d_in, (int)pitch, hgt, nbands, band_rows,
+                                      c->h_flags + 63, c->stream)) != hipSuccess)
+            return set_error("upload kernel", e), ORB_ERR_HIP;
+    } else {
+        // pageable 2-D upload (measured faster than a host copy into pinned staging + one DMA: 0.149 vs 0.168
+        // ms per C3 frame end to end, tools/host_latency; profiles/r03/latency_probe_upload.json)
+        if ((e = hipMemcpy2DAsync(c->d_in, pitch, img, stride, w, hgt, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return set_error("upload image", e), ORB_ERR_HIP;
+    }
     // output block [count | overflow flag | 8 B pad | keypoints | descriptors] in pinned, host-coherent
     // memory: k_describe writes the keypoints, descriptors and count straight into it (and copies the
     // octree's overflow flag), so no download follows the kernels
@@ -661,10 +690,23 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     int* hcnt = reinterpret_cast<int*>(hp);
     orb_keypoint* hk = reinterpret_cast<orb_keypoint*>(hp + 16);
     uint8_t* hd = hp + 16 + kbytes;
-    if ((st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, hk, hd, hcnt, kcap, nullptr, true,
-                             hcnt + 1)) != ORB_OK)
-        return st;
+    st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, hk, hd, hcnt, kcap, nullptr, true, hcnt + 1);
+    if (c->upload_stream) {
+        // the host half of the streamed upload, band by band, each band's flag raised after its bytes (x86 stores
+        // are ordered; the release store keeps the compiler from sinking the copy past it).  Also after a failed
+        // launch above: the upload kernel is already running and waits for these flags.
+        for (int b = 0; b < nbands; b++) {
+            const int r0 = b * band_rows, r1 = std::min(hgt, r0 + band_rows);
+            for (int r = r0; r < r1; r++) std::memcpy(c->h_img + (size_t)r * pitch, img + (size_t)r * stride, (size_t)w);
+            __atomic_store_n(c->h_flags + b, c->upload_seq, __ATOMIC_RELEASE);
+        }
+    }
+    if (st != ORB_OK) return st;
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("extract", e), ORB_ERR_HIP;
+    if (c->upload_stream && __atomic_load_n(c->h_flags + 63, __ATOMIC_ACQUIRE)) {
+        c->h_flags[63] = 0;
+        return set_error("streamed image upload timed out", hipSuccess), ORB_ERR_INTERNAL;
+    }
     if (hcnt[1]) {
         set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
         return ORB_ERR_INTERNAL;

@@ -77,6 +77,13 @@ struct Ctx {
     // host-image path (orb_extract)
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
+    // streamed upload (k_upload_stream; ORBGPU_UPLOAD=0: the pageable hipMemcpy2DAsync instead): the image's pinned
+    // host-coherent staging copy and the per-band flags the host raises (call sequence numbers)
+    bool upload_stream = false;
+    uint8_t* h_img = nullptr;
+    size_t himg_cap = 0;
+    uint32_t* h_flags = nullptr;
+    uint32_t upload_seq = 0;
     // orb_extract's outputs [count | flag | pad | keypoints | descriptors]: host-coherent pinned memory the
     // kernels write directly (no download)
     void* h_pinned = nullptr;

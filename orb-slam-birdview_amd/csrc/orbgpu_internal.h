@@ -254,6 +254,9 @@ hipError_t launch_stereo(const Geom* d_geom, const Geom& g, const StereoSide& L,
 
 // glibc sinf/cosf (glibc_trig.h) over n angles, for the trig pin test (orb_debug_sincosf)
 hipError_t launch_debug_sincosf(const float* d_x, int n, float* d_s, float* d_c, hipStream_t stream);
+// The host path's streamed image upload (k_upload_stream): band b copied once h_flags[b] == seq.
+hipError_t launch_upload_stream(const uint8_t* h_img, const uint32_t* h_flags, uint32_t seq, uint8_t* d_img, int pitch,
+                                int h, int nbands, int band_rows, uint32_t* h_fail, hipStream_t stream);
 
 // OpenCV 3.2 resize INTER_LINEAR coefficients for sw -> dw (orbgpu_abi.hip), appended to `out`
 void resize_coefs(int sw, int dw, std::vector<ResizeCoef>& out, bool vertical);

@@ -14,5 +14,6 @@ for zc in 0 1 2 0 1 2; do
 done
 # the forked host path: extraction / mirror tests (forked by default), then its latency A/B
 $T tests/test_gpu_extract.py tests/test_host_mirror.py tests/test_gpu_variants.py > gpurun_out/zc/pytest_fork.log 2>&1; rc=$?; tail -2 gpurun_out/zc/pytest_fork.log; [ $rc -eq 0 ] || exit 1
-bash tools/host_quick.sh ORBGPU_FORK=0 > gpurun_out/zc/host_fork.log 2>&1 || { tail -5 gpurun_out/zc/host_fork.log; exit 1; }
+ORBGPU_UPLOAD=1 $T tests/test_gpu_extract.py tests/test_host_mirror.py > gpurun_out/zc/pytest_upload.log 2>&1; rc=$?; tail -2 gpurun_out/zc/pytest_upload.log; [ $rc -eq 0 ] || exit 1
+bash tools/host_quick.sh ORBGPU_FORK=0 ORBGPU_UPLOAD=1 "ORBGPU_UPLOAD=1 ORBGPU_FORK=0" > gpurun_out/zc/host_fork.log 2>&1 || { tail -5 gpurun_out/zc/host_fork.log; exit 1; }
 cat gpurun_out/zc/host_fork.log | cut -c1-200
