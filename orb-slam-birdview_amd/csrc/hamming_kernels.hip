@@ -283,8 +283,9 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
  * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
  * pass and is merged into the running keys once per stage (NS = 2: one merge per 64 trains instead of
  * two). */
-template <bool PRE, int NW, int NS, bool PIPE>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW waves of 32
-                                                 // queries; PIPE: stage j's MFMAs beside stage j-1's top-2
+template <bool PRE, int NW, int NS, bool PIPE, int LA = 0>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW
+                                                 // waves of 32 queries; PIPE: stage j's MFMAs beside stage j-1's top-2;
+                                                 // LA > 0: each A-fragment read issued LA MFMAs ahead of its MFMA
 __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
                                                        int* __restrict__ idx_o, int* __restrict__ second_o,
                                                        int vblocks) {
@@ -450,17 +451,33 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             // the matrix pipe and the VALU busy together (every stage but the last is full)
             v16i_t accA[NS], accB[NS];
             auto step = [&](int j, v16i_t (&accNew)[NS], const v16i_t (&accOld)[NS]) {
-                const bool more = j + 1 < nst;
+                // LA > 0: the next stage's rows are fetched and staged unconditionally (after the last stage they
+                // are the slice's last row again, written to the buffer no one reads any more): no branch splits
+                // the step's scheduling region
+                const bool more = LA > 0 || j + 1 < nst;
                 Chunk wn;
                 if (more) wn = fetch(min(t0 + TR * (j + 1) + er, t1 - 1));
+                if (LA > 0) __builtin_amdgcn_sched_barrier(0);   // the global loads issue first, their latency under the step
                 mfma_stage(j & 1, accNew);
                 reduce_full(accOld, t0 + TR * (j - 1));
                 // interleave: the A-fragment reads ahead, then each MFMA followed by a share of the top-2
+if (LA == 0) {
 #pragma unroll
-                for (int i = 0; i < 8 * NS; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, VG, 0);  // VG VALU
+                    for (int i = 0; i < 8 * NS; i++) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x002, VG, 0);  // VG VALU
+                    }
+                } else {
+                    // the first LA reads up front, then read i + LA after MFMA i: LA reads in flight while the
+                    // chain runs (read i -> wait -> MFMA i exposes the LDS latency on every MFMA)
+                    __builtin_amdgcn_sched_group_barrier(0x100, LA, 0);
+#pragma unroll
+                    for (int i = 0; i < 8 * NS; i++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        if (i + LA < 8 * NS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, VG, 0);
+                    }
                 }
                 if (more) stage((j + 1) & 1, wn);
                 __syncthreads();
@@ -505,9 +522,10 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
 
 // k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81pPo"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
-// expansion of chunk c + 1 overlapped with the top-2 of chunk c (Top2Overlap)
+// expansion of chunk c + 1 overlapped with the top-2 of chunk c (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
+// reads 2 / 4 MFMAs ahead
 struct Top2Cfg {
-    int waves = 8, stage = 1;
+    int waves = 8, stage = 1, la = 0;
     bool pipe = true, persist = true, overlap = true;
 };
 static const Top2Cfg& top2_cfg() {
@@ -520,6 +538,7 @@ static const Top2Cfg& top2_cfg() {
         t.pipe = std::strchr(e, 'p') != nullptr;
         t.persist = std::strchr(e, 'P') != nullptr;
         t.overlap = std::strchr(e, 'o') != nullptr;
+        t.la = std::strchr(e, 'L') ? 4 : std::strchr(e, 'l') ? 2 : 0;
         return t;
     }();
     return c;
@@ -580,6 +599,9 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
                                        : (pp ? k_top2_mfma<true, 8, 1, true> : k_top2_mfma<true, 8, 1, false>))
                             : (ns == 2 ? (pp ? k_top2_mfma<true, 4, 2, true> : k_top2_mfma<true, 4, 2, false>)
                                        : (pp ? k_top2_mfma<true, 4, 1, true> : k_top2_mfma<true, 4, 1, false>));
+        if (pp && cfg.la && nw == 8)
+            kern = ns == 2 ? (cfg.la == 4 ? k_top2_mfma<true, 8, 2, true, 4> : k_top2_mfma<true, 8, 2, true, 2>)
+                           : (cfg.la == 4 ? k_top2_mfma<true, 8, 1, true, 4> : k_top2_mfma<true, 8, 1, true, 2>);
         int slots = 1 << 30;   // persistent: one workgroup per resident slot (a multiple of 8: virtual blocks keep
         if (cfg.persist) {     // their XCD)
             int dev = 0, ncu = 256, per = 0;
