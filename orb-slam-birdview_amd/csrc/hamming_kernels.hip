@@ -520,13 +520,13 @@ if (LA == 0) {
     }   // virtual blocks
 }
 
-// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81pPo"): '4' / '8' waves per workgroup,
+// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81p"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
 // expansion of chunk c + 1 overlapped with the top-2 of chunk c (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
 // reads 2 / 4 MFMAs ahead
-struct Top2Cfg {
+struct Top2Cfg {   // default "81p" (r04 A/B, profiles/r04/v2_hamming_ab.txt: persistent equal, chunk overlap -28 %)
     int waves = 8, stage = 1, la = 0;
-    bool pipe = true, persist = true, overlap = true;
+    bool pipe = true, persist = false, overlap = false;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {
