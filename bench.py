@@ -58,6 +58,7 @@ CONFIGS = {   # BASELINE.json configs; C3 is the headline single-GPU workload
 }
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 PEAK_I8_OPS = 5.0e15             # MI355X_MICROARCH.md: I8 MFMA = 2x the ~2.5 PF dense BF16 rate per clock
+PEAK_FP4_OPS = 10.0e15           # MI355X_MICROARCH.md: FP4 (e2m1) MFMA = 4x the dense BF16 rate per clock
 KNAMES = ["resize", "fast", "octree", "describe", "hamming", "stereo"]   # ORB_K_* order
 
 
@@ -551,13 +552,16 @@ def main():
         evals = evals_step * hs
         htmax, hevals = reduce_max_sum(dist, th1 - th0, evals)
         kt = hms[4] / 1e3 / max(hl[4], 1)
+        fp4 = L.orb_hamming_top2_mfma_bits() == 4
+        mkey, mpeak = ("mfma_fp4", PEAK_FP4_OPS) if fp4 else ("mfma_i8", PEAK_I8_OPS)
         ham = {"matches_per_s": round(hevals / htmax, 1),
                "queries_per_s": round(hevals / float(np.mean(counts)) / htmax, 1),
                "pair": f"frame f vs f+1 descriptors (~{int(np.mean(counts))} each), {pairs} pairs per launch",
                "kernel_avg_us": round(kt * 1e6, 2),
-               # k_top2_mfma: one +-1 int8 32x32x32 MFMA tile per 32x32 pairs x 256 bits = 512 ops per pair
-               "mfma_i8": ({"achieved_ops_per_s": round(512.0 * evals_step / kt, 1), "peak_ops_per_s": PEAK_I8_OPS,
-                            "frac": round(512.0 * evals_step / kt / PEAK_I8_OPS, 4)} if kt > 0 else None),
+               # k_top2_mfma: 512 MFMA ops per pair (32x32 pairs x K = 256 bits x 2 per tile), on the +-1 int8 form
+               # against the dense I8 peak or on the +-4 e2m1 form (ORBGPU_TOP2 'f') against the dense FP4 peak
+               mkey: ({"achieved_ops_per_s": round(512.0 * evals_step / kt, 1), "peak_ops_per_s": mpeak,
+                       "frac": round(512.0 * evals_step / kt / mpeak, 4)} if kt > 0 else None),
                "kernel_hbm_gbs": round((32.0 * 2 * float(counts.sum()) + 12 * float(counts.sum())) / kt / 1e9, 2)
                if kt > 0 else None}
         if rank == 0 and world == 1 and not args.no_cpu:

@@ -2223,9 +2223,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
  * host-coherent memory and raises a per-band flag (the call's sequence number); this kernel is launched before
  * the host copy starts, each workgroup waits for its band's flag (one lane polls with a system-scope load and
  * s_sleep) and copies the band into HBM over PCIe.  So the PCIe transfer overlaps the host memcpy, and the
- * extraction kernels, queued behind this one before the host copy, start as soon as the last band lands (a
- * pageable hipMemcpy2DAsync returns only after its DMA, and the first kernel then starts ~18 us later,
- * profiles/r03/v11_host_path_timeline.txt).  The poll is bounded: a band that never arrives sets the host-side
+ * extraction kernels, launched right after the host copy, queue behind this one (a pageable hipMemcpy2DAsync
+ * returns only after its DMA, and the first kernel then starts ~18 us later, profiles/r03/v11_host_path_timeline.txt).  The poll is bounded: a band that never arrives sets the host-side
  * failure flag *err and the workgroup exits (every wave reaches the end).  Band b = rows [b R, min(h, (b + 1) R)); blockIdx.y splits a band. */
 __global__ __launch_bounds__(256) void k_upload_stream(const uint8_t* __restrict__ h_img, const uint32_t* h_flags,
                                                        uint32_t seq, uint8_t* __restrict__ d_img, int pitch, int h,
@@ -2251,7 +2250,17 @@ __global__ __launch_bounds__(256) void k_upload_stream(const uint8_t* __restrict
     const size_t n16 = (size_t)(r1 - r0) * pitch / 16;   // pitch is a multiple of 64
     const uint4* src = reinterpret_cast<const uint4*>(h_img + (size_t)r0 * pitch);
     uint4* dst = reinterpret_cast<uint4*>(d_img + (size_t)r0 * pitch);
-    for (size_t i = blockIdx.y * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.y * 256) dst[i] = src[i];
+    // four loads in flight per thread before the stores (PCIe latency ~2 us per round trip)
+    const size_t st = (size_t)gridDim.y * 256;
+    for (size_t i = blockIdx.y * 256 + threadIdx.x; i < n16; i += 4 * st) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * st < n16) v[u] = src[i + u * st];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * st < n16) dst[i + u * st] = v[u];
+    }
 }
 
 hipError_t launch_upload_stream(const uint8_t* h_img, const uint32_t* h_flags, uint32_t seq, uint8_t* d_img, int pitch,

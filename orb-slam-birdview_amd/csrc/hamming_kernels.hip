@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "orbgpu_internal.h"
 
@@ -226,8 +227,12 @@ __global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, c
  * (-amdgpu-mfma-vgpr-form: no v_accvgpr_read per result). */
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
 constexpr int kMfTr = 32;      // trains per tile (MFMA rows)
 constexpr int kMfPitch = 272;  // LDS bytes per expanded train (256 + 16)
+constexpr int kMfPitch4 = 144; // the same for the fp4 form (128 + 16: 36 dwords, odd multiple of 4, so the 16 lanes
+                               // of a ds_read_b128 group hit 16 distinct 4-bank slots)
 
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {   // v_med3_u32
     unsigned r;
@@ -266,6 +271,34 @@ __global__ __launch_bounds__(256) void k_expand_pm1(Top2Batch a, int max_nt, int
     d[1] = pm1x16(w >> 16);
 }
 
+// 8 bits -> bit 0 of 8 nibbles (bit i -> nibble i)
+__device__ __forceinline__ uint32_t spread8_nib(uint32_t b) {
+    uint32_t x = b & 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    return (x | (x << 3)) & 0x11111111u;
+}
+// 32 descriptor bits -> 32 e2m1 (fp4) values, element e = bit e (byte e / 2, low nibble first): X where the bit
+// is clear, the negated X where it is set (the sign is nibble bit 3).  X = 0x6 (+4) for the trains, 0xE (-4) for
+// the queries, so q t = -16 for equal bits and +16 for different ones.
+template <uint32_t X>
+__device__ __forceinline__ v4i_t fp4x32(uint32_t w) {
+    return v4i_t{(int)(X * 0x11111111u ^ (spread8_nib(w) << 3)), (int)(X * 0x11111111u ^ (spread8_nib(w >> 8) << 3)),
+                 (int)(X * 0x11111111u ^ (spread8_nib(w >> 16) << 3)), (int)(X * 0x11111111u ^ (spread8_nib(w >> 24) << 3))};
+}
+/* The fp4 form of k_expand_pm1: 128 bytes per train (descriptor dword s -> bytes 16 s .. 16 s + 15), at the
+ * same slot rows as the int8 form (a.tx rows of 256 bytes, the first half used). */
+__global__ __launch_bounds__(256) void k_expand_fp4(Top2Batch a, int max_nt, int slot0) {
+    const int p = slot0 + blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int row = i >> 3, s = i & 7;
+    const int tf = a.tx_frames ? a.tx_frames[p] : (a.frames ? a.frames[p].y : 0);
+    const int nt = a.counts ? a.counts[tf] : a.nt;
+    if (row >= min(nt, max_nt)) return;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(a.t + ((long long)tf * a.t_stride + row) * 32)[s];
+    v4i_t* d = reinterpret_cast<v4i_t*>(const_cast<uint8_t*>(a.tx) + ((long long)p * a.tx_stride + row) * 128 + 16 * s);
+    d[0] = fp4x32<0x6u>(w);
+}
+
 // 4 query bits -> 4 bytes of +-S (S = 16 or 32): -S where the bit is set, +S where it is clear
 template <int S>
 __device__ __forceinline__ int pmSx4(uint32_t n) {
@@ -283,19 +316,33 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
  * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
  * pass and is merged into the running keys once per stage (NS = 2: one merge per 64 trains instead of
  * two). */
-template <bool PRE, int NW, int NS, bool PIPE, int LA = 0>   // PRE: trains pre-expanded by k_expand_pm1 (a.tx); NW
-                                                 // waves of 32 queries; PIPE: stage j's MFMAs beside stage j-1's top-2;
-                                                 // LA > 0: each A-fragment read issued LA MFMAs ahead of its MFMA
+/* FP4: the same top-2 on v_mfma_f32_32x32x64_f8f6f4 with e2m1 operands (the FP4 rate: twice the i8 MFMA's K per
+ * instruction in the same cycles, MI355X_MICROARCH.md §Matrix cores): trains +-4, queries -+4, so q . t = 32 dist -
+ * 4096 exactly (integers, f32 accumulation), four MFMAs per 32 x 32 tile, 128 expanded bytes per train.  The
+ * accumulator is seeded with 2^23 + 4096 + stage row: every result lies in [2^23, 2^24), where an f32's low
+ * mantissa bits are the integer itself, so the low 16 bits of its bit pattern are the same key dist << 5 | row as
+ * the int8 form's.  The K order inside a fragment does not matter: both operands use one bit -> element map. */
+template <bool PRE, int NW, int NS, bool PIPE, int LA = 0, bool FP4 = false>   // PRE: trains pre-expanded by
+                                                 // k_expand_pm1 / k_expand_fp4 (a.tx); NW waves of 32 queries; PIPE:
+                                                 // stage j's MFMAs beside stage j-1's top-2; LA > 0: each A-fragment
+                                                 // read issued LA MFMAs ahead of its MFMA
 __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
                                                        int* __restrict__ idx_o, int* __restrict__ second_o,
                                                        int vblocks) {
     constexpr int NT = NW * 64, QB = NW * 32, TR = NS * kMfTr;   // threads, queries, trains per stage
-    constexpr int CH = 16 * TR / NT;   // 16-byte chunks of the stage's expanded trains each thread stages
-    constexpr int SC = 16 * NS;        // query scale
+    constexpr int TRB = FP4 ? 128 : 256;                         // expanded bytes per train
+    constexpr int PIT = FP4 ? kMfPitch4 : kMfPitch;              // their LDS pitch
+    constexpr int KS = FP4 ? 4 : 8;                              // MFMAs per 32-train subtile (K = 256)
+    constexpr int NCH = TRB / 16 * TR;                           // 16-byte chunks of a stage
+    constexpr int CH = NCH >= NT ? NCH / NT : 1;  // chunks each staging thread stages
+    constexpr int SACT = NCH / CH;                // staging threads (FP4 with 8 waves: the first four waves)
+    constexpr int SC = 16 * NS;        // query scale (int8 form)
     constexpr int KB = 5 + (NS == 2);  // stage-local key: dist << KB | stage row
-    constexpr int VG = NS == 2 ? 5 : 6; // VALU issued after each MFMA of the pipelined stage
+    constexpr int VG = FP4 ? 9 : NS == 2 ? 5 : 6; // VALU issued after each MFMA of the pipelined stage
     static_assert(CH >= 1 && CH <= 4, "staging chunks");
-    __shared__ __attribute__((aligned(16))) uint8_t s_t[2][TR * kMfPitch];
+    static_assert(!FP4 || (PRE && NS == 1), "fp4: pre-expanded trains, one subtile per stage");
+    using acc_t = typename std::conditional<FP4, v16f_t, v16i_t>::type;
+    __shared__ __attribute__((aligned(16))) uint8_t s_t[2][TR * PIT];
     // 1-D grid of (pair, slice, query block), query block fastest.  Blocks are dealt round-robin over the 8
     // XCDs (b and b + 8 share one), so XCD x takes a contiguous run of that sequence: the query blocks of a
     // pair, which all stream the same expanded trains, then share one L2 (dealt round-robin, every pair's
@@ -318,8 +365,9 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     const int t0 = sli * a.slice, t1 = min(nt, t0 + a.slice);
     const int h = lane >> 5, c = lane & 31;
     const int qi = qblk + wv * 32 + c;
-    // B operand: K-step s = descriptor dword s, lane half h = its bits 16h .. 16h+15
-    v4i_t qf[8];
+    // B operand: K-step s = descriptor dword s, lane half h = its bits 16h .. 16h+15 (fp4: K-step s = dwords 2s
+    // and 2s + 1, lane half h = dword 2s + h)
+    v4i_t qf[KS];
     {
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
         if (qi < nq) {
@@ -328,19 +376,25 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             q1 = qp[1];
         }
         const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        if (FP4) {
 #pragma unroll
-        for (int s = 0; s < 8; s++) qf[s] = pmSx16<SC>(qd[s] >> (16 * h));
+            for (int s = 0; s < KS; s++) qf[s] = fp4x32<0xEu>(h ? qd[2 * s + 1] : qd[2 * s]);
+        } else {
+#pragma unroll
+            for (int s = 0; s < KS; s++) qf[s] = pmSx16<SC>(qd[s] >> (16 * h));
+        }
     }
     const uint32_t* __restrict__ T = reinterpret_cast<const uint32_t*>(a.t + (long long)fr.y * a.t_stride * 32);
     // PRE: this pair's expanded trains through a buffer descriptor (SGPRs), 32-bit offsets
     const int txs = a.tx_slot ? a.tx_slot[p] : p;   // the pair's expansion slot
-    const uint64_t txb = PRE ? reinterpret_cast<uint64_t>(a.tx + (long long)txs * a.tx_stride * 256) : 0;
+    const uint64_t txb = PRE ? reinterpret_cast<uint64_t>(a.tx + (long long)txs * a.tx_stride * TRB) : 0;
     const auto TXR = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(txb >> 32)) << 32) |
                                 (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)txb)),
         0, 0x7FFFFFFF, 0x00020000);
     // staging: thread -> stage row er, chunks ec .. ec + CH - 1 (16 expanded bytes = 16 descriptor bits each)
-    const int er = (tid * CH) >> 4, ec = (tid * CH) & 15;
+    const int er = (tid * CH) / (TRB / 16), ec = (tid * CH) % (TRB / 16);
+    const bool stager = SACT == NT || tid < SACT;   // (wave-uniform)
     struct Chunk {
         uint32_t w[(CH + 1) / 2];   // !PRE: the descriptor dwords holding the chunks' bits
         v4i_t x[CH];                // PRE: the expanded bytes
@@ -350,7 +404,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         if (PRE) {
 #pragma unroll
             for (int i = 0; i < CH; i++)
-                k.x[i] = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, row * 256 + 16 * (ec + i), 0, 0));
+                k.x[i] = stager ? __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, row * TRB + 16 * (ec + i), 0, 0))
+                                : v4i_t{0, 0, 0, 0};
         } else {
 #pragma unroll
             for (int i = 0; i < (CH + 1) / 2; i++) k.w[i] = T[(long long)row * 8 + (ec >> 1) + i];
@@ -358,7 +413,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         return k;
     };
     auto stage = [&](int buf, const Chunk& k) {
-        v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * kMfPitch + ec * 16]);
+        if (!stager) return;
+        v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * PIT + ec * 16]);
 #pragma unroll
         for (int i = 0; i < CH; i++) d[i] = PRE ? k.x[i] : pm1x16(k.w[i >> 1] >> (16 * ((ec + i) & 1)));
     };
@@ -370,35 +426,48 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     // the top-2 runs in v_med3_f16 + v_min_f16 (VOP2, full rate: 2.5 cycles per wave instruction against 4.3 for
     // v_min_u32 / v_med3_u32, profiles/r02/valu_rate.txt; compiler builtins the scheduler can interleave with the
     // MFMAs; the file builds with -fno-honor-nans so that v_min_f16 needs no canonicalising v_max_f16).
-    v16i_t kc[NS];
+    acc_t kc[NS];
 #pragma unroll
     for (int u = 0; u < NS; u++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) kc[u][r] = 256 * SC + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+        for (int r = 0; r < 16; r++) {
+            const int row = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (FP4) kc[u][r] = (float)(8388608 + 4096 + row);   // exact: 2^23 + 4096 + row (see above)
+            else kc[u][r] = 256 * SC + row;
+        }
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
-    auto mfma_stage = [&](int buf, v16i_t (&acc)[NS]) {
+    auto mfma_stage = [&](int buf, acc_t (&acc)[NS]) {
 #pragma unroll
         for (int u = 0; u < NS; u++) {
-            const uint8_t* A = &s_t[buf][(32 * u + c) * kMfPitch + 16 * h];
+            const uint8_t* A = &s_t[buf][(32 * u + c) * PIT + 16 * h];
             acc[u] = kc[u];
 #pragma unroll
-            for (int s = 0; s < 8; s++)   // one chain per subtile: the other waves on the SIMD hide its latency
-                acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_t*>(A + 32 * s), qf[s],
-                                                               acc[u], 0, 0, 0);
+            for (int s = 0; s < KS; s++) {   // one chain per subtile: the other waves on the SIMD hide its latency
+                const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+                if constexpr (FP4) {
+                    const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
+                    const v8i_t b8 = {qf[s][0], qf[s][1], qf[s][2], qf[s][3], 0, 0, 0, 0};
+                    // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
+                    acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[u], 4, 4, 0, 0, 0, 0);
+                } else {
+                    acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, qf[s], acc[u], 0, 0, 0);
+                }
+            }
         }
     };
     // a stage's top-2 by med3 / min (2 ops per distance), merged into the running keys dist << 16 | train
     // index once per stage.  A full stage gives every lane 16 NS keys: no tests.
     constexpr unsigned RM = (1u << KB) - 1;
-    auto top2f = [&](const v16i_t (&acc)[NS], unsigned& lbu, unsigned& lsu, auto keep) {
+    auto top2f = [&](const acc_t (&acc)[NS], unsigned& lbu, unsigned& lsu, auto keep) {
         const _Float16 inf = __builtin_bit_cast(_Float16, (unsigned short)0x7C00u);
         _Float16 lbh = inf, lsh = inf;
 #pragma unroll
         for (int u = 0; u < NS; u++)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                // (via an int: clang's __builtin_bit_cast of an ext_vector element reads element 0)
-                const int ki = acc[u][r];
+                // (via a scalar: clang's __builtin_bit_cast of an ext_vector element reads element 0)
+                const auto kv = acc[u][r];
+                const int ki = __builtin_bit_cast(int, kv);
                 const _Float16 key = keep(u, r) ? __builtin_bit_cast(_Float16, (unsigned short)ki) : inf;
                 lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
                 lbh = __builtin_fminf16(lbh, key);
@@ -406,7 +475,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         lbu = __builtin_bit_cast(unsigned short, lbh);
         lsu = __builtin_bit_cast(unsigned short, lsh);
     };
-    auto reduce_full = [&](const v16i_t (&acc)[NS], int tb) {
+    auto reduce_full = [&](const acc_t (&acc)[NS], int tb) {
         unsigned lbt, lst;
         top2f(acc, lbt, lst, [](int, int) { return true; });
         const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
@@ -415,7 +484,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
         s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
     };
-    auto reduce_any = [&](const v16i_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
+    auto reduce_any = [&](const acc_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
         if (tb + TR <= t1) {
             reduce_full(acc, tb);
             return;
@@ -440,7 +509,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 const bool more = j + 1 < nst;
                 Chunk wn;
                 if (more) wn = fetch(min(tb + TR + er, t1 - 1));
-                v16i_t acc[NS];
+                acc_t acc[NS];
                 mfma_stage(j & 1, acc);
                 reduce_any(acc, tb);
                 if (more) stage((j + 1) & 1, wn);
@@ -449,8 +518,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         } else {
             // software-pipelined: stage j's MFMA chains are issued beside stage j-1's top-2, so one wave keeps
             // the matrix pipe and the VALU busy together (every stage but the last is full)
-            v16i_t accA[NS], accB[NS];
-            auto step = [&](int j, v16i_t (&accNew)[NS], const v16i_t (&accOld)[NS]) {
+            acc_t accA[NS], accB[NS];
+            auto step = [&](int j, acc_t (&accNew)[NS], const acc_t (&accOld)[NS]) {
                 // LA > 0: the next stage's rows are fetched and staged unconditionally (after the last stage they
                 // are the slice's last row again, written to the buffer no one reads any more): no branch splits
                 // the step's scheduling region
@@ -463,7 +532,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 // interleave: the A-fragment reads ahead, then each MFMA followed by a share of the top-2
 if (LA == 0) {
 #pragma unroll
-                    for (int i = 0; i < 8 * NS; i++) {
+                    for (int i = 0; i < KS * NS; i++) {
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
                         __builtin_amdgcn_sched_group_barrier(0x002, VG, 0);  // VG VALU
@@ -473,9 +542,9 @@ if (LA == 0) {
                     // chain runs (read i -> wait -> MFMA i exposes the LDS latency on every MFMA)
                     __builtin_amdgcn_sched_group_barrier(0x100, LA, 0);
 #pragma unroll
-                    for (int i = 0; i < 8 * NS; i++) {
+                    for (int i = 0; i < KS * NS; i++) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                        if (i + LA < 8 * NS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        if (i + LA < KS * NS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x002, VG, 0);
                     }
                 }
@@ -523,10 +592,10 @@ if (LA == 0) {
 // k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81p"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
 // expansion of chunk c + 1 overlapped with the top-2 of chunk c (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
-// reads 2 / 4 MFMAs ahead
+// reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile)
 struct Top2Cfg {   // default "81p" (r04 A/B, profiles/r04/v2_hamming_ab.txt: persistent equal, chunk overlap -28 %)
     int waves = 8, stage = 1, la = 0;
-    bool pipe = true, persist = false, overlap = false;
+    bool pipe = true, persist = false, overlap = false, fp4 = false;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {
@@ -539,12 +608,15 @@ static const Top2Cfg& top2_cfg() {
         t.persist = std::strchr(e, 'P') != nullptr;
         t.overlap = std::strchr(e, 'o') != nullptr;
         t.la = std::strchr(e, 'L') ? 4 : std::strchr(e, 'l') ? 2 : 0;
+        t.fp4 = std::strchr(e, 'f') != nullptr;
+        if (t.fp4) t.waves = 8, t.stage = 1;
         return t;
     }();
     return c;
 }
 static int top2_waves() { return top2_cfg().waves; }
 bool top2_overlap_enabled() { return top2_cfg().overlap; }
+bool top2_fp4_enabled() { return top2_cfg().fp4; }
 int top2_queries_per_block() { return 32 * top2_cfg().waves; }
 
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
@@ -602,6 +674,10 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
         if (pp && cfg.la && nw == 8)
             kern = ns == 2 ? (cfg.la == 4 ? k_top2_mfma<true, 8, 2, true, 4> : k_top2_mfma<true, 8, 2, true, 2>)
                            : (cfg.la == 4 ? k_top2_mfma<true, 8, 1, true, 4> : k_top2_mfma<true, 8, 1, true, 2>);
+        if (cfg.fp4)
+            kern = !pp ? k_top2_mfma<true, 8, 1, false, 0, true>
+                       : cfg.la ? k_top2_mfma<true, 8, 1, true, 2, true> : k_top2_mfma<true, 8, 1, true, 0, true>;
+        auto expand = cfg.fp4 ? k_expand_fp4 : k_expand_pm1;
         int slots = 1 << 30;   // persistent: one workgroup per resident slot (a multiple of 8: virtual blocks keep
         if (cfg.persist) {     // their XCD)
             int dev = 0, ncu = 256, per = 0;
@@ -622,7 +698,7 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
             int s0 = 0;
             for (int cix = 0; cix < ov->nchunks; cix++) {
                 const int s1 = std::min(ov->slot_end[cix], nslots);
-                if (s1 > s0) hipLaunchKernelGGL(k_expand_pm1, dim3(gx, s1 - s0), dim3(256), 0, ov->s2, a, max_nt, s0);
+                if (s1 > s0) hipLaunchKernelGGL(expand, dim3(gx, s1 - s0), dim3(256), 0, ov->s2, a, max_nt, s0);
                 s0 = std::max(s0, s1);
                 if ((e = hipEventRecord(ov->ev[cix], ov->s2)) != hipSuccess) return e;
             }
@@ -640,7 +716,7 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
             }
             return hipGetLastError();
         }
-        hipLaunchKernelGGL(k_expand_pm1, dim3(gx, nslots), dim3(256), 0, stream, a, max_nt, 0);
+        hipLaunchKernelGGL(expand, dim3(gx, nslots), dim3(256), 0, stream, a, max_nt, 0);
         hipLaunchKernelGGL(kern, dim3((unsigned)std::min(vblocks, slots)), dim3(64 * nw), 0, stream, a, d_part, d_best,
                            d_best_idx, d_second, vblocks);
     }

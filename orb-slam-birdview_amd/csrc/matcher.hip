@@ -245,6 +245,8 @@ int orb_hamming_top2_slices(int npairs, int max_nq, int max_nt) {
     return orbgpu::top2_launch_slices(npairs, max_nq, max_nt);
 }
 
+int orb_hamming_top2_mfma_bits(void) { return orbgpu::top2_fp4_enabled() ? 4 : 8; }
+
 int orb_hamming_topk(orb_ctx* h, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_off,
                      const int* cand_idx, const int* train_thr, int k, int* out_dist, int* out_idx, int* out_nvalid) {
     Ctx* c = reinterpret_cast<Ctx*>(h);
@@ -552,6 +554,7 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     std::vector<int> best(nitems, -1);
     if (nitems) {
         Stage st{c};
+        st.zc = 1;   // one kernel over small inputs: reading the pinned mirror beats the DMA (Stage::zc)
         const size_t o_qd = st.add((size_t)nitems * 32), o_qi = st.add((size_t)nitems * 16),
                      o_td = st.add((size_t)nt * 32), o_ti = st.add((size_t)nt * 16), o_r = st.add((size_t)nitems * 8),
                      o_c = st.add((size_t)ncand * 4);

@@ -512,7 +512,7 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (const char* ev = std::getenv("ORBGPU_FORK")) c->fork = ev[0] != '0';
     if (const char* ev = std::getenv("ORBGPU_UPLOAD")) c->upload_stream = ev[0] != '0';
     if (const char* ev = std::getenv("ORBGPU_FORK_BATCH")) c->fork_batch = ev[0] == '1';
-    if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : 0;
+    if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : -1;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);
@@ -690,17 +690,17 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     int* hcnt = reinterpret_cast<int*>(hp);
     orb_keypoint* hk = reinterpret_cast<orb_keypoint*>(hp + 16);
     uint8_t* hd = hp + 16 + kbytes;
-    st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, hk, hd, hcnt, kcap, nullptr, true, hcnt + 1);
     if (c->upload_stream) {
         // the host half of the streamed upload, band by band, each band's flag raised after its bytes (x86 stores
-        // are ordered; the release store keeps the compiler from sinking the copy past it).  Also after a failed
-        // launch above: the upload kernel is already running and waits for these flags.
+        // are ordered; the release store keeps the compiler from sinking the copy past it).  Before the extraction
+        // launches: the upload kernel pulls each band over PCIe while the host copies the next
         for (int b = 0; b < nbands; b++) {
             const int r0 = b * band_rows, r1 = std::min(hgt, r0 + band_rows);
             for (int r = r0; r < r1; r++) std::memcpy(c->h_img + (size_t)r * pitch, img + (size_t)r * stride, (size_t)w);
             __atomic_store_n(c->h_flags + b, c->upload_seq, __ATOMIC_RELEASE);
         }
     }
+    st = c->run_extract(c->d_in, 1, (long long)pitch * hgt, (int)pitch, hk, hd, hcnt, kcap, nullptr, true, hcnt + 1);
     if (st != ORB_OK) return st;
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("extract", e), ORB_ERR_HIP;
     if (c->upload_stream && __atomic_load_n(c->h_flags + 63, __ATOMIC_ACQUIRE)) {

@@ -27,8 +27,9 @@ struct Ctx {
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
-    // the host path's second stream and fork / join events (Ctx::run_extract latency mode; ORBGPU_FORK=0: off)
-    bool fork = true;
+    // the host path's second stream and fork / join events (Ctx::run_extract latency mode; ORBGPU_FORK=1: on.  Off by
+    // default: 0.1154-0.1198 ms per C3 frame forked against 0.1074 ms in one stream, profiles/r04/v3_host_path.txt)
+    bool fork = false;
     bool fork_batch = false;   // ORBGPU_FORK_BATCH=1: batches of <= 8 frames fork too (graph branches)
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -103,10 +104,11 @@ struct Ctx {
     // in one DMA, its outputs come back in one (matcher.hip Stage)
     uint8_t* h_mstage = nullptr;
     size_t mstage_cap = 0;
-    // ORBGPU_MATCH_ZC (A/B switch, default 0): 0 = a call's inputs go up in one DMA into d_scratch; 1 = the
-    // kernels read them straight from the (coherent) pinned mirror, no DMA; 2 = the same from a second,
-    // non-coherent (GPU-cacheable) pinned mirror h_min.  Outputs are always stored into h_mstage.
-    int match_zc = 0;
+    // ORBGPU_MATCH_ZC (A/B switch; unset = each call's measured choice, Stage::zc): 0 = a call's inputs go up in
+    // one DMA into d_scratch; 1 = the kernels read them straight from the (coherent) pinned mirror, no DMA; 2 =
+    // the same from a second, non-coherent (GPU-cacheable) pinned mirror h_min.  Outputs are always stored into
+    // h_mstage.
+    int match_zc = -1;
     uint8_t* h_min = nullptr;
     size_t min_cap = 0;
     // the right extractor's frame + pyramid when it runs on another GPU (orb_compute_stereo_matches)
@@ -177,6 +179,12 @@ struct Arena {
 struct Stage {
     Ctx* c;
     size_t off = 0;
+    // the call's input mode when ORBGPU_MATCH_ZC is unset (see Ctx::match_zc).  r04 per call (profiles/r04/
+    // v3_matcher_zc.txt): the single-kernel calls with small inputs (SearchForTriangulation, ComputeBoW) gain from
+    // reading the pinned mirror (no DMA before the kernel); the searches whose kernels re-read their inputs many
+    // times (the BoW searches, the window search: every candidate's descriptor; stereo) lose, so they keep the DMA
+    int zc = 0;
+    int mode() const { return c->match_zc >= 0 ? c->match_zc : zc; }
     size_t add(size_t bytes) {
         off = Arena::align(off);
         const size_t o = off;
@@ -200,7 +208,7 @@ struct Stage {
                 return set_error("matcher pinned staging", e), ORB_ERR_NOMEM;
             c->mstage_cap = cap;
         }
-        if (c->match_zc == 2 && (need > c->min_cap || !c->h_min)) {
+        if (mode() == 2 && (need > c->min_cap || !c->h_min)) {
             if (c->h_min) (void)hipHostFree(c->h_min);
             c->h_min = nullptr;
             c->min_cap = 0;
@@ -216,15 +224,15 @@ struct Stage {
     T* h(size_t o) const { return reinterpret_cast<T*>(c->h_mstage + o); }   // outputs (host view)
     template <class T>
     T* d(size_t o) const { return reinterpret_cast<T*>(c->d_scratch + o); }
-    uint8_t* in_base() const { return c->match_zc == 2 ? c->h_min : c->h_mstage; }
+    uint8_t* in_base() const { return mode() == 2 ? c->h_min : c->h_mstage; }
     template <class T>
     T* hi(size_t o) const { return reinterpret_cast<T*>(in_base() + o); }   // inputs, written by the host
     template <class T>
     T* di(size_t o) const {   // inputs, as the kernels read them
-        return c->match_zc ? reinterpret_cast<T*>(in_base() + o) : d<T>(o);
+        return mode() ? reinterpret_cast<T*>(in_base() + o) : d<T>(o);
     }
     hipError_t up(size_t from, size_t to) const {
-        if (c->match_zc) return hipSuccess;   // the kernels read the pinned mirror itself
+        if (mode()) return hipSuccess;   // the kernels read the pinned mirror itself
         return to > from ? hipMemcpyAsync(c->d_scratch + from, c->h_mstage + from, to - from, hipMemcpyHostToDevice,
                                           c->stream)
                          : hipSuccess;

@@ -205,6 +205,7 @@ struct Top2Overlap {
     int slot_end[kTop2MaxChunks];
 };
 bool top2_overlap_enabled();
+bool top2_fp4_enabled();   // ORBGPU_TOP2 'f': the e2m1 MFMA form of k_top2_mfma
 int top2_queries_per_block();
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
                                      int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream,

@@ -211,6 +211,7 @@ int orb_vocab_transform(orb_ctx* h, const orb_vocab* v, const uint8_t* desc, int
     // one DMA up (descriptors) through the context's pinned staging; the results come back by the kernel's
     // own stores to it
     Stage st{c};
+    st.zc = 1;   // the descriptors are read once per tree level from L2 after the first touch (Stage::zc)
     const size_t o_desc = st.add((size_t)n * 32), o_w = st.add((size_t)n * 4), o_wt = st.add((size_t)n * 4),
                  o_nd = st.add((size_t)n * 4), o_end = st.off;
     const int r = st.alloc();

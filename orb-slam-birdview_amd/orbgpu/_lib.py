@@ -71,6 +71,7 @@ SIGNATURES = {
     "orb_hamming_top2_device": (ci, [vp, vp, ci, vp, ci, vp, vp, vp]),
     "orb_hamming_top2_frames_device": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, vp, vp]),
     "orb_hamming_top2_slices": (ci, [ci, ci, ci]),
+    "orb_hamming_top2_mfma_bits": (ci, []),
     "orb_search_by_bow_kf_f": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp, vp, OrbFeatVec, vp,
                                     ctypes.POINTER(ci)]),
     "orb_search_by_bow_kf_kf": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, OrbFeatVec, vp,

@@ -283,6 +283,24 @@ def test_diagnostic_switches_leave_results_unchanged(orbgpu_mod, oracle_mod, mon
     b.close()
 
 
+@pytest.mark.parametrize("env", [{"ORBGPU_FORK": "1"}, {"ORBGPU_UPLOAD": "1"}, {"ORBGPU_FORK": "1", "ORBGPU_UPLOAD": "1"}])
+def test_host_path_switches_bit_exact(orbgpu_mod, oracle_mod, monkeypatch, env):
+    """The host path's (orb_extract, one frame in flight) A/B switches: level 0 forked onto a second stream, and the
+    streamed image upload (host band copy + flags polled by k_upload_stream).  Both off by default (DESIGN §5.2);
+    each must give the oracle's bytes, over consecutive frames of two sizes on one extractor (flag sequence numbers
+    and the pinned staging reused across calls)."""
+    from orbgpu.synth import synth_frame
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = orbgpu_mod.ORBextractor(2000, 1.2, 8, 20, 7)
+    o = oracle_mod.OracleExtractor(2000)
+    for i, (w, h) in enumerate([(1280, 720), (1280, 720), (641, 479), (1280, 720)]):
+        img = synth_frame(w, h, 70 + i)
+        gk, gd = g(img)
+        ok, od = o(img)
+        assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), (env, w, h)
+
+
 def test_bench_configuration_bit_exact(orbgpu_mod, oracle_mod):
     """The exact configuration bench.py times: C3, B = 256 frames per batch, two extractor contexts
     (own stream and buffers) launched alternately with several batches in flight, through the hipGraph

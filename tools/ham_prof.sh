@@ -4,7 +4,7 @@
 # passes over the same run (SQ issue / MFMA counters; FETCH_SIZE; WRITE_SIZE), each its own run with
 # --kernel-trace only.  tools/ham_report.py turns gpurun_out/ham/ into profiles/<round>/<tag>_hamming.json.
 # Every GPU step has its own limit; the script stops at the first failure.
-OUT=gpurun_out/ham; rm -rf $OUT; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${HAM_OUT:-gpurun_out/ham}; rm -rf $OUT; mkdir -p $OUT; export TMPDIR=/tmp
 ARGS="--steps 20 --warmup 3 --no-cpu --no-host-path --no-stereo --no-bird --no-c4 --no-matcher --no-profile-pass"
 step() { local name=$1 lim=$2; shift 2; echo "== $name"; timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "rc=$rc" >> $OUT/$name.log; echo "$name rc=$rc"; [ $rc -eq 0 ] || tail -20 $OUT/$name.log; return $rc; }
 step bench 240 python3 bench.py $ARGS || exit 1

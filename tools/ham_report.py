@@ -3,10 +3,10 @@
 trace, the bench line's own HIP-event figure, SQ / MFMA counters and HBM bytes per launch, and the
 MFMA-i8 roofline fraction recomputed from the trace.
 
-  ops per launch = 512 x sum over the 255 pairs of n_query x n_train    (one +-1 i8 32x32x32 MFMA tile
-                   covers 32 x 32 pairs x 256 bits = 512 ops per pair; bench.py `hamming.mfma_i8`)
+  ops per launch = 512 x sum over the 255 pairs of n_query x n_train    (32 x 32 pairs x K = 256 bits x 2 = 512
+                   ops per pair; bench.py `hamming.mfma_i8`, or `mfma_fp4` for the e2m1 form)
   frac           = ops per launch / (leg wall time in the trace: the launch's first kernel start to its last
-                   kernel end, expansion and top-2 chunks overlapping on two streams) / PEAK_I8_OPS
+                   kernel end, expansion and top-2 chunks overlapping on two streams) / the form's dense peak
 Counter sections are per dispatch (one chunk); rocprofv3 serialises dispatches while it counts.
 
 FETCH_SIZE is doubled (gfx950 reports half of wide streaming reads, MI355X_MICROARCH.md §HBM); WRITE_SIZE
@@ -21,7 +21,8 @@ import sys
 from collections import defaultdict
 
 PEAK_I8_OPS = 5.0e15   # dense int8 MFMA: 2x the bf16 rate (2.5 PF dense), MI355X_MICROARCH.md §Matrix cores
-KERNELS = ("k_expand_pm1", "k_top2_mfma", "k_top2b_merge")
+PEAK_FP4_OPS = 10.0e15  # dense fp4 (e2m1) MFMA: 4x the bf16 rate (ORBGPU_TOP2 'f')
+KERNELS = ("k_expand_pm1", "k_expand_fp4", "k_top2_mfma", "k_top2b_merge")
 
 
 def kname(s):
@@ -74,7 +75,9 @@ def bench_line(path):
 def main(root):
     line = bench_line(os.path.join(root, "bench.log"))
     ham = line["hamming"]
-    ops = ham["mfma_i8"]["achieved_ops_per_s"] * ham["kernel_avg_us"] * 1e-6   # 512 x evals per launch
+    mkey = "mfma_fp4" if "mfma_fp4" in ham else "mfma_i8"
+    peak = PEAK_FP4_OPS if mkey == "mfma_fp4" else PEAK_I8_OPS
+    ops = ham[mkey]["achieved_ops_per_s"] * ham["kernel_avg_us"] * 1e-6   # 512 x evals per launch
     dur, tfile, spans = trace(os.path.join(root, "trace"))
     legs = int(os.environ.get("HAM_LEGS", "21"))   # bench.py's Hamming leg: one warm launch + max(2, steps) timed
     ls = leg_spans(spans, legs)[1:]                # the warm launch dropped
@@ -86,8 +89,9 @@ def main(root):
            "trace_leg_us": round(t_launch, 3),
            "trace_leg_note": "per launch of orb_hamming_top2_frames_device: first kernel start to last kernel end "
                              "(expansion chunks on the second stream overlap the top-2 chunks)",
-           "frac_from_trace": round(ops / (t_launch * 1e-6) / PEAK_I8_OPS, 4),
-           "frac_bench_line": ham["mfma_i8"]["frac"]}
+           "mfma_form": mkey, "peak_ops_per_s": peak,
+           "frac_from_trace": round(ops / (t_launch * 1e-6) / peak, 4),
+           "frac_bench_line": ham[mkey]["frac"]}
     sq, n = counters(os.path.join(root, "sq"))
     sq2, _ = counters(os.path.join(root, "sq2"))
     for k in sq:

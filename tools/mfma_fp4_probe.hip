@@ -1,0 +1,113 @@
+// Pins the fp4 (e2m1) operand lane map of v_mfma_scale_f32_32x32x64_f8f6f4 (cbsz = blgp = 4, scales 0: the
+// unscaled form) before k_top2_fp4 relies on it.  Each lane's 16-byte A / B fragment holds 32 fp4 values (two per
+// byte); the probe fills the fragments with random e2m1 values, runs one MFMA, and scores candidate maps of
+// (lane half h, element e) -> k against the result: H0 k = 32 h + e (element e in byte e / 2, low nibble first),
+// H1 the nibbles swapped, H2 k = 2 e + h, H3 16-element chunks alternating lane halves.  The D map is the
+// dtype-independent 32x32 one (row (reg & 3) + 8 (reg >> 2) + 4 h, column lane & 31).  Also checks that +-4 x
+// +-4 sums over K = 64 (what the Hamming top-2 accumulates) come out exact.
+//   hipcc --offload-arch=gfx950 -O2 -o tools/mfma_fp4_probe tools/mfma_fp4_probe.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__global__ void k(const int* A, const int* B, float* D) {   // A, B: 64 lanes x 4 dwords (fragment order)
+    const int l = threadIdx.x;
+    v8i a = {A[4 * l], A[4 * l + 1], A[4 * l + 2], A[4 * l + 3], 0, 0, 0, 0};
+    v8i b = {B[4 * l], B[4 * l + 1], B[4 * l + 2], B[4 * l + 3], 0, 0, 0, 0};
+    v16f c = {};
+    c = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 0, 0, 0);
+    for (int r = 0; r < 16; r++) D[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 32 + (l & 31)] = c[r];
+}
+
+static float e2m1(int n) {   // sign, 2 exponent bits, 1 mantissa bit
+    static const float mag[8] = {0.f, 0.5f, 1.f, 1.5f, 2.f, 3.f, 4.f, 6.f};
+    return (n & 8) ? -mag[n & 7] : mag[n & 7];
+}
+static int nib(const unsigned char* frag, int lane, int e) {   // element e of a lane's 16-byte fragment
+    const unsigned char b = frag[16 * lane + e / 2];
+    return (e & 1) ? b >> 4 : b & 15;
+}
+
+static int kmap(int hyp, int h, int e) {
+    switch (hyp) {
+        case 0: return 32 * h + e;
+        case 1: return 32 * h + (e ^ 1);
+        case 2: return 2 * e + h;
+        default: return 32 * (e / 16) + 16 * h + (e % 16);
+    }
+}
+
+static int run(const unsigned char* fa, const unsigned char* fb, float* out) {
+    int *dA, *dB;
+    float* dD;
+    hipMalloc(&dA, 1024);
+    hipMalloc(&dB, 1024);
+    hipMalloc(&dD, 1024 * 4);
+    hipMemcpy(dA, fa, 1024, hipMemcpyHostToDevice);
+    hipMemcpy(dB, fb, 1024, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, dA, dB, dD);
+    const hipError_t e = hipMemcpy(out, dD, 1024 * 4, hipMemcpyDeviceToHost);
+    hipFree(dA);
+    hipFree(dB);
+    hipFree(dD);
+    return e == hipSuccess ? 0 : 1;
+}
+
+int main() {
+    unsigned char fa[1024], fb[1024];
+    float D[1024];
+    srand(7);
+    for (int i = 0; i < 1024; i++) {
+        fa[i] = (unsigned char)(rand() & 0xFF);
+        fb[i] = (unsigned char)(rand() & 0xFF);
+    }
+    if (run(fa, fb, D)) return printf("launch failed\n"), 2;
+    int best = -1;
+    for (int hyp = 0; hyp < 4; hyp++) {
+        float A[32][64], B[64][32];
+        for (int l = 0; l < 64; l++)
+            for (int e = 0; e < 32; e++) {
+                const int kk = kmap(hyp, l >> 5, e);
+                A[l & 31][kk] = e2m1(nib(fa, l, e));
+                B[kk][l & 31] = e2m1(nib(fb, l, e));
+            }
+        int bad = 0;
+        for (int i = 0; i < 32; i++)
+            for (int j = 0; j < 32; j++) {
+                double s = 0;
+                for (int kk = 0; kk < 64; kk++) s += (double)A[i][kk] * B[kk][j];
+                bad += (float)s != D[i * 32 + j];
+            }
+        printf("H%d: %d of 1024 differ\n", hyp, bad);
+        if (!bad && best < 0) best = hyp;
+    }
+    // +-4 x +-4 over K = 64: exact integers up to 1024
+    for (int i = 0; i < 1024; i++) {
+        fa[i] = (unsigned char)((rand() & 1 ? 0x6 : 0xE) | ((rand() & 1 ? 0x6 : 0xE) << 4));
+        fb[i] = (unsigned char)((rand() & 1 ? 0x6 : 0xE) | ((rand() & 1 ? 0x6 : 0xE) << 4));
+    }
+    if (run(fa, fb, D)) return printf("launch failed\n"), 2;
+    int bad = 0;
+    const int hyp = best < 0 ? 0 : best;
+    for (int i = 0; i < 32; i++)
+        for (int j = 0; j < 32; j++) {
+            int s = 0;
+            for (int l = 0; l < 64; l++) {
+                if ((l & 31) != i) continue;
+                for (int e = 0; e < 32; e++) {
+                    const int kk = kmap(hyp, l >> 5, e);
+                    // B element (kk, j) lives at lane j + 32 (kk's half) under hyp: find it
+                    for (int l2 = (j & 31); l2 < 64; l2 += 32)
+                        for (int e2 = 0; e2 < 32; e2++)
+                            if (kmap(hyp, l2 >> 5, e2) == kk) s += (int)e2m1(nib(fa, l, e)) * (int)e2m1(nib(fb, l2, e2));
+                }
+            }
+            bad += (float)s != D[i * 32 + j];
+        }
+    printf("+-4 sums under H%d: %d of 1024 differ\n", hyp, bad);
+    if (best < 0 || bad) return printf("FAIL\n"), 1;
+    printf("ok H%d\n", best);
+    return 0;
+}

@@ -21,7 +21,7 @@ for f in sorted(glob.glob(os.path.join(OUT, "bench*.log"))):
         if d.get(k):
             print("  ", k, d[k].get("ms_per_frame"))
     if d.get("hamming"):
-        print("   hamming", d["hamming"]["matches_per_s"] / 1e12, "T/s mfma frac", (d["hamming"].get("mfma_i8") or {}).get("frac"))
+        print("   hamming", d["hamming"]["matches_per_s"] / 1e12, "T/s mfma frac", (d["hamming"].get("mfma_i8") or d["hamming"].get("mfma_fp4") or {}).get("frac"))
     if d.get("cpu_baseline"):
         c = d["cpu_baseline"]
         print("   cpu", c["value"], c["cores"], c.get("host_estimate_value"), "speedup", d.get("speedup_vs_cpu_allcore"),
