@@ -2,8 +2,9 @@
 // (DescriptorDistance, ORBmatcher.cc:1647-1663):
 //  - k_topk / k_triangulation: 8 x (v_xor_b32 + v_bcnt_u32_b32) per pair on the VALU, for the
 //    vocabulary-gated candidate lists (CSR);
-//  - k_top2_mfma: the all-pairs top-2 on the matrix cores, bits as +-1 int8 so that
-//    q . t = 256 - 2 popcount(q ^ t) (v_mfma_i32_32x32x32_i8; bound: the I8 MFMA peak).
+//  - k_top2_mfma: the all-pairs top-2 on the matrix cores, bits as +-4 e2m1 (fp4) values so that
+//    q . t = 32 dist - 4096 exactly (v_mfma_f32_32x32x64_f8f6f4; bound: the dense FP4 MFMA peak),
+//    or, as an A/B form, as +-1 int8 (v_mfma_i32_32x32x32_i8, the I8 peak).
 // The selection logic that depends on the order of earlier accepted matches (SearchByBoW's taken set,
 // SearchForInitialization's vMatchedDistance) is replayed on the host from these exact top-k lists
 // (matcher.hip).
@@ -589,13 +590,13 @@ if (LA == 0) {
     }   // virtual blocks
 }
 
-// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "81p"): '4' / '8' waves per workgroup,
+// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "8fp"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
-// expansion of chunk c + 1 overlapped with the top-2 of chunk c (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
+// expansion of the pairs after the first eighth overlapped with the first eighth's top-2 (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
 // reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile)
-struct Top2Cfg {   // default "81p" (r04 A/B, profiles/r04/v2_hamming_ab.txt: persistent equal, chunk overlap -28 %)
+struct Top2Cfg {   // default "8fp": the fp4 form, pipelined (r04 A/B, profiles/r04/v4_hamming_ab.txt: 190 vs 252 us)
     int waves = 8, stage = 1, la = 0;
-    bool pipe = true, persist = false, overlap = false, fp4 = false;
+    bool pipe = true, persist = false, overlap = false, fp4 = true;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {

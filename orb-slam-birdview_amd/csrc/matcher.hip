@@ -390,8 +390,11 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     if (top2_overlap_enabled() && top2_launch_slices(npairs, kp_cap, kp_cap) == 1 && npairs >= 32) {
         bool mono = true;
         for (int p = 1; p < npairs && mono; p++) mono = up[(size_t)2 * npairs + p] >= up[(size_t)2 * npairs + p - 1];
-        const int per_chunk = std::max(1, 512 / std::max(1, (kp_cap + top2_queries_per_block() - 1) / top2_queries_per_block()));
-        const int nch = std::min(kTop2MaxChunks, (npairs + per_chunk - 1) / per_chunk);
+        // two chunks, the first small: only its expansion runs alone, the second's (7/8 of the pairs) runs beside
+        // the first's top-2, and the second's top-2 has a full grid (r04: eight equal chunks measured 28 % slower,
+        // each chunk's grid too small to fill the chip, profiles/r04/v2_hamming_ab.txt)
+        const int first = std::max(8, npairs / 8);
+        const int nch = first < npairs ? 2 : 1;
         if (mono && nch > 1) {
             if (!c->stream2 && (e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess)
                 return set_error("second stream", e), ORB_ERR_HIP;
@@ -401,7 +404,9 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
             ov.s2 = c->stream2;
             ov.ev_fork = c->ham_ev[kTop2MaxChunks];
             ov.nchunks = nch;
-            for (int k = 0; k <= nch; k++) ov.pair_beg[k] = (int)((long long)npairs * k / nch);
+            ov.pair_beg[0] = 0;
+            ov.pair_beg[1] = first;
+            ov.pair_beg[2] = npairs;
             for (int k = 0; k < nch; k++) {
                 ov.ev[k] = c->ham_ev[k];
                 ov.slot_end[k] = up[(size_t)2 * npairs + ov.pair_beg[k + 1] - 1] + 1;
