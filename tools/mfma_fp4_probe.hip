@@ -1,10 +1,12 @@
-// Pins the fp4 (e2m1) operand lane map of v_mfma_scale_f32_32x32x64_f8f6f4 (cbsz = blgp = 4, scales 0: the
-// unscaled form) before k_top2_fp4 relies on it.  Each lane's 16-byte A / B fragment holds 32 fp4 values (two per
-// byte); the probe fills the fragments with random e2m1 values, runs one MFMA, and scores candidate maps of
-// (lane half h, element e) -> k against the result: H0 k = 32 h + e (element e in byte e / 2, low nibble first),
-// H1 the nibbles swapped, H2 k = 2 e + h, H3 16-element chunks alternating lane halves.  The D map is the
-// dtype-independent 32x32 one (row (reg & 3) + 8 (reg >> 2) + 4 h, column lane & 31).  Also checks that +-4 x
-// +-4 sums over K = 64 (what the Hamming top-2 accumulates) come out exact.
+// Pins what k_top2_mfma's fp4 form relies on in v_mfma_scale_f32_32x32x64_f8f6f4 (cbsz = blgp = 4, scales 0: the
+// unscaled form): A row r and B column c live in lanes r and r + 32 (16 bytes = 32 e2m1 values each), one
+// (lane half, element) -> k map serves both operands, the D map is the dtype-independent 32x32 one (row (reg & 3) +
+// 8 (reg >> 2) + 4 h, column lane & 31), and +-4 x +-4 sums over K = 64 come out exact.  The probe fills the
+// fragments with random e2m1 values, runs one MFMA and scores candidate k maps: H0 k = 32 h + e (element e in byte
+// e / 2, low nibble first), H1 nibbles swapped, H2 k = 2 e + h, H3 16-element chunks alternating lane halves.  Any
+// bijective map applied to both operands gives the same product, so all four matching (as on the r04 box,
+// profiles/r04/v4_hamming_ab.txt) confirms the lane / row maps and the exactness, not the K order, which the
+// Hamming top-2 does not depend on (a full K = 256 reduction over one bit -> element map on both sides).
 //   hipcc --offload-arch=gfx950 -O2 -o tools/mfma_fp4_probe tools/mfma_fp4_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
