@@ -312,6 +312,14 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
     return v4i_t{pmSx4<S>(w), pmSx4<S>(w >> 4), pmSx4<S>(w >> 8), pmSx4<S>(w >> 12)};
 }
 
+// Explicit wait states between an fp4 MFMA chain's last instruction and the first VALU read of its result (20:
+// the 16-pass XDL figure).  hipcc pads this pair as an 8-pass XDL (12 states); every fp4 form whose top-2 read
+// directly follows the chain's last MFMA gave wrong second distances on the r04 box (the unpipelined build and
+// k_top2_res, profiles/r04/v6_hamming_ab.txt), the pipelined form, whose reads trail by a stage, never did.  The
+// "+v" operand ties the pad to the accumulator, so no read of it is scheduled above the pad.
+__device__ __forceinline__ void fp4_result_pad(v16f_t& acc) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc)); }
+__device__ __forceinline__ void fp4_result_pad(v16i_t&) {}
+
 /* NS 32-train subtiles per stage (one accumulator chain each).  With the queries scaled to -S / +S,
  * S = 16 NS, and the accumulators seeded with 256 S + subtile * 32 + row, every result is the stage-local key
  * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
@@ -486,7 +494,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
         s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
     };
-    auto reduce_any = [&](const acc_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
+    auto reduce_any = [&](acc_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
+        if (FP4) fp4_result_pad(acc[0]);   // (this read can directly follow the chain's last MFMA)
         if (tb + TR <= t1) {
             reduce_full(acc, tb);
             return;
@@ -682,7 +691,8 @@ __global__ __launch_bounds__(kResNW * 64) void k_top2_res(Top2Batch a, uint2* __
         b = min(b, gb);
         s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
     };
-    auto reduce_any = [&](const v16f_t& acc, int tb) {
+    auto reduce_any = [&](v16f_t& acc, int tb) {
+        fp4_result_pad(acc);   // (this read directly follows the chain's last MFMA)
         if (tb + 32 <= t1) {
             reduce_full(acc, tb);
             return;
@@ -777,7 +787,7 @@ static const Top2Cfg& top2_cfg() {
         if (t.res) t.fp4 = true;
         // the fp4 form is built pipelined only (its unpipelined build gave wrong seconds on the r04 box, 1 of 3
         // tests, profiles/r04/v4_hamming_ab.txt; not investigated further)
-        if (t.fp4) t.waves = t.res ? kResNW : 8, t.stage = 1, t.pipe = true;
+        if (t.fp4) t.waves = t.res ? kResNW : 8, t.stage = 1, t.pipe = !std::strchr(e, 'u');   // 'u': unpipelined
         return t;
     }();
     return c;
@@ -843,7 +853,9 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
         if (pp && cfg.la && nw == 8)
             kern = ns == 2 ? (cfg.la == 4 ? k_top2_mfma<true, 8, 2, true, 4> : k_top2_mfma<true, 8, 2, true, 2>)
                            : (cfg.la == 4 ? k_top2_mfma<true, 8, 1, true, 4> : k_top2_mfma<true, 8, 1, true, 2>);
-        if (cfg.fp4) kern = cfg.la ? k_top2_mfma<true, 8, 1, true, 2, true> : k_top2_mfma<true, 8, 1, true, 0, true>;
+        if (cfg.fp4)
+            kern = !pp ? k_top2_mfma<true, 8, 1, false, 0, true>
+                       : cfg.la ? k_top2_mfma<true, 8, 1, true, 2, true> : k_top2_mfma<true, 8, 1, true, 0, true>;
         if (cfg.res) kern = k_top2_res;
         auto expand = cfg.fp4 ? k_expand_fp4 : k_expand_pm1;
         int slots = 1 << 30;   // persistent: one workgroup per resident slot (a multiple of 8: virtual blocks keep

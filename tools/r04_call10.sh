@@ -3,6 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/ab10; export TMPDIR=/tmp
 T="timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+ORBGPU_TOP2=8fu $T tests/test_gpu_matcher.py > gpurun_out/ab10/pytest_8fu.log 2>&1; rc=$?; echo "8fu (unpipelined fp4, padded): $(tail -1 gpurun_out/ab10/pytest_8fu.log)"
 ORBGPU_TOP2=R $T tests/test_gpu_matcher.py > gpurun_out/ab10/pytest_R.log 2>&1; rc=$?; echo "R: $(tail -1 gpurun_out/ab10/pytest_R.log)"; [ $rc -eq 0 ] || { tail -40 gpurun_out/ab10/pytest_R.log; exit 1; }
 ARGS="--steps 50 --warmup 5 --no-cpu --no-host-path --no-stereo --no-bird --no-c4 --no-matcher --no-profile-pass"
 for v in 8fp R 8fp R; do
