@@ -7,6 +7,14 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
+
+def _diff(got, want, best=None):
+    """First mismatches of two distance arrays (for assertion messages)."""
+    got, want = np.asarray(got), np.asarray(want)
+    bad = np.flatnonzero(got != want)[:8]
+    return {"n_bad": int((got != want).sum()), "at": bad.tolist(), "got": got[bad].tolist(), "want": want[bad].tolist(),
+            "best_there": None if best is None else np.asarray(best)[bad].tolist()}
+
 def frames(orbgpu_mod):
     """Two extracted views (second shifted by a few px) -> realistic descriptor sets with matches."""
     from orbgpu.synth import synth_frame
@@ -94,7 +102,7 @@ def test_top2_device_vs_numpy(orbgpu_mod):
     srt = np.sort(D, 1)
     assert np.array_equal(res[0], srt[:, 0])
     assert np.array_equal(res[1], D.argmin(1))   # first index on ties
-    assert np.array_equal(res[2], srt[:, 1])
+    assert np.array_equal(res[2], srt[:, 1]), _diff(res[2], srt[:, 1], res[0])
     assert res[1][3] == 1500
     for p in [dq, dt] + out:
         L.orb_device_free(b.h, p)
@@ -316,7 +324,7 @@ def test_top2_device_extreme_distances_and_ties(orbgpu_mod):
     D = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
     srt = np.sort(D, 1)
     assert np.array_equal(res[0], srt[:, 0]) and np.array_equal(res[1], D.argmin(1))
-    assert np.array_equal(res[2], srt[:, 1])
+    assert np.array_equal(res[2], srt[:, 1]), _diff(res[2], srt[:, 1], res[0])
     assert (res[0][0], res[1][0], res[2][0]) == (0, 0, 0)
     assert res[0][1] == 0 and res[1][1] == 97 and res[0][2] == 0 and res[1][2] == 102
     for p in [dq, dt] + out:
@@ -403,7 +411,7 @@ def test_top2_frames_bench_shape(orbgpu_mod):
         n = len(dq)
         assert np.array_equal(res[0][:n], best), p
         assert np.array_equal(res[1][:n], idx), p
-        assert np.array_equal(res[2][:n], second), p
+        assert np.array_equal(res[2][:n], second), (p, _diff(res[2][:n], second, best))
     for d in out:
         L.orb_device_free(bx.h, d)
     bx.close()
