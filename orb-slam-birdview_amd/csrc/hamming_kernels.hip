@@ -320,6 +320,19 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
 __device__ __forceinline__ void fp4_result_pad(v16f_t& acc) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc)); }
 __device__ __forceinline__ void fp4_result_pad(v16i_t&) {}
 
+/* An fp4 chain's A fragments, held in their own registers until the chain's result has been read.  Every fp4
+ * build whose allocator reused a fragment's registers for the next LDS read while the chain could still be in
+ * flight (the unpipelined form and k_top2_res: `ds_read v[74:77]` right after the MFMA reading v[74:77]) lost
+ * second-best keys on the r04 box (profiles/r04/v6_hamming_ab.txt); the 20-state result pad did not help, so the
+ * fragments are kept live (an empty asm using them, placed after the chain's result is consumed) and the next
+ * reads go to other registers. */
+struct Fp4Frag {
+    v4i_t a[4];
+};
+__device__ __forceinline__ void fp4_frag_keep(const Fp4Frag& f) {
+    asm volatile("" ::"v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3]));
+}
+
 /* NS 32-train subtiles per stage (one accumulator chain each).  With the queries scaled to -S / +S,
  * S = 16 NS, and the accumulators seeded with 256 S + subtile * 32 + row, every result is the stage-local key
  * dist * 32 NS + (subtile * 32 + row): the top-2 of a stage's 16 NS keys per lane runs in one med3 / min
@@ -446,14 +459,18 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             else kc[u][r] = 256 * SC + row;
         }
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
-    auto mfma_stage = [&](int buf, acc_t (&acc)[NS]) {
+    auto mfma_stage = [&](int buf, acc_t (&acc)[NS], Fp4Frag& fr) {
 #pragma unroll
         for (int u = 0; u < NS; u++) {
             const uint8_t* A = &s_t[buf][(32 * u + c) * PIT + 16 * h];
             acc[u] = kc[u];
+            if constexpr (FP4) {
+#pragma unroll
+                for (int s = 0; s < KS; s++) fr.a[s] = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+            }
 #pragma unroll
             for (int s = 0; s < KS; s++) {   // one chain per subtile: the other waves on the SIMD hide its latency
-                const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+                const v4i_t av = FP4 ? fr.a[s] : *reinterpret_cast<const v4i_t*>(A + 32 * s);
                 if constexpr (FP4) {
                     const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
                     const v8i_t b8 = {qf[s][0], qf[s][1], qf[s][2], qf[s][3], 0, 0, 0, 0};
@@ -521,8 +538,10 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 Chunk wn;
                 if (more) wn = fetch(min(tb + TR + er, t1 - 1));
                 acc_t acc[NS];
-                mfma_stage(j & 1, acc);
+                Fp4Frag fr;
+                mfma_stage(j & 1, acc, fr);
                 reduce_any(acc, tb);
+                if (FP4) fp4_frag_keep(fr);
                 if (more) stage((j + 1) & 1, wn);
                 __syncthreads();
             }
@@ -530,7 +549,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             // software-pipelined: stage j's MFMA chains are issued beside stage j-1's top-2, so one wave keeps
             // the matrix pipe and the VALU busy together (every stage but the last is full)
             acc_t accA[NS], accB[NS];
-            auto step = [&](int j, acc_t (&accNew)[NS], const acc_t (&accOld)[NS]) {
+            Fp4Frag frA, frB;
+            auto step = [&](int j, acc_t (&accNew)[NS], const acc_t (&accOld)[NS], Fp4Frag& frNew, const Fp4Frag& frOld) {
                 // LA > 0: the next stage's rows are fetched and staged unconditionally (after the last stage they
                 // are the slice's last row again, written to the buffer no one reads any more): no branch splits
                 // the step's scheduling region
@@ -538,8 +558,9 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 Chunk wn;
                 if (more) wn = fetch(min(t0 + TR * (j + 1) + er, t1 - 1));
                 if (LA > 0) __builtin_amdgcn_sched_barrier(0);   // the global loads issue first, their latency under the step
-                mfma_stage(j & 1, accNew);
+                mfma_stage(j & 1, accNew, frNew);
                 reduce_full(accOld, t0 + TR * (j - 1));
+                if (FP4) fp4_frag_keep(frOld);
                 // interleave: the A-fragment reads ahead, then each MFMA followed by a share of the top-2
 if (LA == 0) {
 #pragma unroll
@@ -566,20 +587,22 @@ if (LA == 0) {
                 const bool more = 1 < nst;
                 Chunk wn;
                 if (more) wn = fetch(min(t0 + TR + er, t1 - 1));
-                mfma_stage(0, accA);
+                mfma_stage(0, accA, frA);
                 if (more) stage(1, wn);
                 __syncthreads();
             }
             int j = 1;
             for (; j + 1 < nst; j += 2) {
-                step(j, accB, accA);
-                step(j + 1, accA, accB);
+                step(j, accB, accA, frB, frA);
+                step(j + 1, accA, accB, frA, frB);
             }
             if (j < nst) {
-                step(j, accB, accA);
+                step(j, accB, accA, frB, frA);
                 reduce_any(accB, t0 + TR * (nst - 1));
+                if (FP4) fp4_frag_keep(frB);
             } else {
                 reduce_any(accA, t0 + TR * (nst - 1));
+                if (FP4) fp4_frag_keep(frA);
             }
         }
     }
@@ -650,12 +673,14 @@ __global__ __launch_bounds__(kResNW * 64) void k_top2_res(Top2Batch a, uint2* __
 #pragma unroll
     for (int r = 0; r < 16; r++) kc[r] = (float)(8388608 + 4096 + (r & 3) + 8 * (r >> 2) + 4 * h);
     unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-    auto mfma = [&](int j, v16f_t& acc) {
+    auto mfma = [&](int j, v16f_t& acc, Fp4Frag& fr) {
         const uint8_t* A = &s_t[(32 * j + c) * PIT + 16 * h];
         acc = kc;
 #pragma unroll
+        for (int s = 0; s < KS; s++) fr.a[s] = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+#pragma unroll
         for (int s = 0; s < KS; s++) {
-            const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+            const v4i_t av = fr.a[s];
             const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
             const v8i_t b8 = {qf[s][0], qf[s][1], qf[s][2], qf[s][3], 0, 0, 0, 0};
             acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc, 4, 4, 0, 0, 0, 0);
@@ -722,9 +747,11 @@ __global__ __launch_bounds__(kResNW * 64) void k_top2_res(Top2Batch a, uint2* __
         __syncthreads();
         const int nst = (cn + 31) / 32;
         v16f_t accA, accB;
-        auto step = [&](int j, v16f_t& accNew, const v16f_t& accOld) {
-            mfma(j, accNew);
+        Fp4Frag frA, frB;
+        auto step = [&](int j, v16f_t& accNew, const v16f_t& accOld, Fp4Frag& frNew, const Fp4Frag& frOld) {
+            mfma(j, accNew, frNew);
             reduce_full(accOld, cb + 32 * (j - 1));
+            fp4_frag_keep(frOld);
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two A-fragment reads ahead
 #pragma unroll
             for (int i = 0; i < KS; i++) {
@@ -733,17 +760,19 @@ __global__ __launch_bounds__(kResNW * 64) void k_top2_res(Top2Batch a, uint2* __
                 __builtin_amdgcn_sched_group_barrier(0x002, 9, 0);
             }
         };
-        mfma(0, accA);
+        mfma(0, accA, frA);
         int j = 1;
         for (; j + 1 < nst; j += 2) {
-            step(j, accB, accA);
-            step(j + 1, accA, accB);
+            step(j, accB, accA, frB, frA);
+            step(j + 1, accA, accB, frA, frB);
         }
         if (j < nst) {
-            step(j, accB, accA);
+            step(j, accB, accA, frB, frA);
             reduce_any(accB, cb + 32 * (nst - 1));
+            fp4_frag_keep(frB);
         } else {
             reduce_any(accA, cb + 32 * (nst - 1));
+            fp4_frag_keep(frA);
         }
     }
     const unsigned ob = __shfl_xor(b, 32), os = __shfl_xor(s2, 32);

@@ -6,8 +6,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-
 def _diff(got, want, best=None):
     """First mismatches of two distance arrays (for assertion messages)."""
     got, want = np.asarray(got), np.asarray(want)
@@ -15,6 +13,8 @@ def _diff(got, want, best=None):
     return {"n_bad": int((got != want).sum()), "at": bad.tolist(), "got": got[bad].tolist(), "want": want[bad].tolist(),
             "best_there": None if best is None else np.asarray(best)[bad].tolist()}
 
+
+@pytest.fixture(scope="module")
 def frames(orbgpu_mod):
     """Two extracted views (second shifted by a few px) -> realistic descriptor sets with matches."""
     from orbgpu.synth import synth_frame
