@@ -317,7 +317,10 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
 // directly follows the chain's last MFMA gave wrong second distances on the r04 box (the unpipelined build and
 // k_top2_res, profiles/r04/v6_hamming_ab.txt), the pipelined form, whose reads trail by a stage, never did.  The
 // "+v" operand ties the pad to the accumulator, so no read of it is scheduled above the pad.
-__device__ __forceinline__ void fp4_result_pad(v16f_t& acc) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc)); }
+__device__ __forceinline__ void fp4_result_pad(v16f_t& acc) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
+}
 __device__ __forceinline__ void fp4_result_pad(v16i_t&) {}
 
 /* An fp4 chain's A fragments, held in their own registers until the chain's result has been read.  Every fp4
