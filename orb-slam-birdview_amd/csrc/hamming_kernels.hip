@@ -312,29 +312,23 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
     return v4i_t{pmSx4<S>(w), pmSx4<S>(w >> 4), pmSx4<S>(w >> 8), pmSx4<S>(w >> 12)};
 }
 
-// Explicit wait states between an fp4 MFMA chain's last instruction and the first VALU read of its result (20:
-// the 16-pass XDL figure).  hipcc pads this pair as an 8-pass XDL (12 states); every fp4 form whose top-2 read
-// directly follows the chain's last MFMA gave wrong second distances on the r04 box (the unpipelined build and
-// k_top2_res, profiles/r04/v6_hamming_ab.txt), the pipelined form, whose reads trail by a stage, never did.  The
-// "+v" operand ties the pad to the accumulator, so no read of it is scheduled above the pad.
-__device__ __forceinline__ void fp4_result_pad(v16f_t& acc) {
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
+// The 16 key bits of an f16 top-2 result, read from the whole register and masked.  The compiler takes the
+// upper half of a 16-bit VALU result as zero and folds the zero-extension away; the fp4 forms lost second-best
+// keys on the r04 box in builds where that register's upper half held an earlier 32-bit value (experiment,
+// profiles/r04/v6_hamming_ab.txt).  Reading through the asm hides the assumption, so the mask is kept.
+__device__ __forceinline__ unsigned f16_bits(_Float16 x) {
+    unsigned r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r & 0xFFFFu;
 }
-__device__ __forceinline__ void fp4_result_pad(v16i_t&) {}
 
-/* An fp4 chain's A fragments, held in their own registers until the chain's result has been read.  Every fp4
- * build whose allocator reused a fragment's registers for the next LDS read while the chain could still be in
- * flight (the unpipelined form and k_top2_res: `ds_read v[74:77]` right after the MFMA reading v[74:77]) lost
- * second-best keys on the r04 box (profiles/r04/v6_hamming_ab.txt); the 20-state result pad did not help, so the
- * fragments are kept live (an empty asm using them, placed after the chain's result is consumed) and the next
- * reads go to other registers. */
+// (experiment hooks, empty: an explicit wait-state pad after an fp4 chain and keeping its A fragments live)
 struct Fp4Frag {
     v4i_t a[4];
 };
-__device__ __forceinline__ void fp4_frag_keep(const Fp4Frag& f) {
-    asm volatile("" ::"v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3]));
-}
+__device__ __forceinline__ void fp4_frag_keep(const Fp4Frag&) {}
+__device__ __forceinline__ void fp4_result_pad(v16f_t&) {}
+__device__ __forceinline__ void fp4_result_pad(v16i_t&) {}
 
 /* NS 32-train subtiles per stage (one accumulator chain each).  With the queries scaled to -S / +S,
  * S = 16 NS, and the accumulators seeded with 256 S + subtile * 32 + row, every result is the stage-local key
@@ -502,8 +496,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
                 lbh = __builtin_fminf16(lbh, key);
             }
-        lbu = __builtin_bit_cast(unsigned short, lbh);
-        lsu = __builtin_bit_cast(unsigned short, lsh);
+        lbu = f16_bits(lbh);
+        lsu = f16_bits(lsh);
     };
     auto reduce_full = [&](const acc_t (&acc)[NS], int tb) {
         unsigned lbt, lst;
@@ -700,8 +694,8 @@ __global__ __launch_bounds__(kResNW * 64) void k_top2_res(Top2Batch a, uint2* __
             lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
             lbh = __builtin_fminf16(lbh, key);
         }
-        lbu = __builtin_bit_cast(unsigned short, lbh);
-        lsu = __builtin_bit_cast(unsigned short, lsh);
+        lbu = f16_bits(lbh);
+        lsu = f16_bits(lsh);
     };
     auto merge = [&](unsigned lbt, unsigned lst, int tb) {
         constexpr unsigned kInf = 0x7C00u;

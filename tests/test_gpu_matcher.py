@@ -412,6 +412,27 @@ def test_top2_frames_bench_shape(orbgpu_mod):
         assert np.array_equal(res[0][:n], best), p
         assert np.array_equal(res[1][:n], idx), p
         assert np.array_equal(res[2][:n], second), (p, _diff(res[2][:n], second, best))
+    # every pair: the whole launch's outputs against exact distances from a float32 GEMM of the unpacked bits
+    # (popcount(q ^ t) = |q| + |t| - 2 q.t, exact integers in float32), and a second launch bit-identical
+    allr = [np.zeros((B - 1) * cap, np.int32) for _ in range(3)]
+    for r, d in zip(allr, out):
+        L.orb_memcpy_d2h(bx.h, r.ctypes.data, d, r.nbytes)
+    bits = [np.unpackbits(bx.results(f)[1], axis=1).astype(np.float32) for f in range(B)]
+    for p in range(B - 1):
+        Q, T = bits[p], bits[p + 1]
+        D = (Q.sum(1)[:, None] + T.sum(1)[None, :] - 2 * (Q @ T.T)).astype(np.int32)
+        n = len(Q)
+        sl = slice(p * cap, p * cap + n)
+        assert np.array_equal(allr[0][sl], D.min(1)), p
+        assert np.array_equal(allr[1][sl], D.argmin(1)), p
+        sec = np.partition(D, 1, axis=1)[:, 1]
+        assert np.array_equal(allr[2][sl], sec), (p, _diff(allr[2][sl], sec, D.min(1)))
+    bx.hamming_top2_frames(qf, tf, *out)
+    bx.sync()
+    for r, d in zip(allr, out):
+        again = np.zeros_like(r)
+        L.orb_memcpy_d2h(bx.h, again.ctypes.data, d, again.nbytes)
+        assert np.array_equal(again, r)
     for d in out:
         L.orb_device_free(bx.h, d)
     bx.close()
