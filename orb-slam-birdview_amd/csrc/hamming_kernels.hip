@@ -312,23 +312,17 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
     return v4i_t{pmSx4<S>(w), pmSx4<S>(w >> 4), pmSx4<S>(w >> 8), pmSx4<S>(w >> 12)};
 }
 
-// The 16 key bits of an f16 top-2 result, read from the whole register and masked.  The compiler takes the
-// upper half of a 16-bit VALU result as zero and folds the zero-extension away; the fp4 forms lost second-best
-// keys on the r04 box in builds where that register's upper half held an earlier 32-bit value (experiment,
-// profiles/r04/v6_hamming_ab.txt).  Reading through the asm hides the assumption, so the mask is kept.
+// The 16 key bits of an f16 top-2 result, read from the whole register and masked.  hipcc (ROCm 7.2) takes the
+// upper half of a 16-bit VALU result (v_min_f16 / v_med3_f16) as zero and folds the zero-extension into the
+// key's shift; on gfx950 that half keeps whatever the register held, and builds whose allocator had put a 32-bit
+// value there lost second-best keys (wrong seconds in 4-11 of 2,006 queries, deterministic per build; an
+// explicit MFMA wait-state pad and keeping operands live changed nothing; this mask fixed every form,
+// profiles/r04/v6_hamming_ab.txt).  The asm hides the assumption, so the mask is kept.
 __device__ __forceinline__ unsigned f16_bits(_Float16 x) {
     unsigned r;
     asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
     return r & 0xFFFFu;
 }
-
-// (experiment hooks, empty: an explicit wait-state pad after an fp4 chain and keeping its A fragments live)
-struct Fp4Frag {
-    v4i_t a[4];
-};
-__device__ __forceinline__ void fp4_frag_keep(const Fp4Frag&) {}
-__device__ __forceinline__ void fp4_result_pad(v16f_t&) {}
-__device__ __forceinline__ void fp4_result_pad(v16i_t&) {}
 
 /* NS 32-train subtiles per stage (one accumulator chain each).  With the queries scaled to -S / +S,
  * S = 16 NS, and the accumulators seeded with 256 S + subtile * 32 + row, every result is the stage-local key
@@ -456,18 +450,14 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             else kc[u][r] = 256 * SC + row;
         }
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
-    auto mfma_stage = [&](int buf, acc_t (&acc)[NS], Fp4Frag& fr) {
+    auto mfma_stage = [&](int buf, acc_t (&acc)[NS]) {
 #pragma unroll
         for (int u = 0; u < NS; u++) {
             const uint8_t* A = &s_t[buf][(32 * u + c) * PIT + 16 * h];
             acc[u] = kc[u];
-            if constexpr (FP4) {
-#pragma unroll
-                for (int s = 0; s < KS; s++) fr.a[s] = *reinterpret_cast<const v4i_t*>(A + 32 * s);
-            }
 #pragma unroll
             for (int s = 0; s < KS; s++) {   // one chain per subtile: the other waves on the SIMD hide its latency
-                const v4i_t av = FP4 ? fr.a[s] : *reinterpret_cast<const v4i_t*>(A + 32 * s);
+                const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
                 if constexpr (FP4) {
                     const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
                     const v8i_t b8 = {qf[s][0], qf[s][1], qf[s][2], qf[s][3], 0, 0, 0, 0};
@@ -508,8 +498,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
         s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
     };
-    auto reduce_any = [&](acc_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
-        if (FP4) fp4_result_pad(acc[0]);   // (this read can directly follow the chain's last MFMA)
+    auto reduce_any = [&](const acc_t (&acc)[NS], int tb) {   // the slice's last stage, maybe partial
         if (tb + TR <= t1) {
             reduce_full(acc, tb);
             return;
@@ -535,10 +524,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 Chunk wn;
                 if (more) wn = fetch(min(tb + TR + er, t1 - 1));
                 acc_t acc[NS];
-                Fp4Frag fr;
-                mfma_stage(j & 1, acc, fr);
+                mfma_stage(j & 1, acc);
                 reduce_any(acc, tb);
-                if (FP4) fp4_frag_keep(fr);
                 if (more) stage((j + 1) & 1, wn);
                 __syncthreads();
             }
@@ -546,8 +533,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             // software-pipelined: stage j's MFMA chains are issued beside stage j-1's top-2, so one wave keeps
             // the matrix pipe and the VALU busy together (every stage but the last is full)
             acc_t accA[NS], accB[NS];
-            Fp4Frag frA, frB;
-            auto step = [&](int j, acc_t (&accNew)[NS], const acc_t (&accOld)[NS], Fp4Frag& frNew, const Fp4Frag& frOld) {
+            auto step = [&](int j, acc_t (&accNew)[NS], const acc_t (&accOld)[NS]) {
                 // LA > 0: the next stage's rows are fetched and staged unconditionally (after the last stage they
                 // are the slice's last row again, written to the buffer no one reads any more): no branch splits
                 // the step's scheduling region
@@ -555,9 +541,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                 Chunk wn;
                 if (more) wn = fetch(min(t0 + TR * (j + 1) + er, t1 - 1));
                 if (LA > 0) __builtin_amdgcn_sched_barrier(0);   // the global loads issue first, their latency under the step
-                mfma_stage(j & 1, accNew, frNew);
+                mfma_stage(j & 1, accNew);
                 reduce_full(accOld, t0 + TR * (j - 1));
-                if (FP4) fp4_frag_keep(frOld);
                 // interleave: the A-fragment reads ahead, then each MFMA followed by a share of the top-2
 if (LA == 0) {
 #pragma unroll
@@ -584,22 +569,20 @@ if (LA == 0) {
                 const bool more = 1 < nst;
                 Chunk wn;
                 if (more) wn = fetch(min(t0 + TR + er, t1 - 1));
-                mfma_stage(0, accA, frA);
+                mfma_stage(0, accA);
                 if (more) stage(1, wn);
                 __syncthreads();
             }
             int j = 1;
             for (; j + 1 < nst; j += 2) {
-                step(j, accB, accA, frB, frA);
-                step(j + 1, accA, accB, frA, frB);
+                step(j, accB, accA);
+                step(j + 1, accA, accB);
             }
             if (j < nst) {
-                step(j, accB, accA, frB, frA);
+                step(j, accB, accA);
                 reduce_any(accB, t0 + TR * (nst - 1));
-                if (FP4) fp4_frag_keep(frB);
             } else {
                 reduce_any(accA, t0 + TR * (nst - 1));
-                if (FP4) fp4_frag_keep(frA);
             }
         }
     }
@@ -620,182 +603,14 @@ if (LA == 0) {
     }   // virtual blocks
 }
 
-/* Resident-chunk form of the fp4 top-2 (ORBGPU_TOP2 'R'): one 16-wave workgroup (512 queries) per CU loads 1,024
- * of its pair's expanded trains into LDS at once (147 KB at the 144-B pitch) and every wave then runs its 32
- * stages over them with no further barrier: k_top2_mfma's per-stage double buffer costs a workgroup barrier and a
- * staging round trip every 32 trains, which left the fp4 kernel's waves 73 % stalled (profiles/r04/
- * v4_hamming_fp4.json: WAIT_ANY + WAIT_INST_ANY of WAVE_CYCLES).  Keys, seeds, top-2 and output as k_top2_mfma's
- * fp4 form; the stages are software-pipelined the same way, A-fragment reads two MFMAs ahead. */
-constexpr int kResT = 1024, kResNW = 16;
-__global__ __launch_bounds__(kResNW * 64) void k_top2_res(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
-                                                          int* __restrict__ idx_o, int* __restrict__ second_o,
-                                                          int vblocks) {
-    constexpr int NT = kResNW * 64, QB = kResNW * 32, KS = 4, KB = 5, PIT = kMfPitch4;
-    constexpr unsigned RM = (1u << KB) - 1;
-    __shared__ __attribute__((aligned(16))) uint8_t s_t[kResT * PIT];
-    for (int vb = blockIdx.x; vb < vblocks; vb += gridDim.x) {
-    __syncthreads();   // (a previous item's last LDS reads precede this item's loads)
-    const int nb = vblocks, xq = nb >> 3, xr = nb & 7, xcd = vb & 7, xj = vb >> 3;   // XCD-grouped (k_top2_mfma)
-    const int lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xj;
-    const int qbi = lb % a.qblocks, rest = lb / a.qblocks;
-    const int sli = rest % a.nslices, p = rest / a.nslices;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
-    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
-    const int qblk = qbi * QB;
-    if (qblk >= nq) continue;   // whole workgroup
-    const int t0 = sli * a.slice, t1 = min(nt, t0 + a.slice);
-    const int h = lane >> 5, c = lane & 31;
-    const int qi = qblk + wv * 32 + c;
-    v4i_t qf[KS];
-    {
-        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-        if (qi < nq) {
-            const uint4* qp = reinterpret_cast<const uint4*>(a.q + ((long long)fr.x * a.q_stride + qi) * 32);
-            q0 = qp[0];
-            q1 = qp[1];
-        }
-        const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-        const uint32_t hm = h ? 0xFFFFFFFFu : 0u;   // (a select, not qd[2 s + h]: a dynamic index goes to scratch)
-#pragma unroll
-        for (int s = 0; s < KS; s++) qf[s] = fp4x32<0xEu>(qd[2 * s] ^ ((qd[2 * s] ^ qd[2 * s + 1]) & hm));
-    }
-    const int txs = a.tx_slot ? a.tx_slot[p] : p;
-    const uint64_t txb = reinterpret_cast<uint64_t>(a.tx + (long long)txs * a.tx_stride * 128);
-    const auto TXR = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(txb >> 32)) << 32) |
-                                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)txb)),
-        0, 0x7FFFFFFF, 0x00020000);
-    v16f_t kc;
-#pragma unroll
-    for (int r = 0; r < 16; r++) kc[r] = (float)(8388608 + 4096 + (r & 3) + 8 * (r >> 2) + 4 * h);
-    unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
-    auto mfma = [&](int j, v16f_t& acc, Fp4Frag& fr) {
-        const uint8_t* A = &s_t[(32 * j + c) * PIT + 16 * h];
-        acc = kc;
-#pragma unroll
-        for (int s = 0; s < KS; s++) fr.a[s] = *reinterpret_cast<const v4i_t*>(A + 32 * s);
-#pragma unroll
-        for (int s = 0; s < KS; s++) {
-            const v4i_t av = fr.a[s];
-            const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
-            const v8i_t b8 = {qf[s][0], qf[s][1], qf[s][2], qf[s][3], 0, 0, 0, 0};
-            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc, 4, 4, 0, 0, 0, 0);
-        }
-    };
-    auto top2f = [&](const v16f_t& acc, unsigned& lbu, unsigned& lsu, auto keep) {
-        const _Float16 inf = __builtin_bit_cast(_Float16, (unsigned short)0x7C00u);
-        _Float16 lbh = inf, lsh = inf;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float kv = acc[r];
-            const int ki = __builtin_bit_cast(int, kv);
-            const _Float16 key = keep(r) ? __builtin_bit_cast(_Float16, (unsigned short)ki) : inf;
-            lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
-            lbh = __builtin_fminf16(lbh, key);
-        }
-        lbu = f16_bits(lbh);
-        lsu = f16_bits(lsh);
-    };
-    auto merge = [&](unsigned lbt, unsigned lst, int tb) {
-        constexpr unsigned kInf = 0x7C00u;
-        if (lbt == kInf) return;   // (only a partial stage leaves a lane without keys)
-        const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
-        s2 = umed3(b, gb, s2);
-        b = min(b, gb);
-        if (lst != kInf) s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
-    };
-    auto reduce_full = [&](const v16f_t& acc, int tb) {
-        unsigned lbt, lst;
-        top2f(acc, lbt, lst, [](int) { return true; });
-        const unsigned gb = ((lbt << (16 - KB)) & 0xFFFF0000u) + (lbt & RM) + (unsigned)tb;
-        s2 = umed3(b, gb, s2);
-        b = min(b, gb);
-        s2 = min(s2, (lst << (16 - KB)) | 0xFFFFu);
-    };
-    auto reduce_any = [&](v16f_t& acc, int tb) {
-        fp4_result_pad(acc);   // (this read directly follows the chain's last MFMA)
-        if (tb + 32 <= t1) {
-            reduce_full(acc, tb);
-            return;
-        }
-        unsigned lbt, lst;
-        top2f(acc, lbt, lst, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
-        merge(lbt, lst, tb);
-    };
-    for (int cb = t0; cb < t1; cb += kResT) {
-        const int cn = min(kResT, t1 - cb);
-        if (cb > t0) __syncthreads();   // every wave's reads of the previous chunk are done
-        {
-            // the chunk's rows into LDS, every load issued before the first store; rows past the chunk reload its
-            // last row (their keys are masked)
-            v4i_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = tid + u * NT, row = min(i >> 3, cn - 1);
-                v[u] = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, (cb + row) * 128 + 16 * (i & 7), 0, 0));
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = tid + u * NT;
-                *reinterpret_cast<v4i_t*>(&s_t[(i >> 3) * PIT + 16 * (i & 7)]) = v[u];
-            }
-        }
-        __syncthreads();
-        const int nst = (cn + 31) / 32;
-        v16f_t accA, accB;
-        Fp4Frag frA, frB;
-        auto step = [&](int j, v16f_t& accNew, const v16f_t& accOld, Fp4Frag& frNew, const Fp4Frag& frOld) {
-            mfma(j, accNew, frNew);
-            reduce_full(accOld, cb + 32 * (j - 1));
-            fp4_frag_keep(frOld);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two A-fragment reads ahead
-#pragma unroll
-            for (int i = 0; i < KS; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (i + 2 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 9, 0);
-            }
-        };
-        mfma(0, accA, frA);
-        int j = 1;
-        for (; j + 1 < nst; j += 2) {
-            step(j, accB, accA, frB, frA);
-            step(j + 1, accA, accB, frA, frB);
-        }
-        if (j < nst) {
-            step(j, accB, accA, frB, frA);
-            reduce_any(accB, cb + 32 * (nst - 1));
-            fp4_frag_keep(frB);
-        } else {
-            reduce_any(accA, cb + 32 * (nst - 1));
-            fp4_frag_keep(frA);
-        }
-    }
-    const unsigned ob = __shfl_xor(b, 32), os = __shfl_xor(s2, 32);
-    s2 = min(min(s2, os), max(b, ob));
-    b = min(b, ob);
-    if (h == 0 && qi < nq) {
-        const long long o = (long long)p * a.out_stride + qi;
-        if (a.nslices == 1) {
-            best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
-            idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
-            second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
-        } else {
-            part[((long long)p * a.nslices + sli) * a.out_stride + qi] = make_uint2(b, s2);
-        }
-    }
-    }   // virtual blocks
-}
-
-// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "8fp"): '4' / '8' waves per workgroup,
+// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "8f"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
 // expansion of the pairs after the first eighth overlapped with the first eighth's top-2 (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
-// reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile), 'R' the fp4 form
-// with 1,024 trains resident per 16-wave workgroup (k_top2_res)
-struct Top2Cfg {   // default "8fp": the fp4 form, pipelined (r04 A/B, profiles/r04/v4_hamming_ab.txt: 190 vs 252 us)
+// reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile)
+struct Top2Cfg {   // default "8f": the fp4 form, unpipelined (r04 A/B, profiles/r04/v6_hamming_ab.txt: 184 us, pipelined
+                   // 188, int8 262)
     int waves = 8, stage = 1, la = 0;
-    bool pipe = true, persist = false, overlap = false, fp4 = true, res = false;
+    bool pipe = false, persist = false, overlap = false, fp4 = true;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {
@@ -809,11 +624,7 @@ static const Top2Cfg& top2_cfg() {
         t.overlap = std::strchr(e, 'o') != nullptr;
         t.la = std::strchr(e, 'L') ? 4 : std::strchr(e, 'l') ? 2 : 0;
         t.fp4 = std::strchr(e, 'f') != nullptr;
-        t.res = std::strchr(e, 'R') != nullptr;
-        if (t.res) t.fp4 = true;
-        // the fp4 form is built pipelined only (its unpipelined build gave wrong seconds on the r04 box, 1 of 3
-        // tests, profiles/r04/v4_hamming_ab.txt; not investigated further)
-        if (t.fp4) t.waves = t.res ? kResNW : 8, t.stage = 1, t.pipe = !std::strchr(e, 'u');   // 'u': unpipelined
+        if (t.fp4) t.waves = 8, t.stage = 1;
         return t;
     }();
     return c;
@@ -855,8 +666,7 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
     Top2Batch a = a0;
     const Top2Cfg& cfg = top2_cfg();
-    // (the resident form needs pre-expanded trains; without them the 8-wave in-kernel expansion form runs)
-    const int nw = cfg.res && !(a.tx && max_nt > 0) ? 8 : cfg.waves, ns = cfg.stage;
+    const int nw = cfg.waves, ns = cfg.stage;
     const int qb = (max_nq + 32 * nw - 1) / (32 * nw);
     a.slice = top2_slice_len(npairs, max_nq, max_nt);
     const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);   // 1: k_top2_mfma writes the outputs itself
@@ -882,7 +692,6 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
         if (cfg.fp4)
             kern = !pp ? k_top2_mfma<true, 8, 1, false, 0, true>
                        : cfg.la ? k_top2_mfma<true, 8, 1, true, 2, true> : k_top2_mfma<true, 8, 1, true, 0, true>;
-        if (cfg.res) kern = k_top2_res;
         auto expand = cfg.fp4 ? k_expand_fp4 : k_expand_pm1;
         int slots = 1 << 30;   // persistent: one workgroup per resident slot (a multiple of 8: virtual blocks keep
         if (cfg.persist) {     // their XCD)
