@@ -353,9 +353,14 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     constexpr int KB = 5 + (NS == 2);  // stage-local key: dist << KB | stage row
     constexpr int VG = FP4 ? 9 : NS == 2 ? 5 : 6; // VALU issued after each MFMA of the pipelined stage
     static_assert(CH >= 1 && CH <= 4, "staging chunks");
-    static_assert(!FP4 || (PRE && NS == 1), "fp4: pre-expanded trains, one subtile per stage");
+    static_assert(!FP4 || NS == 1, "fp4: one subtile per stage");
     using acc_t = typename std::conditional<FP4, v16f_t, v16i_t>::type;
     __shared__ __attribute__((aligned(16))) uint8_t s_t[2][TR * PIT];
+    // fp4 without pre-expanded trains: byte -> 8 e2m1 nibbles (+4 where the bit is clear, -4 where set), so a staged
+    // train dword costs four LDS lookups instead of ~32 VALU
+    __shared__ uint32_t s_lut[FP4 && !PRE ? 256 : 1];
+    if (FP4 && !PRE)
+        for (int i = threadIdx.x; i < 256; i += NT) s_lut[i] = 0x66666666u ^ (spread8_nib((uint32_t)i) << 3);
     // 1-D grid of (pair, slice, query block), query block fastest.  Blocks are dealt round-robin over the 8
     // XCDs (b and b + 8 share one), so XCD x takes a contiguous run of that sequence: the query blocks of a
     // pair, which all stream the same expanded trains, then share one L2 (dealt round-robin, every pair's
@@ -420,6 +425,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             for (int i = 0; i < CH; i++)
                 k.x[i] = stager ? __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, row * TRB + 16 * (ec + i), 0, 0))
                                 : v4i_t{0, 0, 0, 0};
+        } else if (FP4) {   // chunk ec = descriptor dword ec (32 bits -> 16 expanded bytes)
+            k.w[0] = stager ? T[(long long)row * 8 + ec] : 0u;
         } else {
 #pragma unroll
             for (int i = 0; i < (CH + 1) / 2; i++) k.w[i] = T[(long long)row * 8 + (ec >> 1) + i];
@@ -429,6 +436,11 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     auto stage = [&](int buf, const Chunk& k) {
         if (!stager) return;
         v4i_t* d = reinterpret_cast<v4i_t*>(&s_t[buf][er * PIT + ec * 16]);
+        if (FP4 && !PRE) {
+            const uint32_t w = k.w[0];
+            d[0] = v4i_t{(int)s_lut[w & 255u], (int)s_lut[(w >> 8) & 255u], (int)s_lut[(w >> 16) & 255u], (int)s_lut[w >> 24]};
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < CH; i++) d[i] = PRE ? k.x[i] : pm1x16(k.w[i >> 1] >> (16 * ((ec + i) & 1)));
     };
@@ -606,11 +618,12 @@ if (LA == 0) {
 // k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "8f"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
 // expansion of the pairs after the first eighth overlapped with the first eighth's top-2 (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
-// reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile)
+// reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile), 'x' (with 'f') no expansion
+// kernel: each stage's train dwords are expanded while staged (k_top2_mfma<false, ..., FP4>)
 struct Top2Cfg {   // default "8f": the fp4 form, unpipelined (r04 A/B, profiles/r04/v6_hamming_ab.txt: 184 us, pipelined
                    // 188, int8 262)
     int waves = 8, stage = 1, la = 0;
-    bool pipe = false, persist = false, overlap = false, fp4 = true;
+    bool pipe = false, persist = false, overlap = false, fp4 = true, noexp = false;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {
@@ -624,6 +637,7 @@ static const Top2Cfg& top2_cfg() {
         t.overlap = std::strchr(e, 'o') != nullptr;
         t.la = std::strchr(e, 'L') ? 4 : std::strchr(e, 'l') ? 2 : 0;
         t.fp4 = std::strchr(e, 'f') != nullptr;
+        t.noexp = std::strchr(e, 'x') != nullptr;
         if (t.fp4) t.waves = 8, t.stage = 1;
         return t;
     }();
@@ -675,9 +689,10 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     const int vblocks = (int)((long long)qb * nsu * npairs);
     // max_nt == 0 (an empty train set, e.g. a previous frame without keypoints): no expansion launch (a
     // zero-sized grid is an error); k_top2_mfma then sees no tiles and writes the no-match sentinels
-    if (!(a.tx && max_nt > 0)) {
+    if (!(a.tx && max_nt > 0) || (cfg.fp4 && cfg.noexp)) {
         auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
                             : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
+        if (cfg.fp4) kern = k_top2_mfma<false, 8, 1, false, 0, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)vblocks), dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx,
                            d_second, vblocks);
     } else {
