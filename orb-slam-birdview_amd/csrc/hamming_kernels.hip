@@ -615,15 +615,15 @@ if (LA == 0) {
     }   // virtual blocks
 }
 
-// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "8f"): '4' / '8' waves per workgroup,
+// k_top2_mfma's configuration (ORBGPU_TOP2, an A/B switch; default "8fx"): '4' / '8' waves per workgroup,
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
 // expansion of the pairs after the first eighth overlapped with the first eighth's top-2 (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
 // reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile), 'x' (with 'f') no expansion
 // kernel: each stage's train dwords are expanded while staged (k_top2_mfma<false, ..., FP4>)
-struct Top2Cfg {   // default "8f": the fp4 form, unpipelined (r04 A/B, profiles/r04/v6_hamming_ab.txt: 184 us, pipelined
-                   // 188, int8 262)
+struct Top2Cfg {   // default "8fx": the fp4 form, unpipelined, trains expanded while staged (r04 A/B,
+                   // profiles/r04/v9_hamming_ab.txt: 161-162 us; with the expansion kernel 181; pipelined 188; int8 262)
     int waves = 8, stage = 1, la = 0;
-    bool pipe = false, persist = false, overlap = false, fp4 = true, noexp = false;
+    bool pipe = false, persist = false, overlap = false, fp4 = true, noexp = true;
 };
 static const Top2Cfg& top2_cfg() {
     static const Top2Cfg c = [] {
@@ -646,6 +646,7 @@ static const Top2Cfg& top2_cfg() {
 static int top2_waves() { return top2_cfg().waves; }
 bool top2_overlap_enabled() { return top2_cfg().overlap; }
 bool top2_fp4_enabled() { return top2_cfg().fp4; }
+bool top2_needs_expansion() { return !(top2_cfg().fp4 && top2_cfg().noexp); }
 int top2_queries_per_block() { return 32 * top2_cfg().waves; }
 
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {

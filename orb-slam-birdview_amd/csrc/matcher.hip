@@ -304,10 +304,12 @@ int orb_hamming_top2_device(orb_ctx* h, const uint8_t* d_q, int nq, const uint8_
     if (nt > 65535) return set_error("orb_hamming_top2_device: more than 65535 trains", hipSuccess), ORB_ERR_ARG;
     Arena a{c};
     const int ns = top2_batch_slices(1, nq, nt);
-    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(uint2)) + Arena::align((size_t)nt * 256) + 512);
+    const bool exp = top2_needs_expansion();
+    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(uint2)) + Arena::align(exp ? (size_t)nt * 256 : 1) + 512);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     uint2* part = a.take<uint2>((size_t)ns * nq);
-    uint8_t* tx = a.take<uint8_t>((size_t)nt * 256);   // trains expanded to +-1 int8 once (k_expand_pm1)
+    // trains expanded once (k_expand_pm1 / k_expand_fp4) when the configured form reads them pre-expanded
+    uint8_t* tx = exp ? a.take<uint8_t>((size_t)nt * 256) : nullptr;
     Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq, tx, nt, nullptr, nullptr, 0};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2_batch(tb, 1, nq, nt, d_best, d_best_idx, d_second, part, c->stream);
@@ -352,12 +354,14 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     const int nslots = (int)up.size() - 3 * npairs;
     Arena a{c};
     const int ns = top2_batch_slices(npairs, kp_cap, kp_cap);
+    const bool exp = top2_needs_expansion();
     hipError_t e = a.reserve(Arena::align(up.size() * 4) + Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) +
-                             Arena::align((size_t)nslots * kp_cap * 256) + 768);
+                             Arena::align(exp ? (size_t)nslots * kp_cap * 256 : 1) + 768);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     int* d_up = a.take<int>(up.size());
     uint2* part = a.take<uint2>((size_t)npairs * ns * kp_cap);
-    uint8_t* tx = a.take<uint8_t>((size_t)nslots * kp_cap * 256);   // each distinct train frame expanded once
+    // each distinct train frame expanded once, when the configured form reads pre-expanded trains
+    uint8_t* tx = exp ? a.take<uint8_t>((size_t)nslots * kp_cap * 256) : nullptr;
     {   // the pinned slot this call uploads from: its previous upload (two calls ago) must have been read
         const int sl = c->pairs_slot;
         c->pairs_slot ^= 1;

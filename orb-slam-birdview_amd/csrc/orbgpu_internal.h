@@ -206,6 +206,7 @@ struct Top2Overlap {
 };
 bool top2_overlap_enabled();
 bool top2_fp4_enabled();   // ORBGPU_TOP2 'f': the e2m1 MFMA form of k_top2_mfma
+bool top2_needs_expansion();   // false: the default fp4 form expands each stage's trains while staging them
 int top2_queries_per_block();
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
                                      int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream,
