@@ -638,7 +638,8 @@ static const Top2Cfg& top2_cfg() {
         t.la = std::strchr(e, 'L') ? 4 : std::strchr(e, 'l') ? 2 : 0;
         t.fp4 = std::strchr(e, 'f') != nullptr;
         t.noexp = std::strchr(e, 'x') != nullptr;
-        if (t.fp4) t.waves = 8, t.stage = 1;
+        if (t.fp4) t.stage = 1;   // fp4: 8 waves, or 4 with '4' and 'x'
+        if (t.fp4 && !(t.noexp && t.waves == 4)) t.waves = 8;
         return t;
     }();
     return c;
@@ -693,7 +694,7 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (!(a.tx && max_nt > 0) || (cfg.fp4 && cfg.noexp)) {
         auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
                             : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
-        if (cfg.fp4) kern = k_top2_mfma<false, 8, 1, false, 0, true>;
+        if (cfg.fp4) kern = nw == 4 ? k_top2_mfma<false, 4, 1, false, 0, true> : k_top2_mfma<false, 8, 1, false, 0, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)vblocks), dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx,
                            d_second, vblocks);
     } else {
