@@ -353,7 +353,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     constexpr int KB = 5 + (NS == 2);  // stage-local key: dist << KB | stage row
     constexpr int VG = FP4 ? 9 : NS == 2 ? 5 : 6; // VALU issued after each MFMA of the pipelined stage
     static_assert(CH >= 1 && CH <= 4, "staging chunks");
-    static_assert(!FP4 || NS == 1, "fp4: one subtile per stage");
+    static_assert(!FP4 || PRE == false || NS == 1, "fp4 with pre-expanded trains: one subtile per stage");
     using acc_t = typename std::conditional<FP4, v16f_t, v16i_t>::type;
     __shared__ __attribute__((aligned(16))) uint8_t s_t[2][TR * PIT];
     // fp4 without pre-expanded trains: byte -> 8 e2m1 nibbles (+4 where the bit is clear, -4 where set), so a staged
@@ -458,10 +458,17 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
 #pragma unroll
         for (int r = 0; r < 16; r++) {
             const int row = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (FP4) kc[u][r] = (float)(8388608 + 4096 + row);   // exact: 2^23 + 4096 + row (see above)
+            if (FP4) kc[u][r] = (float)(8388608 + 4096 * NS + row);   // exact: 2^23 + 4096 NS + row (see above)
             else kc[u][r] = 256 * SC + row;
         }
     const int nst = t1 > t0 ? (t1 - t0 + TR - 1) / TR : 0;   // stages (uniform)
+    // e8m0 block scales (byte 0 of a register: 127 = 2^0, 128 = 2^1), from registers (a constant scale operand is
+    // read as an f32 inline constant, MI355X builtin note in ck's amd_xdlops.hpp); used by the fp4 NS = 2 form only
+    int sc_a = 127, sc_b = 128;
+    if (FP4 && NS == 2) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(sc_a) : "v"(sc_a));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(sc_b) : "v"(sc_b));
+    }
     auto mfma_stage = [&](int buf, acc_t (&acc)[NS]) {
 #pragma unroll
         for (int u = 0; u < NS; u++) {
@@ -474,7 +481,10 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
                     const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
                     const v8i_t b8 = {qf[s][0], qf[s][1], qf[s][2], qf[s][3], 0, 0, 0, 0};
                     // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
-                    acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[u], 4, 4, 0, 0, 0, 0);
+                    if (NS == 1)
+                        acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[u], 4, 4, 0, 0, 0, 0);
+                    else   // block scale 2^1 on the queries: q . t = 64 dist - 8192, keys dist << 6 | row of 64
+                        acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[u], 4, 4, 0, sc_a, 0, sc_b);
                 } else {
                     acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, qf[s], acc[u], 0, 0, 0);
                 }
@@ -638,8 +648,8 @@ static const Top2Cfg& top2_cfg() {
         t.la = std::strchr(e, 'L') ? 4 : std::strchr(e, 'l') ? 2 : 0;
         t.fp4 = std::strchr(e, 'f') != nullptr;
         t.noexp = std::strchr(e, 'x') != nullptr;
-        if (t.fp4) t.stage = 1;   // fp4: 8 waves, or 4 with '4' and 'x'
-        if (t.fp4 && !(t.noexp && t.waves == 4)) t.waves = 8;
+        if (t.fp4 && !t.noexp) t.stage = 1;   // fp4: one subtile, or two with '2' and 'x' (scaled queries)
+        if (t.fp4 && !(t.noexp && t.waves == 4)) t.waves = 8;   // 8 waves, or 4 with '4' and 'x' 
         return t;
     }();
     return c;
@@ -694,7 +704,9 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
     if (!(a.tx && max_nt > 0) || (cfg.fp4 && cfg.noexp)) {
         auto kern = nw == 8 ? (ns == 2 ? k_top2_mfma<false, 8, 2, false> : k_top2_mfma<false, 8, 1, false>)
                             : (ns == 2 ? k_top2_mfma<false, 4, 2, false> : k_top2_mfma<false, 4, 1, false>);
-        if (cfg.fp4) kern = nw == 4 ? k_top2_mfma<false, 4, 1, false, 0, true> : k_top2_mfma<false, 8, 1, false, 0, true>;
+        if (cfg.fp4)
+            kern = nw == 4 ? k_top2_mfma<false, 4, 1, false, 0, true>
+                           : ns == 2 ? k_top2_mfma<false, 8, 2, false, 0, true> : k_top2_mfma<false, 8, 1, false, 0, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)vblocks), dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx,
                            d_second, vblocks);
     } else {

@@ -57,6 +57,19 @@ static int run(const unsigned char* fa, const unsigned char* fb, float* out) {
     return e == hipSuccess ? 0 : 1;
 }
 
+// the same product with block scales from registers: scale A 2^0 (e8m0 127), scale B 2^1 (128) -> every result x2
+__global__ void ks(const int* A, const int* B, float* D, int sa, int sb) {
+    const int l = threadIdx.x;
+    v8i a = {A[4 * l], A[4 * l + 1], A[4 * l + 2], A[4 * l + 3], 0, 0, 0, 0};
+    v8i b = {B[4 * l], B[4 * l + 1], B[4 * l + 2], B[4 * l + 3], 0, 0, 0, 0};
+    int ra, rb;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ra) : "v"(sa));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(rb) : "v"(sb));
+    v16f c = {};
+    c = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, ra, 0, rb);
+    for (int r = 0; r < 16; r++) D[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 32 + (l & 31)] = c[r];
+}
+
 int main() {
     unsigned char fa[1024], fb[1024];
     float D[1024];
@@ -109,6 +122,23 @@ int main() {
             bad += (float)s != D[i * 32 + j];
         }
     printf("+-4 sums under H%d: %d of 1024 differ\n", hyp, bad);
+    // scaled form: the unscaled result of the same operands, doubled
+    {
+        float D2[1024];
+        int *dA, *dB;
+        float* dD;
+        hipMalloc(&dA, 1024);
+        hipMalloc(&dB, 1024);
+        hipMalloc(&dD, 1024 * 4);
+        hipMemcpy(dA, fa, 1024, hipMemcpyHostToDevice);
+        hipMemcpy(dB, fb, 1024, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(ks, dim3(1), dim3(64), 0, 0, dA, dB, dD, 127, 128);
+        hipMemcpy(D2, dD, sizeof D2, hipMemcpyDeviceToHost);
+        int sbad = 0;
+        for (int i = 0; i < 1024; i++) sbad += D2[i] != 2.0f * D[i];
+        printf("scaled (A 2^0, B 2^1) vs 2x unscaled: %d of 1024 differ\n", sbad);
+        bad += sbad;
+    }
     if (best < 0 || bad) return printf("FAIL\n"), 1;
     printf("ok H%d\n", best);
     return 0;
