@@ -1501,12 +1501,6 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             // sort the > 1-key nodes by (size, seq) descending (:684-685): dense keys, then each
             // node's rank = number of larger keys (keys are unique)
             unsigned long long* skey = reinterpret_cast<unsigned long long*>(rxB);
-            // 32-bit keys size << 20 | seq when both fit (sizes <= C < 4096, seqs < 2^20; the node ids go to
-            // a second array): half the LDS bytes per comparison and single-dword compares (r04: the ranking is
-            // 11 k of a C5 frame's 56 k level-0 cycles, profiles/r04/v8_octree_stamps.txt)
-            const bool k32 = C < 4096 && nextSeq < (1 << 20);   // (workgroup-uniform)
-            uint32_t* skey32 = rxB;
-            uint32_t* tix = ryB;
             int* dd = cntB;     // rank -> #children - 1
             int* dpre = seqB;   // rank -> exclusive prefix of dd
             int nsort = 0;
@@ -1515,18 +1509,12 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const bool big = t < S && cntA[t] > 1;
                 int tot;
                 const int pos = nsort + oct_scan<NT>(big ? 1 : 0, sc, par, tot);
-                // seq in 24 (20) bits: creation order, or its complement for ORB_VARIANT_TIE_REVERSE (a later-
+                // seq in 24 bits: creation order, or its complement for ORB_VARIANT_TIE_REVERSE (a later-
                 // created node counts as the smaller pointer); roots (seq < 0) never reach this sort
-                if (big) {
-                    if (k32) {
-                        skey32[pos] = ((uint32_t)cntA[t] << 20) | ((uint32_t)(seqA[t] ^ tieMask) & 0xFFFFFu);
-                        tix[pos] = (uint32_t)t;
-                    } else {
-                        skey[pos] = ((unsigned long long)cntA[t] << 40) |
-                                    ((unsigned long long)((unsigned)(seqA[t] ^ tieMask) & 0xFFFFFFu) << 16) |
-                                    (unsigned long long)t;
-                    }
-                }
+                if (big)
+                    skey[pos] = ((unsigned long long)cntA[t] << 40) |
+                                ((unsigned long long)((unsigned)(seqA[t] ^ tieMask) & 0xFFFFFFu) << 16) |
+                                (unsigned long long)t;
                 nsort += tot;
             }
             if (tid == 0) sv[2] = nsort;
@@ -1536,47 +1524,24 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             // strided 8-key slice, summed with xor shuffles inside the lane group
             const int G = nsort <= NT / 8 ? 8 : nsort <= NT / 4 ? 4 : nsort <= NT / 2 ? 2 : 1;
             const int lg = tid & (G - 1);
-            if (k32) {
-                for (int j0 = 0; j0 < nsort * G; j0 += NT) {   // uniform trip count (shuffles below)
-                    const int j = (j0 + tid) / G;
-                    const bool ok = j < nsort;
-                    const uint32_t key = ok ? skey32[j] : 0xFFFFFFFFu;
-                    int r = 0;
-                    for (int i = 8 * lg; i + 8 <= nsort; i += 8 * G) {
-                        const uint4* p = reinterpret_cast<const uint4*>(skey32 + i);
-                        const uint4 a = p[0], b = p[1];
-                        r += (a.x > key) + (a.y > key) + (a.z > key) + (a.w > key) + (b.x > key) + (b.y > key) +
-                             (b.z > key) + (b.w > key);
-                    }
-                    if (lg == 0)
-                        for (int i = nsort & ~7; i < nsort; i++) r += skey32[i] > key;
-                    for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o);
-                    if (ok && lg == 0) {
-                        const int t = (int)tix[j];
-                        ord[r] = t;
-                        dd[r] = __popc(quad_mask(&quad[4 * t])) - 1;
-                    }
+            for (int j0 = 0; j0 < nsort * G; j0 += NT) {   // uniform trip count (shuffles below)
+                const int j = (j0 + tid) / G;
+                const bool ok = j < nsort;
+                const unsigned long long key = ok ? skey[j] : ~0ull;
+                int r = 0;
+                for (int i = 8 * lg; i + 8 <= nsort; i += 8 * G) {
+                    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(skey + i);
+                    const ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
+                    r += (a.x > key) + (a.y > key) + (b.x > key) + (b.y > key) + (c.x > key) + (c.y > key) +
+                         (d.x > key) + (d.y > key);
                 }
-            } else {
-                for (int j0 = 0; j0 < nsort * G; j0 += NT) {   // uniform trip count (shuffles below)
-                    const int j = (j0 + tid) / G;
-                    const bool ok = j < nsort;
-                    const unsigned long long key = ok ? skey[j] : ~0ull;
-                    int r = 0;
-                    for (int i = 8 * lg; i + 8 <= nsort; i += 8 * G) {
-                        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(skey + i);
-                        const ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
-                        r += (a.x > key) + (a.y > key) + (b.x > key) + (b.y > key) + (c.x > key) + (c.y > key) +
-                             (d.x > key) + (d.y > key);
-                    }
-                    if (lg == 0)
-                        for (int i = nsort & ~7; i < nsort; i++) r += skey[i] > key;
-                    for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o);
-                    if (ok && lg == 0) {
-                        const int t = (int)(key & 0xFFFF);
-                        ord[r] = t;
-                        dd[r] = __popc(quad_mask(&quad[4 * t])) - 1;
-                    }
+                if (lg == 0)
+                    for (int i = nsort & ~7; i < nsort; i++) r += skey[i] > key;
+                for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o);
+                if (ok && lg == 0) {
+                    const int t = (int)(key & 0xFFFF);
+                    ord[r] = t;
+                    dd[r] = __popc(quad_mask(&quad[4 * t])) - 1;
                 }
             }
             __syncthreads();
