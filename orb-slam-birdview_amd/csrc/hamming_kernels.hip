@@ -425,10 +425,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
             for (int i = 0; i < CH; i++)
                 k.x[i] = stager ? __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(TXR, row * TRB + 16 * (ec + i), 0, 0))
                                 : v4i_t{0, 0, 0, 0};
-        } else if (FP4) {   // chunk ec = descriptor dword ec (32 bits -> 16 expanded bytes); every thread loads (the
-                            // row is clamped into the slice), only the staging threads store: no select that would
-                            // wait for the load
-            k.w[0] = T[(long long)row * 8 + ec];
+        } else if (FP4) {   // chunk ec = descriptor dword ec (32 bits -> 16 expanded bytes)
+            k.w[0] = stager ? T[(long long)row * 8 + ec] : 0u;
         } else {
 #pragma unroll
             for (int i = 0; i < (CH + 1) / 2; i++) k.w[i] = T[(long long)row * 8 + (ec >> 1) + i];
@@ -542,31 +540,16 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
         stage(0, fetch(min(t0 + er, t1 - 1)));
         __syncthreads();
         if (!PIPE) {
-            // the rows of stage j + 2 are loaded during stage j (two stages of work under an L2 round trip; loading
-            // only the next stage's left the staging waves, and through the barrier every wave, waiting on it)
-            // (unrolled by two so the two row registers alternate roles: a register copy would wait for the load)
-            // (the loads are unconditional: rows past the slice are clamped to its last row and never staged)
-            Chunk wA = fetch(min(t0 + TR + er, t1 - 1)), wB;
-            for (int j = 0; j < nst; j += 2) {
-                {
-                    const int tb = t0 + TR * j;
-                    wB = fetch(min(tb + 2 * TR + er, t1 - 1));
-                    acc_t acc[NS];
-                    mfma_stage(j & 1, acc);
-                    reduce_any(acc, tb);
-                    if (j + 1 < nst) stage((j + 1) & 1, wA);
-                    __syncthreads();
-                }
-                if (j + 1 >= nst) break;   // (uniform)
-                {
-                    const int tb = t0 + TR * (j + 1);
-                    wA = fetch(min(tb + 2 * TR + er, t1 - 1));
-                    acc_t acc[NS];
-                    mfma_stage((j + 1) & 1, acc);
-                    reduce_any(acc, tb);
-                    if (j + 2 < nst) stage(j & 1, wB);
-                    __syncthreads();
-                }
+            for (int j = 0; j < nst; j++) {
+                const int tb = t0 + TR * j;
+                const bool more = j + 1 < nst;
+                Chunk wn;
+                if (more) wn = fetch(min(tb + TR + er, t1 - 1));
+                acc_t acc[NS];
+                mfma_stage(j & 1, acc);
+                reduce_any(acc, tb);
+                if (more) stage((j + 1) & 1, wn);
+                __syncthreads();
             }
         } else {
             // software-pipelined: stage j's MFMA chains are issued beside stage j-1's top-2, so one wave keeps
