@@ -535,9 +535,16 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     // Compact inputs (the upload is the call's cost): queries in item order, and per common
     // node its candidates without a map point (and stereo ones only if asked, :725-733) as compact train
     // indices, in the node's order (the reference keeps the last candidate reaching the minimum)
-    std::vector<int> item_q, cand, train_of;           // item -> idx1; candidates; compact train -> idx2
-    std::vector<int2> rng;
-    std::vector<int> tmap(n2 > 0 ? n2 : 1, -1);       // idx2 -> compact train
+    std::vector<int>& item_q = c->tri_item_q;     // item -> idx1
+    std::vector<int>& cand = c->tri_cand;         // candidates (compact train indices)
+    std::vector<int>& train_of = c->tri_train_of; // compact train -> idx2
+    std::vector<int2>& rng = c->tri_rng;
+    std::vector<int>& tmap = c->tri_tmap;         // idx2 -> compact train (all -1 between calls)
+    item_q.clear();
+    cand.clear();
+    train_of.clear();
+    rng.clear();
+    if ((int)tmap.size() < n2) tmap.resize(n2, -1);
     for_common_nodes(fv1, fv2, [&](int a, int b) {
         const int cb = (int)cand.size();
         for (int i = fv2.offsets[b]; i < fv2.offsets[b + 1]; i++) {
@@ -560,7 +567,9 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         }
     });
     const int nitems = (int)item_q.size(), nt = (int)train_of.size(), ncand = (int)cand.size();
-    std::vector<int> best(nitems, -1);
+    for (int j = 0; j < nt; j++) tmap[train_of[j]] = -1;   // (restore the invariant)
+    std::vector<int>& best = c->tri_best;
+    best.assign(nitems, -1);
     if (nitems) {
         Stage st{c};
         st.zc = 1;   // one kernel over small inputs: reading the pinned mirror beats the DMA (Stage::zc)
@@ -610,8 +619,11 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         const int* hb = st.h<int>(o_b);
         for (int i = 0; i < nitems; i++) best[i] = hb[i] >= 0 ? train_of[hb[i]] : -1;
     }
-    std::vector<int> vMatches12(n1, -1);
-    std::vector<int> rotHist[HISTO_LENGTH];
+    std::vector<int>& vMatches12 = c->tri_match;
+    vMatches12.assign(n1, -1);
+    static_assert(HISTO_LENGTH == 30, "Ctx::tri_hist");
+    std::vector<int>* rotHist = c->tri_hist;
+    for (int i = 0; i < HISTO_LENGTH; i++) rotHist[i].clear();
     int nmatches = 0;
     for (int i = 0; i < nitems; i++) {
         if (best[i] < 0) continue;

@@ -91,6 +91,11 @@ struct Ctx {
     size_t pinned_cap = 0;
 
     std::vector<int> pairs_upload_host;   // orb_hamming_top2_frames_device: pair lists / slots assembled here
+    // orb_search_for_triangulation's host lists, kept across calls (capacity reused: a call is ~30 us, and its
+    // dozens of small allocations were a measurable part of it); tri_tmap stays all -1 between calls
+    std::vector<int> tri_item_q, tri_cand, tri_train_of, tri_tmap, tri_best, tri_match;
+    std::vector<int2> tri_rng;
+    std::vector<int> tri_hist[30];
     // ... and staged through two pinned slots used in turn: a slot is rewritten only after the event recorded
     // behind its previous upload has completed (the call returns before its copy runs)
     int* h_pairs[2] = {nullptr, nullptr};
