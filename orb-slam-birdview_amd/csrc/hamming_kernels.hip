@@ -312,6 +312,12 @@ __device__ __forceinline__ v4i_t pmSx16(uint32_t w) {
     return v4i_t{pmSx4<S>(w), pmSx4<S>(w >> 4), pmSx4<S>(w >> 8), pmSx4<S>(w >> 12)};
 }
 
+// the top-2's step (k_top2_mfma top2f): two keys per min3 / med3 / min (1), or one per med3 / min (0, r04 v10)
+#ifndef ORBGPU_TOP2_PAIRS
+#define ORBGPU_TOP2_PAIRS 1
+#endif
+constexpr bool TOP2_PAIRS = ORBGPU_TOP2_PAIRS != 0;
+
 // The 16 key bits of an f16 top-2 result, read from the whole register and masked.  hipcc (ROCm 7.2) takes the
 // upper half of a 16-bit VALU result (v_min_f16 / v_med3_f16) as zero and folds the zero-extension into the
 // key's shift; on gfx950 that half keeps whatever the register held, and builds whose allocator had put a 32-bit
@@ -497,17 +503,33 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(Top2Batch a, uint2* __res
     auto top2f = [&](const acc_t (&acc)[NS], unsigned& lbu, unsigned& lsu, auto keep) {
         const _Float16 inf = __builtin_bit_cast(_Float16, (unsigned short)0x7C00u);
         _Float16 lbh = inf, lsh = inf;
+        auto key_of = [&](int u, int r) {
+            // (via a scalar: clang's __builtin_bit_cast of an ext_vector element reads element 0)
+            const auto kv = acc[u][r];
+            const int ki = __builtin_bit_cast(int, kv);
+            return keep(u, r) ? __builtin_bit_cast(_Float16, (unsigned short)ki) : inf;
+        };
+        if constexpr (TOP2_PAIRS) {
+            // two keys per step, 3 ops: best' = min3(best, x, y), second' = min(second, med3(best, x, y)) -- the
+            // second smallest of {best <= second, x, y} in every order of the four (a stage's keys are distinct)
 #pragma unroll
-        for (int u = 0; u < NS; u++)
+            for (int u = 0; u < NS; u++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                // (via a scalar: clang's __builtin_bit_cast of an ext_vector element reads element 0)
-                const auto kv = acc[u][r];
-                const int ki = __builtin_bit_cast(int, kv);
-                const _Float16 key = keep(u, r) ? __builtin_bit_cast(_Float16, (unsigned short)ki) : inf;
-                lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
-                lbh = __builtin_fminf16(lbh, key);
-            }
+                for (int r = 0; r < 16; r += 2) {
+                    const _Float16 x = key_of(u, r), y = key_of(u, r + 1);
+                    lsh = __builtin_fminf16(lsh, __builtin_amdgcn_fmed3h(lbh, x, y));
+                    lbh = __builtin_fminf16(__builtin_fminf16(lbh, x), y);
+                }
+        } else {
+#pragma unroll
+            for (int u = 0; u < NS; u++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const _Float16 key = key_of(u, r);
+                    lsh = __builtin_amdgcn_fmed3h(lbh, key, lsh);
+                    lbh = __builtin_fminf16(lbh, key);
+                }
+        }
         lbu = f16_bits(lbh);
         lsu = f16_bits(lsh);
     };
