@@ -729,6 +729,7 @@ hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq
         if (cfg.fp4)
             kern = nw == 4 ? k_top2_mfma<false, 4, 1, false, 0, true>
                            : ns == 2 ? k_top2_mfma<false, 8, 2, false, 0, true> : k_top2_mfma<false, 8, 1, false, 0, true>;
+        if (cfg.fp4 && cfg.pipe && nw == 8 && ns == 1) kern = k_top2_mfma<false, 8, 1, true, 0, true>;   // "8fxp" (A/B)
         hipLaunchKernelGGL(kern, dim3((unsigned)vblocks), dim3(64 * nw), 0, stream, a, d_part, d_best, d_best_idx,
                            d_second, vblocks);
     } else {
