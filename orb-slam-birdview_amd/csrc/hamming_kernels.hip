@@ -651,7 +651,8 @@ if (LA == 0) {
 // '1' / '2' subtiles per stage, 'p' software-pipelined stages, 'P' persistent workgroups (one per slot), 'o' the
 // expansion of the pairs after the first eighth overlapped with the first eighth's top-2 (Top2Overlap), 'l' / 'L' (with 'p') A-fragment
 // reads 2 / 4 MFMAs ahead, 'f' the fp4 form (8 waves, one subtile), 'x' (with 'f') no expansion
-// kernel: each stage's train dwords are expanded while staged (k_top2_mfma<false, ..., FP4>)
+// kernel: each stage's train dwords are expanded while staged (k_top2_mfma<false, ..., FP4>; with 'p' too: "8fxp",
+// 171-173 us against 157-160, profiles/r04/v14_top2_pairs.txt)
 struct Top2Cfg {   // default "8fx": the fp4 form, unpipelined, trains expanded while staged (r04 A/B,
                    // profiles/r04/v9_hamming_ab.txt: 161-162 us; with the expansion kernel 181; pipelined 188; int8 262)
     int waves = 8, stage = 1, la = 0;
