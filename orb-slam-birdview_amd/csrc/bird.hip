@@ -17,7 +17,6 @@
 // with the same library call the OpenCV build makes.
 #include <algorithm>
 #include <cfloat>
-#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -611,16 +610,6 @@ struct Bird {
     BirdCand* d_cand = nullptr;
     size_t cand_cap = 0;
     size_t cand_guess = 16384;      // candidates downloaded with the counts (next frame: this one's + 1/8)
-    // host phase timing (ORBGPU_BIRD_TIMING=1: mean microseconds per call printed every 100 calls)
-    bool timing = std::getenv("ORBGPU_BIRD_TIMING") != nullptr;
-    double tacc[8]{};
-    int tcalls = 0;
-    std::chrono::steady_clock::time_point t0;
-    void tstamp(int k) {
-        if (!timing) return;
-        const auto now = std::chrono::steady_clock::now();
-        tacc[k] += std::chrono::duration<double, std::micro>(now - t0).count();
-    }
     orb_keypoint* d_kps = nullptr;
     int* d_keep = nullptr;
     uint8_t* d_desc = nullptr;
@@ -913,7 +902,6 @@ int Bird::detect_select(bool with_mask, std::vector<HostKP>& sel, int blur_level
                           hipSuccess) ||
             (e = hipStreamSynchronize(stream)) != hipSuccess)
             return set_error("birdview candidate download", e), ORB_ERR_HIP;
-        tstamp(1);
         std::memcpy(last_lvlcnt.data(), hp, nl * sizeof(int));
         size_t total = 0;
         for (int l = 0; l < nl; l++) total += last_lvlcnt[l];
@@ -1083,12 +1071,10 @@ static int bird_run(orb_bird* b, bool with_mask, bool subpix_compute, orb_keypoi
                     uint8_t* desc) {
     int r;
     std::vector<HostKP> sel;
-    if (b->timing) b->t0 = std::chrono::steady_clock::now();
     if ((r = b->build_pyramid(b->g.nlevels, with_mask)) != ORB_OK) return r;
     // the fused call blurs every level while the host selects (compute() would blur max octave + 1 of
     // them; the extra levels are never read)
     if ((r = b->detect_select(with_mask, sel, subpix_compute ? b->g.nlevels : 0)) != ORB_OK) return r;
-    b->tstamp(2);
     const int ns = (int)sel.size();
     if (!subpix_compute && ns > cap) {
         *n = ns;
@@ -1120,15 +1106,7 @@ static int bird_run(orb_bird* b, bool with_mask, bool subpix_compute, orb_keypoi
                (e = hipMemcpyAsync(hp + kb, b->d_keep, fb, hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
                (e = hipMemcpyAsync(hp + kb + fb, b->d_desc, db, hipMemcpyDeviceToHost, b->stream)) != hipSuccess))
         return set_error("birdview result download", e), ORB_ERR_HIP;
-    b->tstamp(3);
     if ((e = hipStreamSynchronize(b->stream)) != hipSuccess) return set_error("birdview sync", e), ORB_ERR_HIP;
-    b->tstamp(4);
-    if (b->timing && ++b->tcalls % 100 == 0) {
-        std::fprintf(stderr, "bird timing (us, cumulative from call start): counts+cands sync %.1f  selection done %.1f  "
-                             "phase-2 issued %.1f  final sync %.1f\n", b->tacc[1] / 100, b->tacc[2] / 100,
-                     b->tacc[3] / 100, b->tacc[4] / 100);
-        for (double& t : b->tacc) t = 0;
-    }
     const orb_keypoint* rk = (const orb_keypoint*)hp;
     const int* keep = (const int*)(hp + kb);
     const uint8_t* rd = hp + kb + fb;

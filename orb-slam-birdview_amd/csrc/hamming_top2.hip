@@ -1,0 +1,296 @@
+// The all-pairs Hamming top-2 on the matrix cores: for every query descriptor of a (query set, train set) pair,
+// the smallest distance, its train index (first on ties) and the second-smallest distance -- the brute-force
+// inner loop of ORBmatcher::SearchByBoW (ORBmatcher.cc:205-226: the strict '<' updates of bestDist1 /
+// bestDist2 over one vocabulary node's features; DescriptorDistance :1647-1663).
+//
+// Distances as an fp4 GEMM.  Descriptor bits become e2m1 values, trains +-4 and queries -+4 (the sign is
+// the bit), so q . t = 16 (#different - #equal) = 32 dist - 4096 exactly, and a 32 x 32 tile of distances over
+// K = 256 bits is four v_mfma_scale_f32_32x32x64_f8f6f4 (both operands e2m1, unit scales: DESIGN.md §4.6).
+// The accumulator starts at 2^23 + 4096 + row, so every result lies in [2^23, 2^24), where an f32's mantissa
+// is the integer itself: the low 16 bits of its bit pattern are the tile-local key dist << 5 | row, a finite
+// positive f16 (< 2^15) ordered like the integer, and the top-2 runs in f16 min / min3 / med3 (built with
+// -fno-honor-nans: no canonicalising ops).
+//
+// This translation unit holds only the top-2 and its merge (the -fno-honor-nans flag stays off the
+// geometry-checking matcher kernels, hamming_kernels.hip).
+#include <algorithm>
+
+#include "orbgpu_internal.h"
+
+namespace orbgpu {
+
+namespace {
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+
+constexpr int kTr = 32;              // trains per stage (MFMA rows)
+constexpr int kChains = 2;           // query fragments per wave: two independent 32-column MFMA chains
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kQb = kWaves * 32 * kChains;   // queries per workgroup (256)
+constexpr int kPitch = 144;          // LDS bytes per expanded train (128 + 16: 36 dwords, so the 16 lanes of a
+                                     // ds_read_b128 group hit 16 distinct 4-bank slots)
+constexpr int kStageBytes = kTr * kPitch;
+constexpr float kSeed = 8388608.f + 4096.f;   // 2^23 + 4096: q . t + seed in [2^23, 2^23 + 8192]
+
+// Descriptor bits -> e2m1 values by byte permutation: output dword j, byte k is tbl[(w >> (8k + 2j)) & 3], the
+// two fp4 values of bits 8k + 2j (low nibble) and 8k + 2j + 1.  Queries and trains share this bit -> element
+// map (the order of K inside an MFMA does not matter when both operands use the same one).
+//   trains:  bit clear -> 0x6 (+4), set -> 0xE (-4):  tbl bytes {66, 6E, E6, EE}
+//   queries: bit clear -> 0xE (-4), set -> 0x6 (+4):  tbl bytes {EE, E6, 6E, 66}
+constexpr uint32_t kTblTrain = 0xEEE66E66u;
+constexpr uint32_t kTblQuery = 0x666EE6EEu;
+
+__device__ __forceinline__ v4i_t expand_fp4(uint32_t w, uint32_t tbl) {
+    constexpr uint32_t m = 0x03030303u;
+    return v4i_t{(int)__builtin_amdgcn_perm(tbl, tbl, w & m), (int)__builtin_amdgcn_perm(tbl, tbl, (w >> 2) & m),
+                 (int)__builtin_amdgcn_perm(tbl, tbl, (w >> 4) & m), (int)__builtin_amdgcn_perm(tbl, tbl, (w >> 6) & m)};
+}
+
+// The 16 key bits of an f16 result, read from the whole register and masked.  hipcc (ROCm 7.2) takes the upper
+// half of a 16-bit VALU result as zero; on gfx950 it keeps whatever the register held (r04: wrong second
+// distances in builds whose allocator had put a 32-bit value there).  The asm hides the assumption.
+__device__ __forceinline__ unsigned f16_bits(_Float16 x) {
+    unsigned r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r & 0xFFFFu;
+}
+__device__ __forceinline__ _Float16 f16_of(unsigned bits) { return __builtin_bit_cast(_Float16, (unsigned short)bits); }
+
+constexpr unsigned kInf16 = 0x7C00u;   // f16 +inf: no key
+
+}  // namespace
+
+/* One workgroup: 256 queries (4 waves x 2 chains x 32) of one pair against one train slice, in stages of 32 trains.
+ * Per stage every thread expands one train descriptor dword (v_perm, no table) into LDS (double-buffered, one
+ * barrier); each wave reads the stage's A fragments once (four ds_read_b128) and issues them against both of its
+ * query fragments (eight MFMAs, two independent accumulator chains).  Each chain's 16 keys per lane go through a
+ * two-stream top-2 (min / min3 / med3), and the stage's (best, second) is merged into the running state in the
+ * same f16 key space: best replaced only when the stage's distance is strictly smaller (an earlier stage wins a
+ * tie), its stage base kept beside it, so the first index wins as the reference's strict '<' does; second =
+ * min3(second, stage second, max(best, stage best)). */
+__global__ __launch_bounds__(kThreads) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
+                                                        int* __restrict__ idx_o, int* __restrict__ second_o) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_t[2][kStageBytes];
+    // 1-D grid of (pair, slice, query block), query block fastest.  Blocks are dealt round-robin over the 8 XCDs
+    // (b and b + 8 share one), so XCD x takes a contiguous run of that sequence: the query blocks of a pair, which
+    // all stream the same trains, share one L2.
+    const int nb = gridDim.x, vb = blockIdx.x, xq = nb >> 3, xr = nb & 7, xcd = vb & 7, xj = vb >> 3;
+    const int lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xj;
+    const int qbi = lb % a.qblocks, rest = lb / a.qblocks;
+    const int sli = rest % a.nslices, p = rest / a.nslices;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
+    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
+    const int qblk = qbi * kQb;
+    if (qblk >= nq) return;   // whole workgroup
+    const int t0 = sli * a.slice, t1 = min(nt, t0 + a.slice);
+    const int h = lane >> 5, c = lane & 31;
+    // B operands: chain u's column c is query qblk + 64 wv + 32 u + c; K-step s = descriptor dwords 2s, 2s + 1,
+    // lane half h = dword 2s + h (the A fragments below read the same dword of the train)
+    v4i_t qf[kChains][4];
+#pragma unroll
+    for (int u = 0; u < kChains; u++) {
+        const int qi = qblk + 64 * wv + 32 * u + c;
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+        if (qi < nq) {
+            const uint4* qp = reinterpret_cast<const uint4*>(a.q + ((long long)fr.x * a.q_stride + qi) * 32);
+            q0 = qp[0];
+            q1 = qp[1];
+        }
+        const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        const uint32_t hm = h ? 0xFFFFFFFFu : 0u;   // (a select, not qd[2 s + h]: a dynamic index goes to scratch)
+#pragma unroll
+        for (int s = 0; s < 4; s++) qf[u][s] = expand_fp4(qd[2 * s] ^ ((qd[2 * s] ^ qd[2 * s + 1]) & hm), kTblQuery);
+    }
+    // the slice's packed trains through a buffer descriptor (base and size in SGPRs): rows past t1 read as 0 (their
+    // keys are masked), so the last stage needs no clamp (the stage offset goes in voffset: soffset is not
+    // range-checked)
+    const uint64_t tbase = reinterpret_cast<uint64_t>(a.t + ((long long)fr.y * a.t_stride + t0) * 32);
+    const auto TR = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(tbase >> 32)) << 32) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)tbase)),
+        0, max(t1 - t0, 0) * 32, 0x00020000);
+    // staging: thread -> stage row tid >> 3, descriptor dword tid & 7 (16 expanded bytes)
+    const int soff = (tid >> 3) * kPitch + (tid & 7) * 16;
+    auto fetch = [&](int j) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b32(TR, tid * 4 + j * (kTr * 32), 0, 0);
+    };
+    auto stage = [&](int buf, uint32_t w) {
+        *reinterpret_cast<v4i_t*>(&s_t[buf][soff]) = expand_fp4(w, kTblTrain);
+    };
+    // accumulator seed: 2^23 + 4096 + row, row = the accumulator element's train row in the tile
+    v16f_t seed;
+#pragma unroll
+    for (int r = 0; r < 16; r++) seed[r] = kSeed + (float)((r & 3) + 8 * (r >> 2) + 4 * h);
+    // running state per chain: best key (f16 bits dist << 5 | row), its stage base, second key
+    _Float16 rb[kChains], rs[kChains];
+    int rst[kChains];
+#pragma unroll
+    for (int u = 0; u < kChains; u++) {
+        rb[u] = f16_of(kInf16);
+        rs[u] = f16_of(kInf16);
+        rst[u] = 0;
+    }
+    // a chain's stage top-2 in two independent streams (rows r = 0..7 and 8..15, keys taken in pairs), merged,
+    // then folded into the running state
+    auto top2 = [&](const v16f_t& acc, int u, int tb, auto keep) {
+        auto key = [&](int r) {
+            const float kv = acc[r];   // (via a scalar: clang's bit_cast of an ext_vector element reads element 0)
+            const int ki = __builtin_bit_cast(int, kv);
+            return keep(r) ? __builtin_bit_cast(_Float16, (unsigned short)ki) : f16_of(kInf16);
+        };
+        _Float16 b2[2], s2[2];
+#pragma unroll
+        for (int st = 0; st < 2; st++) {
+            const _Float16 x0 = key(8 * st), x1 = key(8 * st + 1);
+            b2[st] = __builtin_fminf16(x0, x1);
+            s2[st] = __builtin_fmaxf16(x0, x1);
+#pragma unroll
+            for (int r = 8 * st + 2; r < 8 * st + 8; r += 2) {
+                // second smallest of {best <= second, x, y}: min(second, med3(best, x, y)) (a stage's keys are distinct)
+                const _Float16 x = key(r), y = key(r + 1);
+                s2[st] = __builtin_fminf16(s2[st], __builtin_amdgcn_fmed3h(b2[st], x, y));
+                b2[st] = __builtin_fminf16(__builtin_fminf16(b2[st], x), y);
+            }
+        }
+        const _Float16 sb = __builtin_fminf16(b2[0], b2[1]);
+        const _Float16 ss = __builtin_fminf16(__builtin_fminf16(s2[0], s2[1]), __builtin_fmaxf16(b2[0], b2[1]));
+        // running merge: the stage's best replaces the running one only at a strictly smaller distance (its key
+        // below the running key with the row bits cleared)
+        const bool take = sb < f16_of(f16_bits(rb[u]) & 0xFFE0u);
+        rs[u] = __builtin_fminf16(__builtin_fminf16(rs[u], ss), __builtin_fmaxf16(rb[u], sb));
+        rb[u] = take ? sb : rb[u];
+        rst[u] = take ? tb : rst[u];
+    };
+    const int nst = t1 > t0 ? (t1 - t0 + kTr - 1) / kTr : 0;   // stages (uniform)
+    if (nst > 0) {
+        stage(0, fetch(0));
+        __syncthreads();
+        for (int j = 0; j < nst; j++) {
+            const int tb = t0 + kTr * j;
+            const bool more = j + 1 < nst;
+            uint32_t wn = 0;
+            if (more) wn = fetch(j + 1);   // the next stage's dword: its latency under this stage
+            const uint8_t* A = &s_t[j & 1][c * kPitch + 16 * h];
+            v16f_t acc[kChains];
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+                const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
+#pragma unroll
+                for (int u = 0; u < kChains; u++) {
+                    const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
+                    // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
+                    acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, s == 0 ? seed : acc[u], 4, 4, 0,
+                                                                             0, 0, 0);
+                }
+            }
+            if (tb + kTr <= t1) {
+#pragma unroll
+                for (int u = 0; u < kChains; u++) top2(acc[u], u, tb, [](int) { return true; });
+            } else {   // the slice's last stage, partial: rows at or past t1 hold no train
+#pragma unroll
+                for (int u = 0; u < kChains; u++)
+                    top2(acc[u], u, tb, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
+            }
+            if (more) stage((j + 1) & 1, wn);
+            __syncthreads();
+        }
+    }
+    // per chain: running keys -> dist << 16 | train index; the two lane halves hold different train rows of the
+    // same query
+#pragma unroll
+    for (int u = 0; u < kChains; u++) {
+        const unsigned kb = f16_bits(rb[u]), ks = f16_bits(rs[u]);
+        unsigned b = kb == kInf16 ? 0xFFFFFFFFu : ((kb >> 5) << 16) | (unsigned)(rst[u] + (int)(kb & 31u));
+        // the second's index is never output: dist << 16 | 0xFFFF orders it after any equal best
+        unsigned s2 = ks == kInf16 ? 0xFFFFFFFFu : ((ks >> 5) << 16) | 0xFFFFu;
+        const unsigned ob = __shfl_xor(b, 32), os = __shfl_xor(s2, 32);
+        s2 = min(min(s2, os), max(b, ob));
+        b = min(b, ob);
+        const int qi = qblk + 64 * wv + 32 * u + c;
+        if (h == 0 && qi < nq) {
+            const long long o = (long long)p * a.out_stride + qi;
+            if (a.nslices == 1) {
+                best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
+                idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
+                second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
+            } else {
+                part[((long long)p * a.nslices + sli) * a.out_stride + qi] = make_uint2(b, s2);
+            }
+        }
+    }
+}
+
+/* Slices of one (query set, train set) pair's top-2 (k_top2_mfma with nslices > 1) are merged here: keys
+ * dist << 16 | train index compose by min (first index on ties) and second = the second-smallest key.  Counts
+ * may be read on the device (an extraction batch's d_counts), so a whole batch of frame pairs needs no host round
+ * trip. */
+__global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, const uint2* __restrict__ part,
+                                                     int* __restrict__ best_o, int* __restrict__ idx_o,
+                                                     int* __restrict__ second_o) {
+    const int p = blockIdx.y;
+    const int2 fr = a.frames ? a.frames[p] : make_int2(0, 0);
+    const int nq = a.counts ? a.counts[fr.x] : a.nq, nt = a.counts ? a.counts[fr.y] : a.nt;
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    if (qi >= nq) return;
+    const int used = min(nslices, (nt + a.slice - 1) / a.slice);   // slices past nt were never written
+    unsigned b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
+    for (int s = 0; s < used; s++) {
+        const uint2 v = part[((long long)p * nslices + s) * a.out_stride + qi];
+        s2 = min(min(s2, v.y), max(b, v.x));
+        b = min(b, v.x);
+    }
+    const long long o = (long long)p * a.out_stride + qi;
+    best_o[o] = b == 0xFFFFFFFFu ? 257 : (int)(b >> 16);
+    idx_o[o] = b == 0xFFFFFFFFu ? -1 : (int)(b & 0xFFFF);
+    second_o[o] = s2 == 0xFFFFFFFFu ? 257 : (int)(s2 >> 16);
+}
+
+// Train slices: a launch aims at >= kTargetBlocks workgroups (two rounds of four per CU); slices are whole 32-train
+// stages of >= 64 trains.  top2_batch_slices is the partial buffer's capacity (the callers size it), the launch
+// uses top2_launch_slices <= that many.  (max_nt == 0: one empty slice of one stage, nothing divides by zero.)
+constexpr int kTargetBlocks = 2048;
+int top2_batch_slices(int npairs, int max_nq, int max_nt) {
+    npairs = std::max(npairs, 1);
+    const int qb = std::max(1, (max_nq + kQb - 1) / kQb);
+    int ns = (kTargetBlocks + npairs * qb - 1) / (npairs * qb);
+    ns = std::min(ns, std::max(1, (max_nt + 63) / 64));
+    return std::max(ns, 1);
+}
+
+static int top2_slice_len(int npairs, int max_nq, int max_nt) {
+    const int ns = top2_batch_slices(npairs, max_nq, max_nt);
+    return std::max(((max_nt + ns - 1) / ns + kTr - 1) / kTr * kTr, kTr);
+}
+
+int top2_launch_slices(int npairs, int max_nq, int max_nt) {
+    if (npairs <= 0 || max_nq <= 0 || max_nt < 0) return 0;
+    const int len = top2_slice_len(npairs, max_nq, max_nt);
+    return std::max(1, (max_nt + len - 1) / len);
+}
+
+hipError_t launch_hamming_top2_batch(const Top2Batch& a0, int npairs, int max_nq, int max_nt, int* d_best,
+                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream) {
+    if (npairs <= 0 || max_nq <= 0) return hipSuccess;
+    if (max_nt > 65535) return hipErrorInvalidValue;   // keys hold a 16-bit train index
+    Top2Batch a = a0;
+    a.slice = top2_slice_len(npairs, max_nq, max_nt);
+    const int nsu = std::max(1, (max_nt + a.slice - 1) / a.slice);   // 1: k_top2_mfma writes the outputs itself
+    a.qblocks = (max_nq + kQb - 1) / kQb;
+    a.nslices = nsu;
+    const long long blocks = (long long)a.qblocks * nsu * npairs;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    // (max_nt == 0, e.g. a previous frame without keypoints: k_top2_mfma sees no stage and writes the sentinels)
+    hipLaunchKernelGGL(k_top2_mfma, dim3((unsigned)blocks), dim3(kThreads), 0, stream, a, d_part, d_best, d_best_idx,
+                       d_second);
+    if (nsu > 1)
+        hipLaunchKernelGGL(k_top2b_merge, dim3((max_nq + 255) / 256, npairs), dim3(256), 0, stream, a, nsu, d_part,
+                           d_best, d_best_idx, d_second);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

@@ -245,7 +245,7 @@ int orb_hamming_top2_slices(int npairs, int max_nq, int max_nt) {
     return orbgpu::top2_launch_slices(npairs, max_nq, max_nt);
 }
 
-int orb_hamming_top2_mfma_bits(void) { return orbgpu::top2_fp4_enabled() ? 4 : 8; }
+int orb_hamming_top2_mfma_bits(void) { return 4; }   // the e2m1 form is the only one (hamming_top2.hip)
 
 int orb_hamming_topk(orb_ctx* h, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_off,
                      const int* cand_idx, const int* train_thr, int k, int* out_dist, int* out_idx, int* out_nvalid) {
@@ -304,13 +304,10 @@ int orb_hamming_top2_device(orb_ctx* h, const uint8_t* d_q, int nq, const uint8_
     if (nt > 65535) return set_error("orb_hamming_top2_device: more than 65535 trains", hipSuccess), ORB_ERR_ARG;
     Arena a{c};
     const int ns = top2_batch_slices(1, nq, nt);
-    const bool exp = top2_needs_expansion();
-    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(uint2)) + Arena::align(exp ? (size_t)nt * 256 : 1) + 512);
+    hipError_t e = a.reserve(Arena::align((size_t)ns * nq * sizeof(uint2)) + 512);
     if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
     uint2* part = a.take<uint2>((size_t)ns * nq);
-    // trains expanded once (k_expand_pm1 / k_expand_fp4) when the configured form reads them pre-expanded
-    uint8_t* tx = exp ? a.take<uint8_t>((size_t)nt * 256) : nullptr;
-    Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq, tx, nt, nullptr, nullptr, 0};
+    Top2Batch tb{d_q, d_t, 0, 0, nullptr, nq, nt, nullptr, 0, nq, 0, 0};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
     e = launch_hamming_top2_batch(tb, 1, nq, nt, d_best, d_best_idx, d_second, part, c->stream);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
@@ -329,97 +326,70 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     for (int p = 0; p < npairs; p++)
         if (q_frames[p] < 0 || t_frames[p] < 0)
             return set_error("orb_hamming_top2_frames_device: negative frame index", hipSuccess), ORB_ERR_ARG;
-    // each distinct train frame is expanded to +-1 once (consecutive-frame pairs share their frames), so the
-    // expansion scratch grows with the distinct frames, not with the pairs
-    // [pairs (q, t) | slot per pair | train frame per slot], assembled on the host, one upload from a pinned slot
-    std::vector<int>& up = c->pairs_upload_host;
-    up.assign((size_t)npairs * 3, 0);
-    {
-        std::vector<std::pair<int, int>> order(npairs);
-        for (int p = 0; p < npairs; p++) order[p] = {t_frames[p], p};
-        std::sort(order.begin(), order.end());
-        int nsl = 0;
-        for (int i = 0; i < npairs; i++) {
-            if (i == 0 || order[i].first != order[i - 1].first) {
-                up.push_back(order[i].first);
-                nsl++;
-            }
-            up[(size_t)2 * npairs + order[i].second] = nsl - 1;
-        }
+    hipError_t e;
+    // the pair list (q, t per pair) lives in its own device buffer and goes up only when it differs from the
+    // previous call's: a caller that matches the same frame slots every batch (the bench, a tracking loop over a
+    // ring of slots) pays no copy and no host wait per call.  A changed list is stream-ordered behind the launches
+    // that still read the old one.
+    bool same = (int)c->pairs_last.size() == 2 * npairs && c->d_pairs;
+    for (int p = 0; p < npairs && same; p++)
+        same = c->pairs_last[2 * p] == q_frames[p] && c->pairs_last[2 * p + 1] == t_frames[p];
+    if (!same) {
+        c->pairs_last.resize((size_t)2 * npairs);
         for (int p = 0; p < npairs; p++) {
-            up[2 * p] = q_frames[p];
-            up[2 * p + 1] = t_frames[p];
+            c->pairs_last[2 * p] = q_frames[p];
+            c->pairs_last[2 * p + 1] = t_frames[p];
         }
-    }
-    const int nslots = (int)up.size() - 3 * npairs;
-    Arena a{c};
-    const int ns = top2_batch_slices(npairs, kp_cap, kp_cap);
-    const bool exp = top2_needs_expansion();
-    hipError_t e = a.reserve(Arena::align(up.size() * 4) + Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) +
-                             Arena::align(exp ? (size_t)nslots * kp_cap * 256 : 1) + 768);
-    if (e != hipSuccess) return set_error("scratch", e), ORB_ERR_NOMEM;
-    int* d_up = a.take<int>(up.size());
-    uint2* part = a.take<uint2>((size_t)npairs * ns * kp_cap);
-    // each distinct train frame expanded once, when the configured form reads pre-expanded trains
-    uint8_t* tx = exp ? a.take<uint8_t>((size_t)nslots * kp_cap * 256) : nullptr;
-    {   // the pinned slot this call uploads from: its previous upload (two calls ago) must have been read
+        const size_t bytes = (size_t)npairs * sizeof(int2);
+        if (bytes > c->dpairs_cap || !c->d_pairs) {
+            if (c->d_pairs) {
+                // (a launch queued earlier may still read the old buffer)
+                if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
+                (void)hipFree(c->d_pairs);
+            }
+            c->d_pairs = nullptr;
+            c->dpairs_cap = 0;
+            if ((e = hipMalloc((void**)&c->d_pairs, std::max<size_t>(bytes, 4096))) != hipSuccess) {
+                c->pairs_last.clear();
+                return set_error("hipMalloc pairs", e), ORB_ERR_NOMEM;
+            }
+            c->dpairs_cap = std::max<size_t>(bytes, 4096);
+        }
+        // staged through two pinned slots used in turn: a slot is rewritten only after the event recorded behind
+        // its previous upload has completed (the call returns before its copy runs)
         const int sl = c->pairs_slot;
         c->pairs_slot ^= 1;
         if (c->pairs_ev[sl] && (e = hipEventSynchronize(c->pairs_ev[sl])) != hipSuccess)
             return set_error("pairs staging event", e), ORB_ERR_HIP;
         if (!c->pairs_ev[sl] && (e = hipEventCreateWithFlags(&c->pairs_ev[sl], hipEventDisableTiming)) != hipSuccess)
             return set_error("pairs staging event", e), ORB_ERR_HIP;
-        if (up.size() * 4 > c->pairs_cap[sl]) {
+        if (bytes > c->pairs_cap[sl]) {
             if (c->h_pairs[sl]) (void)hipHostFree(c->h_pairs[sl]);
             c->h_pairs[sl] = nullptr;
             c->pairs_cap[sl] = 0;
-            const size_t cap = std::max<size_t>(up.size() * 4, 4096);
-            if ((e = hipHostMalloc((void**)&c->h_pairs[sl], cap, hipHostMallocDefault)) != hipSuccess)
+            const size_t cap = std::max<size_t>(bytes, 4096);
+            if ((e = hipHostMalloc((void**)&c->h_pairs[sl], cap, hipHostMallocDefault)) != hipSuccess) {
+                c->pairs_last.clear();
                 return set_error("pairs pinned staging", e), ORB_ERR_NOMEM;
+            }
             c->pairs_cap[sl] = cap;
         }
-        std::memcpy(c->h_pairs[sl], up.data(), up.size() * 4);
-        if ((e = hipMemcpyAsync(d_up, c->h_pairs[sl], up.size() * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        std::memcpy(c->h_pairs[sl], c->pairs_last.data(), bytes);
+        if ((e = hipMemcpyAsync(c->d_pairs, c->h_pairs[sl], bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+            (e = hipEventRecord(c->pairs_ev[sl], c->stream)) != hipSuccess) {
+            c->pairs_last.clear();
             return set_error("upload pairs", e), ORB_ERR_HIP;
-        if ((e = hipEventRecord(c->pairs_ev[sl], c->stream)) != hipSuccess)
-            return set_error("pairs staging event", e), ORB_ERR_HIP;
-    }
-    const int2* d_frames = reinterpret_cast<const int2*>(d_up);
-    Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, d_frames, 0, kp_cap, tx, kp_cap,
-                 d_up + 2 * npairs, d_up + 3 * npairs, nslots};
-    // overlap plan: chunks of one persistent round of query blocks each (pairs' slots non-decreasing, one
-    // train slice), up to kTop2MaxChunks; chunk c's expansion runs on the second stream beside chunk c-1's top-2
-    Top2Overlap ov{};
-    const Top2Overlap* ovp = nullptr;
-    if (top2_overlap_enabled() && top2_launch_slices(npairs, kp_cap, kp_cap) == 1 && npairs >= 32) {
-        bool mono = true;
-        for (int p = 1; p < npairs && mono; p++) mono = up[(size_t)2 * npairs + p] >= up[(size_t)2 * npairs + p - 1];
-        // two chunks, the first small: only its expansion runs alone, the second's (7/8 of the pairs) runs beside
-        // the first's top-2, and the second's top-2 has a full grid (r04: eight equal chunks measured 28 % slower,
-        // each chunk's grid too small to fill the chip, profiles/r04/v2_hamming_ab.txt)
-        const int first = std::max(8, npairs / 8);
-        const int nch = first < npairs ? 2 : 1;
-        if (mono && nch > 1) {
-            if (!c->stream2 && (e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess)
-                return set_error("second stream", e), ORB_ERR_HIP;
-            for (hipEvent_t& ev : c->ham_ev)
-                if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess)
-                    return set_error("top-2 events", e), ORB_ERR_HIP;
-            ov.s2 = c->stream2;
-            ov.ev_fork = c->ham_ev[kTop2MaxChunks];
-            ov.nchunks = nch;
-            ov.pair_beg[0] = 0;
-            ov.pair_beg[1] = first;
-            ov.pair_beg[2] = npairs;
-            for (int k = 0; k < nch; k++) {
-                ov.ev[k] = c->ham_ev[k];
-                ov.slot_end[k] = up[(size_t)2 * npairs + ov.pair_beg[k + 1] - 1] + 1;
-            }
-            ovp = &ov;
         }
     }
+    Arena a{c};
+    const int ns = top2_batch_slices(npairs, kp_cap, kp_cap);
+    if ((e = a.reserve(Arena::align((size_t)npairs * ns * kp_cap * sizeof(uint2)) + 512)) != hipSuccess)
+        return set_error("scratch", e), ORB_ERR_NOMEM;
+    uint2* part = a.take<uint2>((size_t)npairs * ns * kp_cap);
+    Top2Batch tb{d_desc, d_desc, kp_cap, kp_cap, d_counts, 0, 0, reinterpret_cast<const int2*>(c->d_pairs), 0, kp_cap,
+                 0, 0};
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-    e = launch_hamming_top2_batch(tb, npairs, kp_cap, kp_cap, d_best, d_best_idx, d_second, part, c->stream, ovp);
+    e = launch_hamming_top2_batch(tb, npairs, kp_cap, kp_cap, d_best, d_best_idx, d_second, part, c->stream);
     if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
     return e == hipSuccess ? ORB_OK : (set_error("top2 kernel", e), ORB_ERR_HIP);
 }

@@ -345,7 +345,6 @@ ExtractBuffers Ctx::buffers() const {
     std::memcpy(b.rcoef_off, rcoef_off, sizeof rcoef_off);
     b.d_chain = d_chain;
     b.chain = chain;
-    if (no_chain) b.chain.nseg = 0;
     b.d_pyr = d_pyr;
     b.d_cands = d_cands;
     b.d_candFirst = d_candFirst;
@@ -381,9 +380,8 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     // the few-launch pyramid trades redundant work for fewer dependent launches: it pays for one frame
     // in flight (the host path), not when several batches share the GPU (measured)
     if (!latency) bufs.chain.nseg = 0;
-    // one frame in flight: level 0's FAST -> octree on a second stream beside the pyramid
-    // (ORBGPU_FORK_BATCH=1: also small batches, captured into the graph as two branches; an A/B switch)
-    if ((latency || (fork_batch && nframes <= 8)) && fork && !prof_on && !fast_stamps && geom.nlevels > 1) {
+    // one frame in flight (ORBGPU_FORK=1): level 0's FAST -> octree on a second stream beside the pyramid
+    if (latency && fork && !prof_on && !fast_stamps && geom.nlevels > 1) {
         hipError_t fe = hipSuccess;
         if (!stream2 && (fe = hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking)) != hipSuccess)
             return set_error("second stream", fe), ORB_ERR_HIP;
@@ -504,15 +502,11 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     // diagnostics only (tests/test_gpu_extract.py checks both leave the results unchanged):
     // ORBGPU_FAST_STAMPS=1 records kernel phase timestamps, ORBGPU_GRAPH=0 launches without graph replay
     if (const char* e = std::getenv("ORBGPU_FAST_STAMPS")) c->fast_stamps = e[0] == '1';
-    // ORBGPU_NO_CHAIN=1: small batches take the per-level pyramid launches (A/B diagnostic; same results)
-    if (const char* e = std::getenv("ORBGPU_NO_CHAIN")) c->no_chain = e[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_GRAPH")) c->use_graph = ev[0] != '0';
     // ORBGPU_STEREO_STAGE=1: orb_compute_stereo_matches stages the right side as for a peer device
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_FORK")) c->fork = ev[0] != '0';
     if (const char* ev = std::getenv("ORBGPU_UPLOAD")) c->upload_stream = ev[0] != '0';
-    if (const char* ev = std::getenv("ORBGPU_FORK_BATCH")) c->fork_batch = ev[0] == '1';
-    if (const char* ev = std::getenv("ORBGPU_MATCH_ZC")) c->match_zc = (ev[0] >= '0' && ev[0] <= '2') ? ev[0] - '0' : -1;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);
@@ -548,12 +542,11 @@ void orb_destroy(orb_ctx* h) {
     }
     void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in,
-                    c->d_scratch, c->d_peer};
+                    c->d_scratch, c->d_peer, c->d_pairs};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_mstage) (void)hipHostFree(c->h_mstage);
-    if (c->h_min) (void)hipHostFree(c->h_min);
     if (c->h_img) (void)hipHostFree(c->h_img);
     if (c->h_flags) (void)hipHostFree(c->h_flags);
     for (int i = 0; i < 2; i++) {
@@ -566,8 +559,6 @@ void orb_destroy(orb_ctx* h) {
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    for (hipEvent_t ev : c->ham_ev)
-        if (ev) (void)hipEventDestroy(ev);
     delete c;
 }
 

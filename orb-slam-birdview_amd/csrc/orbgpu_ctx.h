@@ -23,17 +23,14 @@ struct Ctx {
     int num_cu = 256;
     bool fast_stamps = false;     // ORBGPU_FAST_STAMPS=1: the kernels record phase timestamps (diagnostic)
     bool stereo_stage = false;    // ORBGPU_STEREO_STAGE=1: stereo stages the right side as for a peer GPU (test)
-    bool no_chain = false;        // ORBGPU_NO_CHAIN=1: no one-launch pyramid for small batches (A/B diagnostic)
     unsigned long long* d_stamps = nullptr;
     size_t stamps_cap = 0;
     hipStream_t stream = nullptr;
     // the host path's second stream and fork / join events (Ctx::run_extract latency mode; ORBGPU_FORK=1: on.  Off by
     // default: 0.1154-0.1198 ms per C3 frame forked against 0.1074 ms in one stream, profiles/r04/v3_host_path.txt)
     bool fork = false;
-    bool fork_batch = false;   // ORBGPU_FORK_BATCH=1: batches of <= 8 frames fork too (graph branches)
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    hipEvent_t ham_ev[kTop2MaxChunks + 1] = {};   // the overlapped batched top-2: fork + one per chunk
 
     // ORBextractor tables (ORBextractor.cc:410-470)
     float scale[ORBGPU_MAX_LEVELS]{}, inv_scale[ORBGPU_MAX_LEVELS]{}, sigma2[ORBGPU_MAX_LEVELS]{},
@@ -90,14 +87,16 @@ struct Ctx {
     void* h_pinned = nullptr;
     size_t pinned_cap = 0;
 
-    std::vector<int> pairs_upload_host;   // orb_hamming_top2_frames_device: pair lists / slots assembled here
     // orb_search_for_triangulation's host lists, kept across calls (capacity reused: a call is ~30 us, and its
     // dozens of small allocations were a measurable part of it); tri_tmap stays all -1 between calls
     std::vector<int> tri_item_q, tri_cand, tri_train_of, tri_tmap, tri_best, tri_match;
     std::vector<int2> tri_rng;
     std::vector<int> tri_hist[30];
-    // ... and staged through two pinned slots used in turn: a slot is rewritten only after the event recorded
-    // behind its previous upload has completed (the call returns before its copy runs)
+    // orb_hamming_top2_frames_device: the pair list on the device (re-uploaded only when it changes), the list it
+    // holds, and two pinned staging slots used in turn
+    int* d_pairs = nullptr;
+    size_t dpairs_cap = 0;
+    std::vector<int> pairs_last;
     int* h_pairs[2] = {nullptr, nullptr};
     size_t pairs_cap[2] = {0, 0};
     hipEvent_t pairs_ev[2] = {nullptr, nullptr};
@@ -109,13 +108,6 @@ struct Ctx {
     // in one DMA, its outputs come back in one (matcher.hip Stage)
     uint8_t* h_mstage = nullptr;
     size_t mstage_cap = 0;
-    // ORBGPU_MATCH_ZC (A/B switch; unset = each call's measured choice, Stage::zc): 0 = a call's inputs go up in
-    // one DMA into d_scratch; 1 = the kernels read them straight from the (coherent) pinned mirror, no DMA; 2 =
-    // the same from a second, non-coherent (GPU-cacheable) pinned mirror h_min.  Outputs are always stored into
-    // h_mstage.
-    int match_zc = -1;
-    uint8_t* h_min = nullptr;
-    size_t min_cap = 0;
     // the right extractor's frame + pyramid when it runs on another GPU (orb_compute_stereo_matches)
     uint8_t* d_peer = nullptr;
     size_t peer_cap = 0;
@@ -180,32 +172,36 @@ struct Arena {
 
 // A host call's device arena and its pinned host mirror (Ctx::h_mstage): regions are laid out once
 // with add(), inputs are written into the mirror at the device offsets, one DMA takes the input span up
-// and one brings the output span back (per-call latency: a pageable copy per array cost ~10 us each).
+// (or the kernels read the mirror itself, zc = 1), and the kernels store their outputs straight into the mirror
+// (host-coherent), so nothing is downloaded.  Regions added after end_mirror() are device-only working space:
+// the pinned mirror is not sized for them.
 struct Stage {
     Ctx* c;
     size_t off = 0;
-    // the call's input mode when ORBGPU_MATCH_ZC is unset (see Ctx::match_zc).  r04 per call (profiles/r04/
-    // v3_matcher_zc.txt): the single-kernel calls with small inputs (SearchForTriangulation, ComputeBoW) gain from
-    // reading the pinned mirror (no DMA before the kernel); the searches whose kernels re-read their inputs many
-    // times (the BoW searches, the window search: every candidate's descriptor; stereo) lose, so they keep the DMA
+    size_t mirror_end = 0;   // 0: every region has a host mirror
+    // the call's input mode.  r04 per call (profiles/r04/v3_matcher_zc.txt): the single-kernel calls with small
+    // inputs (SearchForTriangulation, ComputeBoW) gain from reading the pinned mirror (zc = 1: no DMA before the
+    // kernel); the searches whose kernels re-read their inputs many times (the BoW searches, the window search:
+    // every candidate's descriptor; stereo) lose, so they keep the DMA (zc = 0)
     int zc = 0;
-    int mode() const { return c->match_zc >= 0 ? c->match_zc : zc; }
     size_t add(size_t bytes) {
         off = Arena::align(off);
         const size_t o = off;
         off += std::max<size_t>(bytes, 1);
         return o;
     }
+    void end_mirror() { mirror_end = Arena::align(off); }
     int alloc() {
         const size_t need = Arena::align(off) + 4096;
         Arena a{c};
         hipError_t e = a.reserve(need);
         if (e != hipSuccess) return set_error("matcher scratch", e), ORB_ERR_NOMEM;
-        if (need > c->mstage_cap || !c->h_mstage) {
+        const size_t hneed = (mirror_end ? mirror_end : Arena::align(off)) + 4096;
+        if (hneed > c->mstage_cap || !c->h_mstage) {
             if (c->h_mstage) (void)hipHostFree(c->h_mstage);
             c->h_mstage = nullptr;
             c->mstage_cap = 0;
-            const size_t cap = std::max<size_t>(need, 1 << 20);
+            const size_t cap = std::max<size_t>(hneed, 1 << 20);
             // mapped + coherent explicitly: the matcher kernels store their results straight into this mirror
             // and the host reads them after the stream synchronisation, with no D2H copy
             if ((e = hipHostMalloc((void**)&c->h_mstage, cap, hipHostMallocMapped | hipHostMallocCoherent)) !=
@@ -213,31 +209,20 @@ struct Stage {
                 return set_error("matcher pinned staging", e), ORB_ERR_NOMEM;
             c->mstage_cap = cap;
         }
-        if (mode() == 2 && (need > c->min_cap || !c->h_min)) {
-            if (c->h_min) (void)hipHostFree(c->h_min);
-            c->h_min = nullptr;
-            c->min_cap = 0;
-            const size_t cap = std::max<size_t>(need, 1 << 20);
-            if ((e = hipHostMalloc((void**)&c->h_min, cap, hipHostMallocMapped | hipHostMallocNonCoherent)) !=
-                hipSuccess)
-                return set_error("matcher pinned input mirror", e), ORB_ERR_NOMEM;
-            c->min_cap = cap;
-        }
         return ORB_OK;
     }
     template <class T>
     T* h(size_t o) const { return reinterpret_cast<T*>(c->h_mstage + o); }   // outputs (host view)
     template <class T>
     T* d(size_t o) const { return reinterpret_cast<T*>(c->d_scratch + o); }
-    uint8_t* in_base() const { return mode() == 2 ? c->h_min : c->h_mstage; }
     template <class T>
-    T* hi(size_t o) const { return reinterpret_cast<T*>(in_base() + o); }   // inputs, written by the host
+    T* hi(size_t o) const { return reinterpret_cast<T*>(c->h_mstage + o); }   // inputs, written by the host
     template <class T>
     T* di(size_t o) const {   // inputs, as the kernels read them
-        return mode() ? reinterpret_cast<T*>(in_base() + o) : d<T>(o);
+        return zc ? reinterpret_cast<T*>(c->h_mstage + o) : d<T>(o);
     }
     hipError_t up(size_t from, size_t to) const {
-        if (mode()) return hipSuccess;   // the kernels read the pinned mirror itself
+        if (zc) return hipSuccess;   // the kernels read the pinned mirror itself
         return to > from ? hipMemcpyAsync(c->d_scratch + from, c->h_mstage + from, to - from, hipMemcpyHostToDevice,
                                           c->stream)
                          : hipSuccess;

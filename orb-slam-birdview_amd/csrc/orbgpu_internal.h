@@ -127,7 +127,7 @@ struct RcoefOff {   // per-level offsets into the coefficient table (a kernel ar
     int o[ORBGPU_MAX_LEVELS];
 };   // batches up to this many frames take the one-launch pyramid
 
-// Kernel launchers (extract_kernels.hip / hamming_kernels.hip).
+// Kernel launchers (extract_kernels.hip / hamming_kernels.hip / hamming_top2.hip).
 struct ExtractBuffers {
     const Geom* d_geom;
     const ResizeCoef* d_rcoef;     // per level: w_l x-coefs then h_l y-coefs, at rcoef_off[l]
@@ -166,8 +166,8 @@ hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, i
                                int* d_nvalid, hipStream_t stream);
 
 
-// Batched all-pairs top-2 (k_expand_pm1 + k_top2_mfma): pair p = (query frame frames[p].x, train frame frames[p].y)
-// of descriptor arrays q / t with q_stride / t_stride descriptors per frame; counts[frame] on the
+// Batched all-pairs top-2 (k_top2_mfma, hamming_top2.hip): pair p = (query frame frames[p].x, train frame
+// frames[p].y) of descriptor arrays q / t with q_stride / t_stride descriptors per frame; counts[frame] on the
 // device, or nq / nt for every pair when counts == NULL (frames == NULL: one pair, frame 0).
 struct Top2Batch {
     const uint8_t* q;
@@ -178,39 +178,13 @@ struct Top2Batch {
     const int2* frames;
     int slice;
     long long out_stride;   // outputs / partials of pair p at p * out_stride + query
-    // trains already expanded to +-1 int8 (256 B each; pair p's at tx + slot * tx_stride * 256 with
-    // slot = tx_slot[p], or p when tx_slot is NULL), or NULL: k_top2_mfma then expands every train tile
-    // itself.  tx_frames (n_tx_frames entries): the train frame of each slot, so that a frame shared by
-    // several pairs is expanded once (NULL: one slot per pair, frames[p].y)
-    const uint8_t* tx;
-    long long tx_stride;
-    const int* tx_slot;
-    const int* tx_frames;
-    int n_tx_frames;
     // set by launch_hamming_top2_batch: query blocks per pair and train slices per pair of the 1-D grid
     int qblocks, nslices;
 };
 int top2_batch_slices(int npairs, int max_nq, int max_nt);   // partial buffer: npairs * slices * out_stride uint2
 int top2_launch_slices(int npairs, int max_nq, int max_nt);   // slices one launch uses (1 = direct write)
-// Overlapped form of the batched top-2: pairs [pair_beg[c], pair_beg[c + 1]) use expansion slots below
-// slot_end[c] (slots non-decreasing over the pairs); chunk c's slots are expanded on s2 (event ev[c]) while the
-// launch stream runs chunk c - 1's top-2.  Only with one train slice.
-constexpr int kTop2MaxChunks = 8;
-struct Top2Overlap {
-    hipStream_t s2;
-    hipEvent_t ev_fork;
-    hipEvent_t ev[kTop2MaxChunks];
-    int nchunks;
-    int pair_beg[kTop2MaxChunks + 1];
-    int slot_end[kTop2MaxChunks];
-};
-bool top2_overlap_enabled();
-bool top2_fp4_enabled();   // ORBGPU_TOP2 'f': the e2m1 MFMA form of k_top2_mfma
-bool top2_needs_expansion();   // false: the default fp4 form expands each stage's trains while staging them
-int top2_queries_per_block();
 hipError_t launch_hamming_top2_batch(const Top2Batch& a, int npairs, int max_nq, int max_nt, int* d_best,
-                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream,
-                                     const Top2Overlap* ov = nullptr);
+                                     int* d_best_idx, int* d_second, uint2* d_part, hipStream_t stream);
 
 // Window candidates from the Frame grid (orb_window_match_grid): per item the query feature, its
 // window centre and the grid geometry; ranks (dist, grid slot) like k_topk ranks (dist, list position).

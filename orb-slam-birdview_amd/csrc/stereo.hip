@@ -383,6 +383,7 @@ int orb_compute_stereo_matches(orb_ctx* left, orb_ctx* right, int nL, const orb_
     const size_t o_cnt = st.add(16);
     const size_t o_in_end = st.off;
     const size_t o_u = st.add((size_t)cap * 4), o_d = st.add((size_t)cap * 4), o_nm = st.add(4);
+    st.end_mirror();
     const size_t o_s = st.add(stereo_scratch_ints(cl->geom, 1, scap) * 4);   // device-only working space
     if (const int r = st.alloc(); r != ORB_OK) return r;
     std::memcpy(st.hi<uint8_t>(o_kL), kpsL, (size_t)nL * 28);

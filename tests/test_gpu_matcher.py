@@ -203,6 +203,42 @@ def test_search_for_triangulation(orbgpu_mod, oracle_mod, frames, only_stereo, c
     assert len(op) > 0
 
 
+@pytest.mark.parametrize("case", ["F_nan", "F_inf", "F_zero", "epipole_nan"])
+def test_search_for_triangulation_nonfinite(orbgpu_mod, oracle_mod, frames, case):
+    """Degenerate geometry keeps the reference's IEEE semantics (ORBmatcher.cc:140-157, :725-733): a NaN or
+    infinite F12 entry, an all-zero F12 (den == 0) and a NaN epipole.  A NaN epipolar distance never passes
+    `dsqr < 3.84 sigma2`, a NaN epipole distance never trips the `< 100 scale` rejection; the GPU kernel is built
+    without -fno-honor-nans and must agree with the oracle pair for pair."""
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(16)
+    mp1 = (rng.random(len(da)) < 0.3).astype(np.uint8)
+    mp2 = (rng.random(len(db)) < 0.3).astype(np.uint8)
+    ur1 = np.where(rng.random(len(da)) < 0.5, 10.0, -1.0).astype(np.float32)
+    ur2 = np.where(rng.random(len(db)) < 0.5, 10.0, -1.0).astype(np.float32)
+    F = np.array([[0, 0, 0], [0, 0, -1], [0, 1, 0]], np.float32) + rng.normal(0, 1e-4, (3, 3)).astype(np.float32)
+    ex, ey = 320.0, 240.0
+    if case == "F_nan":
+        F[2, 2] = np.nan
+    elif case == "F_inf":
+        F[0, 0] = np.inf   # a = x1 * inf: inf, or NaN where x1 == 0; den = inf
+    elif case == "F_zero":
+        F[:] = 0
+    else:
+        ex = float("nan")
+    t = oracle_mod.OracleExtractor(1000).tables()
+    fva, fvb = _featvec(da, 8), _featvec(db, 8)
+    m = orbgpu_mod.ORBmatcher(0.6, True)
+    pairs = m.SearchForTriangulation(da, ka, mp1, ur1, fva, db, kb, mp2, ur2, fvb, F, ex, ey, t["scale"],
+                                     t["sigma2"], False)
+    oa, _ = _oracle_fv(oracle_mod, fva)
+    ob, _ = _oracle_fv(oracle_mod, fvb)
+    op = oracle_mod.search_for_triangulation(True, False, da, ka, mp1, ur1, oa, db, kb, mp2, ur2, ob, F, ex, ey,
+                                             t["scale"], t["sigma2"])
+    assert np.array_equal(pairs, op)
+    if case == "epipole_nan":
+        assert len(op) > 0
+
+
 @pytest.mark.parametrize("level0_only,window", [(True, 100), (False, 15), (True, 40)])
 def test_window_match(orbgpu_mod, oracle_mod, frames, level0_only, window):
     ka, da, kb, db = frames
@@ -361,6 +397,38 @@ def test_top2_frames_batch_vs_numpy(orbgpu_mod):
         assert np.array_equal(res[0][sl], srt[:, 0])
         assert np.array_equal(res[1][sl], D.argmin(1))
         assert np.array_equal(res[2][sl], srt[:, 1])
+    for d in out:
+        L.orb_device_free(bx.h, d)
+    bx.close()
+
+
+def test_top2_frames_pair_list_changes(orbgpu_mod):
+    """The pair list stays on the device between calls and is re-sent only when it changes
+    (orb_hamming_top2_frames_device): alternate lists of different lengths on one context, each call checked
+    against numpy, including a repeat of the first list after the others."""
+    from orbgpu import _lib
+    from orbgpu.synth import synth_batch
+    B = 5
+    bx = orbgpu_mod.BatchExtractor(800, 640, 480, B)
+    bx.upload(synth_batch(640, 480, B, first=70))
+    bx.launch()
+    bx.sync()
+    cap = bx.kp_cap
+    L = _lib.lib()
+    lists = [([0, 1, 2], [1, 2, 3]), ([3, 4], [4, 0]), ([0, 1, 2], [1, 2, 3]), ([4, 2, 1, 0, 3], [0, 0, 4, 2, 3]),
+             ([4, 2, 1, 0, 3], [0, 0, 4, 2, 3]), ([1], [1])]
+    out = [bx._alloc(5 * cap * 4) for _ in range(3)]
+    for qf, tf in lists:
+        bx.hamming_top2_frames(qf, tf, *out)
+        bx.sync()
+        res = [np.zeros(len(qf) * cap, np.int32) for _ in range(3)]
+        for r, d in zip(res, out):
+            L.orb_memcpy_d2h(bx.h, r.ctypes.data, d, r.nbytes)
+        for p, (a, b) in enumerate(zip(qf, tf)):
+            best, idx, second = _top2_numpy(bx.results(a)[1], bx.results(b)[1])
+            sl = slice(p * cap, p * cap + len(best))
+            assert np.array_equal(res[0][sl], best) and np.array_equal(res[1][sl], idx), (qf, tf, p)
+            assert np.array_equal(res[2][sl], second), (qf, tf, p)
     for d in out:
         L.orb_device_free(bx.h, d)
     bx.close()
