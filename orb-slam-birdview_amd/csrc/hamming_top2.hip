@@ -25,7 +25,12 @@ typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
 
-constexpr int kTr = 32;              // trains per stage (MFMA rows)
+// Shape (r05 A/B, profiles/r05/hamming_ab.txt): 4 waves x 2 chains, stages of two 32-train tiles, the next stage's
+// dwords fetched at the start of the current one.  Measured against it on one box: one tile per stage 143-145 us,
+// four tiles 142 (130 VGPRs: 3 waves per SIMD), 8 waves x 2 chains 149-152, fetching two stages ahead 138-139 (equal)
+constexpr int kTile = 32;            // trains per MFMA tile (rows)
+constexpr int kTps = 2;              // tiles per stage (one barrier per stage)
+constexpr int kTr = kTile * kTps;    // trains per stage
 constexpr int kChains = 2;           // query fragments per wave: two independent 32-column MFMA chains
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
@@ -63,10 +68,10 @@ constexpr unsigned kInf16 = 0x7C00u;   // f16 +inf: no key
 
 }  // namespace
 
-/* One workgroup: 256 queries (4 waves x 2 chains x 32) of one pair against one train slice, in stages of 32 trains.
- * Per stage every thread expands one train descriptor dword (v_perm, no table) into LDS (double-buffered, one
- * barrier); each wave reads the stage's A fragments once (four ds_read_b128) and issues them against both of its
- * query fragments (eight MFMAs, two independent accumulator chains).  Each chain's 16 keys per lane go through a
+/* One workgroup: 256 queries (4 waves x 2 chains x 32) of one pair against one train slice, in stages of 64 trains.
+ * Per stage every thread expands two train descriptor dwords (v_perm, no table) into LDS (double-buffered, one
+ * barrier); per 32-train tile each wave reads the A fragments once (four ds_read_b128) and issues them against both
+ * of its query fragments (eight MFMAs, two independent accumulator chains).  Each chain's 16 keys per lane go through a
  * two-stream top-2 (min / min3 / med3), and the stage's (best, second) is merged into the running state in the
  * same f16 key space: best replaced only when the stage's distance is strictly smaller (an earlier stage wins a
  * tie), its stage base kept beside it, so the first index wins as the reference's strict '<' does; second =
@@ -113,13 +118,24 @@ __global__ __launch_bounds__(kThreads) void k_top2_mfma(Top2Batch a, uint2* __re
         reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(tbase >> 32)) << 32) |
                                 (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)tbase)),
         0, max(t1 - t0, 0) * 32, 0x00020000);
-    // staging: thread -> stage row tid >> 3, descriptor dword tid & 7 (16 expanded bytes)
+    // staging: thread -> stage rows (tid >> 3) + k * kThreads / 8, descriptor dword tid & 7 (16 expanded bytes each)
+    constexpr int kSper = kTr * 8 / kThreads;   // dwords each thread stages
+    static_assert(kSper >= 1 && kSper * kThreads == kTr * 8, "staging map");
     const int soff = (tid >> 3) * kPitch + (tid & 7) * 16;
-    auto fetch = [&](int j) -> uint32_t {
-        return __builtin_amdgcn_raw_buffer_load_b32(TR, tid * 4 + j * (kTr * 32), 0, 0);
+    struct Fetched {
+        uint32_t w[kSper];
     };
-    auto stage = [&](int buf, uint32_t w) {
-        *reinterpret_cast<v4i_t*>(&s_t[buf][soff]) = expand_fp4(w, kTblTrain);
+    auto fetch = [&](int j) -> Fetched {
+        Fetched f;
+#pragma unroll
+        for (int k = 0; k < kSper; k++)
+            f.w[k] = __builtin_amdgcn_raw_buffer_load_b32(TR, tid * 4 + k * kThreads * 4 + j * (kTr * 32), 0, 0);
+        return f;
+    };
+    auto stage = [&](int buf, const Fetched& f) {
+#pragma unroll
+        for (int k = 0; k < kSper; k++)
+            *reinterpret_cast<v4i_t*>(&s_t[buf][soff + k * (kThreads / 8) * kPitch]) = expand_fp4(f.w[k], kTblTrain);
     };
     // accumulator seed: 2^23 + 4096 + row, row = the accumulator element's train row in the tile
     v16f_t seed;
@@ -170,31 +186,34 @@ __global__ __launch_bounds__(kThreads) void k_top2_mfma(Top2Batch a, uint2* __re
         stage(0, fetch(0));
         __syncthreads();
         for (int j = 0; j < nst; j++) {
-            const int tb = t0 + kTr * j;
             const bool more = j + 1 < nst;
-            uint32_t wn = 0;
-            if (more) wn = fetch(j + 1);   // the next stage's dword: its latency under this stage
-            const uint8_t* A = &s_t[j & 1][c * kPitch + 16 * h];
-            v16f_t acc[kChains];
+            Fetched wn{};
+            if (more) wn = fetch(j + 1);   // the next stage's dwords: their latency under this stage
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
-                const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
+            for (int tile = 0; tile < kTps; tile++) {
+                const int tb = t0 + kTr * j + kTile * tile;
+                const uint8_t* A = &s_t[j & 1][(kTile * tile + c) * kPitch + 16 * h];
+                v16f_t acc[kChains];
 #pragma unroll
-                for (int u = 0; u < kChains; u++) {
-                    const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
-                    // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
-                    acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, s == 0 ? seed : acc[u], 4, 4, 0,
-                                                                             0, 0, 0);
+                for (int s = 0; s < 4; s++) {
+                    const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+                    const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
+#pragma unroll
+                    for (int u = 0; u < kChains; u++) {
+                        const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
+                        // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
+                        acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, s == 0 ? seed : acc[u], 4, 4,
+                                                                                 0, 0, 0, 0);
+                    }
                 }
-            }
-            if (tb + kTr <= t1) {
+                if (tb + kTile <= t1) {
 #pragma unroll
-                for (int u = 0; u < kChains; u++) top2(acc[u], u, tb, [](int) { return true; });
-            } else {   // the slice's last stage, partial: rows at or past t1 hold no train
+                    for (int u = 0; u < kChains; u++) top2(acc[u], u, tb, [](int) { return true; });
+                } else {   // the slice's last tile, partial or empty: rows at or past t1 hold no train
 #pragma unroll
-                for (int u = 0; u < kChains; u++)
-                    top2(acc[u], u, tb, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
+                    for (int u = 0; u < kChains; u++)
+                        top2(acc[u], u, tb, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
+                }
             }
             if (more) stage((j + 1) & 1, wn);
             __syncthreads();
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(256) void k_top2b_merge(Top2Batch a, int nslices, c
 // Train slices: a launch aims at >= kTargetBlocks workgroups (two rounds of four per CU); slices are whole 32-train
 // stages of >= 64 trains.  top2_batch_slices is the partial buffer's capacity (the callers size it), the launch
 // uses top2_launch_slices <= that many.  (max_nt == 0: one empty slice of one stage, nothing divides by zero.)
-constexpr int kTargetBlocks = 2048;
+constexpr int kTargetBlocks = 8192 / kWaves;   // 8192 waves
 int top2_batch_slices(int npairs, int max_nq, int max_nt) {
     npairs = std::max(npairs, 1);
     const int qb = std::max(1, (max_nq + kQb - 1) / kQb);

@@ -230,8 +230,8 @@ def test_search_for_triangulation_nonfinite(orbgpu_mod, oracle_mod, frames, case
     m = orbgpu_mod.ORBmatcher(0.6, True)
     pairs = m.SearchForTriangulation(da, ka, mp1, ur1, fva, db, kb, mp2, ur2, fvb, F, ex, ey, t["scale"],
                                      t["sigma2"], False)
-    oa, _ = _oracle_fv(oracle_mod, fva)
-    ob, _ = _oracle_fv(oracle_mod, fvb)
+    oa, _keep_a = _oracle_fv(oracle_mod, fva)   # (the second element keeps the CSR arrays alive)
+    ob, _keep_b = _oracle_fv(oracle_mod, fvb)
     op = oracle_mod.search_for_triangulation(True, False, da, ka, mp1, ur1, oa, db, kb, mp2, ur2, ob, F, ex, ey,
                                              t["scale"], t["sigma2"])
     assert np.array_equal(pairs, op)

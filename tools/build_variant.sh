@@ -1,0 +1,28 @@
+#!/bin/bash
+# A/B build of liborbgpu with compile-time switches in ONE translation unit (run here, on the CPU):
+#   tools/build_variant.sh <name> <csrc file stem> [-DNAME=VALUE ...]
+# compiles csrc/<stem>.hip with the Makefile's flags plus the given defines, links it with the in-tree build's
+# other objects and writes ab/liborbgpu_<name>.so (ab/ is git-ignored; it travels to the GPU box, where
+# tools/gpu_run.sh "ab=ab/liborbgpu_<name>.so,tree" runs the bench under each).  Nothing in the product reads
+# these defines at run time: a variant that wins is made the code, the others are deleted.
+set -e
+NAME=${1:?name}; STEM=${2:?csrc stem}; shift 2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+PKG=$ROOT/orb-slam-birdview_amd
+make -s -C $PKG liborbgpu.so
+FLAGS=$(make -s -C $PKG --no-print-directory --eval 'print-hipflags: ; @echo $(HIPFLAGS)' print-hipflags)
+EXTRA=""
+case $STEM in
+  hamming_top2) EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans -fno-slp-vectorize" ;;
+  extract_kernels) EXTRA="-mllvm -amdgpu-mfma-vgpr-form" ;;
+esac
+mkdir -p $ROOT/ab/obj_$NAME
+/opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c $PKG/csrc/$STEM.hip -o $ROOT/ab/obj_$NAME/$STEM.o
+OBJS=""
+for o in $PKG/build/*.o; do
+  b=$(basename $o)
+  if [ "$b" = "$STEM.o" ]; then OBJS="$OBJS $ROOT/ab/obj_$NAME/$STEM.o"; else OBJS="$OBJS $o"; fi
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -mcode-object-version=5 -shared -fPIC -o $ROOT/ab/liborbgpu_$NAME.so $OBJS
+rm -rf $ROOT/ab/obj_$NAME
+echo "ab/liborbgpu_$NAME.so"
