@@ -26,8 +26,11 @@ typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
 
 // Shape (r05 A/B, profiles/r05/hamming_ab.txt): 4 waves x 2 chains, stages of two 32-train tiles, the next stage's
-// dwords fetched at the start of the current one.  Measured against it on one box: one tile per stage 143-145 us,
-// four tiles 142 (130 VGPRs: 3 waves per SIMD), 8 waves x 2 chains 149-152, fetching two stages ahead 138-139 (equal)
+// dwords fetched at the start of the current one, tile T + 1's MFMAs interleaved with tile T's top-2 (151 VGPRs,
+// 3 waves per SIMD).  Measured on one box: one tile per stage 143-145 us, two 137-141, four 142 (130 VGPRs),
+// 8 waves x 2 chains 149-152, fetching two stages ahead 138-139 (equal); the interleaved form 135-136 against
+// 140-143 (6 / 10 VALU per MFMA: 139 / 134-136).  Diagnostic builds that drop the MFMAs (92 us) or cut the top-2
+// to one min (85 us) show the two phases adding up rather than overlapping: that is what the interleave attacks.
 constexpr int kTile = 32;            // trains per MFMA tile (rows)
 constexpr int kTps = 2;              // tiles per stage (one barrier per stage)
 constexpr int kTr = kTile * kTps;    // trains per stage
@@ -71,11 +74,11 @@ constexpr unsigned kInf16 = 0x7C00u;   // f16 +inf: no key
 /* One workgroup: 256 queries (4 waves x 2 chains x 32) of one pair against one train slice, in stages of 64 trains.
  * Per stage every thread expands two train descriptor dwords (v_perm, no table) into LDS (double-buffered, one
  * barrier); per 32-train tile each wave reads the A fragments once (four ds_read_b128) and issues them against both
- * of its query fragments (eight MFMAs, two independent accumulator chains).  Each chain's 16 keys per lane go through a
- * two-stream top-2 (min / min3 / med3), and the stage's (best, second) is merged into the running state in the
- * same f16 key space: best replaced only when the stage's distance is strictly smaller (an earlier stage wins a
- * tie), its stage base kept beside it, so the first index wins as the reference's strict '<' does; second =
- * min3(second, stage second, max(best, stage best)). */
+ * of its query fragments (eight MFMAs, two independent accumulator chains), interleaved with the previous tile's
+ * top-2 (two accumulator sets).  Each chain's 16 keys per lane go through a two-stream top-2 (min / min3 / med3),
+ * and the tile's (best, second) is merged into the running state in the same f16 key space: best replaced only
+ * when the tile's distance is strictly smaller (an earlier tile wins a tie), its tile base kept beside it, so the
+ * first index wins as the reference's strict '<' does; second = min3(second, tile second, max(best, tile best)). */
 __global__ __launch_bounds__(kThreads) void k_top2_mfma(Top2Batch a, uint2* __restrict__ part, int* __restrict__ best_o,
                                                         int* __restrict__ idx_o, int* __restrict__ second_o) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[2][kStageBytes];
@@ -182,42 +185,66 @@ __global__ __launch_bounds__(kThreads) void k_top2_mfma(Top2Batch a, uint2* __re
         rst[u] = take ? tb : rst[u];
     };
     const int nst = t1 > t0 ? (t1 - t0 + kTr - 1) / kTr : 0;   // stages (uniform)
+    // tile T = (stage j, tile k): the eight MFMAs (two chains) into acc, then the top-2 of both chains
+    auto mfma_tile = [&](int buf, int tile, v16f_t (&acc)[kChains]) {
+        const uint8_t* A = &s_t[buf][(kTile * tile + c) * kPitch + 16 * h];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
+            const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
+#pragma unroll
+            for (int u = 0; u < kChains; u++) {
+                const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
+                // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
+                acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, s == 0 ? seed : acc[u], 4, 4, 0, 0,
+                                                                         0, 0);
+            }
+        }
+    };
+    auto top2_tile = [&](const v16f_t (&acc)[kChains], int tb) {
+        if (tb + kTile <= t1) {
+#pragma unroll
+            for (int u = 0; u < kChains; u++) top2(acc[u], u, tb, [](int) { return true; });
+        } else {   // the slice's last tile, partial or empty: rows at or past t1 hold no train
+#pragma unroll
+            for (int u = 0; u < kChains; u++)
+                top2(acc[u], u, tb, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
+        }
+    };
+    static_assert(kTps == 2, "pipelined form: two tiles per stage");
+    // software-pipelined: tile T + 1's MFMAs are issued interleaved with tile T's top-2, so one wave keeps the
+    // matrix pipe and the VALU busy together (waves of a SIMD otherwise run their MFMA and VALU phases in step)
+    auto interleave = [&]() {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // eight VALU
+        }
+    };
     if (nst > 0) {
         stage(0, fetch(0));
         __syncthreads();
-        for (int j = 0; j < nst; j++) {
-            const bool more = j + 1 < nst;
-            Fetched wn{};
-            if (more) wn = fetch(j + 1);   // the next stage's dwords: their latency under this stage
+        v16f_t accA[kChains], accB[kChains];
+        mfma_tile(0, 0, accA);
+        // every stage but the last is full: no masking, no branch inside the interleaved regions
+        for (int j = 0; j + 1 < nst; j++) {
+            const Fetched wn = fetch(j + 1);
+            const int tb = t0 + kTr * j;
+            mfma_tile(j & 1, 1, accB);
 #pragma unroll
-            for (int tile = 0; tile < kTps; tile++) {
-                const int tb = t0 + kTr * j + kTile * tile;
-                const uint8_t* A = &s_t[j & 1][(kTile * tile + c) * kPitch + 16 * h];
-                v16f_t acc[kChains];
-#pragma unroll
-                for (int s = 0; s < 4; s++) {
-                    const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
-                    const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
-#pragma unroll
-                    for (int u = 0; u < kChains; u++) {
-                        const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
-                        // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
-                        acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, s == 0 ? seed : acc[u], 4, 4,
-                                                                                 0, 0, 0, 0);
-                    }
-                }
-                if (tb + kTile <= t1) {
-#pragma unroll
-                    for (int u = 0; u < kChains; u++) top2(acc[u], u, tb, [](int) { return true; });
-                } else {   // the slice's last tile, partial or empty: rows at or past t1 hold no train
-#pragma unroll
-                    for (int u = 0; u < kChains; u++)
-                        top2(acc[u], u, tb, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
-                }
-            }
-            if (more) stage((j + 1) & 1, wn);
+            for (int u = 0; u < kChains; u++) top2(accA[u], u, tb, [](int) { return true; });
+            interleave();
+            stage((j + 1) & 1, wn);
             __syncthreads();
+            mfma_tile((j + 1) & 1, 0, accA);
+#pragma unroll
+            for (int u = 0; u < kChains; u++) top2(accB[u], u, tb + kTile, [](int) { return true; });
+            interleave();
         }
+        const int j = nst - 1;
+        mfma_tile(j & 1, 1, accB);
+        top2_tile(accA, t0 + kTr * j);
+        top2_tile(accB, t0 + kTr * j + kTile);
     }
     // per chain: running keys -> dist << 16 | train index; the two lane halves hold different train rows of the
     // same query
