@@ -2380,6 +2380,7 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
         RcoefOff ro;
         std::memcpy(ro.o, b.rcoef_off, sizeof ro.o);
         const bool gen = (g.variant & ORB_VARIANT_RESIZE_GENERIC) != 0;
+        for (int l = 1; l <= b.chain.first_base; l++) resize(l, stream);
         for (int sgi = 0; sgi < b.chain.nseg; sgi++) {
             const ChainSegment& sg = b.chain.seg[sgi];
             hipLaunchKernelGGL(gen ? k_pyramid_chain<true> : k_pyramid_chain<false>, dim3(sg.njobs, nframes), dim3(256),

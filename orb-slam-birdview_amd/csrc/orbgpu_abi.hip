@@ -218,14 +218,14 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
  * a region's span is its end columns' / rows' source indices).  Regions above the base start at a
  * multiple of 4 and span a multiple of 4 columns; the base region is clipped to the level. */
 static void build_chain(const Geom& g, const std::vector<ResizeCoef>& coefs, const int* off, std::vector<ChainJob>& jobs,
-                        ChainPlan& plan) {
+                        ChainPlan& plan, int first_base, int seg_len) {
     jobs.clear();
     plan = ChainPlan{};
     const int nl = g.nlevels;
-    if (nl < 2) return;
+    if (nl < 2 || first_base >= nl - 1) return;
     auto r4 = [](int x) { return (x + 3) & ~3; };
-    for (int base = 0; base < nl - 1; base += kChainSeg) {
-        const int top = std::min(base + kChainSeg, nl - 1);
+    for (int base = first_base; base < nl - 1; base += seg_len) {
+        const int top = std::min(base + seg_len, nl - 1);
         ChainSegment sg;
         sg.job0 = (int)jobs.size();
         int bufb = 0, coefe = 0;
@@ -268,6 +268,7 @@ static void build_chain(const Geom& g, const std::vector<ResizeCoef>& coefs, con
         }
         plan.seg[plan.nseg++] = sg;
     }
+    plan.first_base = first_base;
 }
 
 int Ctx::ensure_geometry(int W, int H) {
@@ -294,18 +295,26 @@ int Ctx::ensure_geometry(int W, int H) {
     if ((e = hipMemcpyAsync(d_rcoef, coefs.data(), coefs.size() * sizeof(ResizeCoef), hipMemcpyHostToDevice,
                             stream)) != hipSuccess)
         return set_error("upload coefs", e), ORB_ERR_HIP;
-    std::vector<ChainJob> cjobs;
-    ChainPlan cplan;
-    build_chain(g, coefs, off, cjobs, cplan);
-    if (cplan.nseg) {
-        if ((e = grow(d_chain, chain_cap, cjobs.size())) != hipSuccess) return set_error("hipMalloc chain", e), ORB_ERR_NOMEM;
-        if ((e = hipMemcpyAsync(d_chain, cjobs.data(), cjobs.size() * sizeof(ChainJob), hipMemcpyHostToDevice, stream)) !=
+    // the host path's plan (one frame in flight: levels 1..7 from the frame in segments of kChainSeg) and, for
+    // small batches, levels 1..kSmallChainBase per level and the rest from that level in one segment
+    ChainPlan cplan, cplan2;
+    for (int which = 0; which < 2; which++) {
+        std::vector<ChainJob> cjobs;
+        ChainPlan& pl = which ? cplan2 : cplan;
+        if (which == 1 && kSmallChainBase <= 0) break;
+        build_chain(g, coefs, off, cjobs, pl, which ? kSmallChainBase : 0, which ? ORBGPU_MAX_LEVELS : kChainSeg);
+        if (!pl.nseg) continue;
+        ChainJob*& dj = which ? d_chain2 : d_chain;
+        size_t& cap = which ? chain2_cap : chain_cap;
+        if ((e = grow(dj, cap, cjobs.size())) != hipSuccess) return set_error("hipMalloc chain", e), ORB_ERR_NOMEM;
+        if ((e = hipMemcpyAsync(dj, cjobs.data(), cjobs.size() * sizeof(ChainJob), hipMemcpyHostToDevice, stream)) !=
             hipSuccess)
             return set_error("upload chain", e), ORB_ERR_HIP;
     }
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
     geom = g;
     chain = cplan;
+    chain_small = cplan2;
     std::memcpy(rcoef_off, off, sizeof off);
     have_geom = true;
     ++geom_serial;
@@ -377,9 +386,12 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
     ExtractBuffers bufs = buffers();
     if (err) bufs.d_err = err;
     bufs.err_host = err_host;
-    // the few-launch pyramid trades redundant work for fewer dependent launches: it pays for one frame
-    // in flight (the host path), not when several batches share the GPU (measured)
-    if (!latency) bufs.chain.nseg = 0;
+    // the few-launch pyramid trades redundant work for fewer dependent launches: the whole plan pays for one
+    // frame in flight (the host path); batches of a frame or two (C5 at one frame per GPU) take the small plan
+    if (!latency) {
+        bufs.chain = chain_small;
+        bufs.d_chain = d_chain2;
+    }
     // one frame in flight (ORBGPU_FORK=1): level 0's FAST -> octree on a second stream beside the pyramid
     if (latency && fork && !prof_on && !fast_stamps && geom.nlevels > 1) {
         hipError_t fe = hipSuccess;
@@ -540,7 +552,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.b);
         (void)hipEventDestroy(pr.e);
     }
-    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
+    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_chain2, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in,
                     c->d_scratch, c->d_peer, c->d_pairs};
     for (void* b : bufs)

@@ -51,6 +51,9 @@ struct Ctx {
     ChainJob* d_chain = nullptr;   // the one-launch pyramid's jobs (small batches)
     size_t chain_cap = 0;
     ChainPlan chain{};
+    ChainJob* d_chain2 = nullptr;  // the small-batch plan (levels past kSmallChainBase in one launch)
+    size_t chain2_cap = 0;
+    ChainPlan chain_small{};
     CellDesc* d_cells = nullptr;
     size_t cells_cap = 0;
 

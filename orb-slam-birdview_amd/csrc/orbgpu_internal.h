@@ -120,8 +120,15 @@ struct ChainSegment {
 };
 struct ChainPlan {
     int nseg = 0;           // 0: the plan does not fit (per-level launches only)
+    int first_base = 0;     // levels 1..first_base are per-level launches before the segments
     ChainSegment seg[ORBGPU_MAX_LEVELS];
 };
+// Batches of up to kChainMaxFrames frames in the batch path (C5 at one frame per GPU) compute levels 1..3 with one
+// launch each and levels 4..7 from level 3 in one k_pyramid_chain launch (r05, profiles/r05/c5b1_pyramid_ab.txt: C5
+// one frame per step, four in flight, 171 M features/s against 164-169 with seven per-level launches; chaining from
+// level 2 157-159, level 1 137, level 4 167-174: the chained launch's per-tile level walk is long, so only the small
+// top levels pay for their launches)
+constexpr int kSmallChainBase = 3;
 constexpr int kChainMaxFrames = 2;
 struct RcoefOff {   // per-level offsets into the coefficient table (a kernel argument)
     int o[ORBGPU_MAX_LEVELS];

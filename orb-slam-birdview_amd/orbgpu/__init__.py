@@ -52,6 +52,35 @@ class _Ctx:
     def __del__(self):
         self.close()
 
+    # debug views (parity tests pinpoint the failing stage)
+    def debug_candidates(self, level, frame=0):
+        cap = 1 << 16
+        while True:
+            out = np.zeros((cap, 3), np.int32)
+            n = lib().orb_debug_candidates(self.h, frame, level, _p(out), cap)
+            if n >= 0:
+                return out[:n]
+            if n == -1:
+                raise OrbError(n, "orb_debug_candidates")
+            cap = -n
+
+    def debug_level_image(self, level, frame=0):
+        """Pyramid level `level` of frame `frame` of the last extraction (orb_debug_level_image)."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check(lib().orb_debug_level_image(self.h, frame, level, None, ctypes.byref(w), ctypes.byref(h)),
+              "orb_debug_level_image")
+        out = np.zeros((h.value, w.value), np.uint8)
+        check(lib().orb_debug_level_image(self.h, frame, level, _p(out), ctypes.byref(w), ctypes.byref(h)),
+              "orb_debug_level_image")
+        return out
+
+    def debug_level_keypoints(self, level, frame=0):
+        out = np.zeros((1 << 15, 3), np.int32)
+        n = lib().orb_debug_level_keypoints(self.h, frame, level, _p(out), len(out))
+        if n < 0:
+            raise OrbError(n, "orb_debug_level_keypoints")
+        return out[:n]
+
 
 class ORBextractor(_Ctx):
     """ORB_SLAM2::ORBextractor (ORBextractor.cc:410-470, 1043-1132) on one MI355X.  `variant` selects the
@@ -131,26 +160,6 @@ class ORBextractor(_Ctx):
             buf = (ctypes.c_uint8 * (stride.value * h.value)).from_address(ptr.value)
             out.append(np.ctypeslib.as_array(buf).reshape(h.value, stride.value)[:, :w.value].copy())
         return out
-
-    # debug views (parity tests pinpoint the failing stage)
-    def debug_candidates(self, level, frame=0):
-        cap = 1 << 16
-        while True:
-            out = np.zeros((cap, 3), np.int32)
-            n = lib().orb_debug_candidates(self.h, frame, level, _p(out), cap)
-            if n >= 0:
-                return out[:n]
-            if n == -1:
-                raise OrbError(n, "orb_debug_candidates")
-            cap = -n
-
-    def debug_level_keypoints(self, level, frame=0):
-        out = np.zeros((1 << 15, 3), np.int32)
-        n = lib().orb_debug_level_keypoints(self.h, frame, level, _p(out), len(out))
-        if n < 0:
-            raise OrbError(n, "orb_debug_level_keypoints")
-        return out[:n]
-
 
 class BatchExtractor(_Ctx):
     """Device-resident batched extraction (orb_extract_batch_device): frames already in HBM."""

@@ -407,3 +407,25 @@ def test_geometry_limits_are_errors(orbgpu_mod):
     g = orbgpu_mod.ORBextractor(12000, 1.2, 8, 20, 7)
     with pytest.raises(OrbError):
         g(np.zeros((2160, 3840), np.uint8))
+
+
+@pytest.mark.parametrize("w,h,nf,B", [(1280, 720, 4000, 1), (1280, 720, 2000, 2), (640, 480, 1000, 1)])
+def test_small_batch_pyramid_plan_bit_exact(orbgpu_mod, oracle_mod, w, h, nf, B):
+    """Batches of one or two frames (C5 at one frame per GPU) take the small-batch pyramid plan (orbgpu_abi.hip
+    build_chain: the first levels per launch, the rest chained from the last of them in one k_pyramid_chain launch);
+    keypoints, descriptors and every pyramid level are byte-identical to the oracle's."""
+    from orbgpu.synth import bench_frames
+    frames = bench_frames(w, h, B, first=11)
+    e = orbgpu_mod.BatchExtractor(nf, w, h, B)
+    e.upload(frames)
+    for _ in range(2):   # the graph's capture, then a replay
+        e.launch()
+        e.sync()
+        o = oracle_mod.OracleExtractor(nf)
+        for f in range(B):
+            ok, od = o(frames[f])
+            gk, gd = e.results(f)
+            assert gk.tobytes() == ok.tobytes() and np.array_equal(gd, od), (B, f)
+            for l in range(1, 8):
+                assert np.array_equal(e.debug_level_image(l, f), o.level(l)), (f, l)
+    e.close()
