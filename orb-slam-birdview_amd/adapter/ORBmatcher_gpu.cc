@@ -65,8 +65,11 @@ struct ThreadCtx {
 // one context per (host thread, device): the matchers are stack objects called from several threads
 orb_ctx* ctx() {
     static thread_local ThreadCtx tc;
-    const char* e = getenv("ORBGPU_DEVICE");
-    const int dev = e ? atoi(e) : 0;
+    static thread_local int dev = -1;   // ORBGPU_DEVICE, read once per thread (getenv scans the environment)
+    if (dev < 0) {
+        const char* e = getenv("ORBGPU_DEVICE");
+        dev = e ? atoi(e) : 0;
+    }
     if (tc.ctx && tc.device == dev) return tc.ctx;
     if (tc.ctx) orb_destroy(tc.ctx);
     tc.ctx = nullptr;
@@ -101,10 +104,10 @@ const orb_keypoint* keys_of(const std::vector<cv::KeyPoint>& k) {
     return k.empty() ? &dummy : reinterpret_cast<const orb_keypoint*>(k.data());
 }
 
-std::vector<float> angles_of(const std::vector<cv::KeyPoint>& k) {
-    std::vector<float> a(k.size() ? k.size() : 1, 0.f);
+const float* angles_of(const std::vector<cv::KeyPoint>& k, std::vector<float>& a) {
+    a.assign(k.size() ? k.size() : 1, 0.f);
     for (size_t i = 0; i < k.size(); i++) a[i] = k[i].angle;
-    return a;
+    return a.data();
 }
 
 // DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>) as the C-ABI's CSR; std::map order
@@ -113,7 +116,12 @@ struct FeatCsr {
     std::vector<uint32_t> ids;
     std::vector<int> off, idx;
     orb_featvec fv;
-    explicit FeatCsr(const DBoW2::FeatureVector& f) {
+    FeatCsr() = default;
+    explicit FeatCsr(const DBoW2::FeatureVector& f) { assign(f); }
+    FeatCsr& assign(const DBoW2::FeatureVector& f) {   // (storage reused across calls)
+        ids.clear();
+        off.clear();
+        idx.clear();
         off.push_back(0);
         for (DBoW2::FeatureVector::const_iterator it = f.begin(); it != f.end(); ++it) {
             ids.push_back(it->first);
@@ -125,14 +133,28 @@ struct FeatCsr {
         fv.node_ids = ids.empty() ? nullptr : ids.data();
         fv.offsets = off.data();
         fv.indices = idx.data();
+        return *this;
     }
 };
 
+// A host thread's conversion buffers, reused across calls: a matcher call is tens of microseconds, and the
+// dozen small allocations of building its flat views fresh every time were a measurable part of it
+struct Scratch {
+    FeatCsr f1, f2;
+    std::vector<uint8_t> mp1, mp2, t1, t2;
+    std::vector<float> ur1, ur2, a1, a2;
+    std::vector<int> pairs;
+};
+Scratch& scratch() {
+    static thread_local Scratch s;
+    return s;
+}
+
 // pMP && !pMP->isBad() per feature (the BoW searches' admission test, :191-197, :558-562, :574-580)
-std::vector<uint8_t> good_points(const std::vector<MapPoint*>& v) {
-    std::vector<uint8_t> f(v.size() ? v.size() : 1, 0);
+const uint8_t* good_points(const std::vector<MapPoint*>& v, std::vector<uint8_t>& f) {
+    f.assign(v.size() ? v.size() : 1, 0);
     for (size_t i = 0; i < v.size(); i++) f[i] = v[i] && !v[i]->isBad();
-    return f;
+    return f.data();
 }
 
 }  // namespace orbgpu_adapter
@@ -142,15 +164,17 @@ using namespace orbgpu_adapter;
 int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
     const std::vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
     vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL));
-    const std::vector<uint8_t> mp = good_points(vpMapPointsKF);
-    const std::vector<float> aKF = angles_of(pKF->mvKeysUn), aF = angles_of(F.mvKeys);
-    FeatCsr fkf(pKF->mFeatVec), ff(F.mFeatVec);
-    std::vector<uint8_t> t1, t2;
-    std::vector<int> match(F.N > 0 ? F.N : 1, -1);
+    Scratch& S = scratch();
+    const uint8_t* mp = good_points(vpMapPointsKF, S.mp1);
+    const float *aKF = angles_of(pKF->mvKeysUn, S.a1), *aF = angles_of(F.mvKeys, S.a2);
+    const FeatCsr& fkf = S.f1.assign(pKF->mFeatVec);
+    const FeatCsr& ff = S.f2.assign(F.mFeatVec);
+    std::vector<int>& match = S.pairs;
+    match.assign(F.N > 0 ? F.N : 1, -1);
     int nmatches = 0;
-    check(orb_search_by_bow_kf_f(ctx(), mfNNratio, mbCheckOrientation, pKF->N, desc_rows(pKF->mDescriptors, pKF->N, t1),
-                                 aKF.data(), mp.data(), fkf.fv, F.N, desc_rows(F.mDescriptors, F.N, t2), aF.data(),
-                                 ff.fv, match.data(), &nmatches),
+    check(orb_search_by_bow_kf_f(ctx(), mfNNratio, mbCheckOrientation, pKF->N, desc_rows(pKF->mDescriptors, pKF->N, S.t1),
+                                 aKF, mp, fkf.fv, F.N, desc_rows(F.mDescriptors, F.N, S.t2), aF, ff.fv, match.data(),
+                                 &nmatches),
           "SearchByBoW(KeyFrame*, Frame&)");
     for (int iF = 0; iF < F.N; iF++)
         if (match[iF] >= 0) vpMapPointMatches[iF] = vpMapPointsKF[match[iF]];
@@ -161,16 +185,18 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
     const std::vector<MapPoint*> vpMapPoints1 = pKF1->GetMapPointMatches();
     const std::vector<MapPoint*> vpMapPoints2 = pKF2->GetMapPointMatches();
     vpMatches12 = std::vector<MapPoint*>(vpMapPoints1.size(), static_cast<MapPoint*>(NULL));
-    const std::vector<uint8_t> mp1 = good_points(vpMapPoints1), mp2 = good_points(vpMapPoints2);
-    const std::vector<float> a1 = angles_of(pKF1->mvKeysUn), a2 = angles_of(pKF2->mvKeysUn);
-    FeatCsr f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
-    std::vector<uint8_t> t1, t2;
+    Scratch& S = scratch();
+    const uint8_t *mp1 = good_points(vpMapPoints1, S.mp1), *mp2 = good_points(vpMapPoints2, S.mp2);
+    const float *a1 = angles_of(pKF1->mvKeysUn, S.a1), *a2 = angles_of(pKF2->mvKeysUn, S.a2);
+    const FeatCsr& f1 = S.f1.assign(pKF1->mFeatVec);
+    const FeatCsr& f2 = S.f2.assign(pKF2->mFeatVec);
     const int n1 = (int)vpMapPoints1.size(), n2 = (int)vpMapPoints2.size();
-    std::vector<int> match(n1 > 0 ? n1 : 1, -1);
+    std::vector<int>& match = S.pairs;
+    match.assign(n1 > 0 ? n1 : 1, -1);
     int nmatches = 0;
-    check(orb_search_by_bow_kf_kf(ctx(), mfNNratio, mbCheckOrientation, n1, desc_rows(pKF1->mDescriptors, n1, t1),
-                                  a1.data(), mp1.data(), f1.fv, n2, desc_rows(pKF2->mDescriptors, n2, t2), a2.data(),
-                                  mp2.data(), f2.fv, match.data(), &nmatches),
+    check(orb_search_by_bow_kf_kf(ctx(), mfNNratio, mbCheckOrientation, n1, desc_rows(pKF1->mDescriptors, n1, S.t1), a1,
+                                  mp1, f1.fv, n2, desc_rows(pKF2->mDescriptors, n2, S.t2), a2, mp2, f2.fv, match.data(),
+                                  &nmatches),
           "SearchByBoW(KeyFrame*, KeyFrame*)");
     for (int i1 = 0; i1 < n1; i1++)
         if (match[i1] >= 0) vpMatches12[i1] = vpMapPoints2[match[i1]];
@@ -189,22 +215,28 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
     const float ey = pKF2->fy * C2.at<float>(1) * invz + pKF2->cy;
 
     const int n1 = pKF1->N, n2 = pKF2->N;
-    std::vector<uint8_t> mp1(n1 > 0 ? n1 : 1, 0), mp2(n2 > 0 ? n2 : 1, 0);   // GetMapPoint(idx) != NULL (:699, :722)
+    Scratch& S = scratch();
+    std::vector<uint8_t>&mp1 = S.mp1, &mp2 = S.mp2;   // GetMapPoint(idx) != NULL (:699, :722)
+    mp1.assign(n1 > 0 ? n1 : 1, 0);
+    mp2.assign(n2 > 0 ? n2 : 1, 0);
     for (int i = 0; i < n1; i++) mp1[i] = pKF1->GetMapPoint(i) != NULL;
     for (int i = 0; i < n2; i++) mp2[i] = pKF2->GetMapPoint(i) != NULL;
     float F[9];
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) F[3 * r + c] = F12.at<float>(r, c);   // CheckDistEpipolarLine (:143-147)
-    std::vector<float> ur1(pKF1->mvuRight.begin(), pKF1->mvuRight.end()), ur2(pKF2->mvuRight.begin(), pKF2->mvuRight.end());
+    std::vector<float>&ur1 = S.ur1, &ur2 = S.ur2;
+    ur1.assign(pKF1->mvuRight.begin(), pKF1->mvuRight.end());
+    ur2.assign(pKF2->mvuRight.begin(), pKF2->mvuRight.end());
     ur1.resize(n1 > 0 ? n1 : 1, -1.f);
     ur2.resize(n2 > 0 ? n2 : 1, -1.f);
-    FeatCsr f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
-    std::vector<uint8_t> t1, t2;
-    std::vector<int> pairs(2 * (size_t)(n1 > 0 ? n1 : 1));
+    const FeatCsr& f1 = S.f1.assign(pKF1->mFeatVec);
+    const FeatCsr& f2 = S.f2.assign(pKF2->mFeatVec);
+    std::vector<int>& pairs = S.pairs;
+    pairs.resize(2 * (size_t)(n1 > 0 ? n1 : 1));
     int np = 0;
-    check(orb_search_for_triangulation(ctx(), mbCheckOrientation, bOnlyStereo, n1, desc_rows(pKF1->mDescriptors, n1, t1),
+    check(orb_search_for_triangulation(ctx(), mbCheckOrientation, bOnlyStereo, n1, desc_rows(pKF1->mDescriptors, n1, S.t1),
                                        keys_of(pKF1->mvKeysUn), mp1.data(), ur1.data(), f1.fv, n2,
-                                       desc_rows(pKF2->mDescriptors, n2, t2), keys_of(pKF2->mvKeysUn), mp2.data(),
+                                       desc_rows(pKF2->mDescriptors, n2, S.t2), keys_of(pKF2->mvKeysUn), mp2.data(),
                                        ur2.data(), f2.fv, F, ex, ey, pKF2->mvScaleFactors.data(),
                                        pKF2->mvLevelSigma2.data(), (int)pKF2->mvScaleFactors.size(), pairs.data(),
                                        n1 > 0 ? n1 : 1, &np),
