@@ -26,11 +26,13 @@ typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
 
 // Shape (r05 A/B, profiles/r05/hamming_ab.txt): 4 waves x 2 chains, stages of two 32-train tiles, the next stage's
-// dwords fetched at the start of the current one, tile T + 1's MFMAs interleaved with tile T's top-2 (151 VGPRs,
-// 3 waves per SIMD).  Measured on one box: one tile per stage 143-145 us, two 137-141, four 142 (130 VGPRs),
-// 8 waves x 2 chains 149-152, fetching two stages ahead 138-139 (equal); the interleaved form 135-136 against
-// 140-143 (6 / 10 VALU per MFMA: 139 / 134-136).  Diagnostic builds that drop the MFMAs (92 us) or cut the top-2
-// to one min (85 us) show the two phases adding up rather than overlapping: that is what the interleave attacks.
+// dwords fetched at the start of the current one, one chain's MFMAs interleaved with the other chain's top-2 (124
+// VGPRs, 4 waves per SIMD).  Measured on one box: one tile per stage 143-145 us, two 137-141, four 142 (130
+// VGPRs), 8 waves x 2 chains 149-152, fetching two stages ahead 138-139 (equal); the interleaved forms 130-136
+// against 131-143 without (two accumulator sets, tile T + 1's MFMAs beside tile T's top-2: 151 VGPRs, 135-136;
+// chain-staggered, one set: 130-131).  Diagnostic builds (profiles/r05/hamming_ab.txt): without the MFMAs 92 us,
+// with the top-2 cut to one min 85 us, with neither (staging, barriers, fragment reads) 46-47 us: the MFMA and
+// top-2 phases still mostly add up.
 constexpr int kTile = 32;            // trains per MFMA tile (rows)
 constexpr int kTps = 2;              // tiles per stage (one barrier per stage)
 constexpr int kTr = kTile * kTps;    // trains per stage
@@ -74,8 +76,8 @@ constexpr unsigned kInf16 = 0x7C00u;   // f16 +inf: no key
 /* One workgroup: 256 queries (4 waves x 2 chains x 32) of one pair against one train slice, in stages of 64 trains.
  * Per stage every thread expands two train descriptor dwords (v_perm, no table) into LDS (double-buffered, one
  * barrier); per 32-train tile each wave reads the A fragments once (four ds_read_b128) and issues them against both
- * of its query fragments (eight MFMAs, two independent accumulator chains), interleaved with the previous tile's
- * top-2 (two accumulator sets).  Each chain's 16 keys per lane go through a two-stream top-2 (min / min3 / med3),
+ * of its query fragments (eight MFMAs, two accumulator chains), each chain's four interleaved with the other
+ * chain's top-2.  Each chain's 16 keys per lane go through a two-stream top-2 (min / min3 / med3),
  * and the tile's (best, second) is merged into the running state in the same f16 key space: best replaced only
  * when the tile's distance is strictly smaller (an earlier tile wins a tie), its tile base kept beside it, so the
  * first index wins as the reference's strict '<' does; second = min3(second, tile second, max(best, tile best)). */
@@ -185,66 +187,72 @@ __global__ __launch_bounds__(kThreads) void k_top2_mfma(Top2Batch a, uint2* __re
         rst[u] = take ? tb : rst[u];
     };
     const int nst = t1 > t0 ? (t1 - t0 + kTr - 1) / kTr : 0;   // stages (uniform)
-    // tile T = (stage j, tile k): the eight MFMAs (two chains) into acc, then the top-2 of both chains
-    auto mfma_tile = [&](int buf, int tile, v16f_t (&acc)[kChains]) {
+    // chain-staggered: one chain's four MFMAs interleaved with the other chain's top-2, so a single accumulator per
+    // chain suffices (no second set): phase (t, 1) = MFMAs of chain 1, tile t + top-2 of chain 0, tile t; phase
+    // (t, 0) = MFMAs of chain 0, tile t + 1 + top-2 of chain 1, tile t.  A tile's A fragments are read once and
+    // serve both phases that use them.
+    auto frags = [&](int buf, int tile, v8i_t (&a8)[4]) {
         const uint8_t* A = &s_t[buf][(kTile * tile + c) * kPitch + 16 * h];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             const v4i_t av = *reinterpret_cast<const v4i_t*>(A + 32 * s);
-            const v8i_t a8 = {av[0], av[1], av[2], av[3], 0, 0, 0, 0};
-#pragma unroll
-            for (int u = 0; u < kChains; u++) {
-                const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
-                // cbsz = blgp = 4: both operands e2m1; zero scales select the unscaled form (4-VGPR operands)
-                acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, s == 0 ? seed : acc[u], 4, 4, 0, 0,
-                                                                         0, 0);
-            }
+            a8[s] = v8i_t{av[0], av[1], av[2], av[3], 0, 0, 0, 0};
         }
     };
-    auto top2_tile = [&](const v16f_t (&acc)[kChains], int tb) {
-        if (tb + kTile <= t1) {
+    auto mfma_chain = [&](const v8i_t (&a8)[4], int u, v16f_t& acc) {
 #pragma unroll
-            for (int u = 0; u < kChains; u++) top2(acc[u], u, tb, [](int) { return true; });
-        } else {   // the slice's last tile, partial or empty: rows at or past t1 hold no train
-#pragma unroll
-            for (int u = 0; u < kChains; u++)
-                top2(acc[u], u, tb, [&](int r) { return tb + (r & 3) + 8 * (r >> 2) + 4 * h < t1; });
+        for (int s = 0; s < 4; s++) {
+            const v8i_t b8 = {qf[u][s][0], qf[u][s][1], qf[u][s][2], qf[u][s][3], 0, 0, 0, 0};
+            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8[s], b8, s == 0 ? seed : acc, 4, 4, 0, 0, 0, 0);
         }
     };
-    static_assert(kTps == 2, "pipelined form: two tiles per stage");
-    // software-pipelined: tile T + 1's MFMAs are issued interleaved with tile T's top-2, so one wave keeps the
-    // matrix pipe and the VALU busy together (waves of a SIMD otherwise run their MFMA and VALU phases in step)
-    auto interleave = [&]() {
+    auto inter4 = [&]() {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        for (int i = 0; i < 4; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // eight VALU
         }
     };
+    auto all = [](int) { return true; };
     if (nst > 0) {
         stage(0, fetch(0));
         __syncthreads();
-        v16f_t accA[kChains], accB[kChains];
-        mfma_tile(0, 0, accA);
-        // every stage but the last is full: no masking, no branch inside the interleaved regions
+        v16f_t acc0, acc1;
+        v8i_t fa[4], fb[4];
+        frags(0, 0, fa);
+        mfma_chain(fa, 0, acc0);
         for (int j = 0; j + 1 < nst; j++) {
             const Fetched wn = fetch(j + 1);
             const int tb = t0 + kTr * j;
-            mfma_tile(j & 1, 1, accB);
-#pragma unroll
-            for (int u = 0; u < kChains; u++) top2(accA[u], u, tb, [](int) { return true; });
-            interleave();
+            mfma_chain(fa, 1, acc1);   // tile 2j, chain 1
+            top2(acc0, 0, tb, all);
+            inter4();
+            frags(j & 1, 1, fb);
+            mfma_chain(fb, 0, acc0);   // tile 2j + 1, chain 0
+            top2(acc1, 1, tb, all);
+            inter4();
+            mfma_chain(fb, 1, acc1);   // tile 2j + 1, chain 1
+            top2(acc0, 0, tb + kTile, all);
+            inter4();
             stage((j + 1) & 1, wn);
             __syncthreads();
-            mfma_tile((j + 1) & 1, 0, accA);
-#pragma unroll
-            for (int u = 0; u < kChains; u++) top2(accB[u], u, tb + kTile, [](int) { return true; });
-            interleave();
+            frags((j + 1) & 1, 0, fa);
+            mfma_chain(fa, 0, acc0);   // tile 2j + 2, chain 0
+            top2(acc1, 1, tb + kTile, all);
+            inter4();
         }
-        const int j = nst - 1;
-        mfma_tile(j & 1, 1, accB);
-        top2_tile(accA, t0 + kTr * j);
-        top2_tile(accB, t0 + kTr * j + kTile);
+        const int j = nst - 1, tb = t0 + kTr * j;
+        auto masked = [&](int tb_) {
+            return [=](int r) { return tb_ + (r & 3) + 8 * (r >> 2) + 4 * h < t1; };
+        };
+        mfma_chain(fa, 1, acc1);
+        top2(acc0, 0, tb, masked(tb));
+        top2(acc1, 1, tb, masked(tb));
+        frags(j & 1, 1, fb);
+        mfma_chain(fb, 0, acc0);
+        mfma_chain(fb, 1, acc1);
+        top2(acc0, 0, tb + kTile, masked(tb + kTile));
+        top2(acc1, 1, tb + kTile, masked(tb + kTile));
     }
     // per chain: running keys -> dist << 16 | train index; the two lane halves hold different train rows of the
     // same query
