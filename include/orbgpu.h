@@ -223,9 +223,8 @@ int orb_hamming_top2_frames_device(orb_ctx* ctx, const uint8_t* d_desc, const in
  * second itself; more = per-slice partial results merged by a second kernel.  Host only (test / tuning). */
 int orb_hamming_top2_slices(int npairs, int max_nq, int max_nt);
 
-/* Operand width of the all-pairs top-2's matrix-core form in this process: 8 = +-1 int8
- * (v_mfma_i32_32x32x32_i8, bound by the dense I8 peak), 4 = +-4 e2m1 fp4 (v_mfma_f32_32x32x64_f8f6f4, the dense
- * FP4 peak; ORBGPU_TOP2 containing 'f').  Both give identical results.  Host only (bench / tests). */
+/* Operand width of the all-pairs top-2's matrix-core form: 4 = +-4 e2m1 fp4 (v_mfma_scale_f32_32x32x64_f8f6f4,
+ * bound by the dense FP4 peak; the only form since round 5).  Host only (bench / tests). */
 int orb_hamming_top2_mfma_bits(void);
 
 /* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21) as CSR. */
