@@ -188,20 +188,16 @@ __global__ __launch_bounds__(256) void k_window_topk(const uint8_t* __restrict__
  * wavefront: dist <= TH_LOW, epipole distance gate for mono pairs, CheckDistEpipolarLine
  * (:140-157, float with the final comparison in double).  The reference keeps the LAST candidate
  * reaching the running minimum ('dist > bestDist' skips only strictly larger), so the key is
- * dist << 32 | ~pos. */
-__global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict__ qdesc,
-                                                       const float4* __restrict__ qinfo,
-                                                       const uint8_t* __restrict__ tdesc,
-                                                       const float4* __restrict__ tinfo,
-                                                       const int2* __restrict__ ranges, const int* __restrict__ cand,
-                                                       int nitems, TriParams tp, int* __restrict__ best_out) {
-    const int it = blockIdx.x * 4 + (threadIdx.x >> 6);
+ * dist << 32 | ~pos.  The inputs live in host memory (the call's pinned mirror): the item record is one
+ * wave-uniform read, then each lane reads its candidates' records. */
+__global__ __launch_bounds__(256) void k_triangulation(const TriItem* __restrict__ items,
+                                                       const TriTrain* __restrict__ trains, int nitems, TriParams tp,
+                                                       int* __restrict__ best_out) {
+    const int it = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (it >= nitems) return;
-    const uint4* qp = reinterpret_cast<const uint4*>(qdesc + (long long)it * 32);
-    const uint4 qa = qp[0], qb = qp[1];
-    const float4 q = qinfo[it];   // x, y, stereo (1 / 0)
-    const bool st1 = q.z != 0.f;
+    const TriItem q = items[it];
+    const bool st1 = q.stereo != 0;
     const float* F = tp.F;
     // CheckDistEpipolarLine's float expressions with the contractions the reference's -O3 -march=native
     // build applies (tools/ref_flags_probe.cpp fixes each form)
@@ -210,13 +206,13 @@ __global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict
     const float lc = __builtin_fmaf(q.y, F[5], q.x * F[2]) + F[8];
     const float den = __builtin_fmaf(la, la, lb * lb);
     unsigned long long bestKey = ~0ull;
-    const int c0 = ranges[it].x, c1 = ranges[it].y;
+    const int c0 = q.c0, c1 = q.c1;
     for (int pos = c0 + lane; pos < c1; pos += 64) {
-        const int j = cand[pos];   // (no map point, stereo if asked: filtered on the host, :725-733)
-        const uint4* tq = reinterpret_cast<const uint4*>(tdesc + (long long)j * 32);
-        const int dist = hamming256(qa, qb, tq[0], tq[1]);
+        const TriTrain& tr = trains[pos];   // (no map point, stereo if asked: filtered on the host, :725-733)
+        const uint4 ta = tr.desc[0], tb = tr.desc[1];
+        const float4 t = tr.info;   // x, y, octave, stereo
+        const int dist = hamming256(q.desc[0], q.desc[1], ta, tb);
         if (dist > 50) continue;
-        const float4 t = tinfo[j];   // x, y, octave, stereo
         const int oct = (int)t.z;
         const bool st2 = t.w != 0.f;
         if (!st1 && !st2) {
@@ -231,11 +227,7 @@ __global__ __launch_bounds__(256) void k_triangulation(const uint8_t* __restrict
         bestKey = key < bestKey ? key : bestKey;
     }
     bestKey = wave_min_u64(bestKey);
-    if (lane == 0) {
-        int r = -1;
-        if (bestKey != ~0ull) r = cand[c0 + (0x7FFFFFFF - (int)(bestKey & 0xFFFFFFFFu))];
-        best_out[it] = r;
-    }
+    if (lane == 0) best_out[it] = bestKey != ~0ull ? c0 + (0x7FFFFFFF - (int)(bestKey & 0xFFFFFFFFu)) : -1;
 }
 
 hipError_t launch_hamming_topk(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, const int2* d_ranges,
@@ -259,12 +251,11 @@ hipError_t launch_window_topk(const uint8_t* d_q, const int* d_item_q, const flo
     return hipGetLastError();
 }
 
-hipError_t launch_triangulation(const uint8_t* d_qdesc, const float4* d_qinfo, const uint8_t* d_tdesc,
-                                const float4* d_tinfo, const int2* d_ranges, const int* d_cand, int nitems,
-                                const TriParams& tp, int* d_best, hipStream_t stream) {
+hipError_t launch_triangulation(const TriItem* d_items, const TriTrain* d_trains, int nitems, const TriParams& tp,
+                                int* d_best, hipStream_t stream) {
     if (nitems <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_triangulation, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_qdesc, d_qinfo, d_tdesc, d_tinfo,
-                       d_ranges, d_cand, nitems, tp, d_best);
+    hipLaunchKernelGGL(k_triangulation, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_items, d_trains, nitems, tp,
+                       d_best);
     return hipGetLastError();
 }
 

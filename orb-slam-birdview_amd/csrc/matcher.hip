@@ -502,71 +502,58 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
     if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
-    // Compact inputs (the upload is the call's cost): queries in item order, and per common
-    // node its candidates without a map point (and stereo ones only if asked, :725-733) as compact train
-    // indices, in the node's order (the reference keeps the last candidate reaching the minimum)
+    // The inputs, written once into the pinned mirror the kernel reads (the upload is the call's cost,
+    // DESIGN §4.8): per common node its candidates without a map point (and stereo ones only if asked,
+    // :725-733) as train records in the node's order (the reference keeps the last candidate reaching the
+    // minimum), then one item record per query of the node that has candidates (a query with none matches
+    // nothing).  Sizes are bounded by the FeatureVectors' lengths, so the mirror is sized before the walk.
     std::vector<int>& item_q = c->tri_item_q;     // item -> idx1
-    std::vector<int>& cand = c->tri_cand;         // candidates (compact train indices)
-    std::vector<int>& train_of = c->tri_train_of; // compact train -> idx2
-    std::vector<int2>& rng = c->tri_rng;
-    std::vector<int>& tmap = c->tri_tmap;         // idx2 -> compact train (all -1 between calls)
+    std::vector<int>& train_of = c->tri_train_of; // train record -> idx2
+    const int cap_items = fv1.nnodes > 0 ? fv1.offsets[fv1.nnodes] : 0;
+    const int cap_trains = fv2.nnodes > 0 ? fv2.offsets[fv2.nnodes] : 0;
     item_q.clear();
-    cand.clear();
     train_of.clear();
-    rng.clear();
-    if ((int)tmap.size() < n2) tmap.resize(n2, -1);
-    for_common_nodes(fv1, fv2, [&](int a, int b) {
-        const int cb = (int)cand.size();
-        for (int i = fv2.offsets[b]; i < fv2.offsets[b + 1]; i++) {
-            const int idx2 = fv2.indices[i];
-            if (has_mp2[idx2]) continue;
-            if (only_stereo && !(uright2[idx2] >= 0)) continue;
-            if (tmap[idx2] < 0) {
-                tmap[idx2] = (int)train_of.size();
+    Stage st{c};
+    st.zc = 1;   // one kernel over small inputs: reading the pinned mirror beats the DMA (Stage::zc)
+    const size_t o_it = st.add((size_t)cap_items * sizeof(TriItem)),
+                 o_tr = st.add((size_t)cap_trains * sizeof(TriTrain)), o_b = st.add((size_t)cap_items * 4);
+    if (cap_items > 0 && cap_trains > 0) {
+        int r = st.alloc();
+        if (r != ORB_OK) return r;
+        TriItem* items = st.hi<TriItem>(o_it);
+        TriTrain* trains = st.hi<TriTrain>(o_tr);
+        for_common_nodes(fv1, fv2, [&](int a, int b) {
+            const int cb = (int)train_of.size();
+            for (int i = fv2.offsets[b]; i < fv2.offsets[b + 1]; i++) {
+                const int idx2 = fv2.indices[i];
+                if (has_mp2[idx2]) continue;
+                if (only_stereo && !(uright2[idx2] >= 0)) continue;
+                TriTrain& t = trains[train_of.size()];
+                std::memcpy(t.desc, desc2 + (size_t)idx2 * 32, 32);
+                t.info = make_float4(kps2[idx2].x, kps2[idx2].y, (float)kps2[idx2].octave, uright2[idx2] >= 0 ? 1.f : 0.f);
                 train_of.push_back(idx2);
             }
-            cand.push_back(tmap[idx2]);
-        }
-        const int ce = (int)cand.size();
-        for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
-            const int idx1 = fv1.indices[i];
-            if (has_mp1[idx1]) continue;                              // :694-696
-            if (only_stereo && !(uright1[idx1] >= 0)) continue;       // :698-702
-            item_q.push_back(idx1);
-            rng.push_back(make_int2(cb, ce));
-        }
-    });
-    const int nitems = (int)item_q.size(), nt = (int)train_of.size(), ncand = (int)cand.size();
-    for (int j = 0; j < nt; j++) tmap[train_of[j]] = -1;   // (restore the invariant)
+            const int ce = (int)train_of.size();
+            if (ce == cb) return;
+            for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
+                const int idx1 = fv1.indices[i];
+                if (has_mp1[idx1]) continue;                              // :694-696
+                if (only_stereo && !(uright1[idx1] >= 0)) continue;       // :698-702
+                TriItem& q = items[item_q.size()];
+                std::memcpy(q.desc, desc1 + (size_t)idx1 * 32, 32);
+                q.x = kps1[idx1].x;
+                q.y = kps1[idx1].y;
+                q.c0 = cb;
+                q.c1 = ce;
+                q.stereo = uright1[idx1] >= 0 ? 1 : 0;
+                item_q.push_back(idx1);
+            }
+        });
+    }
+    const int nitems = (int)item_q.size();
     std::vector<int>& best = c->tri_best;
     best.assign(nitems, -1);
     if (nitems) {
-        Stage st{c};
-        st.zc = 1;   // one kernel over small inputs: reading the pinned mirror beats the DMA (Stage::zc)
-        const size_t o_qd = st.add((size_t)nitems * 32), o_qi = st.add((size_t)nitems * 16),
-                     o_td = st.add((size_t)nt * 32), o_ti = st.add((size_t)nt * 16), o_r = st.add((size_t)nitems * 8),
-                     o_c = st.add((size_t)ncand * 4);
-        const size_t o_in_end = st.off, o_b = st.add((size_t)nitems * 4), o_end = st.off;
-        int r = st.alloc();
-        if (r != ORB_OK) return r;
-        uint8_t* qd = st.hi<uint8_t>(o_qd);
-        float4* qi = st.hi<float4>(o_qi);
-        for (int i = 0; i < nitems; i++) {
-            const int idx1 = item_q[i];
-            std::memcpy(qd + (size_t)i * 32, desc1 + (size_t)idx1 * 32, 32);
-            qi[i] = make_float4(kps1[idx1].x, kps1[idx1].y, uright1[idx1] >= 0 ? 1.f : 0.f, 0.f);
-        }
-        uint8_t* td = st.hi<uint8_t>(o_td);
-        float4* ti = st.hi<float4>(o_ti);
-        for (int j = 0; j < nt; j++) {
-            const int idx2 = train_of[j];
-            std::memcpy(td + (size_t)j * 32, desc2 + (size_t)idx2 * 32, 32);
-            ti[j] = make_float4(kps2[idx2].x, kps2[idx2].y, (float)kps2[idx2].octave, uright2[idx2] >= 0 ? 1.f : 0.f);
-        }
-        if (nitems) std::memcpy(st.hi<int2>(o_r), rng.data(), (size_t)nitems * 8);
-        if (ncand) std::memcpy(st.hi<int>(o_c), cand.data(), (size_t)ncand * 4);
-        hipError_t e = st.up(0, o_in_end);
-        if (e != hipSuccess) return set_error("upload", e), ORB_ERR_HIP;
         TriParams tp;
         std::memset(&tp, 0, sizeof tp);
         std::memcpy(tp.F, F12, sizeof tp.F);
@@ -578,12 +565,11 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         }
         tp.only_stereo = only_stereo;
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-        e = launch_triangulation(st.di<uint8_t>(o_qd), st.di<float4>(o_qi), st.di<uint8_t>(o_td), st.di<float4>(o_ti),
-                                 st.di<int2>(o_r), st.di<int>(o_c), nitems, tp, st.h<int>(o_b), c->stream);
+        hipError_t e = launch_triangulation(st.di<TriItem>(o_it), st.di<TriTrain>(o_tr), nitems, tp, st.h<int>(o_b),
+                                            c->stream);
         if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
         if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
         // the kernel writes its results straight into the pinned mirror (host-coherent memory): no D2H command
-        (void)o_end;
         if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return set_error("download", e), ORB_ERR_HIP;
         const int* hb = st.h<int>(o_b);

@@ -210,12 +210,24 @@ struct TriParams {
     float sigma2[ORBGPU_MAX_LEVELS];
     int only_stereo;
 };
-// One work item per query (compacted on the host: descriptor, (x, y, stereo) in item order), its
-// candidates a [begin, end) range of d_cand (compact train indices: the trains without a map point, and
-// stereo ones only if asked, in the reference's per-node order); returns the best compact train (or -1).
-hipError_t launch_triangulation(const uint8_t* d_qdesc, const float4* d_qinfo, const uint8_t* d_tdesc,
-                                const float4* d_tinfo, const int2* d_ranges, const int* d_cand, int nitems,
-                                const TriParams& tp, int* d_best, hipStream_t stream);
+// SearchForTriangulation's staged inputs, read by k_triangulation straight from the pinned mirror (over PCIe):
+// one record per query (item) holding everything its wave needs, and the candidate trains' records in
+// candidate order, so a wave's reads are two dependent round trips (its item record, then its candidates').
+struct TriItem {          // 64 B
+    uint4 desc[2];
+    float x, y;
+    int c0, c1;           // the item's candidates: train records [c0, c1)
+    int stereo;           // mvuRight >= 0
+    int pad[3];
+};
+struct TriTrain {         // 48 B
+    uint4 desc[2];
+    float4 info;          // x, y, octave, stereo (1 / 0)
+};
+static_assert(sizeof(TriItem) == 64 && sizeof(TriTrain) == 48, "k_triangulation's record layout");
+// One work item per query with candidates; returns per item the best train record (or -1).
+hipError_t launch_triangulation(const TriItem* d_items, const TriTrain* d_trains, int nitems, const TriParams& tp,
+                                int* d_best, hipStream_t stream);
 
 // Frame::ComputeStereoMatches (stereo.hip).  One side of a rectified pair: its pyramid (level 0 in
 // `frames`, levels >= 1 in `pyr`) and extraction outputs, for pair p at frame frame0 + p*frame_step.
