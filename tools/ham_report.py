@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Summarise tools/ham_prof.sh: per-launch kernel durations of the Hamming leg from the rocprofv3 kernel
 trace, the bench line's own HIP-event figure, SQ / MFMA counters and HBM bytes per launch, and the
-MFMA-i8 roofline fraction recomputed from the trace.
+FP4 MFMA roofline fraction recomputed from the trace.
 
   ops per launch = 512 x sum over the 255 pairs of n_query x n_train    (32 x 32 pairs x K = 256 bits x 2 = 512
-                   ops per pair; bench.py `hamming.mfma_i8`, or `mfma_fp4` for the e2m1 form)
-  frac           = ops per launch / (leg wall time in the trace: the launch's first kernel start to its last
-                   kernel end, expansion and top-2 chunks overlapping on two streams) / the form's dense peak
-Counter sections are per dispatch (one chunk); rocprofv3 serialises dispatches while it counts.
+                   ops per pair; bench.py `hamming.mfma_fp4`)
+  frac           = ops per launch / (mean k_top2_mfma + mean k_top2b_merge duration in the trace: one launch is
+                   the top-2 kernel and, when the trains are sliced, the merge after it on the same stream) / 10 PF
+Counter sections are per dispatch; rocprofv3 serialises dispatches while it counts.
 
 FETCH_SIZE is doubled (gfx950 reports half of wide streaming reads, MI355X_MICROARCH.md §HBM); WRITE_SIZE
 is taken as is.  Usage: python3 tools/ham_report.py gpurun_out/ham > report.json
@@ -20,9 +20,8 @@ import re
 import sys
 from collections import defaultdict
 
-PEAK_I8_OPS = 5.0e15   # dense int8 MFMA: 2x the bf16 rate (2.5 PF dense), MI355X_MICROARCH.md §Matrix cores
-PEAK_FP4_OPS = 10.0e15  # dense fp4 (e2m1) MFMA: 4x the bf16 rate (ORBGPU_TOP2 'f')
-KERNELS = ("k_expand_pm1", "k_expand_fp4", "k_top2_mfma", "k_top2b_merge")
+PEAK_FP4_OPS = 10.0e15  # dense fp4 (e2m1) MFMA: 4x the bf16 rate (2.5 PF dense), MI355X_MICROARCH.md §Matrix cores
+KERNELS = ("k_top2_mfma", "k_top2b_merge")
 
 
 def kname(s):
@@ -35,21 +34,11 @@ def kname(s):
 def trace(d):
     fn = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     dur = defaultdict(list)
-    spans = []
     for row in csv.DictReader(open(fn[0])):
         k = kname(row["Kernel_Name"])
         if k:
-            t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
-            dur[k].append((t1 - t0) / 1e3)
-            spans.append((t0, t1))
-    return dur, fn[0], sorted(spans)
-
-
-def leg_spans(spans, legs):
-    """Wall time (us) of each Hamming leg launch: its kernels (expansion chunks on the side stream, top-2 chunks
-    on the launch stream, which overlap) from the first start to the last end."""
-    per = len(spans) // legs
-    return [(max(e for _, e in spans[i * per:(i + 1) * per]) - spans[i * per][0]) / 1e3 for i in range(legs)]
+            dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
+    return dur, fn[0]
 
 
 def counters(d):
@@ -75,20 +64,15 @@ def bench_line(path):
 def main(root):
     line = bench_line(os.path.join(root, "bench.log"))
     ham = line["hamming"]
-    mkey = "mfma_fp4" if "mfma_fp4" in ham else "mfma_i8"
-    peak = PEAK_FP4_OPS if mkey == "mfma_fp4" else PEAK_I8_OPS
+    mkey, peak = "mfma_fp4", PEAK_FP4_OPS
     ops = ham[mkey]["achieved_ops_per_s"] * ham["kernel_avg_us"] * 1e-6   # 512 x evals per launch
-    dur, tfile, spans = trace(os.path.join(root, "trace"))
-    legs = int(os.environ.get("HAM_LEGS", "21"))   # bench.py's Hamming leg: one warm launch + max(2, steps) timed
-    ls = leg_spans(spans, legs)[1:]                # the warm launch dropped
-    t_launch = sum(ls) / len(ls)
+    dur, tfile = trace(os.path.join(root, "trace"))
     mean = {k: sum(v) / len(v) for k, v in dur.items()}
+    t_launch = sum(mean.values())
     out = {"bench_line_hamming": ham, "ops_per_launch": ops, "trace_file": os.path.relpath(tfile, root),
            "trace_dispatches": {k: len(v) for k, v in dur.items()},
            "trace_mean_us_per_dispatch": {k: round(v, 3) for k, v in mean.items()},
-           "trace_leg_us": round(t_launch, 3),
-           "trace_leg_note": "per launch of orb_hamming_top2_frames_device: first kernel start to last kernel end "
-                             "(expansion chunks on the second stream overlap the top-2 chunks)",
+           "trace_launch_us": round(t_launch, 3),
            "mfma_form": mkey, "peak_ops_per_s": peak,
            "frac_from_trace": round(ops / (t_launch * 1e-6) / peak, 4),
            "frac_bench_line": ham[mkey]["frac"]}
