@@ -646,8 +646,8 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
     const size_t kbytes = ((size_t)kcap * sizeof(orb_keypoint) + 63) & ~(size_t)63;   // descriptors 64-B aligned
     const size_t need = 16 + kbytes + (size_t)kcap * 32;
     if ((e = grow(c->d_in, c->in_cap, pitch * hgt)) != hipSuccess) return set_error("device allocation", e), ORB_ERR_NOMEM;
-    // every allocation before the first launch: with the streamed upload the kernels queued below wait for the
-    // host copy at the end, so nothing in between may block on the stream (hipHostFree / hipFree do)
+    // every allocation before the first launch: with the streamed upload the upload kernel queued below polls for
+    // the host copy that follows it, so nothing in between may block on the stream (hipHostFree / hipFree do)
     if (need > c->pinned_cap) {
         if (c->h_pinned) (void)hipHostFree(c->h_pinned);
         c->h_pinned = nullptr;
@@ -676,7 +676,7 @@ int orb_extract(orb_ctx* h, const uint8_t* img, int w, int hgt, size_t stride, o
             std::memset(c->h_flags, 0, 64 * sizeof(uint32_t));
         }
         if (++c->upload_seq == 0) c->upload_seq = 1;   // (flags start at 0)
-        // the upload kernel first, the extraction kernels behind it (below), then the host copy raising the flags
+        // the upload kernel first; the host copy raising the band flags follows (below), then the extraction launches
         if ((e = launch_upload_stream(c->h_img, c->h_flags, c->upload_seq, c->d_in, (int)pitch, hgt, nbands, band_rows,
                                       c->h_flags + 63, c->stream)) != hipSuccess)
             return set_error("upload kernel", e), ORB_ERR_HIP;

@@ -78,8 +78,9 @@ struct Ctx {
     // host-image path (orb_extract)
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
-    // streamed upload (k_upload_stream; ORBGPU_UPLOAD=0: the pageable hipMemcpy2DAsync instead): the image's pinned
-    // host-coherent staging copy and the per-band flags the host raises (call sequence numbers)
+    // streamed upload (k_upload_stream; off by default, ORBGPU_UPLOAD=1 turns it on; off = the pageable
+    // hipMemcpy2DAsync): the image's pinned host-coherent staging copy and the per-band flags the host raises (call
+    // sequence numbers)
     bool upload_stream = false;
     uint8_t* h_img = nullptr;
     size_t himg_cap = 0;
