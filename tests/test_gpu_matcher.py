@@ -203,6 +203,46 @@ def test_search_for_triangulation(orbgpu_mod, oracle_mod, frames, only_stereo, c
     assert len(op) > 0
 
 
+@pytest.mark.parametrize("shape", ["one_node", "disjoint", "trains_all_mapped", "empty_fv1", "repeated_ids"])
+def test_search_for_triangulation_node_shapes(orbgpu_mod, oracle_mod, frames, shape):
+    """The staging shapes of orb_search_for_triangulation (one item record per query, the candidates' train records
+    in node order, queries of a node without candidates not staged): one node holding every feature
+    (candidate ranges far longer than a wave), FeatureVectors without a common node, every train carrying a map
+    point, an empty FeatureVector, and a train index listed in two nodes.  Pair for pair against the oracle."""
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(21)
+    mp1 = (rng.random(len(da)) < 0.3).astype(np.uint8)
+    mp2 = (rng.random(len(db)) < 0.3).astype(np.uint8)
+    ur1 = np.where(rng.random(len(da)) < 0.5, 10.0, -1.0).astype(np.float32)
+    ur2 = np.where(rng.random(len(db)) < 0.5, 10.0, -1.0).astype(np.float32)
+    F = np.array([[0, 0, 0], [0, 0, -1], [0, 1, 0]], np.float32) + rng.normal(0, 1e-4, (3, 3)).astype(np.float32)
+    fva, fvb = _featvec(da, 8), _featvec(db, 8)
+    if shape == "one_node":
+        fva, fvb = {3: list(range(len(da)))}, {3: list(range(len(db)))}
+    elif shape == "disjoint":
+        fvb = {k + 100: v for k, v in fvb.items()}
+    elif shape == "trains_all_mapped":
+        mp2[:] = 1
+    elif shape == "empty_fv1":
+        fva = {}
+    else:   # the reference's FeatureVector lists each feature once; a repeated index is staged once per listing
+        k0, k1 = sorted(fvb)[:2]
+        fvb[k1] = fvb[k1] + fvb[k0][:5]
+    t = oracle_mod.OracleExtractor(1000).tables()
+    m = orbgpu_mod.ORBmatcher(0.6, True)
+    pairs = m.SearchForTriangulation(da, ka, mp1, ur1, fva, db, kb, mp2, ur2, fvb, F, 320.0, 240.0, t["scale"],
+                                     t["sigma2"], False)
+    oa, _keep_a = _oracle_fv(oracle_mod, fva)
+    ob, _keep_b = _oracle_fv(oracle_mod, fvb)
+    op = oracle_mod.search_for_triangulation(True, False, da, ka, mp1, ur1, oa, db, kb, mp2, ur2, ob, F, 320.0, 240.0,
+                                             t["scale"], t["sigma2"])
+    assert np.array_equal(pairs, op)
+    if shape == "one_node":
+        assert len(op) > 0
+    if shape in ("disjoint", "trains_all_mapped", "empty_fv1"):
+        assert len(op) == 0
+
+
 @pytest.mark.parametrize("case", ["F_nan", "F_inf", "F_zero", "epipole_nan"])
 def test_search_for_triangulation_nonfinite(orbgpu_mod, oracle_mod, frames, case):
     """Degenerate geometry keeps the reference's IEEE semantics (ORBmatcher.cc:140-157, :725-733): a NaN or
