@@ -11,17 +11,20 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/orb-slam-birdview_amd
 make -s -C $PKG liborbgpu.so
 FLAGS=$(make -s -C $PKG --no-print-directory --eval 'print-hipflags: ; @echo $(HIPFLAGS)' print-hipflags)
-EXTRA=""
-case $STEM in
-  hamming_top2) EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans -fno-slp-vectorize" ;;
-  extract_kernels) EXTRA="-mllvm -amdgpu-mfma-vgpr-form" ;;
-esac
 mkdir -p $ROOT/ab/obj_$NAME
-/opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c $PKG/csrc/$STEM.hip -o $ROOT/ab/obj_$NAME/$STEM.o
+IFS=',' read -ra STEMS <<< "$STEM"
+for st in "${STEMS[@]}"; do
+  EXTRA=""
+  case $st in
+    hamming_top2) EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans -fno-slp-vectorize" ;;
+    extract_kernels) EXTRA="-mllvm -amdgpu-mfma-vgpr-form" ;;
+  esac
+  /opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c $PKG/csrc/$st.hip -o $ROOT/ab/obj_$NAME/$st.o
+done
 OBJS=""
 for o in $PKG/build/*.o; do
   b=$(basename $o)
-  if [ "$b" = "$STEM.o" ]; then OBJS="$OBJS $ROOT/ab/obj_$NAME/$STEM.o"; else OBJS="$OBJS $o"; fi
+  if [ -f $ROOT/ab/obj_$NAME/$b ]; then OBJS="$OBJS $ROOT/ab/obj_$NAME/$b"; else OBJS="$OBJS $o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -mcode-object-version=5 -shared -fPIC -o $ROOT/ab/liborbgpu_$NAME.so $OBJS
 rm -rf $ROOT/ab/obj_$NAME
