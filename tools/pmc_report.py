@@ -20,7 +20,7 @@ import sys
 from collections import defaultdict
 
 SHORT = {"k_fast": "fast", "k_fast_wave": "fast", "k_resize": "resize", "k_resize_tiled": "resize",
-         "k_octree": "octree", "k_describe": "describe", "k_top2_mfma": "hamming", "k_expand_pm1": "hamming_expand", "k_top2b_merge": "hamming_merge",
+         "k_octree": "octree", "k_describe": "describe", "k_top2_mfma": "hamming", "k_top2b_merge": "hamming_merge",
          "k_stereo": "stereo", "k_stereo_cut": "stereo_cut", "k_calib_read_u8": "calib_read_u8",
          "k_calib_read_u32": "calib_read_u32", "k_calib_read_u128": "calib_read_u128",
          "k_calib_write_u32": "calib_write_u32"}
