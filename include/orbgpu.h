@@ -256,7 +256,8 @@ int orb_search_by_bow_kf_kf(orb_ctx* ctx, float nnratio, int check_ori,
  * Keypoints are mvKeysUn; has_mp[i] <=> GetMapPoint(i) != NULL; uright = mvuRight; F12 row-major
  * 3x3; (ex, ey) the epipole of KF1's centre in KF2 (:662-668, computed by the caller from poses);
  * scale2/sigma2_2 = pKF2->mvScaleFactors / mvLevelSigma2.  pairs_out: 2 ints per pair (ascending
- * idx1), *npairs = count (ORB_ERR_CAPACITY if > cap). */
+ * idx1), *npairs = count (ORB_ERR_CAPACITY if > cap).  ORB_ERR_ARG for a FeatureVector CSR whose offsets do not
+ * start at 0 or decrease (the call stages at most offsets[nnodes] records per side). */
 int orb_search_for_triangulation(orb_ctx* ctx, int check_ori, int only_stereo,
                                  int n1, const uint8_t* desc1, const orb_keypoint* kps1, const uint8_t* has_mp1,
                                  const float* uright1, orb_featvec fv1,

@@ -58,6 +58,17 @@ void cull_rotation(const std::vector<int>* rotHist, std::vector<int>& matches, i
     }
 }
 
+// A FeatureVector CSR the walks below can trust: offsets start at 0 and never decrease (so the features of the
+// nodes a walk visits number at most offsets[nnodes], the size the staging is allocated for).  O(nnodes).
+bool featvec_ok(const orb_featvec& v) {
+    if (v.nnodes < 0 || (v.nnodes > 0 && (!v.offsets || !v.indices || !v.node_ids))) return false;
+    if (v.nnodes == 0) return true;
+    if (v.offsets[0] != 0) return false;
+    for (int i = 0; i < v.nnodes; i++)
+        if (v.offsets[i + 1] < v.offsets[i]) return false;
+    return true;
+}
+
 template <class F>
 void for_common_nodes(const orb_featvec& a, const orb_featvec& b, F f) {   // std::map merge (:175-264)
     int i = 0, j = 0;
@@ -502,6 +513,8 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
     if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
+    if (!featvec_ok(fv1) || !featvec_ok(fv2))
+        return set_error("orb_search_for_triangulation: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
     // The inputs, written once into the pinned mirror the kernel reads (the upload is the call's cost,
     // DESIGN §4.8): per common node its candidates without a map point (and stereo ones only if asked,
     // :725-733) as train records in the node's order (the reference keeps the last candidate reaching the

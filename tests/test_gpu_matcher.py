@@ -243,6 +243,41 @@ def test_search_for_triangulation_node_shapes(orbgpu_mod, oracle_mod, frames, sh
         assert len(op) == 0
 
 
+def test_search_for_triangulation_rejects_malformed_featvec(orbgpu_mod, oracle_mod, frames):
+    """A FeatureVector CSR whose offsets decrease or do not start at 0 is refused (ORB_ERR_ARG) before anything is
+    staged: the call sizes its pinned records from offsets[nnodes]."""
+    import ctypes
+    from orbgpu import _lib
+    ka, da, kb, db = frames
+    t = oracle_mod.OracleExtractor(1000).tables()
+    m = orbgpu_mod.ORBmatcher(0.6, True)
+    fva, fvb = _featvec(da, 8), _featvec(db, 8)
+    fb, _keep_b = orbgpu_mod._featvec(fvb)
+    for bad_off in ([0, 5, 3, len(da)], [2, 5, 9, len(da)]):
+        off = np.asarray(bad_off, np.int32)
+        ids = np.arange(len(off) - 1, dtype=np.uint32)
+        idx = np.arange(len(da), dtype=np.int32)
+        fa = orbgpu_mod.OrbFeatVec(len(ids), ids.ctypes.data, off.ctypes.data, idx.ctypes.data)
+        a = [np.ascontiguousarray(x) for x in (da, np.asarray(ka, orbgpu_mod.KP_DTYPE), np.zeros(len(da), np.uint8),
+                                                np.full(len(da), -1, np.float32), db,
+                                                np.asarray(kb, orbgpu_mod.KP_DTYPE), np.zeros(len(db), np.uint8),
+                                                np.full(len(db), -1, np.float32), np.eye(3, dtype=np.float32).reshape(9),
+                                                np.asarray(t["scale"], np.float32), np.asarray(t["sigma2"], np.float32))]
+        pairs = np.zeros((len(da) + 1, 2), np.int32)
+        n = ctypes.c_int()
+        p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+        st = _lib.lib().orb_search_for_triangulation(m._ctx.h, 1, 0, len(da), p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa,
+                                                     len(db), p(a[4]), p(a[5]), p(a[6]), p(a[7]), fb, p(a[8]), 320.0,
+                                                     240.0, p(a[9]), p(a[10]), len(a[9]), p(pairs), len(pairs),
+                                                     ctypes.byref(n))
+        assert _lib.STATUS.get(st) == "ORB_ERR_ARG", st
+    # the context stays usable
+    ok = m.SearchForTriangulation(da, ka, np.zeros(len(da), np.uint8), np.full(len(da), -1, np.float32), fva, db, kb,
+                                  np.zeros(len(db), np.uint8), np.full(len(db), -1, np.float32), fvb,
+                                  np.eye(3, dtype=np.float32), 320.0, 240.0, t["scale"], t["sigma2"])
+    assert ok.ndim == 2
+
+
 @pytest.mark.parametrize("case", ["F_nan", "F_inf", "F_zero", "epipole_nan"])
 def test_search_for_triangulation_nonfinite(orbgpu_mod, oracle_mod, frames, case):
     """Degenerate geometry keeps the reference's IEEE semantics (ORBmatcher.cc:140-157, :725-733): a NaN or
