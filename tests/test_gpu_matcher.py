@@ -203,12 +203,14 @@ def test_search_for_triangulation(orbgpu_mod, oracle_mod, frames, only_stereo, c
     assert len(op) > 0
 
 
-@pytest.mark.parametrize("shape", ["one_node", "disjoint", "trains_all_mapped", "empty_fv1", "repeated_ids"])
+@pytest.mark.parametrize("shape", ["one_node", "disjoint", "trains_all_mapped", "empty_fv1", "repeated_ids",
+                                   "200_nodes", "300_nodes"])
 def test_search_for_triangulation_node_shapes(orbgpu_mod, oracle_mod, frames, shape):
     """The staging shapes of orb_search_for_triangulation (one item record per query, the candidates' train records
     in node order, queries of a node without candidates not staged): one node holding every feature
     (candidate ranges far longer than a wave), FeatureVectors without a common node, every train carrying a map
-    point, an empty FeatureVector, and a train index listed in two nodes.  Pair for pair against the oracle."""
+    point, an empty FeatureVector, a train index listed in two nodes, and 200 / 300 common nodes.  Pair for pair
+    against the oracle."""
     ka, da, kb, db = frames
     rng = np.random.default_rng(21)
     mp1 = (rng.random(len(da)) < 0.3).astype(np.uint8)
@@ -225,6 +227,13 @@ def test_search_for_triangulation_node_shapes(orbgpu_mod, oracle_mod, frames, sh
         mp2[:] = 1
     elif shape == "empty_fv1":
         fva = {}
+    elif shape in ("200_nodes", "300_nodes"):
+        k = int(shape.split("_")[0])
+        fva, fvb = {}, {}
+        for i in range(len(da)):
+            fva.setdefault(i % k, []).append(i)
+        for i in range(len(db)):
+            fvb.setdefault(i % k, []).append(i)
     else:   # the reference's FeatureVector lists each feature once; a repeated index is staged once per listing
         k0, k1 = sorted(fvb)[:2]
         fvb[k1] = fvb[k1] + fvb[k0][:5]
@@ -237,7 +246,7 @@ def test_search_for_triangulation_node_shapes(orbgpu_mod, oracle_mod, frames, sh
     op = oracle_mod.search_for_triangulation(True, False, da, ka, mp1, ur1, oa, db, kb, mp2, ur2, ob, F, 320.0, 240.0,
                                              t["scale"], t["sigma2"])
     assert np.array_equal(pairs, op)
-    if shape == "one_node":
+    if shape in ("one_node", "200_nodes", "300_nodes"):
         assert len(op) > 0
     if shape in ("disjoint", "trains_all_mapped", "empty_fv1"):
         assert len(op) == 0
