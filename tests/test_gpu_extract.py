@@ -429,3 +429,31 @@ def test_small_batch_pyramid_plan_bit_exact(orbgpu_mod, oracle_mod, w, h, nf, B)
             for l in range(1, 8):
                 assert np.array_equal(e.debug_level_image(l, f), o.level(l)), (f, l)
     e.close()
+
+
+def test_extract_capacity_contract(orbgpu_mod):
+    """orb_extract with a too-small output buffer (include/orbgpu.h: ORB_ERR_CAPACITY with *n set to the required
+    count, outputs untouched), then again with exactly that capacity: the same keypoints and descriptors as the
+    wrapper's call."""
+    import ctypes
+    from orbgpu import _lib
+    from orbgpu.synth import synth_frame
+    img = np.ascontiguousarray(synth_frame(320, 240, 0, "scene"))
+    g = orbgpu_mod.ORBextractor(500, 1.2, 8, 20, 7)
+    ref_k, ref_d = g(img)
+    assert len(ref_k) > 10
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    for cap in (0, 10, len(ref_k) - 1):
+        kps = np.zeros(max(cap, 1), orbgpu_mod.KP_DTYPE)
+        desc = np.full((max(cap, 1), 32), 7, np.uint8)
+        n = ctypes.c_int(-1)
+        st = _lib.lib().orb_extract(g.h, p(img), 320, 240, img.strides[0], p(kps), cap, ctypes.byref(n), p(desc))
+        assert _lib.STATUS.get(st) == "ORB_ERR_CAPACITY", st
+        assert n.value == len(ref_k)
+        assert (desc == 7).all()
+    kps = np.zeros(len(ref_k), orbgpu_mod.KP_DTYPE)
+    desc = np.zeros((len(ref_k), 32), np.uint8)
+    n = ctypes.c_int(-1)
+    st = _lib.lib().orb_extract(g.h, p(img), 320, 240, img.strides[0], p(kps), len(ref_k), ctypes.byref(n), p(desc))
+    assert st == 0 and n.value == len(ref_k)
+    assert kps.tobytes() == ref_k.tobytes() and np.array_equal(desc, ref_d)

@@ -287,6 +287,37 @@ def test_search_for_triangulation_rejects_malformed_featvec(orbgpu_mod, oracle_m
     assert ok.ndim == 2
 
 
+def test_search_for_triangulation_capacity(orbgpu_mod, oracle_mod, frames):
+    """pairs_out smaller than the pair count: ORB_ERR_CAPACITY with *npairs = the count and the first cap pairs
+    written (include/orbgpu.h)."""
+    import ctypes
+    from orbgpu import _lib
+    ka, da, kb, db = frames
+    t = oracle_mod.OracleExtractor(1000).tables()
+    F = np.array([[0, 0, 0], [0, 0, -1], [0, 1, 0]], np.float32)
+    fva, fvb = _featvec(da, 8), _featvec(db, 8)
+    m = orbgpu_mod.ORBmatcher(0.6, False)
+    mp1, mp2 = np.zeros(len(da), np.uint8), np.zeros(len(db), np.uint8)
+    ur1, ur2 = np.full(len(da), -1, np.float32), np.full(len(db), -1, np.float32)
+    full = m.SearchForTriangulation(da, ka, mp1, ur1, fva, db, kb, mp2, ur2, fvb, F, 1e5, 1e5, t["scale"], t["sigma2"])
+    assert len(full) > 3
+    fa, _keep_a = orbgpu_mod._featvec(fva)
+    fb, _keep_b = orbgpu_mod._featvec(fvb)
+    a = [np.ascontiguousarray(x) for x in (da, np.asarray(ka, orbgpu_mod.KP_DTYPE), mp1, ur1, db,
+                                            np.asarray(kb, orbgpu_mod.KP_DTYPE), mp2, ur2, F.reshape(9),
+                                            np.asarray(t["scale"], np.float32), np.asarray(t["sigma2"], np.float32))]
+    cap = 3
+    pairs = np.full((cap, 2), -9, np.int32)
+    n = ctypes.c_int(-1)
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    st = _lib.lib().orb_search_for_triangulation(m._ctx.h, 0, 0, len(da), p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa,
+                                                 len(db), p(a[4]), p(a[5]), p(a[6]), p(a[7]), fb, p(a[8]), 1e5, 1e5,
+                                                 p(a[9]), p(a[10]), len(a[9]), p(pairs), cap, ctypes.byref(n))
+    assert _lib.STATUS.get(st) == "ORB_ERR_CAPACITY", st
+    assert n.value == len(full)
+    assert np.array_equal(pairs, full[:cap])
+
+
 @pytest.mark.parametrize("case", ["F_nan", "F_inf", "F_zero", "epipole_nan"])
 def test_search_for_triangulation_nonfinite(orbgpu_mod, oracle_mod, frames, case):
     """Degenerate geometry keeps the reference's IEEE semantics (ORBmatcher.cc:140-157, :725-733): a NaN or
