@@ -457,3 +457,20 @@ def test_extract_capacity_contract(orbgpu_mod):
     st = _lib.lib().orb_extract(g.h, p(img), 320, 240, img.strides[0], p(kps), len(ref_k), ctypes.byref(n), p(desc))
     assert st == 0 and n.value == len(ref_k)
     assert kps.tobytes() == ref_k.tobytes() and np.array_equal(desc, ref_d)
+
+
+@pytest.mark.parametrize("w,h", [(160, 120), (4100, 64), (64, 4100)])
+def test_extract_geometry_outside_the_reference_domain(orbgpu_mod, w, h):
+    """Frames the reference's grid cannot handle are refused with ORB_ERR_GEOMETRY, not computed: at 160 x 120 the
+    top level's border-trimmed width is below one 30-px cell (ComputeKeyPointsOctTree divides by nCols = 0,
+    ORBextractor.cc:784-786, and DistributeOctTree by nIni = 0, :543-545); past 4096 px the candidates' packed 12-bit
+    coordinates do not fit.  The context stays usable afterwards."""
+    from orbgpu.synth import synth_frame
+    g = orbgpu_mod.ORBextractor(500, 1.2, 8, 20, 7)
+    img = np.zeros((h, w), np.uint8)
+    img[::7, ::5] = 200
+    with pytest.raises(orbgpu_mod.OrbError) as ei:
+        g(img)
+    assert ei.value.status == -4   # ORB_ERR_GEOMETRY
+    k, d = g(np.ascontiguousarray(synth_frame(320, 240, 0, "scene")))
+    assert len(k) > 0 and d.shape == (len(k), 32)
