@@ -227,7 +227,9 @@ int orb_hamming_top2_slices(int npairs, int max_nq, int max_nt);
  * bound by the dense FP4 peak; the only form since round 5).  Host only (bench / tests). */
 int orb_hamming_top2_mfma_bits(void);
 
-/* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21) as CSR. */
+/* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21) as CSR.  The three
+ * FeatureVector matchers below return ORB_ERR_ARG (before any GPU work) for a CSR whose offsets do not start at
+ * 0 or decrease, whose indices leave [0, n) of their side, or whose node ids do not ascend strictly. */
 typedef struct {
     int nnodes;
     const uint32_t* node_ids;   /* ascending */
@@ -256,8 +258,8 @@ int orb_search_by_bow_kf_kf(orb_ctx* ctx, float nnratio, int check_ori,
  * Keypoints are mvKeysUn; has_mp[i] <=> GetMapPoint(i) != NULL; uright = mvuRight; F12 row-major
  * 3x3; (ex, ey) the epipole of KF1's centre in KF2 (:662-668, computed by the caller from poses);
  * scale2/sigma2_2 = pKF2->mvScaleFactors / mvLevelSigma2.  pairs_out: 2 ints per pair (ascending
- * idx1), *npairs = count (ORB_ERR_CAPACITY if > cap).  ORB_ERR_ARG for a FeatureVector CSR whose offsets do not
- * start at 0 or decrease (the call stages at most offsets[nnodes] records per side). */
+ * idx1), *npairs = count (ORB_ERR_CAPACITY if > cap).  ORB_ERR_ARG for a malformed FeatureVector CSR (see
+ * orb_featvec; the call stages at most offsets[nnodes] records per side). */
 int orb_search_for_triangulation(orb_ctx* ctx, int check_ori, int only_stereo,
                                  int n1, const uint8_t* desc1, const orb_keypoint* kps1, const uint8_t* has_mp1,
                                  const float* uright1, orb_featvec fv1,

@@ -59,13 +59,19 @@ void cull_rotation(const std::vector<int>* rotHist, std::vector<int>& matches, i
 }
 
 // A FeatureVector CSR the walks below can trust: offsets start at 0 and never decrease (so the features of the
-// nodes a walk visits number at most offsets[nnodes], the size the staging is allocated for).  O(nnodes).
-bool featvec_ok(const orb_featvec& v) {
+// nodes a walk visits number at most offsets[nnodes], the size the staging is allocated for), every feature index
+// lies in [0, n) (the walks index the descriptors, keypoints and map-point flags with it), and node ids ascend
+// strictly (for_common_nodes is the std::map merge, which assumes ordered unique keys).  O(nnodes + nnz).
+bool featvec_ok(const orb_featvec& v, int n) {
     if (v.nnodes < 0 || (v.nnodes > 0 && (!v.offsets || !v.indices || !v.node_ids))) return false;
     if (v.nnodes == 0) return true;
     if (v.offsets[0] != 0) return false;
-    for (int i = 0; i < v.nnodes; i++)
+    for (int i = 0; i < v.nnodes; i++) {
         if (v.offsets[i + 1] < v.offsets[i]) return false;
+        if (i > 0 && v.node_ids[i] <= v.node_ids[i - 1]) return false;
+    }
+    for (int k = 0; k < v.offsets[v.nnodes]; k++)
+        if (v.indices[k] < 0 || v.indices[k] >= n) return false;
     return true;
 }
 
@@ -346,13 +352,16 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
     for (int p = 0; p < npairs && same; p++)
         same = c->pairs_last[2 * p] == q_frames[p] && c->pairs_last[2 * p + 1] == t_frames[p];
     if (!same) {
-        c->pairs_last.resize((size_t)2 * npairs);
+        // the new list is committed to pairs_last only once its upload is queued: after any failure below the cache
+        // still names what d_pairs holds (or is empty), so a retry with the same list uploads it again
+        std::vector<int> want((size_t)2 * npairs);
         for (int p = 0; p < npairs; p++) {
-            c->pairs_last[2 * p] = q_frames[p];
-            c->pairs_last[2 * p + 1] = t_frames[p];
+            want[2 * p] = q_frames[p];
+            want[2 * p + 1] = t_frames[p];
         }
         const size_t bytes = (size_t)npairs * sizeof(int2);
         if (bytes > c->dpairs_cap || !c->d_pairs) {
+            c->pairs_last.clear();   // d_pairs is about to be replaced: its old contents are no longer cached
             if (c->d_pairs) {
                 // (a launch queued earlier may still read the old buffer)
                 if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
@@ -360,10 +369,8 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
             }
             c->d_pairs = nullptr;
             c->dpairs_cap = 0;
-            if ((e = hipMalloc((void**)&c->d_pairs, std::max<size_t>(bytes, 4096))) != hipSuccess) {
-                c->pairs_last.clear();
+            if ((e = hipMalloc((void**)&c->d_pairs, std::max<size_t>(bytes, 4096))) != hipSuccess)
                 return set_error("hipMalloc pairs", e), ORB_ERR_NOMEM;
-            }
             c->dpairs_cap = std::max<size_t>(bytes, 4096);
         }
         // staged through two pinned slots used in turn: a slot is rewritten only after the event recorded behind
@@ -379,18 +386,17 @@ int orb_hamming_top2_frames_device(orb_ctx* h, const uint8_t* d_desc, const int*
             c->h_pairs[sl] = nullptr;
             c->pairs_cap[sl] = 0;
             const size_t cap = std::max<size_t>(bytes, 4096);
-            if ((e = hipHostMalloc((void**)&c->h_pairs[sl], cap, hipHostMallocDefault)) != hipSuccess) {
-                c->pairs_last.clear();
+            if ((e = hipHostMalloc((void**)&c->h_pairs[sl], cap, hipHostMallocDefault)) != hipSuccess)
                 return set_error("pairs pinned staging", e), ORB_ERR_NOMEM;
-            }
             c->pairs_cap[sl] = cap;
         }
-        std::memcpy(c->h_pairs[sl], c->pairs_last.data(), bytes);
+        std::memcpy(c->h_pairs[sl], want.data(), bytes);
         if ((e = hipMemcpyAsync(c->d_pairs, c->h_pairs[sl], bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
             (e = hipEventRecord(c->pairs_ev[sl], c->stream)) != hipSuccess) {
-            c->pairs_last.clear();
+            c->pairs_last.clear();   // the copy may or may not be queued: d_pairs' contents are unknown
             return set_error("upload pairs", e), ORB_ERR_HIP;
         }
+        c->pairs_last.swap(want);
     }
     Arena a{c};
     const int ns = top2_batch_slices(npairs, kp_cap, kp_cap);
@@ -413,6 +419,8 @@ int orb_search_by_bow_kf_f(orb_ctx* h, float nnratio, int check_ori, int n_kf, c
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
     if (n_kf < 0 || n_f < 0 || !match_f) return ORB_ERR_ARG;
+    if (!featvec_ok(fv_kf, n_kf) || !featvec_ok(fv_f, n_f))
+        return set_error("orb_search_by_bow_kf_f: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
     TopkSession s{c};
     s.cand = fv_f.indices;
     s.ncand = fv_f.nnodes ? fv_f.offsets[fv_f.nnodes] : 0;
@@ -460,6 +468,8 @@ int orb_search_by_bow_kf_kf(orb_ctx* h, float nnratio, int check_ori, int n1, co
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
     if (n1 < 0 || n2 < 0 || !match12) return ORB_ERR_ARG;
+    if (!featvec_ok(fv1, n1) || !featvec_ok(fv2, n2))
+        return set_error("orb_search_by_bow_kf_kf: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
     TopkSession s{c};
     s.cand = fv2.indices;
     s.ncand = fv2.nnodes ? fv2.offsets[fv2.nnodes] : 0;
@@ -513,7 +523,7 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
     if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
-    if (!featvec_ok(fv1) || !featvec_ok(fv2))
+    if (!featvec_ok(fv1, n1) || !featvec_ok(fv2, n2))
         return set_error("orb_search_for_triangulation: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
     // The inputs, written once into the pinned mirror the kernel reads (the upload is the call's cost,
     // DESIGN §4.8): per common node its candidates without a map point (and stereo ones only if asked,

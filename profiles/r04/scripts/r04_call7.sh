@@ -1,4 +1,5 @@
 # Hamming A/B + profile, then the C5 one-frame-per-step fork A/B
+# (archived round-4 record: the tools/r04_*.sh scripts it calls were moved out of tools/ in round 5; not runnable as is)
 set -o pipefail
 mkdir -p gpurun_out/c7; export TMPDIR=/tmp
 bash tools/r04_ham_ab2.sh || exit 1

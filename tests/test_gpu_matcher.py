@@ -253,35 +253,62 @@ def test_search_for_triangulation_node_shapes(orbgpu_mod, oracle_mod, frames, sh
 
 
 def test_search_for_triangulation_rejects_malformed_featvec(orbgpu_mod, oracle_mod, frames):
-    """A FeatureVector CSR whose offsets decrease or do not start at 0 is refused (ORB_ERR_ARG) before anything is
-    staged: the call sizes its pinned records from offsets[nnodes]."""
+    """A FeatureVector CSR whose offsets decrease or do not start at 0, whose feature indices leave [0, n), or whose
+    node ids do not ascend strictly is refused (ORB_ERR_ARG) before anything is staged or walked, by
+    SearchForTriangulation and both SearchByBoW forms: the calls size their pinned records from offsets[nnodes],
+    index descriptors / keypoints / map-point flags with the indices, and merge the two node lists as std::map
+    keys (matcher.hip featvec_ok)."""
     import ctypes
     from orbgpu import _lib
     ka, da, kb, db = frames
+    n1 = len(da)
     t = oracle_mod.OracleExtractor(1000).tables()
     m = orbgpu_mod.ORBmatcher(0.6, True)
     fva, fvb = _featvec(da, 8), _featvec(db, 8)
     fb, _keep_b = orbgpu_mod._featvec(fvb)
-    for bad_off in ([0, 5, 3, len(da)], [2, 5, 9, len(da)]):
-        off = np.asarray(bad_off, np.int32)
-        ids = np.arange(len(off) - 1, dtype=np.uint32)
-        idx = np.arange(len(da), dtype=np.int32)
+    q = n1 // 3
+    idx_ok = np.arange(n1, dtype=np.int32)
+    idx_hi = idx_ok.copy()
+    idx_hi[5] = n1          # one past the last feature
+    idx_neg = idx_ok.copy()
+    idx_neg[7] = -1
+    cases = {   # (node ids, offsets, indices)
+        "offsets_decrease": ([0, 1, 2], [0, 5, 3, n1], idx_ok),
+        "offsets_not_zero": ([0, 1, 2], [2, 5, 9, n1], idx_ok),
+        "index_past_n": ([0, 1, 2], [0, q, 2 * q, n1], idx_hi),
+        "index_negative": ([0, 1, 2], [0, q, 2 * q, n1], idx_neg),
+        "ids_repeated": ([0, 2, 2], [0, q, 2 * q, n1], idx_ok),
+        "ids_descending": ([5, 3, 1], [0, q, 2 * q, n1], idx_ok),
+    }
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    L = _lib.lib()
+    for name, (ids_l, off_l, idx) in cases.items():
+        off = np.asarray(off_l, np.int32)
+        ids = np.asarray(ids_l, np.uint32)
         fa = orbgpu_mod.OrbFeatVec(len(ids), ids.ctypes.data, off.ctypes.data, idx.ctypes.data)
-        a = [np.ascontiguousarray(x) for x in (da, np.asarray(ka, orbgpu_mod.KP_DTYPE), np.zeros(len(da), np.uint8),
-                                                np.full(len(da), -1, np.float32), db,
+        a = [np.ascontiguousarray(x) for x in (da, np.asarray(ka, orbgpu_mod.KP_DTYPE), np.zeros(n1, np.uint8),
+                                                np.full(n1, -1, np.float32), db,
                                                 np.asarray(kb, orbgpu_mod.KP_DTYPE), np.zeros(len(db), np.uint8),
                                                 np.full(len(db), -1, np.float32), np.eye(3, dtype=np.float32).reshape(9),
                                                 np.asarray(t["scale"], np.float32), np.asarray(t["sigma2"], np.float32))]
-        pairs = np.zeros((len(da) + 1, 2), np.int32)
+        pairs = np.zeros((n1 + 1, 2), np.int32)
         n = ctypes.c_int()
-        p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
-        st = _lib.lib().orb_search_for_triangulation(m._ctx.h, 1, 0, len(da), p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa,
-                                                     len(db), p(a[4]), p(a[5]), p(a[6]), p(a[7]), fb, p(a[8]), 320.0,
-                                                     240.0, p(a[9]), p(a[10]), len(a[9]), p(pairs), len(pairs),
-                                                     ctypes.byref(n))
-        assert _lib.STATUS.get(st) == "ORB_ERR_ARG", st
+        st = L.orb_search_for_triangulation(m._ctx.h, 1, 0, n1, p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa,
+                                            len(db), p(a[4]), p(a[5]), p(a[6]), p(a[7]), fb, p(a[8]), 320.0,
+                                            240.0, p(a[9]), p(a[10]), len(a[9]), p(pairs), len(pairs), ctypes.byref(n))
+        assert _lib.STATUS.get(st) == "ORB_ERR_ARG", (name, st)
+        ang1, ang2 = np.zeros(n1, np.float32), np.zeros(len(db), np.float32)
+        mp1, mp2 = np.ones(n1, np.uint8), np.ones(len(db), np.uint8)
+        match = np.full(max(n1, len(db)), -7, np.int32)
+        st = L.orb_search_by_bow_kf_f(m._ctx.h, 0.7, 1, n1, p(a[0]), p(ang1), p(mp1), fa, len(db), p(a[4]), p(ang2),
+                                      fb, p(match), ctypes.byref(n))
+        assert _lib.STATUS.get(st) == "ORB_ERR_ARG", (name, "kf_f", st)
+        st = L.orb_search_by_bow_kf_kf(m._ctx.h, 0.75, 1, n1, p(a[0]), p(ang1), p(mp1), fa, len(db), p(a[4]),
+                                       p(ang2), p(mp2), fb, p(match), ctypes.byref(n))
+        assert _lib.STATUS.get(st) == "ORB_ERR_ARG", (name, "kf_kf", st)
+        assert (match == -7).all(), name   # nothing written
     # the context stays usable
-    ok = m.SearchForTriangulation(da, ka, np.zeros(len(da), np.uint8), np.full(len(da), -1, np.float32), fva, db, kb,
+    ok = m.SearchForTriangulation(da, ka, np.zeros(n1, np.uint8), np.full(n1, -1, np.float32), fva, db, kb,
                                   np.zeros(len(db), np.uint8), np.full(len(db), -1, np.float32), fvb,
                                   np.eye(3, dtype=np.float32), 320.0, 240.0, t["scale"], t["sigma2"])
     assert ok.ndim == 2

@@ -10,21 +10,18 @@ NAME=${1:?name}; STEM=${2:?csrc stem}; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/orb-slam-birdview_amd
 make -s -C $PKG liborbgpu.so
-FLAGS=$(make -s -C $PKG --no-print-directory --eval 'print-hipflags: ; @echo $(HIPFLAGS)' print-hipflags)
 mkdir -p $ROOT/ab/obj_$NAME
 IFS=',' read -ra STEMS <<< "$STEM"
 for st in "${STEMS[@]}"; do
-  EXTRA=""
-  case $st in
-    hamming_top2) EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans -fno-slp-vectorize" ;;
-    extract_kernels) EXTRA="-mllvm -amdgpu-mfma-vgpr-form" ;;
-  esac
-  /opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c $PKG/csrc/$st.hip -o $ROOT/ab/obj_$NAME/$st.o
+  # the Makefile's own flags for this object (HIPFLAGS + EXTRA_<stem>): variants compile as the library does
+  FLAGS=$(make -s -C $PKG --no-print-directory print-flags-$st)
+  /opt/rocm/bin/hipcc $FLAGS "$@" -c $PKG/csrc/$st.hip -o $ROOT/ab/obj_$NAME/$st.o
 done
+# the library's object list from the Makefile (not a glob: a stale object of a deleted source stays out)
 OBJS=""
-for o in $PKG/build/*.o; do
+for o in $(make -s -C $PKG --no-print-directory print-objs); do
   b=$(basename $o)
-  if [ -f $ROOT/ab/obj_$NAME/$b ]; then OBJS="$OBJS $ROOT/ab/obj_$NAME/$b"; else OBJS="$OBJS $o"; fi
+  if [ -f $ROOT/ab/obj_$NAME/$b ]; then OBJS="$OBJS $ROOT/ab/obj_$NAME/$b"; else OBJS="$OBJS $PKG/$o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -mcode-object-version=5 -shared -fPIC -o $ROOT/ab/liborbgpu_$NAME.so $OBJS
 rm -rf $ROOT/ab/obj_$NAME
