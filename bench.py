@@ -59,7 +59,7 @@ CONFIGS = {   # BASELINE.json configs; C3 is the headline single-GPU workload
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 PEAK_FP4_OPS = 10.0e15           # MI355X_MICROARCH.md: FP4 (e2m1) MFMA = 4x the dense BF16 rate per clock
 MIN_WARMUP_S = 0.3                # extraction warm-up floor (seconds of steps) before the timed loop
-KNAMES = ["resize", "fast", "octree", "describe", "hamming", "stereo"]   # ORB_K_* order
+KNAMES = ["resize", "fast", "octree", "describe", "hamming", "stereo", "flow"]   # ORB_K_* order
 
 
 # ---------------------------------------------------------------- distributed plumbing
@@ -162,6 +162,7 @@ def algorithmic_bytes(w, h, kps_per_frame, cands_per_frame):
         "octree": 4 * C + 4 * K,                      # read candidates, write survivors
         "describe": K * (43 * 43 + 28 + 32),          # 43x43 window per keypoint, KeyPoint + descriptor out
         "pipeline": 3 * Ptot + 1321 * K,              # SURVEY §8d B_extract = 3P + 1321K
+        "flow": 3 * Ptot + 1321 * K,                  # the dataflow launch (small batches) runs the whole pipeline
     }
 
 
@@ -518,7 +519,8 @@ def main():
     tmax, total_kps = reduce_max_sum(dist, local_time, float(kps_per_step * args.steps))
     _, total_frames = reduce_max_sum(dist, 0.0, float(B * args.steps))
     ranks = gather(dist, {"rank": rank, "device": local, "host": socket.gethostname(),
-                          "frames_per_step": B, "seconds": round(local_time, 6)})
+                          "frames_per_step": B, "first_frame": first, "keypoints_per_step": kps_per_step,
+                          "seconds": round(local_time, 6)})
 
     # per-kernel breakdown (HIP events on the library's stream) from a separate pass of the same steps
     kms = None
@@ -590,7 +592,8 @@ def main():
     roofline, ms_per_step_k = None, None
     if kms is not None:
         steps = args.steps
-        ms_per_step_k = {KNAMES[i]: kms[i] / steps for i in range(4)}
+        # (a small batch runs as one dataflow launch, ORB_K_FLOW: then that is the only extraction kernel)
+        ms_per_step_k = {KNAMES[i]: kms[i] / steps for i in (0, 1, 2, 3, 6) if klaunch[i] > 0}
         dom = max(ms_per_step_k, key=ms_per_step_k.get)
         dom_bytes = ab[dom] * B
         dom_s = ms_per_step_k[dom] / 1e3

@@ -121,7 +121,8 @@ int   orb_memset_device(orb_ctx* ctx, void* dst, int value, size_t bytes);
 
 /* ---- per-kernel timing with HIP events on the context stream (bench roofline) ---- */
 enum { ORB_K_RESIZE = 0, ORB_K_FAST = 1, ORB_K_OCTREE = 2, ORB_K_DESCRIBE = 3, ORB_K_HAMMING = 4,
-       ORB_K_STEREO = 5, ORB_K_COUNT = 6 };
+       ORB_K_STEREO = 5, ORB_K_FLOW = 6 /* the small-batch dataflow launch: every stage in one kernel */,
+       ORB_K_COUNT = 7 };
 int orb_profile_enable(orb_ctx* ctx, int on);   /* clears accumulated times */
 int orb_profile_read(orb_ctx* ctx, double* ms_total /*ORB_K_COUNT*/, int* launches /*ORB_K_COUNT*/);
 
@@ -133,7 +134,10 @@ int orb_debug_candidates(orb_ctx* ctx, int frame, int level, int* out, int cap);
 int orb_debug_level_keypoints(orb_ctx* ctx, int frame, int level, int* out, int cap);
 int orb_debug_level_image(orb_ctx* ctx, int frame, int level, uint8_t* out, int* w, int* h);
 /* Phase timestamps of the last FAST launch (diagnostic; only with ORBGPU_FAST_STAMPS=1 in the
- * environment at orb_create): 8 s_memtime values per (frame, cell) item.  Returns the count copied. */
+ * environment at orb_create): 8 s_memtime values per (frame, cell) item.  With ORBGPU_FLOW_STAMPS=1 instead,
+ * the last dataflow launch's: 4 values per task in ticket order (100 MHz s_memrealtime when its ticket was
+ * taken, when its wait ended, when it was done; then kind | level << 8 | frame << 16 | workgroup << 32).
+ * Returns the count copied. */
 int orb_debug_fast_stamps(orb_ctx* ctx, uint64_t* out, int cap);
 /* The BRIEF rotation's sin/cos as the kernels compute them (glibc sinf/cosf restated, ORBextractor.cc:113)
  * for n host angles (radians, 0 <= x < 120): s[i] = sinf(x[i]), c[i] = cosf(x[i]).  Pin test only. */

@@ -140,25 +140,31 @@ __device__ __forceinline__ unsigned rs_vpass(unsigned c0, unsigned c1, unsigned 
     return (mul_hi_u24(c0, h0 & ~15u) + mul_hi_u24(c1, h1 & ~15u) + 2) >> 2;
 }
 
-template <int kRsTileH, bool GENERIC>
-__global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
-                                                      const ResizeCoef* __restrict__ coef, int level,
-                                                      const uint8_t* __restrict__ frames, long long framePitch,
-                                                      int rowStride, uint8_t* __restrict__ pyr) {
+// Cache policy of the loads and stores that hand data between workgroups inside one launch (the small-batch
+// dataflow launch k_extract_flow, below): 0 everywhere else; kCpSc1 = sc1, the write-through stores and
+// L1-bypassing loads of MI355X_MICROARCH.md's inter-workgroup hand-off (every producer store and every consumer
+// load of the handed-off bytes carries it, so no release or acquire fence is needed)
+constexpr int kCpSc1 = 16;
+
+// One 128 x TH output tile (bx, by) of level `level` for frame f, by the 256 threads tid = 0..255 of a block (or
+// of a quarter of k_extract_flow's 1024-thread block: every thread of the block reaches its one barrier; an
+// inactive quarter stages nothing and stores nothing).
+template <int kRsTileH, bool GENERIC, int CP>
+__device__ __forceinline__ void resize_tile(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef, int level,
+                                            const uint8_t* __restrict__ frames, long long framePitch, int rowStride,
+                                            uint8_t* __restrict__ pyr, int f, int bx, int by, int tid, uint8_t* s_src,
+                                            int4* s_cx, int4* s_cy, bool active) {
     constexpr int kRows = rs_rows(kRsTileH);
     constexpr int kQ = kRsPitch / 16;                                  // 16-byte chunks per LDS row
     constexpr int kPer = (kRows * kQ + 255) / 256;                     // chunks per thread (upper bound)
-    // the source tile, sized on the host to the level's largest span (LevelGeom::rs_span_rows <= kRows)
-    // rather than kRows: a smaller block footprint, more resident blocks
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
-    __shared__ int4 s_cx[kRsTileW];
-    __shared__ int4 s_cy[kRsTileH];
-    const int f = blockIdx.z;
     const int dw = g->L[level].w, dh = g->L[level].h;
-    const int x0 = blockIdx.x * kRsTileW, y0 = blockIdx.y * kRsTileH;
-    const int tid = threadIdx.x;
+    const int x0 = bx * kRsTileW, y0 = by * kRsTileH;
     const LevelPtr src = level_ptr(g, level - 1, frames, framePitch, rowStride, pyr, f);
     const int nx = min(kRsTileW, dw - x0), ny = min(kRsTileH, dh - y0);
+    if (!active) {
+        __syncthreads();
+        return;
+    }
     // source span (the coefficient tables are monotone); wave-uniform, so these are scalar loads
     const bool vec16 = ((reinterpret_cast<uintptr_t>(src.p) | (uintptr_t)src.stride) & 15) == 0;
     const int sx0 = coef[x0].s0 & (vec16 ? ~15 : ~3), sx1 = coef[x0 + nx - 1].s1;
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
         for (int k = 0; k < kPer; k++) {   // unconditional (clamped) loads: all in flight before the first wait
             const int i = min(tid + 256 * k, total - 1);
             const int r = (int)(__umul24((unsigned)i, magic) >> 16), q = i - (int)__umul24((unsigned)r, (unsigned)nq);
-            const uint32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)__umul24((unsigned)r, (unsigned)src.stride) + 16 * q, 0, 0);
+            const uint32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)__umul24((unsigned)r, (unsigned)src.stride) + 16 * q, 0, CP);
             v[k] = make_uint4(w[0], w[1], w[2], w[3]);
         }
         if (tid < kRsTileW) {
@@ -281,7 +287,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
                 const unsigned v = rs_vpass<GENERIC>(cy0, cy1, h0, h1);
                 packed |= v << (8 * i);
             }
-            __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, CP);
         }
         return;
     }
@@ -300,8 +306,22 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
             const unsigned v = rs_vpass<GENERIC>((unsigned)cy.z, (unsigned)cy.w, h0, h1);
             packed |= v << (8 * i);
         }
-        __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(packed, dsr, (int)(__umul24((unsigned)(y0 + ty), (unsigned)pitch) + dcol), 0, CP);
     }
+}
+
+template <int kRsTileH, bool GENERIC>
+__global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
+                                                      const ResizeCoef* __restrict__ coef, int level,
+                                                      const uint8_t* __restrict__ frames, long long framePitch,
+                                                      int rowStride, uint8_t* __restrict__ pyr) {
+    // the source tile, sized on the host to the level's largest span (LevelGeom::rs_span_rows <= kRows)
+    // rather than kRows: a smaller block footprint, more resident blocks
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
+    __shared__ int4 s_cx[kRsTileW];
+    __shared__ int4 s_cy[kRsTileH];
+    resize_tile<kRsTileH, GENERIC, 0>(g, coef, level, frames, framePitch, rowStride, pyr, blockIdx.z, blockIdx.x,
+                                      blockIdx.y, threadIdx.x, s_src, s_cx, s_cy, true);
 }
 
 /* Few-launch pyramid for small batches (the host path's single frame, C5's per-GPU frame): the levels
@@ -699,6 +719,7 @@ __device__ __forceinline__ bool roi_row_ok(const FastCellT& c, const RoiLanes& r
     return r.yy0 < r.rpr && r.yy0 + k * r.rpr < c.rh;
 }
 
+template <int CP = 0>
 __device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uint32_t (&v)[8]) {
     const RoiLanes r = roi_lanes(c, lane);
     // rows past the ROI lie past the descriptor's num_records ((rh - 1) * stride + 4 nw <= rh * stride
@@ -707,7 +728,7 @@ __device__ __forceinline__ void fast_roi_issue(const FastCellT& c, int lane, uin
     const int off = r.yy0 < r.rpr ? r.off : 0x40000000;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-        v[k] = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, off + k * r.rpr * c.stride, 0, 0);
+        v[k] = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, off + k * r.rpr * c.stride, 0, CP);
 }
 
 // ROI -> 16-bit LDS tile (rows TQ elements apart): ROI column c at element c + 1, so that every
@@ -747,7 +768,7 @@ __device__ __forceinline__ void widen_store(uint32_t* q, uint32_t v, uint32_t pv
 }
 
 // the prefetched rows (round k: ROI row yy0 + k * rpr) and, for a tall ROI, the rows past them
-template <int TQ, bool ODD>
+template <int TQ, bool ODD, int CP>
 __device__ __forceinline__ void widen_rows(const FastCellT& c, const RoiLanes& r, const uint32_t (&v)[8], uint32_t* t32,
                                            int B, bool last) {
     const WidenSel S = ODD ? WidenSel{sgpr_const(0x0c010c00u), sgpr_const(0x0c030c02u)}
@@ -764,21 +785,25 @@ __device__ __forceinline__ void widen_rows(const FastCellT& c, const RoiLanes& r
     }
     if (on)
         for (int yy = r.yy0 + 8 * rpr; yy < rh; yy += rpr) {   // lanes of one row iterate together
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + r.ww) * 4));
+            uint32_t w;
+            if constexpr (CP != 0) w = __builtin_amdgcn_raw_buffer_load_b32(r.rsrc, (int)roi_off(yy, c.stride, 4 * r.ww), 0, CP);
+            else w = *reinterpret_cast<const uint32_t*>(c.base + roi_off(yy, c.stride, (c.x0w + r.ww) * 4));
             const uint32_t pw = ODD ? 0u : dpp_prev_lane(w);
             widen_store<ODD>(t32 + (yy * (TQ / 2) + 2 * r.ww - (B >> 1)), w, pw, last, S);
         }
 }
 
-template <int TQ>
+// (CP: the unaligned byte path below reads only the caller's frame, level 0, never handed-off pyramid bytes: the
+// pyramid levels are 64-byte aligned rows in a 256-byte aligned slot)
+template <int TQ, int CP = 0>
 __device__ __forceinline__ void fast_roi_store(const FastCellT& c, int lane, const uint32_t (&v)[8], uint16_t* tile) {
     uint32_t* t32 = reinterpret_cast<uint32_t*>(tile);
     if (c.aligned) {
         const RoiLanes r = roi_lanes(c, lane);
         const int B = c.iniX & 3;
         const bool last = r.ww == __builtin_amdgcn_readfirstlane(c.nw) - 1;
-        if (B & 1) widen_rows<TQ, true>(c, r, v, t32, B, last);
-        else widen_rows<TQ, false>(c, r, v, t32, B, last);
+        if (B & 1) widen_rows<TQ, true, CP>(c, r, v, t32, B, last);
+        else widen_rows<TQ, false, CP>(c, r, v, t32, B, last);
         return;
     }
     const uint32_t mrw = recip20(c.rw);
@@ -857,7 +882,7 @@ __device__ __forceinline__ int prefilter_cell(const uint32_t* t32, int dh, int r
 // of a scored pixel is kept in the high byte of its tile element (pixels are < 256, and the widening
 // store leaves every high byte 0), so the NMS reads neighbours' M from the tile: no separate map to
 // clear, and unscored pixels read 0.
-template <int TQ>
+template <int TQ, int CP = 0>
 __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const FastCellT& c, int lane,
                                                uint16_t* tile, uint16_t* sList,
                                                uint32_t* __restrict__ cands, uint32_t* __restrict__ candFirst,
@@ -948,8 +973,14 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
             const unsigned long long km = __ballot(k);
             const int slot = kept + lanes_below(km);
             if (k) {
-                if (slot < kCandFirst) candFirst[((long long)c.f * g->ncells + c.cell) * kCandRec + 1 + slot] = packed;
-                else cands[(long long)c.f * g->ncand + c.out_off + slot] = packed;
+                if constexpr (CP != 0) {
+                    uint32_t* dst = slot < kCandFirst ? &candFirst[((long long)c.f * g->ncells + c.cell) * kCandRec + 1 + slot]
+                                                      : &cands[(long long)c.f * g->ncand + c.out_off + slot];
+                    __hip_atomic_store(dst, packed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    if (slot < kCandFirst) candFirst[((long long)c.f * g->ncells + c.cell) * kCandRec + 1 + slot] = packed;
+                    else cands[(long long)c.f * g->ncand + c.out_off + slot] = packed;
+                }
             }
             kept += __popcll(km);
         }
@@ -959,7 +990,10 @@ __device__ __forceinline__ void fast_cell_body(const Geom* __restrict__ g, const
         wave_lds_sync();
     }
     ORBGPU_STAMP(4);
-    if (lane == 0) *cntOut = kept;
+    if (lane == 0) {
+        if constexpr (CP != 0) __hip_atomic_store(cntOut, kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *cntOut = kept;
+    }
     ORBGPU_STAMP(5);
 }
 
@@ -1076,14 +1110,25 @@ __device__ __forceinline__ void child_rect(uint32_t rx, uint32_t ry, int q, uint
     cry = (uint32_t)cy0 | ((uint32_t)cy1 << 16);
 }
 
+// The thread index as the octree code reads it: threadIdx.x, or (CP != 0: inside k_extract_flow's task loop) the
+// same value through an opaque move, so that nothing derived from it is hoisted out of the loop and held live
+// across every task (which pushed the octree from 101 to 128 VGPRs with spills)
+template <int CP>
+__device__ __forceinline__ int tidx() {
+    if constexpr (CP == 0) return threadIdx.x;
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+    return t;
+}
+
 // Exclusive scan over the k_octree block with one barrier: wave totals go to one of two 16-int
 // buffers (`par` flips on every call, which every thread makes in the same order), and every thread
 // adds the totals of the waves before its own.  The buffer written by call k+2 was last read in
 // call k, before every thread reached call k+1's barrier, so no trailing barrier is needed.
-template <int NT>   // the k_octree block size
+template <int NT, int CP = 0>   // NT: the k_octree block size
 __device__ __forceinline__ int oct_scan(int v, int* sc, int& par, int& total) {
     constexpr int NW = NT / 64;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = tidx<CP>() & 63, wave = tidx<CP>() >> 6;
     const int x = wave_incl_scan(v);
     int* buf = sc + 16 * par;
     par ^= 1;
@@ -1102,13 +1147,14 @@ __device__ __forceinline__ int oct_scan(int v, int* sc, int& par, int& total) {
 
 // Wave-aggregated LDS counter add: one atomic per distinct target in the wave (LDS atomics from many
 // lanes to one address serialise at ~2 cycles per lane).  Uniform control flow required.
+template <int CP = 0>
 __device__ __forceinline__ void wave_agg_add(int* ctr, bool ok, int tgt) {
     unsigned long long pending = __ballot(ok);
     while (pending) {
         const int leader = __ffsll((long long)pending) - 1;
         const int tl = __builtin_amdgcn_readlane(tgt, leader);
         const unsigned long long m = __ballot(ok && tgt == tl);
-        if ((int)(threadIdx.x & 63) == leader) atomicAdd(&ctr[tl], __popcll(m));
+        if ((int)(tidx<CP>() & 63) == leader) atomicAdd(&ctr[tl], __popcll(m));
         pending &= ~m;
     }
 }
@@ -1158,13 +1204,20 @@ __device__ __forceinline__ int ff_base(int nIni, int d) { return nIni * (((1 << 
 // One (frame, level) of DistributeOctTree once the candidate count C is known.  KeysInLds selects
 // whether keys / knode live in LDS (after the node tables) or in the per-level global scratch; the
 // two instantiations let the compiler use ds_* or global_* accesses instead of flat ones.
-template <bool KeysInLds, int NT>
+// a store of the octree's outputs (lvlKps, lvlCount): write-through sc1 in the dataflow launch (CP != 0)
+template <int CP, class T>
+__device__ __forceinline__ void oct_out(T* p, T v) {
+    if constexpr (CP != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+template <bool KeysInLds, int NT, int CP = 0>
 __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const LevelGeom& L, int f, int l, int* smem,
                                              int C, uint32_t* keys, uint16_t* knode, uint32_t* __restrict__ lvlKps,
                                              int* __restrict__ lvlCount, int* __restrict__ err, int par,
                                              unsigned long long* __restrict__ ost) {
     const int NC = g->node_cap;
-    const int tid = threadIdx.x;
+    const int tid = tidx<CP>();
     const int tieMask = (g->variant & ORB_VARIANT_TIE_REVERSE) ? 0xFFFFFF : 0;   // :684 tie policy
     // LDS carve: tables P and Q (ping-pong: A = current list, B = next), quad, rank, info, ord, nchr,
     // scan buffers, scalars.  Phase 2's dense sort keys alias B's rx/ry, its per-rank d / prefix
@@ -1202,7 +1255,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
     const float hX = L.hX;
     const int Hn = L.maxBY - kMinBorder;
     if (nIni > NC) {
-        if (tid == 0) { atomicOr(err, 1); lvlCount[f * g->nlevels + l] = 0; }
+        if (tid == 0) { atomicOr(err, 1); oct_out<CP>(&lvlCount[f * g->nlevels + l], 0); }
         return;
     }
     int S = 0, nextSeq = 0, phase = 1, round0 = 0;
@@ -1261,14 +1314,14 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             }
             dn = wave_sum(dn);
             en = wave_sum(en);
-            if ((threadIdx.x & 63) == 0 && (dn | en)) {
+            if ((tidx<CP>() & 63) == 0 && (dn | en)) {
                 atomicAdd(&ffc[2 * (d + 1)], dn);
                 atomicAdd(&ffc[2 * (d + 1) + 1], en);
             }
             if (d == 0) {   // the roots themselves (erased when empty, :577-588)
                 d0 = wave_sum(d0);
                 e0 = wave_sum(e0);
-                if ((threadIdx.x & 63) == 0 && (d0 | e0)) {
+                if ((tidx<CP>() & 63) == 0 && (d0 | e0)) {
                     atomicAdd(&ffc[0], d0);
                     atomicAdd(&ffc[1], e0);
                 }
@@ -1292,7 +1345,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             Eprev = Er;
         }
         if (over) {
-            if (tid == 0) { atomicOr(err, 2); lvlCount[f * g->nlevels + l] = 0; }
+            if (tid == 0) { atomicOr(err, 2); oct_out<CP>(&lvlCount[f * g->nlevels + l], 0); }
             return;
         }
         const int DR = ffc[2 * R];
@@ -1328,7 +1381,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 on = node && (d == R || n == 1);
             }
             int tot;
-            const int pos = run + oct_scan<NT>(on ? 1 : 0, sc, par, tot);
+            const int pos = run + oct_scan<NT, CP>(on ? 1 : 0, sc, par, tot);
             if (on) {
                 const int t = c >> (2 * d);
                 int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1)), y0 = 0, y1 = Hn;
@@ -1405,14 +1458,14 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 r = min((int)((float)x / hX), nIni - 1);
                 knode[i] = (uint16_t)r;
             }
-            wave_agg_add(cntB, ok, r);   // the roots are few: a wave's keys usually share one or two
+            wave_agg_add<CP>(cntB, ok, r);   // the roots are few: a wave's keys usually share one or two
         }
         __syncthreads();
         for (int t0 = 0; t0 < nIni; t0 += NT) {   // keep the non-empty roots in order
             const int t = t0 + tid;
             const int n = t < nIni ? cntB[t] : 0;
             int tot;
-            const int pos = S + oct_scan<NT>(n > 0 ? 1 : 0, sc, par, tot);
+            const int pos = S + oct_scan<NT, CP>(n > 0 ? 1 : 0, sc, par, tot);
             if (n > 0) {
                 const int x0 = (int)(hX * (float)t), x1 = (int)(hX * (float)(t + 1));
                 rxA[pos] = (uint32_t)x0 | ((uint32_t)x1 << 16);
@@ -1430,12 +1483,10 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
     __syncthreads();
     OCT_STAMP(2);
 
-    int p2seen = 0;
     for (int round = round0; round < 4 * NC + 64 && !ffDone; round++) {
         const int prevSize = S;
-        // sub-step stamps of round 0 (slots 12..16) and of the first phase-2 round (20..28)
-        [[maybe_unused]] const int subBase = round == 0 ? 12 : (phase == 2 && !p2seen) ? 20 : -1;
-        if (phase == 2) p2seen = 1;
+        // sub-step stamps of round 0 (slots 12..16) and of the last phase-2 round (20..28)
+        [[maybe_unused]] const int subBase = round == 0 ? 12 : phase == 2 ? 20 : -1;   // (the last phase-2 round's)
 #if ORBGPU_KERNEL_STAMPS
 #define OCT_SUB(k) \
     if (ost && tid == 0 && subBase >= 0 && subBase + (k) < 29) ost[subBase + (k)] = __builtin_amdgcn_s_memtime();
@@ -1482,7 +1533,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                     val = 1 | (__popc(mask) << 16);
                 }
                 int tot;
-                const int pre = oct_scan<NT>(val, sc, par, tot);
+                const int pre = oct_scan<NT, CP>(val, sc, par, tot);
                 if (t < S) {
                     if (val) {
                         rank[t] = nproc + (pre & 0xFFFF);
@@ -1508,7 +1559,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const int t = t0 + tid;
                 const bool big = t < S && cntA[t] > 1;
                 int tot;
-                const int pos = nsort + oct_scan<NT>(big ? 1 : 0, sc, par, tot);
+                const int pos = nsort + oct_scan<NT, CP>(big ? 1 : 0, sc, par, tot);
                 // seq in 24 bits: creation order, or its complement for ORB_VARIANT_TIE_REVERSE (a later-
                 // created node counts as the smaller pointer); roots (seq < 0) never reach this sort
                 if (big)
@@ -1552,10 +1603,10 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const int r = r0 + tid;
                 const int d = r < nsort ? dd[r] : 0;
                 int tot;
-                const int pre = run + oct_scan<NT>(d, sc, par, tot);
+                const int pre = run + oct_scan<NT, CP>(d, sc, par, tot);
                 if (r < nsort) dpre[r] = pre;
                 const unsigned long long fail = __ballot(r < nsort && S + pre + d >= N);
-                if (fail && (threadIdx.x & 63) == 0) atomicMin(&sv[2], r0 + (tid & ~63) + __ffsll((long long)fail) - 1);
+                if (fail && (tidx<CP>() & 63) == 0) atomicMin(&sv[2], r0 + (tid & ~63) + __ffsll((long long)fail) - 1);
                 run += tot;
             }
             __syncthreads();
@@ -1577,7 +1628,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 const int t = t0 + tid;
                 const bool keep = t < S && rank[t] < 0;
                 int tot;
-                const int pre = und + oct_scan<NT>(keep ? 1 : 0, sc, par, tot);
+                const int pre = und + oct_scan<NT, CP>(keep ? 1 : 0, sc, par, tot);
                 if (keep) info[t] = pre;
                 und += tot;
             }
@@ -1586,7 +1637,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         // new list: [children of the last-divided node (n4..n1)] ... [of the first] [undivided nodes]
         const int Snew = CH + S - ndiv;
         if (Snew > NC) {
-            if (tid == 0) { atomicOr(err, 2); lvlCount[f * g->nlevels + l] = 0; }
+            if (tid == 0) { atomicOr(err, 2); oct_out<CP>(&lvlCount[f * g->nlevels + l], 0); }
             return;
         }
         int big = 0;
@@ -1624,7 +1675,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             }
         }
         big = wave_sum(big);
-        if ((threadIdx.x & 63) == 0 && big) atomicAdd(&sv[3], big);
+        if ((tidx<CP>() & 63) == 0 && big) atomicAdd(&sv[3], big);
         __syncthreads();
         OCT_SUB(phase == 1 ? 3 : 7);
         for (int i0 = 0; i0 < C; i0 += 4 * NT) {   // 4 keys per thread, branch-free reads (clamped)
@@ -1672,37 +1723,41 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
     uint32_t* best = (uint32_t*)quad;
     for (int t = tid; t < S; t += NT) best[t] = 0;
     __syncthreads();
+    OCT_STAMP(17);
     for (int i = tid; i < C; i += NT) {
         const uint32_t v = ((keys[i] >> 24) << 24) | (uint32_t)(0xFFFFFF - i);
         atomicMax(&best[knode[i]], v);
     }
     __syncthreads();
+    OCT_STAMP(18);
     uint32_t* outK = lvlKps + (long long)f * g->nkpcap + L.kp_base;
     for (int t = tid; t < S; t += NT) {
         const int i = 0xFFFFFF - (int)(best[t] & 0xFFFFFF);
         const uint32_t k = keys[i];
         const uint32_t x = (k & 0xFFF) + kMinBorder, y = ((k >> 12) & 0xFFF) + kMinBorder;   // :841-847
-        outK[t] = x | (y << 12) | (k & 0xFF000000u);
+        oct_out<CP>(&outK[t], x | (y << 12) | (k & 0xFF000000u));
     }
-    if (tid == 0) lvlCount[f * g->nlevels + l] = S;
+    if (tid == 0) oct_out<CP>(&lvlCount[f * g->nlevels + l], S);
     OCT_STAMP(31);
 #undef OCT_STAMP
 }
 
-template <int NT>   // block size: kOctreeThreads for batches, 1024 for one frame (the host path's latency)
-__global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
-                                                           const uint32_t* __restrict__ cands,
-                                                           const uint32_t* __restrict__ candFirst,
-                                                           uint32_t* __restrict__ keysAll,
-                                                           uint16_t* __restrict__ knodeAll,
-                                                           uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
-                                                           int* __restrict__ err, int lds_keys,
-                                                           unsigned long long* __restrict__ ostamps, int lbase) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
+// a candidate word (record or slot) at element i of the dataflow launch: an sc1 buffer load
+template <int CP>
+__device__ __forceinline__ uint32_t cand_slot(__amdgpu_buffer_rsrc_t rs, unsigned i) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * i), 0, CP);
+}
+
+// One (frame f, level l) of the octree by the whole block of NT threads: the candidate gather, then
+// octree_level.  smem: octree_lds_bytes(node_cap) + lds_keys * 6 bytes.
+template <int NT, int CP>
+__device__ __forceinline__ void octree_task(const Geom* __restrict__ g, int f, int l, int* smem,
+                                            const uint32_t* __restrict__ cands, const uint32_t* __restrict__ candFirst,
+                                            uint32_t* __restrict__ keysAll, uint16_t* __restrict__ knodeAll,
+                                            uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
+                                            int* __restrict__ err, int lds_keys, unsigned long long* __restrict__ ostamps) {
     const int NC = g->node_cap;
-    const int tid = threadIdx.x;
-    // frames along x so that every frame's level-0 block (the longest) is dispatched first
-    const int f = blockIdx.x, l = lbase + (int)blockIdx.y;
+    const int tid = tidx<CP>();
     const LevelGeom& L = g->L[l];
     // optional timestamps (ORBGPU_FAST_STAMPS=1): 32 per (frame, level): 0 start, 1 gathered, 2 roots,
     // 3.. end of round r (up to 9), 12.. / 20.. sub-steps of round 0 / the first phase-2 round,
@@ -1722,6 +1777,10 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
     const uint4* cf = reinterpret_cast<const uint4*>(candFirst) + ((long long)f * g->ncells + L.cell_base) * 2;
     const uint32_t* cr = candFirst + ((long long)f * g->ncells + L.cell_base) * kCandRec;
     static_assert(kCandRec == 8, "two uint4 per cell record");
+    // (CP: the records and slots are read through buffer descriptors with sc1 loads; unused otherwise)
+    // (made where used, so that the plain instantiation carries no descriptor registers)
+    auto crsf = [&]() { return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(cr), 0, ncl * kCandRec * 4, 0x00020000); };
+    auto csrf = [&]() { return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(cs), 0, L.cand_cap * 4, 0x00020000); };
     int* sc = smem + 16 * NC;   // after the node tables (octree_lds_bytes)
     int* sv = sc + 32;
     uint32_t* keysL = reinterpret_cast<uint32_t*>(sv + 8);
@@ -1744,7 +1803,16 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
             for (int k = 0; k < kFirst; k++) v[j][k] = 0;
             const int c = j * NT + tid;
             if (j < nch && c < ncl) {
-                const uint4 r0 = cf[2 * c], r1 = cf[2 * c + 1];
+                uint4 r0, r1;
+                if constexpr (CP != 0) {
+                    const uint32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(crsf(), 32 * c, 0, CP);
+                    const uint32x4_t b = __builtin_amdgcn_raw_buffer_load_b128(crsf(), 32 * c + 16, 0, CP);
+                    r0 = make_uint4(a[0], a[1], a[2], a[3]);
+                    r1 = make_uint4(b[0], b[1], b[2], b[3]);
+                } else {
+                    r0 = cf[2 * c];
+                    r1 = cf[2 * c + 1];
+                }
                 n[j] = (int)r0.x;
                 v[j][0] = r0.y;
                 v[j][1] = r0.z;
@@ -1759,7 +1827,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
         for (int j = 0; j < kMaxChunks; j++) {
             if (j < nch) {   // uniform
                 int tot;
-                off[j] = C + oct_scan<NT>(n[j], sc, par, tot);
+                off[j] = C + oct_scan<NT, CP>(n[j], sc, par, tot);
                 C += tot;
             }
         }
@@ -1772,16 +1840,22 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
 #pragma unroll
                 for (int k = 0; k < kFirst; k++)
                     if (k < n[j]) keys[off[j] + k] = v[j][k];
-                for (int k = kFirst; k < n[j]; k++) keys[off[j] + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+                if constexpr (CP != 0) {
+                    for (int k = kFirst; k < n[j]; k++) keys[off[j] + k] = cand_slot<CP>(csrf(), __umul24((unsigned)c, (unsigned)L.cell_cap) + k);
+                } else {
+                    for (int k = kFirst; k < n[j]; k++) keys[off[j] + k] = cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+                }
             }
         }
     } else {   // many cells (large images / fine grids): two passes, a chunk of NT cells at a time
         int base = 0;
         for (int c0 = 0; c0 < ncl; c0 += NT) {
             const int c = c0 + tid;
-            const int n = c < ncl ? (int)cr[(long long)c * kCandRec] : 0;
+            int n = 0;
+            if constexpr (CP != 0) n = c < ncl ? (int)cand_slot<CP>(crsf(), (unsigned)c * kCandRec) : 0;
+            else n = c < ncl ? (int)cr[(long long)c * kCandRec] : 0;
             int tot;
-            (void)oct_scan<NT>(n, sc, par, tot);
+            (void)oct_scan<NT, CP>(n, sc, par, tot);
             base += tot;
         }
         C = base;
@@ -1790,20 +1864,44 @@ __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
         base = 0;
         for (int c0 = 0; c0 < ncl; c0 += NT) {
             const int c = c0 + tid;
-            const int n = c < ncl ? (int)cr[(long long)c * kCandRec] : 0;
+            int n = 0;
+            if constexpr (CP != 0) n = c < ncl ? (int)cand_slot<CP>(crsf(), (unsigned)c * kCandRec) : 0;
+            else n = c < ncl ? (int)cr[(long long)c * kCandRec] : 0;
             int tot;
-            const int off = base + oct_scan<NT>(n, sc, par, tot);
-            for (int k = 0; k < n; k++)
-                keys[off + k] = k < kFirst ? cr[(long long)c * kCandRec + 1 + k]
-                                           : cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+            const int off = base + oct_scan<NT, CP>(n, sc, par, tot);
+            if constexpr (CP != 0) {
+                for (int k = 0; k < n; k++)
+                    keys[off + k] = k < kFirst ? cand_slot<CP>(crsf(), (unsigned)c * kCandRec + 1 + k)
+                                               : cand_slot<CP>(csrf(), __umul24((unsigned)c, (unsigned)L.cell_cap) + k);
+            } else {
+                for (int k = 0; k < n; k++)
+                    keys[off + k] = k < kFirst ? cr[(long long)c * kCandRec + 1 + k]
+                                               : cs[__umul24((unsigned)c, (unsigned)L.cell_cap) + k];
+            }
             base += tot;
         }
     }
     if (inLds)
-        octree_level<true, NT>(g, L, f, l, smem, C, keys, reinterpret_cast<uint16_t*>(keysL + lds_keys), lvlKps, lvlCount,
+        octree_level<true, NT, CP>(g, L, f, l, smem, C, keys, reinterpret_cast<uint16_t*>(keysL + lds_keys), lvlKps, lvlCount,
                                err, par, ost);
     else
-        octree_level<false, NT>(g, L, f, l, smem, C, keys, knodeAll + o, lvlKps, lvlCount, err, par, ost);
+        octree_level<false, NT, CP>(g, L, f, l, smem, C, keys, knodeAll + o, lvlKps, lvlCount, err, par, ost);
+}
+
+
+template <int NT>   // block size: kOctreeThreads for batches, 1024 for one frame (the host path's latency)
+__global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
+                                                           const uint32_t* __restrict__ cands,
+                                                           const uint32_t* __restrict__ candFirst,
+                                                           uint32_t* __restrict__ keysAll,
+                                                           uint16_t* __restrict__ knodeAll,
+                                                           uint32_t* __restrict__ lvlKps, int* __restrict__ lvlCount,
+                                                           int* __restrict__ err, int lds_keys,
+                                                           unsigned long long* __restrict__ ostamps, int lbase) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    // frames along x so that every frame's level-0 block (the longest) is dispatched first
+    octree_task<NT, 0>(g, blockIdx.x, lbase + (int)blockIdx.y, smem, cands, candFirst, keysAll, knodeAll, lvlKps,
+                       lvlCount, err, lds_keys, ostamps);
 }
 
 /* ------------------------------------------------------------------------------------------------
@@ -1857,6 +1955,9 @@ struct DescSlot {
     LevelPtr src;
 };
 
+// (CP: the octree's counts and keypoints were written by other workgroups of the same launch: sc1 vector loads,
+// never the scalar cache)
+template <int CP = 0>
 __device__ __forceinline__ DescSlot desc_slot(const Geom* __restrict__ g, int f, int s, const int* cnts,
                                               const uint32_t* __restrict__ lvlKps, const uint8_t* frames,
                                               long long framePitch, int rowStride, const uint8_t* pyr) {
@@ -1870,10 +1971,16 @@ __device__ __forceinline__ DescSlot desc_slot(const Geom* __restrict__ g, int f,
     while (l + 1 < nl && s >= g->L[l + 1].kp_base) ++l;
     const LevelGeom& L = g->L[l];
     const int k = s - L.kp_base;
-    if (k >= cnts[l]) return d;
+    auto cnt = [&](int i) -> int {
+        if constexpr (CP != 0) return __hip_atomic_load(&cnts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else return cnts[i];
+    };
+    if (k >= cnt(l)) return d;
     int outIdx = k;
-    for (int i = 0; i < l; i++) outIdx += cnts[i];
-    const uint32_t kp = lvlKps[(long long)f * g->nkpcap + s];
+    for (int i = 0; i < l; i++) outIdx += cnt(i);
+    uint32_t kp;
+    if constexpr (CP != 0) kp = __hip_atomic_load(&lvlKps[(long long)f * g->nkpcap + s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else kp = lvlKps[(long long)f * g->nkpcap + s];
     d.ok = true;
     d.l = l;
     d.x = kp & 0xFFF;
@@ -1890,6 +1997,7 @@ __device__ __forceinline__ DescSlot desc_slot(const Geom* __restrict__ g, int f,
 // dword ww = lane % 12), round r loads row wy0 + 5r (9 rounds).  Lanes 60..63 duplicate lanes 0..3 of
 // the next round (same dword, same value); rows 43..47 of the last round are not read.  The per-lane
 // offset is computed once; each round adds a wave-uniform soffset.
+template <int CP = 0>
 __device__ __forceinline__ void desc_issue(const DescSlot& d, int lane, uint32_t (&v)[9]) {
     const int a0 = (d.x - 21) & ~3;
     // the slot is wave-uniform: a buffer descriptor over the window rows (SGPRs), the lane's dword as
@@ -1904,10 +2012,10 @@ __device__ __forceinline__ void desc_issue(const DescSlot& d, int lane, uint32_t
     const int wy0 = (int)(__umul24((unsigned)lane, 2731u) >> 15), ww = lane - wy0 * 12;   // lane / 12
     const int off = (int)roi_off(wy0, stride, 4 * ww);
 #pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 5 * r * stride, 0);
+    for (int r = 0; r < 8; r++) v[r] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 5 * r * stride, CP);
     // last round: rows 40..42 only (lane < 36); the others take a voffset past the range (reads 0 whether
     // or not the range check counts soffset)
-    v[8] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane < 36 ? off : 0x40000000, 40 * stride, 0);
+    v[8] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane < 36 ? off : 0x40000000, 40 * stride, CP);
 }
 
 // 256 rBRIEF tests of one keypoint, the blurred samples computed at the sample pixels only (the column
@@ -1975,7 +2083,7 @@ __device__ __forceinline__ void brief_sampled(const uint16_t* rt, float a, float
     if (lane < 4) dst[lane] = lane == 0 ? mq[0] : lane == 1 ? mq[1] : lane == 2 ? mq[2] : mq[3];
 }
 
-template <bool FMA>
+template <bool FMA, int CP = 0>
 __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const DescSlot& d, int f, int lane,
                                           const uint32_t (&v)[9], uint8_t* wbase, uint16_t* rt,
                                           orb_keypoint* __restrict__ outK, uint8_t* __restrict__ outD, int kpCap,
@@ -2013,7 +2121,13 @@ __device__ __forceinline__ void desc_body(const Geom* __restrict__ g, const Desc
                 int sy = y - 21 + wy, sx = x - 21 + wx;
                 sy = sy < 0 ? -sy : (sy >= L.h ? 2 * L.h - 2 - sy : sy);
                 sx = sx < 0 ? -sx : (sx >= L.w ? 2 * L.w - 2 - sx : sx);
-                v[r] = idx < kDescWin * kDescWin ? src.p[roi_off(sy, src.stride, sx)] : (uint8_t)0;
+                if constexpr (CP != 0) {   // a border window of a pyramid level: sc1 byte loads
+                    const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src.p), 0, 0x7FFFFFFF, 0x00020000);
+                    v[r] = idx < kDescWin * kDescWin ? __builtin_amdgcn_raw_buffer_load_b8(brs, (int)roi_off(sy, src.stride, sx), 0, CP)
+                                                     : (uint8_t)0;
+                } else {
+                    v[r] = idx < kDescWin * kDescWin ? src.p[roi_off(sy, src.stride, sx)] : (uint8_t)0;
+                }
             }
 #pragma unroll
             for (int r = 0; r < 15; r++) {
@@ -2288,6 +2402,196 @@ hipError_t launch_debug_sincosf(const float* d_x, int n, float* d_s, float* d_c,
     return hipGetLastError();
 }
 
+/* ------------------------------------------------------------------------------------------------
+ * The small-batch dataflow launch (orbgpu_internal.h FlowTask).  One frame leaves most of the chip idle, and the
+ * per-kernel launches serialise every level behind the slowest one at each stage (the chain of ten dependent
+ * launches measured 74-79 us per C5 frame, profiles/r05/c5b1_trace.txt): here each level's FAST, octree and
+ * describe start as soon as that level exists, so the small upper levels and level 0 run beside the pyramid and the
+ * slow middle-level octrees.  Hand-offs between workgroups follow MI355X_MICROARCH.md's write-through form: every
+ * store of handed-off bytes (pyramid levels, candidate records and slots, octree outputs) and every load of them
+ * carries sc1 (kCpSc1: the bodies' CP parameter), each storing wave drains its stores (s_waitcnt vmcnt(0)) before the
+ * workgroup barrier after which one lane raises the task's counter (an agent-scope atomic); a waiting workgroup's
+ * lane 0 polls its counters with relaxed agent loads and s_sleep, then releases the workgroup through a barrier.
+ * Tasks are taken from one ticket counter in the host's topological order, so a task only ever waits on tasks that
+ * running workgroups hold (no residency assumption), and every wait is bounded (a timeout raises an error flag the
+ * host reads).  The launch's last workgroup re-zeroes the counters for the next launch.
+ * --------------------------------------------------------------------------------------------- */
+
+__device__ __forceinline__ int flow_ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void flow_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int flow_add(int* p, int v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The stages of one task.  Each reads the launch's arguments itself from the argument block in device memory (Ap),
+// inside its own branch: nothing but the ticket is carried around the task loop, so the loop adds no registers to the
+// largest body's (kernel-argument fields held across the loop spilled the octree's SGPRs into VGPRs).
+template <int TQ>
+__device__ __forceinline__ void flow_fast(const FlowArgs* __restrict__ Ap, int l, int f, int a, int b, int wv, int lane,
+                                          uint8_t* smem) {
+    if (wv >= b) return;
+    const Geom* __restrict__ g = Ap->g;
+    const int wb = g->fast_wave_bytes;
+    uint16_t* tile = reinterpret_cast<uint16_t*>(smem + (size_t)wv * wb + 16);
+    uint16_t* sList = reinterpret_cast<uint16_t*>(smem + (size_t)wv * wb + ((g->fast_rows * TQ * 2 + 32 + 15) & ~15));
+    const int cell = g->L[l].cell_base + a + wv;
+    const FastCellT c = fast_cell_t(g, Ap->cells, f * g->ncells + cell, Ap->frames, Ap->framePitch, Ap->rowStride,
+                                    Ap->pyr, 0, g->ncells);
+    uint32_t* candFirst = Ap->candFirst;
+    int* cntOut = reinterpret_cast<int*>(candFirst + ((long long)c.f * g->ncells + c.cell) * kCandRec);
+    if (!c.valid) {
+        if (lane == 0) flow_st(cntOut, 0);
+        return;
+    }
+    uint32_t v[8];
+    if (c.aligned) fast_roi_issue<kCpSc1>(c, lane, v);
+    fast_roi_store<TQ, kCpSc1>(c, lane, v, tile);
+    fast_cell_body<TQ, kCpSc1>(g, c, lane, tile, sList, Ap->cands, candFirst, cntOut, nullptr, 0);
+}
+
+__device__ __forceinline__ void flow_resize(const FlowArgs* __restrict__ Ap, int l, int f, int a, int b, int tid,
+                                            uint8_t* smem) {
+    const Geom* __restrict__ g = Ap->g;
+    const int q = tid >> 8;   // 256-thread quarter: one output tile each
+    const int th = (g->L[l].rs_tiled & 2) ? 32 : 16;
+    const int gxl = (g->L[l].w + kRsTileW - 1) / kRsTileW;
+    const int tile = a + q;
+    const int by = tile / gxl, bx = tile - by * gxl;
+    const int rq = Ap->rsQuarter;
+    uint8_t* qb = smem + (size_t)q * rq;
+    int4* scx = reinterpret_cast<int4*>(qb + rq - (kRsTileW + 32) * 16);
+    int4* scy = scx + kRsTileW;
+    const ResizeCoef* cf = Ap->rcoef + Ap->roff.o[l];
+    const bool on = q < b;
+    const bool gen = (g->variant & ORB_VARIANT_RESIZE_GENERIC) != 0;
+    const uint8_t* frames = Ap->frames;
+    const long long fp = Ap->framePitch;
+    const int rs = Ap->rowStride;
+    uint8_t* pyr = Ap->pyr;
+    if (th == 32) {
+        if (gen) resize_tile<32, true, kCpSc1>(g, cf, l, frames, fp, rs, pyr, f, bx, by, tid & 255, qb, scx, scy, on);
+        else resize_tile<32, false, kCpSc1>(g, cf, l, frames, fp, rs, pyr, f, bx, by, tid & 255, qb, scx, scy, on);
+    } else {
+        if (gen) resize_tile<16, true, kCpSc1>(g, cf, l, frames, fp, rs, pyr, f, bx, by, tid & 255, qb, scx, scy, on);
+        else resize_tile<16, false, kCpSc1>(g, cf, l, frames, fp, rs, pyr, f, bx, by, tid & 255, qb, scx, scy, on);
+    }
+}
+
+template <bool FMA>
+__device__ __forceinline__ void flow_describe(const FlowArgs* __restrict__ Ap, int f, int a, int b, int wv, int lane,
+                                              uint8_t* smem) {
+    if (wv >= b) return;
+    const Geom* __restrict__ g = Ap->g;
+    uint8_t* sw = smem + (size_t)wv * kDescWaveBytes;
+    const DescSlot d = desc_slot<kCpSc1>(g, f, a + wv, Ap->lvlCount + f * g->nlevels, Ap->lvlKps, Ap->frames,
+                                         Ap->framePitch, Ap->rowStride, Ap->pyr);
+    if (!d.ok) return;
+    uint32_t v[9];
+    if (d.interior) desc_issue<kCpSc1>(d, lane, v);
+    desc_body<FMA, kCpSc1>(g, d, f, lane, v, sw + kDescWinOff, reinterpret_cast<uint16_t*>(sw), Ap->outK, Ap->outD,
+                           Ap->kpCap, nullptr);
+}
+
+template <int TQ, bool FMA>
+__global__ __launch_bounds__(kFlowThreads) void k_extract_flow(const FlowArgs* __restrict__ Ap0) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t fl_smem[];
+    __shared__ int s_tk[2];
+    if (threadIdx.x == 0) s_tk[0] = flow_add(&Ap0->ctr[0], 1);
+    __syncthreads();
+    int cur = __builtin_amdgcn_readfirstlane(s_tk[0]);   // (uniform: the task's fields become scalar loads)
+    while (cur < Ap0->ntasks) {   // (cur is block-uniform: every thread read the same LDS word)
+        // the thread index and the argument block through opaque moves each task: nothing derived from them is
+        // hoisted out of the loop and held live across every task (the largest body keeps its own register count)
+        int tid;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+        const int lane = tid & 63;
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const FlowArgs* __restrict__ Ap = Ap0;
+        asm volatile("" : "+s"(Ap));
+        const FlowTask t = Ap->tasks[cur];
+        const int kind = t.klf & 0xFF, l = (t.klf >> 8) & 0xFF, f = t.klf >> 16;
+        unsigned long long* st = Ap->stamps ? Ap->stamps + 4 * (size_t)cur : nullptr;
+        if (tid == 0) {
+            if (st) st[0] = __builtin_amdgcn_s_memrealtime();
+            int* ctr = Ap->ctr;
+            s_tk[1] = flow_add(&ctr[0], 1);   // the next ticket, taken now so its round trip overlaps this task
+            if (t.nd > 0 && !flow_ld(&ctr[48])) {   // (once any wait has given up, no task waits any more)
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+                bool late = false;
+                for (int k = 0; k < t.nd && !late; k++)
+                    while (flow_ld(&ctr[t.dep + k]) < t.tgt) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull || flow_ld(&ctr[48])) {
+                            // 0.2 s: give up and flag it (the host sees ORB_ERR_INTERNAL from orb_sync)
+                            __hip_atomic_fetch_or(&ctr[48], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            late = true;
+                            break;
+                        }
+                    }
+            }
+        }
+        __syncthreads();
+        if (st && tid == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+        const int nxt = __builtin_amdgcn_readfirstlane(s_tk[1]);
+        if (kind == kFlowResize) {
+            flow_resize(Ap, l, f, t.a, t.b, tid, fl_smem);
+        } else if (kind == kFlowFast) {
+            flow_fast<TQ>(Ap, l, f, t.a, t.b, wv, lane, fl_smem);
+        } else if (kind == kFlowOctree) {
+            const Geom* __restrict__ g = Ap->g;
+            const int nl = g->nlevels;
+            int* eword = &Ap->ctr[kFlowCtrBase + 4 * nl * f + 3 * nl + l];
+            octree_task<kFlowThreads, kCpSc1>(g, f, l, reinterpret_cast<int*>(fl_smem), Ap->cands, Ap->candFirst,
+                                              Ap->keys, Ap->knode, Ap->lvlKps, Ap->lvlCount, eword, Ap->ldsKeys, nullptr);
+        } else {
+            flow_describe<FMA>(Ap, f, t.a, t.b, wv, lane, fl_smem);
+        }
+        // publish: every wave's stores drained, then one lane raises the task's counter
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (st && tid == 0) {
+            st[2] = __builtin_amdgcn_s_memrealtime();
+            st[3] = (unsigned long long)(unsigned)t.klf | ((unsigned long long)blockIdx.x << 32);
+        }
+        if (tid == 0 && t.sig >= 0) {
+            int* ctr = Ap->ctr;
+            flow_add(&ctr[t.sig], 1);
+            const int nl = Ap->g->nlevels, nfr = Ap->nframes;
+            if (kind == kFlowOctree && flow_add(&ctr[32], 1) == nfr * nl - 1) {
+                // the last octree of the launch: every frame's keypoint count and the overflow flags (the other
+                // octrees' outputs were drained before their counter adds, which this add follows)
+                int e = 0;
+                const int* lc = Ap->lvlCount;
+                for (int fr = 0; fr < nfr; fr++) {
+                    int tot = 0;
+                    for (int i = 0; i < nl; i++) {
+                        tot += flow_ld(&lc[fr * nl + i]);
+                        e |= flow_ld(&ctr[kFlowCtrBase + 4 * nl * fr + 3 * nl + i]);
+                    }
+                    Ap->outN[fr] = tot;
+                }
+                Ap->err[0] = e;
+                Ap->err[1] = 0;
+                if (Ap->errHost) *Ap->errHost = e;
+            }
+        }
+        cur = nxt;
+    }
+    // the launch's last workgroup re-zeroes every counter (the others have taken their last ticket and touch none)
+    if (threadIdx.x == 0) {
+        const FlowArgs* __restrict__ Ap = Ap0;
+        int* ctr = Ap->ctr;
+        if (flow_add(&ctr[16], 1) == (int)gridDim.x - 1) {
+            if (flow_ld(&ctr[48])) {   // a wait gave up: the outputs are not valid
+                Ap->err[1] = 4;
+                if (Ap->errHost) *Ap->errHost = 4;
+            }
+            const int n = kFlowCtrBase + 4 * Ap->g->nlevels * Ap->nframes;
+            for (int i = 0; i < n; i++) flow_st(&ctr[i], 0);
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 static inline unsigned cdiv(unsigned a, unsigned b) { return (a + b - 1) / b; }
 
@@ -2307,10 +2611,138 @@ static int octree_lds_keys_whole_cu(const Geom& g) {
     return room > 0 ? (int)std::min(want, (room / 6) & ~7LL) : 0;
 }
 
+// The dataflow launch's task list (see k_extract_flow): per frame, the stages in the order
+//     R1 F0 O0 R2 F1 O1 ... R(n-1) F(n-2) O(n-2) F(n-1) O(n-1) D0 .. D(n-1)
+// (Rl: level l's resize tiles, Fl: its FAST cells, Ol: its octree, Dl: its describe slots), the frames interleaved
+// task-group by task-group, so the pyramid chain (the critical path to the slow middle-level octrees) is taken
+// first and every octree is held by a workgroup as soon as its cells are.  A describe task of level l waits for the
+// octrees of levels 0..l (its output index adds their counts, ORBextractor.cc:1103).
+bool build_flow(const Geom& g, int nframes, int blocks, std::vector<FlowTask>& tasks, FlowPlan& plan) {
+    tasks.clear();
+    plan = FlowPlan{};
+    const int nl = g.nlevels;
+    if (nframes < 1 || nframes > 0xFFFF) return false;
+    int rsq = 0;   // one resize quarter: the largest source tile + the column / row coefficient slots
+    for (int l = 1; l < nl; l++) {
+        if (!(g.L[l].rs_tiled & 3)) return false;   // (large scale factors: the untiled k_resize)
+        rsq = std::max(rsq, ((g.L[l].rs_span_rows * kRsPitch + 15) & ~15) + (kRsTileW + 32) * 16);
+    }
+    int nres[ORBGPU_MAX_LEVELS] = {0}, nfast[ORBGPU_MAX_LEVELS] = {0};
+    for (int l = 0; l < nl; l++) {
+        if (l > 0) {
+            const int th = (g.L[l].rs_tiled & 2) ? 32 : 16;
+            const int tiles = (int)(cdiv(g.L[l].w, kRsTileW) * cdiv(g.L[l].h, th));
+            nres[l] = (tiles + 3) / 4;
+        }
+        nfast[l] = (g.L[l].nCols * g.L[l].nRows + 15) / 16;
+    }
+    auto ctr = [&](int f, int part, int l) { return kFlowCtrBase + 4 * nl * f + part * nl + l; };
+    auto push = [&](int kind, int l, int f, int sig, int a, int b, int dep, int nd, int tgt) {
+        FlowTask t;
+        t.klf = kind | (l << 8) | (f << 16);
+        t.sig = sig;
+        t.a = a;
+        t.b = b;
+        t.dep = dep;
+        t.nd = nd;
+        t.tgt = tgt;
+        t.pad = 0;
+        tasks.push_back(t);
+    };
+    auto resize = [&](int l) {
+        const int th = (g.L[l].rs_tiled & 2) ? 32 : 16;
+        const int tiles = (int)(cdiv(g.L[l].w, kRsTileW) * cdiv(g.L[l].h, th));
+        for (int i = 0; i < nres[l]; i++)
+            for (int f = 0; f < nframes; f++)
+                push(kFlowResize, l, f, ctr(f, 0, l), 4 * i, std::min(4, tiles - 4 * i), l > 1 ? ctr(f, 0, l - 1) : 0,
+                     l > 1 ? 1 : 0, l > 1 ? nres[l - 1] : 0);
+    };
+    auto fast = [&](int l) {
+        const int n = g.L[l].nCols * g.L[l].nRows;
+        for (int i = 0; i < nfast[l]; i++)
+            for (int f = 0; f < nframes; f++)
+                push(kFlowFast, l, f, ctr(f, 1, l), 16 * i, std::min(16, n - 16 * i), l > 0 ? ctr(f, 0, l) : 0,
+                     l > 0 ? 1 : 0, l > 0 ? nres[l] : 0);
+    };
+    auto octree = [&](int l) {
+        for (int f = 0; f < nframes; f++) push(kFlowOctree, l, f, ctr(f, 2, l), 0, 0, ctr(f, 1, l), 1, nfast[l]);
+    };
+    for (int l = 0; l < nl; l++) {
+        if (l + 1 < nl) resize(l + 1);
+        fast(l);
+        octree(l);
+    }
+    for (int l = 0; l < nl; l++) {
+        const int cap = g.L[l].kp_cap;
+        for (int i = 0; i < cap; i += 16)
+            for (int f = 0; f < nframes; f++)
+                push(kFlowDescribe, l, f, -1, g.L[l].kp_base + i, std::min(16, cap - i), ctr(f, 2, 0), l + 1, 1);
+    }
+    // LDS: the largest of the stages' carves (one 1024-thread workgroup per CU either way: its waves' registers
+    // fill the CU), the rest of the CU's 160 KiB holding the octree's keys
+    constexpr int kLds = 160 * 1024 - 64;
+    const int need = std::max({16 * g.fast_wave_bytes, 16 * kDescWaveBytes + 256, 4 * rsq, (int)octree_lds_bytes(g.node_cap)});
+    if (need > kLds) return false;
+    plan.ntasks = (int)tasks.size();
+    plan.nframes = nframes;
+    plan.nctr = kFlowCtrBase + 4 * nl * nframes;
+    plan.lds_bytes = kLds;
+    const long long room = kLds - (long long)octree_lds_bytes(g.node_cap);
+    const long long want = ((long long)g.max_level_cand + 7) & ~7LL;
+    plan.lds_keys = room > 0 ? (int)std::min(want, (room / 6) & ~7LL) : 0;
+    plan.rs_quarter = rsq;
+    plan.blocks = std::max(1, blocks);
+    return true;
+}
+
+FlowArgs flow_args(const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch, int row_stride, int nframes,
+                   orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int kp_cap) {
+    FlowArgs A;
+    std::memset(&A, 0, sizeof A);   // (compared bytewise by the caller: no indeterminate padding)
+    A.g = b.d_geom;
+    A.rcoef = b.d_rcoef;
+    std::memcpy(A.roff.o, b.rcoef_off, sizeof A.roff.o);
+    A.cells = b.d_cells;
+    A.frames = d_frames;
+    A.framePitch = frame_pitch;
+    A.rowStride = row_stride;
+    A.pyr = b.d_pyr;
+    A.cands = b.d_cands;
+    A.candFirst = b.d_candFirst;
+    A.keys = b.d_keys;
+    A.knode = b.d_knode;
+    A.lvlKps = b.d_lvlKps;
+    A.lvlCount = b.d_lvlCount;
+    A.err = b.d_err;
+    A.errHost = b.err_host;
+    A.outK = d_kps;
+    A.outD = d_desc;
+    A.outN = d_counts;
+    A.kpCap = kp_cap;
+    A.tasks = b.d_flow;
+    A.ntasks = b.flow.ntasks;
+    A.nframes = nframes;
+    A.ctr = b.d_flow_ctr;
+    A.ldsKeys = b.flow.lds_keys;
+    A.rsQuarter = b.flow.rs_quarter;
+    A.stamps = b.d_flow_stamps;
+    return A;
+}
+
 hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch,
                           int row_stride, int nframes, orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                           int kp_cap, hipStream_t stream, KernelMarker marker, void* user) {
     if (nframes <= 0) return hipSuccess;
+    if (b.d_flow && b.flow.nframes == nframes) {   // the small-batch dataflow launch (k_extract_flow)
+        // (its arguments are in device memory, b.d_flow_args, written by the caller for this call: flow_args())
+        const bool fma = !(g.variant & ORB_VARIANT_NO_FMA);
+        auto kern = g.fast_compact ? (fma ? k_extract_flow<48, true> : k_extract_flow<48, false>)
+                                   : (fma ? k_extract_flow<kFastTilePitch, true> : k_extract_flow<kFastTilePitch, false>);
+        if (marker) marker(user, ORB_K_FLOW, 1, stream);
+        hipLaunchKernelGGL(kern, dim3(b.flow.blocks), dim3(kFlowThreads), (size_t)b.flow.lds_bytes, stream, b.d_flow_args);
+        if (marker) marker(user, ORB_K_FLOW, 0, stream);
+        return hipGetLastError();
+    }
     auto resize = [&](int l, hipStream_t s) {
         // 32-row tiles where the level's source spans fit the LDS tile, else 16-row tiles, else the
         // untiled kernel (large scale factors): chosen per level from the geometry (LevelGeom::rs_tiled)

@@ -346,6 +346,38 @@ int Ctx::ensure_frames(int nframes) {
     return ORB_OK;
 }
 
+// The dataflow launch's plan for this geometry and frame count (built on the host, uploaded once per change); false
+// flow_ok: the geometry does not take it (the per-kernel launches run).  Counters are zeroed here once and re-zeroed
+// by every launch's last workgroup.
+int Ctx::ensure_flow(int nframes) {
+    if (flow_ok && flow_serial == geom_serial && flow.nframes == nframes) return ORB_OK;
+    flow_ok = false;
+    std::vector<FlowTask> tasks;
+    FlowPlan pl;
+    const int blocks = std::min(num_cu, flow_blocks > 0 ? flow_blocks : kFlowDefaultBlocks * nframes);
+    if (!build_flow(geom, nframes, blocks, tasks, pl)) return ORB_OK;
+    hipError_t e;
+    // (a launch queued earlier may still read the old task table or counters)
+    if ((tasks.size() > flow_cap || (size_t)pl.nctr > flow_ctr_cap) && (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return set_error("sync", e), ORB_ERR_HIP;
+    if ((e = grow(d_flow, flow_cap, tasks.size())) != hipSuccess) return set_error("hipMalloc flow tasks", e), ORB_ERR_NOMEM;
+    const bool fresh = (size_t)pl.nctr > flow_ctr_cap || !d_flow_ctr;
+    if ((e = grow(d_flow_ctr, flow_ctr_cap, (size_t)pl.nctr)) != hipSuccess)
+        return set_error("hipMalloc flow counters", e), ORB_ERR_NOMEM;
+    if (fresh && (e = hipMemsetAsync(d_flow_ctr, 0, flow_ctr_cap * sizeof(int), stream)) != hipSuccess)
+        return set_error("memset flow counters", e), ORB_ERR_HIP;
+    if ((e = hipMemcpyAsync(d_flow, tasks.data(), tasks.size() * sizeof(FlowTask), hipMemcpyHostToDevice, stream)) !=
+        hipSuccess)
+        return set_error("upload flow tasks", e), ORB_ERR_HIP;
+    if (flow_stamps && (e = grow(d_flow_stamps, flow_stamps_cap, (size_t)pl.ntasks * 4)) != hipSuccess)
+        return set_error("hipMalloc flow stamps", e), ORB_ERR_NOMEM;
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
+    flow = pl;
+    flow_serial = geom_serial;
+    flow_ok = true;
+    return ORB_OK;
+}
+
 ExtractBuffers Ctx::buffers() const {
     ExtractBuffers b;
     b.d_geom = d_geom;
@@ -367,6 +399,10 @@ ExtractBuffers Ctx::buffers() const {
     b.d_stamps = fast_stamps ? d_stamps : nullptr;
     b.fork_s2 = nullptr;
     b.ev_fork = b.ev_join = nullptr;
+    b.d_flow = nullptr;
+    b.d_flow_ctr = nullptr;
+    b.d_flow_args = nullptr;
+    b.d_flow_stamps = nullptr;
     return b;
 }
 
@@ -392,6 +428,32 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
         bufs.chain = chain_small;
         bufs.d_chain = d_chain2;
     }
+    // small batches: the dataflow launch (stamps are per-kernel diagnostics: the per-kernel launches)
+    if (!latency && nframes <= flow_max_frames && !fast_stamps) {
+        const int st = ensure_flow(nframes);
+        if (st != ORB_OK) return st;
+        if (flow_ok) {
+            bufs.d_flow = d_flow;
+            bufs.d_flow_ctr = d_flow_ctr;
+            bufs.flow = flow;
+            // the kernel reads its arguments from device memory: uploaded when they differ from the last call's
+            // (stream-ordered behind the launches still reading the old ones; a pageable copy of 0.2 KB returns once
+            // the runtime has staged it)
+            if (!d_flow_args && (e = hipMalloc((void**)&d_flow_args, sizeof(FlowArgs))) != hipSuccess)
+                return set_error("hipMalloc flow args", e), ORB_ERR_NOMEM;
+            bufs.d_flow_stamps = flow_stamps ? d_flow_stamps : nullptr;
+            const FlowArgs A = flow_args(bufs, d_frames, frame_pitch, row_stride, nframes, d_kps, d_desc, d_counts, kp_cap);
+            if (std::memcmp(&A, &h_flow_args, sizeof A) != 0 || !flow_args_valid) {
+                if ((e = hipMemcpyAsync(d_flow_args, &A, sizeof A, hipMemcpyHostToDevice, stream)) != hipSuccess) {
+                    flow_args_valid = false;
+                    return set_error("upload flow args", e), ORB_ERR_HIP;
+                }
+                h_flow_args = A;
+                flow_args_valid = true;
+            }
+            bufs.d_flow_args = d_flow_args;
+        }
+    }
     // one frame in flight (ORBGPU_FORK=1): level 0's FAST -> octree on a second stream beside the pyramid
     if (latency && fork && !prof_on && !fast_stamps && geom.nlevels > 1) {
         hipError_t fe = hipSuccess;
@@ -416,7 +478,8 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             (uintptr_t)geom_serial, (uintptr_t)d_geom, (uintptr_t)d_rcoef, (uintptr_t)d_cells, (uintptr_t)d_pyr,
             (uintptr_t)d_cands, (uintptr_t)d_candFirst, (uintptr_t)d_keys, (uintptr_t)d_knode, (uintptr_t)d_lvlKps,
             (uintptr_t)d_lvlCount, (uintptr_t)bufs.d_err, (uintptr_t)stream,
-            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)err_host << 4) ^ ((uintptr_t)(bufs.fork_s2 != nullptr) << 3)};
+            (uintptr_t)bufs.chain.nseg ^ ((uintptr_t)err_host << 4) ^ ((uintptr_t)(bufs.fork_s2 != nullptr) << 3) ^
+                ((uintptr_t)bufs.d_flow << 8) ^ ((uintptr_t)bufs.flow.ntasks << 1) ^ ((uintptr_t)bufs.flow.blocks << 20)};
         if (!gexec || key != gkey) {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             if (graph) (void)hipGraphDestroy(graph);
@@ -519,6 +582,11 @@ orb_ctx* orb_create(const orb_params* p, int* status) {
     if (const char* ev = std::getenv("ORBGPU_STEREO_STAGE")) c->stereo_stage = ev[0] == '1';
     if (const char* ev = std::getenv("ORBGPU_FORK")) c->fork = ev[0] != '0';
     if (const char* ev = std::getenv("ORBGPU_UPLOAD")) c->upload_stream = ev[0] != '0';
+    // ORBGPU_FLOW=1: batches of one or two frames take the dataflow launch (A/B and parity of both forms);
+    // ORBGPU_FLOW_BLOCKS=n: its workgroups
+    if (const char* ev = std::getenv("ORBGPU_FLOW")) c->flow_max_frames = ev[0] == '0' ? 0 : 2;
+    if (const char* ev = std::getenv("ORBGPU_FLOW_BLOCKS")) c->flow_blocks = std::atoi(ev);
+    if (const char* ev = std::getenv("ORBGPU_FLOW_STAMPS")) c->flow_stamps = ev[0] == '1';
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate", e);
@@ -552,7 +620,7 @@ void orb_destroy(orb_ctx* h) {
         (void)hipEventDestroy(pr.b);
         (void)hipEventDestroy(pr.e);
     }
-    void* bufs[] = {c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_chain2, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
+    void* bufs[] = {c->d_flow, c->d_flow_ctr, c->d_flow_args, c->d_flow_stamps, c->d_cells, c->d_stamps, c->d_geom, c->d_rcoef, c->d_chain, c->d_chain2, c->d_pyr, c->d_cands, c->d_candFirst, c->d_keys, c->d_knode,
                     c->d_lvlKps, c->d_lvlCount, c->d_err, c->d_in,
                     c->d_scratch, c->d_peer, c->d_pairs};
     for (void* b : bufs)
@@ -625,7 +693,8 @@ int orb_sync(orb_ctx* h) {
     if (c->d_err && (e = hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost)) != hipSuccess)
         return set_error("read error flag", e), ORB_ERR_HIP;
     if (err[0] | err[1]) {
-        set_error("octree node table overflow (raise nfeatures capacity)", hipSuccess);
+        set_error((err[1] & 4) ? "dataflow launch: a task's wait timed out (outputs invalid)"
+                               : "octree node table overflow (raise nfeatures capacity)", hipSuccess);
         return ORB_ERR_INTERNAL;
     }
     return ORB_OK;
@@ -769,6 +838,11 @@ int orb_get_level(orb_ctx* h, int level, const uint8_t** data, int* w, int* hgt,
 int orb_debug_fast_stamps(orb_ctx* h, uint64_t* out, int cap) {
     Ctx* c = reinterpret_cast<Ctx*>(h);
     CTX_GUARD(c);
+    if (c->flow_stamps && c->d_flow_stamps) {   // the dataflow launch's per-task stamps
+        const int n = std::min((int)c->flow_stamps_cap, cap);
+        hipError_t e = hipMemcpy(out, c->d_flow_stamps, (size_t)n * 8, hipMemcpyDeviceToHost);
+        return e == hipSuccess ? n : ORB_ERR_HIP;
+    }
     if (!c->fast_stamps || !c->d_stamps) return 0;
     const int n = std::min((int)c->stamps_cap, cap);
     hipError_t e = hipMemcpy(out, c->d_stamps, (size_t)n * 8, hipMemcpyDeviceToHost);

@@ -139,7 +139,27 @@ struct Ctx {
     hipEvent_t prof_open[ORB_K_COUNT]{};
     std::vector<ProfPair> prof_pairs;
 
+    // the small-batch dataflow launch (k_extract_flow): batches of at most flow_max_frames frames take it
+    // (ORBGPU_FLOW=1; 0, the default, keeps the per-kernel launches); its task list per (geometry, frame count), the
+    // counters it waits on
+    int flow_max_frames = 0;
+    int flow_blocks = 0;            // workgroups per launch (ORBGPU_FLOW_BLOCKS; 0: the default, kFlowDefaultBlocks)
+    FlowTask* d_flow = nullptr;
+    size_t flow_cap = 0;
+    int* d_flow_ctr = nullptr;
+    size_t flow_ctr_cap = 0;
+    FlowPlan flow{};
+    FlowArgs* d_flow_args = nullptr;   // the last uploaded arguments (h_flow_args mirrors them)
+    FlowArgs h_flow_args{};
+    bool flow_args_valid = false;
+    bool flow_stamps = false;       // ORBGPU_FLOW_STAMPS=1: per-task timestamps (orb_debug_fast_stamps returns them)
+    unsigned long long* d_flow_stamps = nullptr;
+    size_t flow_stamps_cap = 0;
+    unsigned flow_serial = 0;       // geom_serial the plan was built for
+    bool flow_ok = false;           // flow holds a plan for (flow_serial, flow.nframes)
+
     int ensure_geometry(int W, int H);
+    int ensure_flow(int nframes);
     int ensure_frames(int nframes);
     ExtractBuffers buffers() const;
     // err: the overflow flag the kernels raise (default d_err); err_host: a host-coherent word k_describe

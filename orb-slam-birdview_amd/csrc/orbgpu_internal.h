@@ -134,6 +134,72 @@ struct RcoefOff {   // per-level offsets into the coefficient table (a kernel ar
     int o[ORBGPU_MAX_LEVELS];
 };   // batches up to this many frames take the one-launch pyramid
 
+// The small-batch dataflow launch (k_extract_flow, extract_kernels.hip): one persistent launch of 1024-thread
+// workgroups that take (stage, level, frame) tasks from a device ticket in a host-built topological order and wait
+// only on the per-(frame, level) counters of what each task reads: level l's FAST / octree / describe start as soon
+// as level l exists, independent of the other levels (ComputeKeyPointsOctTree loops per level, ORBextractor.cc:
+// 765-853; operator() per level, :1076-1103).  Tasks: a resize task = up to 4 output tiles of one level (a 256-thread
+// quarter each), a FAST task = up to 16 cells (a wave each), an octree task = one (frame, level) (the block), a
+// describe task = up to 16 keypoint slots of one level (a wave each).
+enum FlowKind : int { kFlowResize = 0, kFlowFast = 1, kFlowOctree = 2, kFlowDescribe = 3 };
+struct FlowTask {   // 32 B (one scalar dwordx8 load)
+    int klf;       // kind | level << 8 | frame << 16
+    int sig;       // counter raised when the task is done (-1: none)
+    int a, b;      // resize: first tile, tiles; FAST: first cell of the level, cells; describe: first keypoint slot
+                   // (frame-local), slots
+    int dep, nd;   // wait until counters dep .. dep + nd - 1 each reach tgt (nd = 0: no wait)
+    int tgt, pad;
+};
+struct FlowPlan {
+    int ntasks = 0;
+    int nframes = 0;
+    int nctr = 0;          // counter words (zeroed once; the launch's last workgroup re-zeroes them)
+    int lds_bytes = 0;     // dynamic LDS of the launch
+    int lds_keys = 0;      // octree keys kept in LDS
+    int rs_quarter = 0;    // LDS bytes of one resize quarter (source tile + coefficient slots)
+    int blocks = 0;        // workgroups of the launch
+};
+// counter layout: [0] ticket, [16] workgroups done, [32] octrees done, [48] timeout flag, then per frame f at
+// kFlowCtrBase + 4 nl f: resize tasks done [nl], FAST tasks done [nl], octree done [nl], octree error bits [nl]
+constexpr int kFlowCtrBase = 64;
+constexpr int kFlowThreads = 1024;
+constexpr int kFlowDefaultBlocks = 64;   // workgroups per frame of a dataflow launch (a quarter of the CUs: four
+                                         // launches in flight, one per hardware queue, fill the chip)
+// build the task list of nframes frames for geometry g (extract_kernels.hip); false: the geometry does not take the
+// dataflow launch (a level whose resize is not LDS-tiled)
+bool build_flow(const Geom& g, int nframes, int blocks, std::vector<FlowTask>& tasks, FlowPlan& plan);
+
+// The dataflow launch's arguments, read by the kernel from device memory (the caller uploads them when they change)
+struct FlowArgs {
+    const Geom* g;
+    const ResizeCoef* rcoef;
+    RcoefOff roff;
+    const CellDesc* cells;
+    const uint8_t* frames;
+    long long framePitch;
+    int rowStride;
+    uint8_t* pyr;
+    uint32_t* cands;
+    uint32_t* candFirst;
+    uint32_t* keys;
+    uint16_t* knode;
+    uint32_t* lvlKps;
+    int* lvlCount;
+    int* err;        // the host-visible overflow flags [2] (written once, by the workgroup finishing the last octree)
+    int* errHost;    // host-coherent copy of them (orb_extract), or NULL
+    orb_keypoint* outK;
+    uint8_t* outD;
+    int* outN;
+    int kpCap;
+    const FlowTask* tasks;
+    int ntasks;
+    int nframes;
+    int* ctr;
+    int ldsKeys;
+    int rsQuarter;
+    unsigned long long* stamps;   // ORBGPU_FLOW_STAMPS=1 (diagnostic): per task [ticket taken, wait over, done, id]
+};
+
 // Kernel launchers (extract_kernels.hip / hamming_kernels.hip / hamming_top2.hip).
 struct ExtractBuffers {
     const Geom* d_geom;
@@ -159,7 +225,15 @@ struct ExtractBuffers {
     // beside the pyramid and levels 1.. on the launch stream, joined before k_describe (NULL: one stream)
     hipStream_t fork_s2;
     hipEvent_t ev_fork, ev_join;
+    // the dataflow launch (NULL d_flow: the per-kernel launches); its plan matches this call's nframes
+    const FlowTask* d_flow;
+    int* d_flow_ctr;
+    const FlowArgs* d_flow_args;   // this call's arguments (flow_args()), already in device memory
+    unsigned long long* d_flow_stamps;   // ORBGPU_FLOW_STAMPS=1: 4 per task (diagnostic), else NULL
+    FlowPlan flow;
 };
+FlowArgs flow_args(const ExtractBuffers& b, const uint8_t* d_frames, long long frame_pitch, int row_stride, int nframes,
+                   orb_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int kp_cap);
 
 typedef void (*KernelMarker)(void* user, int kernel_id, int begin, hipStream_t stream);
 

@@ -214,8 +214,8 @@ class BatchExtractor(_Ctx):
         check(lib().orb_profile_enable(self.h, int(on)), "orb_profile_enable")
 
     def profile_read(self):
-        ms = np.zeros(6, np.float64)   # ORB_K_COUNT
-        n = np.zeros(6, np.int32)
+        ms = np.zeros(7, np.float64)   # ORB_K_COUNT
+        n = np.zeros(7, np.int32)
         check(lib().orb_profile_read(self.h, _p(ms), _p(n)), "orb_profile_read")
         return ms, n
 

@@ -30,21 +30,24 @@ def main():
     n = L.orb_debug_fast_stamps(bx.h, st.ctypes.data, cap)
     assert n >= cap, (n, cap)
     o = st[B * NCELLS * 8:].reshape(B, NL, 32).astype(np.int64)
-    t0 = o[:, :, 0].min()
+    # slots: 0 start, 1 gathered, 2 fast-forward done, 3 + r end of round r (r < 9; rounds start at the fast-forward
+    # depth R), 12..16 fast-forward sub-steps, 20..28 the first phase-2 round's sub-steps, 29 C, 30 phase-2 start, 31 done
     for lv in range(NL):
         s = o[:, lv]
         tot = s[:, 31] - s[:, 0]
-        nr = [int(np.count_nonzero(r[3:12])) for r in s]
-        rounds = np.array([np.diff(np.concatenate([[r[2]], r[3:3 + k]])) for r, k in zip(s, nr)], dtype=object)
-        mr = max(nr)
+        ends = [sorted(int(x) for x in r[3:12] if x > 0) for r in s]
+        nr = np.mean([len(e) for e in ends])
+        rounds = [np.diff([int(r[2])] + e) for r, e in zip(s, ends)]
+        mr = max(len(x) for x in rounds)
         per_round = [float(np.mean([x[i] for x in rounds if len(x) > i])) for i in range(mr)]
-        last = np.array([r[2 + k] for r, k in zip(s, nr)])
-        print(f"level {lv}: C {s[:, 29].mean():7.0f}  total {tot.mean():8.0f} cyc  start +{(s[:, 0] - t0).mean():7.0f}"
-              f"  gather {(s[:, 1] - s[:, 0]).mean():6.0f}  roots {(s[:, 2] - s[:, 1]).mean():6.0f}"
-              f"  rounds {np.mean(nr):4.1f} (phase2 at {s[:, 30].mean():4.1f})  best {(s[:, 31] - last).mean():6.0f}")
-        print("         per round:", " ".join(f"{x:.0f}" for x in per_round))
-        r0 = np.diff(np.concatenate([s[:, 2:3], s[:, 12:17]], axis=1), axis=1).mean(axis=0)
-        print("         round 0 steps (zero, quad counts, scan, moves, knode):", " ".join(f"{x:.0f}" for x in r0))
+        last = np.array([e[-1] if e else int(r[2]) for r, e in zip(s, ends)])
+        ff = np.diff(np.concatenate([s[:, 1:2], s[:, 12:17], s[:, 2:3]], axis=1), axis=1).mean(axis=0)
+        print(f"level {lv}: C {s[:, 29].mean():6.0f}  total {tot.mean():7.0f} cyc  gather {(s[:, 1] - s[:, 0]).mean():6.0f}"
+              f"  fast-forward {(s[:, 2] - s[:, 1]).mean():6.0f}  rounds {nr:3.1f}: {' '.join(f'{x:.0f}' for x in per_round)}"
+              f"  best+out {(s[:, 31] - last).mean():6.0f} (zero {(s[:, 17] - last).mean():.0f}, max {(s[:, 18] - s[:, 17]).mean():.0f},"
+              f" out {(s[:, 31] - s[:, 18]).mean():.0f})")
+        print("         fast-forward steps (zero, codes, depth sums, stop, list scan, key nodes + quads):",
+              " ".join(f"{x:.0f}" for x in ff))
         p2 = s[:, 20:29]
         ok = p2[:, 0] > 0
         if ok.any():
