@@ -330,16 +330,34 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
  * segment's base level up (ChainJob; the same fixed-point arithmetic as k_resize_tiled, so every value
  * is the per-level launch's), writing only its own tile.  The recomputation is redundant work, but a
  * single frame leaves most of the chip idle, and each dependent launch costs ~5 us of latency. */
-template <bool GENERIC>
-__global__ __launch_bounds__(256) void k_pyramid_chain(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef,
-                                                       const ChainJob* __restrict__ jobs, ChainSegment sg,
-                                                       RcoefOff roff, const uint8_t* __restrict__ frames,
-                                                       long long framePitch, int rowStride, uint8_t* __restrict__ pyr) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-    __shared__ int4 sreg[ORBGPU_MAX_LEVELS];
-    const int f = blockIdx.y;
-    const int tid = threadIdx.x;
-    const ChainJob* J = jobs + sg.job0 + blockIdx.x;
+// a dword / byte of a level the chain reads as its base: plain, or (CP) an sc1 load of a level handed off
+// inside the dataflow launch
+template <int CP>
+__device__ __forceinline__ uint32_t chain_ld32(const uint8_t* p) {
+    if constexpr (CP != 0)
+        return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *reinterpret_cast<const uint32_t*>(p);
+}
+template <int CP>
+__device__ __forceinline__ uint32_t chain_ld8(const uint8_t* p) {
+    if constexpr (CP != 0) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return (w >> (8 * (a & 3))) & 0xFFu;
+    } else {
+        return *p;
+    }
+}
+
+// One ChainJob (an output tile of J->level from level J->base) by the 256 threads tid = 0..255 of a block or of a
+// quarter of k_extract_flow's block (every thread of the block reaches the job's barriers, 2 + level - base of them:
+// jobs run together share level and base).  sm: the segment's carve (sg.lds_bytes), sreg: ORBGPU_MAX_LEVELS int4.
+template <bool GENERIC, int CP>
+__device__ __forceinline__ void chain_job(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef,
+                                          const ChainJob* __restrict__ J, const ChainSegment& sg, const RcoefOff& roff,
+                                          const uint8_t* __restrict__ frames, long long framePitch, int rowStride,
+                                          uint8_t* __restrict__ pyr, int f, int tid, uint8_t* sm, int4* sreg) {
     const int l = J->level, b = J->base;
     if (tid <= l) sreg[tid] = J->reg[tid];
     uint8_t* buf0 = sm;
@@ -389,11 +407,11 @@ __global__ __launch_bounds__(256) void k_pyramid_chain(const Geom* __restrict__ 
                 const uint8_t* rp = src + (long long)(R.z + r) * stride;
                 uint32_t v;
                 if (al && col + 3 < wb) {
-                    v = *reinterpret_cast<const uint32_t*>(rp + col);
+                    v = chain_ld32<CP>(rp + col);
                 } else {
                     v = 0;
                     for (int t = 0; t < 4; t++)
-                        if (col + t < wb) v |= (uint32_t)rp[col + t] << (8 * t);
+                        if (col + t < wb) v |= chain_ld8<CP>(rp + col + t) << (8 * t);
                 }
                 *reinterpret_cast<uint32_t*>(buf0 + r * p0 + 4 * q) = v;
             }
@@ -467,13 +485,26 @@ __global__ __launch_bounds__(256) void k_pyramid_chain(const Geom* __restrict__ 
                 if (!last) {
                     *reinterpret_cast<uint32_t*>(dst + r * nx + 4 * q) = packed;
                 } else if (R.x + 4 * q < wk) {   // the pitch is a multiple of 64: the dword never leaves the row
-                    *reinterpret_cast<uint32_t*>(gl + (long long)(R.z + r) * gpitch + R.x + 4 * q) = packed;
+                    uint32_t* dp = reinterpret_cast<uint32_t*>(gl + (long long)(R.z + r) * gpitch + R.x + 4 * q);
+                    if constexpr (CP != 0) __hip_atomic_store(dp, packed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else *dp = packed;
                 }
             }
         }
         e0 += nx + ny;
         if (!last) __syncthreads();
     }
+}
+
+template <bool GENERIC>
+__global__ __launch_bounds__(256) void k_pyramid_chain(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef,
+                                                       const ChainJob* __restrict__ jobs, ChainSegment sg,
+                                                       RcoefOff roff, const uint8_t* __restrict__ frames,
+                                                       long long framePitch, int rowStride, uint8_t* __restrict__ pyr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    __shared__ int4 sreg[ORBGPU_MAX_LEVELS];
+    chain_job<GENERIC, 0>(g, coef, jobs + sg.job0 + blockIdx.x, sg, roff, frames, framePitch, rowStride, pyr,
+                          blockIdx.y, threadIdx.x, sm, sreg);
 }
 
 /* ------------------------------------------------------------------------------------------------
@@ -1517,6 +1548,7 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             for (int u = 0; u < 4; u++)
                 if (inc[u]) atomicAdd(&quad[tg[u]], 1);
         }
+        if (tid == 0) sv[4] = 0;   // (phase 2's oversize-bin count)
         __syncthreads();
         OCT_SUB(1);
         quadReady = false;
@@ -1549,50 +1581,139 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
             ndiv = nproc;
             OCT_SUB(2);
         } else {
-            // sort the > 1-key nodes by (size, seq) descending (:684-685): dense keys, then each
-            // node's rank = number of larger keys (keys are unique)
-            unsigned long long* skey = reinterpret_cast<unsigned long long*>(rxB);
+            // sort the > 1-key nodes by (size, seq) descending (:684-685).  The list holds the > 1-key nodes in
+            // descending creation order (the roots ascending, then every round puts the last-created children first,
+            // n4..n1, ahead of the older nodes: phase-1 fast-forward and rounds alike), so seq order is list order,
+            // reversed under ORB_VARIANT_TIE_REVERSE, and the sort is a stable counting sort by size over the list:
+            // rank = (nodes with a larger size) + (nodes of the same size earlier in that order).  Sizes below
+            // kRkV - 1 have exact bins; the few larger nodes share the last bin and are ranked pairwise by (size,
+            // order).  (node tables too small for the bin table: the pairwise rank of all keys, below)
             int* dd = cntB;     // rank -> #children - 1
             int* dpre = seqB;   // rank -> exclusive prefix of dd
             int nsort = 0;
-            for (int t0 = 0; t0 < S; t0 += NT) {
-                const int t = t0 + tid;
-                const bool big = t < S && cntA[t] > 1;
-                int tot;
-                const int pos = nsort + oct_scan<NT, CP>(big ? 1 : 0, sc, par, tot);
-                // seq in 24 bits: creation order, or its complement for ORB_VARIANT_TIE_REVERSE (a later-
-                // created node counts as the smaller pointer); roots (seq < 0) never reach this sort
-                if (big)
-                    skey[pos] = ((unsigned long long)cntA[t] << 40) |
-                                ((unsigned long long)((unsigned)(seqA[t] ^ tieMask) & 0xFFFFFFu) << 16) |
-                                (unsigned long long)t;
-                nsort += tot;
-            }
-            if (tid == 0) sv[2] = nsort;
-            __syncthreads();
-            OCT_SUB(2);
-            // G lanes per key (G = 8, 4, 2 or 1 so that the keys fill the block), each comparing a
-            // strided 8-key slice, summed with xor shuffles inside the lane group
-            const int G = nsort <= NT / 8 ? 8 : nsort <= NT / 4 ? 4 : nsort <= NT / 2 ? 2 : 1;
-            const int lg = tid & (G - 1);
-            for (int j0 = 0; j0 < nsort * G; j0 += NT) {   // uniform trip count (shuffles below)
-                const int j = (j0 + tid) / G;
-                const bool ok = j < nsort;
-                const unsigned long long key = ok ? skey[j] : ~0ull;
-                int r = 0;
-                for (int i = 8 * lg; i + 8 <= nsort; i += 8 * G) {
-                    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(skey + i);
-                    const ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
-                    r += (a.x > key) + (a.y > key) + (b.x > key) + (b.y > key) + (c.x > key) + (c.y > key) +
-                         (d.x > key) + (d.y > key);
+            constexpr int kRkV = 32, NWv = NT / 64;   // size bins; waves
+            const bool binned = 2 * NC >= kRkV * 16 && NC >= kRkV;
+            if (binned) {
+                int* T2 = reinterpret_cast<int*>(rxB);   // [bin][wave] counts, then their per-bin exclusive wave prefixes
+                int* HV = seqB;                          // [bin] totals
+                int* ovl = nchr;                         // the oversize bin's nodes (nchr is rewritten before it is read)
+                const int lane = tid & 63, wave = tid >> 6;
+                const bool rev = tieMask != 0;
+                // 1. per wave, over its own contiguous run of the (tie-)ordered list: each node's position among the
+                // earlier nodes of its bin in that run, and the run's bin counts (no barrier inside a wave)
+                if (lane < kRkV) T2[lane * 16 + wave] = 0;   // (sv[4], the oversize count, was zeroed before the last barrier)
+                const int PW = (S + NWv - 1) / NWv;
+                const unsigned long long below = (1ull << lane) - 1ull;
+                for (int c0 = wave * PW; c0 < min(S, (wave + 1) * PW); c0 += 64) {   // wave-uniform
+                    const int pidx = c0 + lane;
+                    const bool in = pidx < min(S, (wave + 1) * PW);
+                    const int t = rev ? S - 1 - pidx : pidx;
+                    const int cnt = in ? cntA[t] : 0;
+                    const bool bg = cnt > 1;
+                    const int v = min(cnt, kRkV - 1);
+                    // the lanes holding this lane's bin: five bit-plane ballots, no loop
+                    unsigned long long m = __ballot(bg);
+#pragma unroll
+                    for (int b = 0; b < 5; b++) {
+                        const unsigned long long bal = __ballot((v >> b) & 1);
+                        m &= ((v >> b) & 1) ? bal : ~bal;
+                    }
+                    // the run's earlier chunks of this bin, then this chunk's count added by the bin's lowest lane
+                    const int prev = bg ? T2[v * 16 + wave] : 0;
+                    __builtin_amdgcn_wave_barrier();
+                    if (bg && (m & below) == 0) T2[v * 16 + wave] = prev + __popcll(m);
+                    wave_lds_sync();
+                    if (bg) {
+                        info[t] = prev + __popcll(m & below);   // (info is rewritten for every node below)
+                        if (v == kRkV - 1) ovl[atomicAdd(&sv[4], 1)] = t;
+                    }
                 }
-                if (lg == 0)
-                    for (int i = nsort & ~7; i < nsort; i++) r += skey[i] > key;
-                for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o);
-                if (ok && lg == 0) {
-                    const int t = (int)(key & 0xFFFF);
+                __syncthreads();
+                // 2. per bin, the exclusive prefix of its wave counts (a 16-lane DPP row per bin) and its total
+                if (tid < kRkV * 16) {
+                    const int x = (tid & 15) < NWv ? T2[tid] : 0;
+                    int y = x;
+                    y += __builtin_amdgcn_update_dpp(0, y, 0x111, 0xf, 0xf, true);
+                    y += __builtin_amdgcn_update_dpp(0, y, 0x112, 0xf, 0xf, true);
+                    y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xf, 0xf, true);
+                    y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xf, 0xf, true);
+                    T2[tid] = y - x;
+                    if ((tid & 15) == 15) HV[tid >> 4] = y;
+                }
+                __syncthreads();
+                // 3. ranks: larger bins' totals + the wave prefix of the node's bin + its position in its wave's run
+#pragma unroll 1
+                for (int i = 0; i < kRkV; i += 4) {
+                    const int4 h = *reinterpret_cast<const int4*>(&HV[i]);
+                    nsort += h.x + h.y + h.z + h.w;
+                }
+                const int nov = sv[4];
+                for (int t = tid; t < S; t += NT) {
+                    const int cnt = cntA[t];
+                    if (cnt <= 1) continue;
+                    const int v = min(cnt, kRkV - 1);
+                    const int pidx = rev ? S - 1 - t : t;
+                    int r = 0;
+                    if (v < kRkV - 1) {
+                        r = info[t] + T2[v * 16 + pidx / PW];
+#pragma unroll 1
+                        for (int i = (v + 1) & ~3; i < kRkV; i += 4) {
+                            const int4 h = *reinterpret_cast<const int4*>(&HV[i]);
+                            r += (i > v ? h.x : 0) + (i + 1 > v ? h.y : 0) + (i + 2 > v ? h.z : 0) + (i + 3 > v ? h.w : 0);
+                        }
+                    } else {   // the oversize bin: pairwise by (size desc, then order)
+                        for (int i = 0; i < nov; i++) {
+                            const int u = ovl[i];
+                            const int cu = cntA[u], pu = rev ? S - 1 - u : u;
+                            r += cu > cnt || (cu == cnt && pu < pidx);
+                        }
+                    }
                     ord[r] = t;
                     dd[r] = __popc(quad_mask(&quad[4 * t])) - 1;
+                }
+                if (tid == 0) sv[2] = nsort;
+                OCT_SUB(2);
+            } else {
+                unsigned long long* skey = reinterpret_cast<unsigned long long*>(rxB);
+                for (int t0 = 0; t0 < S; t0 += NT) {
+                    const int t = t0 + tid;
+                    const bool big = t < S && cntA[t] > 1;
+                    int tot;
+                    const int pos = nsort + oct_scan<NT, CP>(big ? 1 : 0, sc, par, tot);
+                    // seq in 24 bits: creation order, or its complement for ORB_VARIANT_TIE_REVERSE (a later-
+                    // created node counts as the smaller pointer); roots (seq < 0) never reach this sort
+                    if (big)
+                        skey[pos] = ((unsigned long long)cntA[t] << 40) |
+                                    ((unsigned long long)((unsigned)(seqA[t] ^ tieMask) & 0xFFFFFFu) << 16) |
+                                    (unsigned long long)t;
+                    nsort += tot;
+                }
+                if (tid == 0) sv[2] = nsort;
+                __syncthreads();
+                OCT_SUB(2);
+                // G lanes per key (G = 8, 4, 2 or 1 so that the keys fill the block), each comparing a
+                // strided 8-key slice, summed with xor shuffles inside the lane group
+                const int G = nsort <= NT / 8 ? 8 : nsort <= NT / 4 ? 4 : nsort <= NT / 2 ? 2 : 1;
+                const int lg = tid & (G - 1);
+                for (int j0 = 0; j0 < nsort * G; j0 += NT) {   // uniform trip count (shuffles below)
+                    const int j = (j0 + tid) / G;
+                    const bool ok = j < nsort;
+                    const unsigned long long key = ok ? skey[j] : ~0ull;
+                    int r = 0;
+                    for (int i = 8 * lg; i + 8 <= nsort; i += 8 * G) {
+                        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(skey + i);
+                        const ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
+                        r += (a.x > key) + (a.y > key) + (b.x > key) + (b.y > key) + (c.x > key) + (c.y > key) +
+                             (d.x > key) + (d.y > key);
+                    }
+                    if (lg == 0)
+                        for (int i = nsort & ~7; i < nsort; i++) r += skey[i] > key;
+                    for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o);
+                    if (ok && lg == 0) {
+                        const int t = (int)(key & 0xFFFF);
+                        ord[r] = t;
+                        dd[r] = __popc(quad_mask(&quad[4 * t])) - 1;
+                    }
                 }
             }
             __syncthreads();
@@ -2477,6 +2598,24 @@ __device__ __forceinline__ void flow_resize(const FlowArgs* __restrict__ Ap, int
     }
 }
 
+// chain task: up to 4 ChainJobs of one level, one per 256-thread quarter (a quarter past the task's jobs repeats its
+// first job: the same bytes to the same place)
+__device__ __forceinline__ void flow_chain(const FlowArgs* __restrict__ Ap, int f, int a, int b, int seg, int tid,
+                                           uint8_t* smem) {
+    const Geom* __restrict__ g = Ap->g;
+    const int q = tid >> 8;
+    const int rq = Ap->rsQuarter;
+    uint8_t* qb = smem + (size_t)q * rq;
+    int4* sreg = reinterpret_cast<int4*>(qb + rq - ORBGPU_MAX_LEVELS * 16);
+    const ChainJob* J = Ap->chainJobs + a + (q < b ? q : 0);
+    const ChainSegment sg = Ap->chainSeg[seg];
+    RcoefOff ro = Ap->roff;
+    if (g->variant & ORB_VARIANT_RESIZE_GENERIC)
+        chain_job<true, kCpSc1>(g, Ap->rcoef, J, sg, ro, Ap->frames, Ap->framePitch, Ap->rowStride, Ap->pyr, f, tid & 255, qb, sreg);
+    else
+        chain_job<false, kCpSc1>(g, Ap->rcoef, J, sg, ro, Ap->frames, Ap->framePitch, Ap->rowStride, Ap->pyr, f, tid & 255, qb, sreg);
+}
+
 template <bool FMA>
 __device__ __forceinline__ void flow_describe(const FlowArgs* __restrict__ Ap, int f, int a, int b, int wv, int lane,
                                               uint8_t* smem) {
@@ -2533,7 +2672,9 @@ __global__ __launch_bounds__(kFlowThreads) void k_extract_flow(const FlowArgs* _
         __syncthreads();
         if (st && tid == 0) st[1] = __builtin_amdgcn_s_memrealtime();
         const int nxt = __builtin_amdgcn_readfirstlane(s_tk[1]);
-        if (kind == kFlowResize) {
+        if (kind == kFlowChain) {
+            flow_chain(Ap, f, t.a, t.b, t.seg, tid, fl_smem);
+        } else if (kind == kFlowResize) {
             flow_resize(Ap, l, f, t.a, t.b, tid, fl_smem);
         } else if (kind == kFlowFast) {
             flow_fast<TQ>(Ap, l, f, t.a, t.b, wv, lane, fl_smem);
@@ -2617,16 +2758,21 @@ static int octree_lds_keys_whole_cu(const Geom& g) {
 // task-group by task-group, so the pyramid chain (the critical path to the slow middle-level octrees) is taken
 // first and every octree is held by a workgroup as soon as its cells are.  A describe task of level l waits for the
 // octrees of levels 0..l (its output index adds their counts, ORBextractor.cc:1103).
-bool build_flow(const Geom& g, int nframes, int blocks, std::vector<FlowTask>& tasks, FlowPlan& plan) {
+bool build_flow(const Geom& g, int nframes, int blocks, const ChainPlan* chain, const std::vector<ChainJob>* jobs,
+                std::vector<FlowTask>& tasks, FlowPlan& plan) {
     tasks.clear();
     plan = FlowPlan{};
     const int nl = g.nlevels;
     if (nframes < 1 || nframes > 0xFFFF) return false;
-    int rsq = 0;   // one resize quarter: the largest source tile + the column / row coefficient slots
-    for (int l = 1; l < nl; l++) {
+    const bool chained = chain && jobs && chain->nseg > 0 && chain->first_base == 0;
+    int rsq = 0;   // one pyramid quarter: the largest source tile + the column / row coefficient slots (or a chain job)
+    for (int l = 1; l < nl && !chained; l++) {
         if (!(g.L[l].rs_tiled & 3)) return false;   // (large scale factors: the untiled k_resize)
         rsq = std::max(rsq, ((g.L[l].rs_span_rows * kRsPitch + 15) & ~15) + (kRsTileW + 32) * 16);
     }
+    if (chained)
+        for (int sgi = 0; sgi < chain->nseg; sgi++)
+            rsq = std::max(rsq, ((chain->seg[sgi].lds_bytes + 15) & ~15) + ORBGPU_MAX_LEVELS * 16);
     int nres[ORBGPU_MAX_LEVELS] = {0}, nfast[ORBGPU_MAX_LEVELS] = {0};
     for (int l = 0; l < nl; l++) {
         if (l > 0) {
@@ -2646,8 +2792,36 @@ bool build_flow(const Geom& g, int nframes, int blocks, std::vector<FlowTask>& t
         t.dep = dep;
         t.nd = nd;
         t.tgt = tgt;
-        t.pad = 0;
+        t.seg = 0;
         tasks.push_back(t);
+    };
+    // chain tasks: per level, its jobs in groups of 4 (jobs of a level are contiguous, one segment each)
+    int nchain[ORBGPU_MAX_LEVELS] = {0}, cj0[ORBGPU_MAX_LEVELS] = {0}, cjn[ORBGPU_MAX_LEVELS] = {0},
+        cseg[ORBGPU_MAX_LEVELS] = {0}, cbase[ORBGPU_MAX_LEVELS] = {0};
+    if (chained) {
+        for (int sgi = 0; sgi < chain->nseg; sgi++) {
+            const ChainSegment& sg = chain->seg[sgi];
+            for (int j = sg.job0; j < sg.job0 + sg.njobs; j++) {
+                const int l = (*jobs)[j].level;
+                if (cjn[l] == 0) cj0[l] = j;
+                cjn[l]++;
+                cseg[l] = sgi;
+                cbase[l] = (*jobs)[j].base;
+            }
+        }
+        for (int l = 1; l < nl; l++) {
+            if (cjn[l] == 0) return false;
+            nchain[l] = (cjn[l] + 3) / 4;
+            nres[l] = nchain[l];   // (the FAST tasks of level l wait for this many pyramid tasks)
+        }
+    }
+    auto chainl = [&](int l) {
+        for (int i = 0; i < nchain[l]; i++)
+            for (int f = 0; f < nframes; f++) {
+                push(kFlowChain, l, f, ctr(f, 0, l), cj0[l] + 4 * i, std::min(4, cjn[l] - 4 * i),
+                     cbase[l] > 0 ? ctr(f, 0, cbase[l]) : 0, cbase[l] > 0 ? 1 : 0, cbase[l] > 0 ? nres[cbase[l]] : 0);
+                tasks.back().seg = cseg[l];
+            }
     };
     auto resize = [&](int l) {
         const int th = (g.L[l].rs_tiled & 2) ? 32 : 16;
@@ -2667,10 +2841,28 @@ bool build_flow(const Geom& g, int nframes, int blocks, std::vector<FlowTask>& t
     auto octree = [&](int l) {
         for (int f = 0; f < nframes; f++) push(kFlowOctree, l, f, ctr(f, 2, l), 0, 0, ctr(f, 1, l), 1, nfast[l]);
     };
-    for (int l = 0; l < nl; l++) {
-        if (l + 1 < nl) resize(l + 1);
-        fast(l);
-        octree(l);
+    if (!chained) {
+        for (int l = 0; l < nl; l++) {
+            if (l + 1 < nl) resize(l + 1);
+            fast(l);
+            octree(l);
+        }
+    } else {
+        // level 0's cells and octree first (they read only the frame), then the first segment's levels, deepest
+        // first (the slow middle-level octrees are on the critical path), their cells and octrees, then the later
+        // segments' levels (each waits for its base level) with theirs
+        fast(0);
+        octree(0);
+        for (int sgi = 0; sgi < chain->nseg; sgi++) {
+            int lo = nl, hi = 0;
+            for (int l = 1; l < nl; l++)
+                if (cseg[l] == sgi) lo = std::min(lo, l), hi = std::max(hi, l);
+            for (int l = hi; l >= lo; l--) chainl(l);
+            for (int l = hi; l >= lo; l--) {
+                fast(l);
+                octree(l);
+            }
+        }
     }
     for (int l = 0; l < nl; l++) {
         const int cap = g.L[l].kp_cap;
@@ -2726,6 +2918,8 @@ FlowArgs flow_args(const ExtractBuffers& b, const uint8_t* d_frames, long long f
     A.ldsKeys = b.flow.lds_keys;
     A.rsQuarter = b.flow.rs_quarter;
     A.stamps = b.d_flow_stamps;
+    A.chainJobs = b.d_chain;
+    for (int i = 0; i < ORBGPU_MAX_LEVELS; i++) A.chainSeg[i] = b.flow_chain.seg[i];
     return A;
 }
 

@@ -310,6 +310,7 @@ int Ctx::ensure_geometry(int W, int H) {
         if ((e = hipMemcpyAsync(dj, cjobs.data(), cjobs.size() * sizeof(ChainJob), hipMemcpyHostToDevice, stream)) !=
             hipSuccess)
             return set_error("upload chain", e), ORB_ERR_HIP;
+        if (which == 0) chain_jobs_host = cjobs;
     }
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return set_error("sync", e), ORB_ERR_HIP;
     geom = g;
@@ -355,7 +356,10 @@ int Ctx::ensure_flow(int nframes) {
     std::vector<FlowTask> tasks;
     FlowPlan pl;
     const int blocks = std::min(num_cu, flow_blocks > 0 ? flow_blocks : kFlowDefaultBlocks * nframes);
-    if (!build_flow(geom, nframes, blocks, tasks, pl)) return ORB_OK;
+    // (ORBGPU_FLOW_CHAIN=0: per-level resize tasks instead of chain tasks)
+    const bool use_chain = chain.nseg > 0 && !(std::getenv("ORBGPU_FLOW_CHAIN") && std::getenv("ORBGPU_FLOW_CHAIN")[0] == '0');
+    if (!build_flow(geom, nframes, blocks, use_chain ? &chain : nullptr, &chain_jobs_host, tasks, pl)) return ORB_OK;
+    flow_chain_plan = use_chain ? chain : ChainPlan{};
     hipError_t e;
     // (a launch queued earlier may still read the old task table or counters)
     if ((tasks.size() > flow_cap || (size_t)pl.nctr > flow_ctr_cap) && (e = hipStreamSynchronize(stream)) != hipSuccess)
@@ -401,6 +405,7 @@ ExtractBuffers Ctx::buffers() const {
     b.ev_fork = b.ev_join = nullptr;
     b.d_flow = nullptr;
     b.d_flow_ctr = nullptr;
+    b.flow_chain = ChainPlan{};
     b.d_flow_args = nullptr;
     b.d_flow_stamps = nullptr;
     return b;
@@ -436,6 +441,8 @@ int Ctx::run_extract(const uint8_t* d_frames, int nframes, long long frame_pitch
             bufs.d_flow = d_flow;
             bufs.d_flow_ctr = d_flow_ctr;
             bufs.flow = flow;
+            bufs.flow_chain = flow_chain_plan;
+            bufs.d_chain = d_chain;   // (the chain tasks' jobs: the host-path plan, levels from the frame)
             // the kernel reads its arguments from device memory: uploaded when they differ from the last call's
             // (stream-ordered behind the launches still reading the old ones; a pageable copy of 0.2 KB returns once
             // the runtime has staged it)

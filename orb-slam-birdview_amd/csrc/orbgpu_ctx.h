@@ -51,6 +51,7 @@ struct Ctx {
     ChainJob* d_chain = nullptr;   // the one-launch pyramid's jobs (small batches)
     size_t chain_cap = 0;
     ChainPlan chain{};
+    std::vector<ChainJob> chain_jobs_host;   // (the dataflow launch's chain tasks index them)
     ChainJob* d_chain2 = nullptr;  // the small-batch plan (levels past kSmallChainBase in one launch)
     size_t chain2_cap = 0;
     ChainPlan chain_small{};
@@ -149,6 +150,7 @@ struct Ctx {
     int* d_flow_ctr = nullptr;
     size_t flow_ctr_cap = 0;
     FlowPlan flow{};
+    ChainPlan flow_chain_plan{};
     FlowArgs* d_flow_args = nullptr;   // the last uploaded arguments (h_flow_args mirrors them)
     FlowArgs h_flow_args{};
     bool flow_args_valid = false;

@@ -141,14 +141,15 @@ struct RcoefOff {   // per-level offsets into the coefficient table (a kernel ar
 // 765-853; operator() per level, :1076-1103).  Tasks: a resize task = up to 4 output tiles of one level (a 256-thread
 // quarter each), a FAST task = up to 16 cells (a wave each), an octree task = one (frame, level) (the block), a
 // describe task = up to 16 keypoint slots of one level (a wave each).
-enum FlowKind : int { kFlowResize = 0, kFlowFast = 1, kFlowOctree = 2, kFlowDescribe = 3 };
+enum FlowKind : int { kFlowResize = 0, kFlowFast = 1, kFlowOctree = 2, kFlowDescribe = 3, kFlowChain = 4 };
 struct FlowTask {   // 32 B (one scalar dwordx8 load)
     int klf;       // kind | level << 8 | frame << 16
     int sig;       // counter raised when the task is done (-1: none)
     int a, b;      // resize: first tile, tiles; FAST: first cell of the level, cells; describe: first keypoint slot
                    // (frame-local), slots
     int dep, nd;   // wait until counters dep .. dep + nd - 1 each reach tgt (nd = 0: no wait)
-    int tgt, pad;
+    int tgt;
+    int seg;       // chain task: its segment of the chain plan (a = first ChainJob, b = jobs, one per quarter)
 };
 struct FlowPlan {
     int ntasks = 0;
@@ -167,7 +168,11 @@ constexpr int kFlowDefaultBlocks = 64;   // workgroups per frame of a dataflow l
                                          // launches in flight, one per hardware queue, fill the chip)
 // build the task list of nframes frames for geometry g (extract_kernels.hip); false: the geometry does not take the
 // dataflow launch (a level whose resize is not LDS-tiled)
-bool build_flow(const Geom& g, int nframes, int blocks, std::vector<FlowTask>& tasks, FlowPlan& plan);
+// chain (optional): the few-launch pyramid's plan and its jobs (host copy); when given, the pyramid runs as chain-job
+// tasks (a level's tiles straight from its segment's base level, so the levels of a segment need no wait on each
+// other) instead of per-level resize tasks
+bool build_flow(const Geom& g, int nframes, int blocks, const ChainPlan* chain, const std::vector<ChainJob>* jobs,
+                std::vector<FlowTask>& tasks, FlowPlan& plan);
 
 // The dataflow launch's arguments, read by the kernel from device memory (the caller uploads them when they change)
 struct FlowArgs {
@@ -198,6 +203,8 @@ struct FlowArgs {
     int ldsKeys;
     int rsQuarter;
     unsigned long long* stamps;   // ORBGPU_FLOW_STAMPS=1 (diagnostic): per task [ticket taken, wait over, done, id]
+    const ChainJob* chainJobs;    // the chain plan's jobs (chain tasks), and its segments
+    ChainSegment chainSeg[ORBGPU_MAX_LEVELS];
 };
 
 // Kernel launchers (extract_kernels.hip / hamming_kernels.hip / hamming_top2.hip).
@@ -228,6 +235,7 @@ struct ExtractBuffers {
     // the dataflow launch (NULL d_flow: the per-kernel launches); its plan matches this call's nframes
     const FlowTask* d_flow;
     int* d_flow_ctr;
+    ChainPlan flow_chain;          // the plan the dataflow tasks were built with (nseg 0: per-level resize tasks)
     const FlowArgs* d_flow_args;   // this call's arguments (flow_args()), already in device memory
     unsigned long long* d_flow_stamps;   // ORBGPU_FLOW_STAMPS=1: 4 per task (diagnostic), else NULL
     FlowPlan flow;

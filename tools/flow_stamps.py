@@ -6,6 +6,7 @@ import os
 import sys
 
 os.environ["ORBGPU_FLOW_STAMPS"] = "1"
+os.environ.setdefault("ORBGPU_FLOW", "1")
 if len(sys.argv) > 3:
     os.environ["ORBGPU_FLOW_BLOCKS"] = sys.argv[3]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,7 +16,7 @@ import numpy as np  # noqa: E402
 import orbgpu  # noqa: E402
 from orbgpu.synth import bench_frames  # noqa: E402
 
-KINDS = ["resize", "fast", "octree", "describe"]
+KINDS = ["resize", "fast", "octree", "describe", "chain"]
 
 
 def main():
