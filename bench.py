@@ -714,9 +714,13 @@ def main():
     # ---- the ORBmatcher drop-ins per call (SURVEY 8(a) rows a9-a13 at the reference's granularity: one call
     # per frame / keyframe pair) and Frame::ComputeBoW, through the reference-signature adapter, against
     # the oracle's single-thread CPU loops on the same inputs (tools/matcher_latency.cc; rank 0 at N = 1)
-    matcher = None
+    matcher = matcher_c2 = None
     if rank == 0 and world == 1 and not args.no_matcher:
         matcher = matcher_leg(frames[0], w, h, nf, local)
+        if (w, h, nf) != (640, 480, 1000):
+            # and at the reference's TUM size (C2, Examples/Monocular/TUM1.yaml:30-43), where a call is a few us of CPU
+            # work, so the GPU's per-call fixed cost (one upload, the launches, one synchronisation) shows
+            matcher_c2 = matcher_leg(bench_frames(640, 480, 1, first=first)[0], 640, 480, 1000, local)
 
     # ---- birdview stream (BASELINE C4's bird stream): Frame.cc:320-342 fused on one
     # device-resident image + mask per call (orb_bird_extract_device); synchronous per frame (the host
@@ -782,7 +786,7 @@ def main():
                "keypoints_per_frame": round(per_frame_kps, 1),
                "kernels_ms_per_step": ({k: round(v, 4) for k, v in ms_per_step_k.items()} if ms_per_step_k else None),
                "roofline": roofline, "cpu_baseline": cpu, "hamming": ham, "stereo": stereo,
-               "bird": bird, "c4_frame": c4, "host_path": host_path, "matcher": matcher}
+               "bird": bird, "c4_frame": c4, "host_path": host_path, "matcher": matcher, "matcher_c2": matcher_c2}
         if cpu:
             out["speedup_vs_cpu_allcore"] = round(value / cpu["value"], 2)
             if "host_estimate_value" in cpu:

@@ -716,6 +716,8 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t p0, uint32_t p
 #if ORBGPU_KERNEL_STAMPS
 #define ORBGPU_STAMP(k) \
     if (stamps && lane == 0) stamps[(long long)item * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#elif defined(ORBGPU_ISA_MARKS)   // tools/fast_isa_phases.py: phase boundaries as assembly comments (no instruction)
+#define ORBGPU_STAMP(k) asm volatile(";ORBGPU_MARK " #k);
 #else
 #define ORBGPU_STAMP(k)
 #endif
@@ -1297,8 +1299,8 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
         // the quad..nchr area (8 NC ints); entries cnt | pos << 20 once the node is placed.
         int* T = quad;
         int* ffc = reinterpret_cast<int*>(rxB);   // per depth d: [2d] nodes, [2d + 1] nodes with > 1 key
-        const int szF = nIni << (2 * F);
         const int bF = ff_base(nIni, F);
+        const int szF = nIni << (2 * F);
         for (int t = tid; t < szF; t += NT) T[bF + t] = 0;
         for (int t = tid; t < 2 * (kFfMaxDepth + 1); t += NT) ffc[t] = 0;
         __syncthreads();
