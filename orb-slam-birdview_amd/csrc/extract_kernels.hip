@@ -1632,15 +1632,15 @@ __device__ __forceinline__ void octree_level(const Geom* __restrict__ g, const L
                 }
                 __syncthreads();
                 // 2. per bin, the exclusive prefix of its wave counts (a 16-lane DPP row per bin) and its total
-                if (tid < kRkV * 16) {
-                    const int x = (tid & 15) < NWv ? T2[tid] : 0;
+                for (int i = tid; i < kRkV * 16; i += NT) {   // (whole waves: NT is a multiple of 64)
+                    const int x = (i & 15) < NWv ? T2[i] : 0;
                     int y = x;
                     y += __builtin_amdgcn_update_dpp(0, y, 0x111, 0xf, 0xf, true);
                     y += __builtin_amdgcn_update_dpp(0, y, 0x112, 0xf, 0xf, true);
                     y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xf, 0xf, true);
                     y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xf, 0xf, true);
-                    T2[tid] = y - x;
-                    if ((tid & 15) == 15) HV[tid >> 4] = y;
+                    T2[i] = y - x;
+                    if ((i & 15) == 15) HV[i >> 4] = y;
                 }
                 __syncthreads();
                 // 3. ranks: larger bins' totals + the wave prefix of the node's bin + its position in its wave's run
@@ -2012,7 +2012,7 @@ __device__ __forceinline__ void octree_task(const Geom* __restrict__ g, int f, i
 }
 
 
-template <int NT>   // block size: kOctreeThreads for batches, 1024 for one frame (the host path's latency)
+template <int NT>   // block size: kOctreeThreads (512); the dataflow launch runs the same body at 1024
 __global__ __launch_bounds__(NT) void k_octree(const Geom* __restrict__ g,
                                                            const uint32_t* __restrict__ cands,
                                                            const uint32_t* __restrict__ candFirst,
@@ -2972,12 +2972,13 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
     };
     auto octree = [&](int lbase, int nl, hipStream_t s, int* err) {
         // a small batch (the host path's single frame, C5's 8-frame step) has fewer blocks than CUs, so the
-        // level-0 blocks are the whole latency: 1024 threads halve their per-key steps, and the keys get all
-        // the LDS a CU has (no global key scratch: at 4,000 features the node tables alone pass the 52 KiB
-        // of the batch layout); larger batches keep 512 threads and 52 KiB (three blocks per CU)
+        // keys get all the LDS a CU has (no global key scratch: at 4,000 features the node tables alone pass
+        // the 52 KiB of the batch layout); larger batches keep 52 KiB (three blocks per CU).  512 threads in
+        // both: 1024-thread blocks for small batches read 25.8 against 25.0 us per C5 frame after the
+        // counting-sort rank (profiles/r06/octree_block_ab.txt; 256 threads 33.3 us)
         const bool one = nframes * nl <= 256;
         const int lk = one ? octree_lds_keys_whole_cu(g) : octree_lds_keys(g.node_cap);
-        hipLaunchKernelGGL(one ? k_octree<1024> : k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(one ? 1024 : kOctreeThreads),
+        hipLaunchKernelGGL(k_octree<kOctreeThreads>, dim3(nframes, nl), dim3(kOctreeThreads),
                            octree_lds_bytes(g.node_cap) + (size_t)lk * 6, s, b.d_geom, b.d_cands, b.d_candFirst,
                            b.d_keys, b.d_knode, b.d_lvlKps, b.d_lvlCount, err, lk,
                            b.d_stamps ? b.d_stamps + (size_t)nframes * g.ncells * 8 : nullptr, lbase);
