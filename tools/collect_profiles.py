@@ -29,7 +29,7 @@ def main():
     if dirty:
         commit += "+dirty"
     main_line = None
-    for name in ("bench", "bench_c2", "bench_c5", "bench_c5b1"):
+    for name in ("bench", "bench_driver_form", "bench_c2", "bench_c5", "bench_c5b1"):
         p = os.path.join(OUT, name + ".log")
         if not os.path.exists(p):
             continue

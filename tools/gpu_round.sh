@@ -19,6 +19,8 @@ if [ -n "$PMC" ]; then
   export ORBGPU_PMC_JSON=$OUT/pmc/report.json
 fi
 step bench 600 python bench.py || exit 1
+# the driver's own command (BENCH_rNN.json)
+step bench_driver_form 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
 step bench_c2 300 python bench.py --config c2 --no-cpu --no-c4 --no-bird || exit 1
 step bench_c5 300 python bench.py --config c5 --steps 50 --warmup 5 --no-cpu --no-c4 --no-bird --no-stereo || exit 1
 # what one GPU does at N = 8 in C5 (one frame per step, four in flight)
