@@ -399,7 +399,9 @@ def matcher_leg(img, w, h, nf, device):
             return {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
         out = json.loads(r.stdout.strip().splitlines()[-1])
         out["note"] = ("median us per call, one call per frame / keyframe pair as Tracking.cc:1029-1032, "
-                       "LoopClosing.cc:265, LocalMapping.cc:278, Tracking.cc:738-739, Frame.cc:562-569 and Frame.cc:141 make them; "
+                       "LoopClosing.cc:265, LocalMapping.cc:278, Tracking.cc:738-739, Frame.cc:562-569 and Frame.cc:141 make them "
+                       "(SearchForTriangulation_x10: LocalMapping.cc:247-278's neighbour loop over 10 keyframes as one batched "
+                       "call, against 10 runs of the CPU loop); "
                        "GPU = adapter/ORBmatcher_gpu.cc (host inputs, upload + kernels + host replay), CPU = the "
                        "oracle's restatement of each body, single thread, same inputs; outputs compared equal")
         return out

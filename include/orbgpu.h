@@ -272,6 +272,36 @@ int orb_search_for_triangulation(orb_ctx* ctx, int check_ori, int only_stereo,
                                  const float* F12, float ex, float ey, const float* scale2, const float* sigma2_2,
                                  int nlevels2, int* pairs_out, int cap, int* npairs);
 
+/* SearchForTriangulation of one keyframe (KF1) against several (KF2s) in one call: LocalMapping::CreateNewMapPoints
+ * (LocalMapping.cc:247-278) calls SearchForTriangulation(mpCurrentKeyFrame, pKF2, F12, ..., false) once per
+ * neighbour keyframe.  pairs[p] carries what the single call takes for KF2 = pair p (its outputs included);
+ * the result for pair p is exactly orb_search_for_triangulation's for the same inputs, all pairs sharing one
+ * staging, one launch and one synchronisation.  The reference loop adds map points to KF1 between neighbours
+ * (:449), and SearchForTriangulation skips KF1 features that have one (:694-696); with check_ori = 0 (the
+ * LocalMapping call) every query is decided independently, so a caller that drops, while it walks the pairs in
+ * order, the matches of pair p whose idx1 received a map point from pairs < p gets the sequential result exactly.
+ * ORB_ERR_ARG for a malformed pair (nothing runs); ORB_ERR_CAPACITY if any pair's list overflowed (every pair's
+ * *npairs holds its full count, the lists are filled up to cap). */
+typedef struct orb_tri_pair {
+    int n2;
+    const uint8_t* desc2;
+    const orb_keypoint* kps2;
+    const uint8_t* has_mp2;
+    const float* uright2;
+    orb_featvec fv2;
+    const float* F12;            /* row-major 3x3 */
+    float ex, ey;                /* KF1's centre projected in KF2 */
+    const float* scale2;         /* pKF2->mvScaleFactors */
+    const float* sigma2_2;       /* pKF2->mvLevelSigma2 */
+    int nlevels2;
+    int* pairs_out;              /* 2 ints per pair */
+    int cap;
+    int* npairs;
+} orb_tri_pair;
+int orb_search_for_triangulation_batch(orb_ctx* ctx, int check_ori, int only_stereo,
+                                       int n1, const uint8_t* desc1, const orb_keypoint* kps1, const uint8_t* has_mp1,
+                                       const float* uright1, orb_featvec fv1, int npairs, const orb_tri_pair* pairs);
+
 /* int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<Point2f>& vbPrevMatched,
  *     vector<int>& vnMatches12, int windowSize)  ORBmatcher.cc:405-520 (level0_only = 1), and
  * int ORBmatcher::BirdviewMatch(const Frame&, const Frame&, vector<int>&, int)  :1790-1899

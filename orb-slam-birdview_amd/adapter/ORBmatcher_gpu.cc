@@ -14,6 +14,10 @@
  *   int ORBmatcher::BirdviewMatch(Frame&, Frame&, vector<int>&, vector<cv::Point2f>&, int)  :1667-1786
  *   int ORBmatcher::BirdviewMatch(const Frame&, const Frame&, vector<int>&, int)          :1788-1899
  *
+ * plus one addition, SearchForTriangulation(KeyFrame*, const vector<KeyFrame*>&, const vector<cv::Mat>&,
+ * vector<vector<pair<size_t,size_t>>>&, const bool): LocalMapping's neighbour loop in one call (its declaration
+ * goes into include/ORBmatcher.h; INTEGRATION.md §3 shows the caller).
+ *
  * Everything else in ORBmatcher (the projection-gated searches, Fuse, SearchBySim3, DescriptorDistance,
  * CheckDistEpipolarLine, ComputeThreeMaxima) stays the reference's own CPU code.  Callers
  * (Tracking.cc:739,1032,1938; LocalMapping.cc:278; LoopClosing.cc:265) are unchanged.
@@ -245,6 +249,70 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
     vMatchedPairs.reserve(np);
     for (int i = 0; i < np; i++) vMatchedPairs.push_back(std::make_pair((size_t)pairs[2 * i], (size_t)pairs[2 * i + 1]));
     return np;
+}
+
+// SearchForTriangulation of KF1 against several KF2s in one call (orb_search_for_triangulation_batch): the
+// neighbour loop of LocalMapping::CreateNewMapPoints (LocalMapping.cc:247-278) with the F12s computed first.
+// vvMatchedPairs[p] = SearchForTriangulation(pKF1, vpKF2[p], vF12[p], ..., bOnlyStereo) with KF1's map points as
+// they are now; a caller that triangulates pair by pair drops the entries of pair p whose idx1 received a map
+// point from an earlier pair (include/orbgpu.h).  Returns the total number of pairs.
+int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, const std::vector<KeyFrame*>& vpKF2, const std::vector<cv::Mat>& vF12,
+                                       std::vector<std::vector<std::pair<size_t, size_t> > >& vvMatchedPairs,
+                                       const bool bOnlyStereo) {
+    if (vF12.size() != vpKF2.size()) throw std::invalid_argument("SearchForTriangulation: one F12 per KeyFrame");
+    const int n1 = pKF1->N, np = (int)vpKF2.size();
+    Scratch& S = scratch();
+    std::vector<uint8_t>& mp1 = S.mp1;
+    mp1.assign(n1 > 0 ? n1 : 1, 0);
+    for (int i = 0; i < n1; i++) mp1[i] = pKF1->GetMapPoint(i) != NULL;
+    std::vector<float>& ur1 = S.ur1;
+    ur1.assign(pKF1->mvuRight.begin(), pKF1->mvuRight.end());
+    ur1.resize(n1 > 0 ? n1 : 1, -1.f);
+    const FeatCsr& f1 = S.f1.assign(pKF1->mFeatVec);
+    cv::Mat Cw = pKF1->GetCameraCenter();
+    struct Side {   // one KF2's arrays, alive until the call returns
+        std::vector<uint8_t> mp, t;
+        std::vector<float> ur;
+        FeatCsr f;
+        float F[9];
+        std::vector<int> pairs;
+        int n = 0;
+    };
+    std::vector<Side> side(np);
+    std::vector<orb_tri_pair> P(np);
+    for (int p = 0; p < np; p++) {
+        KeyFrame* pKF2 = vpKF2[p];
+        Side& sd = side[p];
+        cv::Mat C2 = pKF2->GetRotation() * Cw + pKF2->GetTranslation();   // the epipole (:664-670)
+        const float invz = 1.0f / C2.at<float>(2);
+        const float ex = pKF2->fx * C2.at<float>(0) * invz + pKF2->cx;
+        const float ey = pKF2->fy * C2.at<float>(1) * invz + pKF2->cy;
+        const int n2 = pKF2->N;
+        sd.mp.assign(n2 > 0 ? n2 : 1, 0);
+        for (int i = 0; i < n2; i++) sd.mp[i] = pKF2->GetMapPoint(i) != NULL;
+        sd.ur.assign(pKF2->mvuRight.begin(), pKF2->mvuRight.end());
+        sd.ur.resize(n2 > 0 ? n2 : 1, -1.f);
+        sd.f.assign(pKF2->mFeatVec);
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) sd.F[3 * r + c] = vF12[p].at<float>(r, c);
+        sd.pairs.resize(2 * (size_t)(n1 > 0 ? n1 : 1));
+        P[p] = orb_tri_pair{n2, desc_rows(pKF2->mDescriptors, n2, sd.t), keys_of(pKF2->mvKeysUn), sd.mp.data(),
+                            sd.ur.data(), sd.f.fv, sd.F, ex, ey, pKF2->mvScaleFactors.data(), pKF2->mvLevelSigma2.data(),
+                            (int)pKF2->mvScaleFactors.size(), sd.pairs.data(), n1 > 0 ? n1 : 1, &sd.n};
+    }
+    check(orb_search_for_triangulation_batch(ctx(), mbCheckOrientation, bOnlyStereo, n1,
+                                             desc_rows(pKF1->mDescriptors, n1, S.t1), keys_of(pKF1->mvKeysUn), mp1.data(),
+                                             ur1.data(), f1.fv, np, P.data()),
+          "SearchForTriangulation(batch)");
+    vvMatchedPairs.assign(np, std::vector<std::pair<size_t, size_t> >());
+    int total = 0;
+    for (int p = 0; p < np; p++) {
+        vvMatchedPairs[p].reserve(side[p].n);
+        for (int i = 0; i < side[p].n; i++)
+            vvMatchedPairs[p].push_back(std::make_pair((size_t)side[p].pairs[2 * i], (size_t)side[p].pairs[2 * i + 1]));
+        total += side[p].n;
+    }
+    return total;
 }
 
 namespace orbgpu_adapter {

@@ -191,38 +191,30 @@ __global__ __launch_bounds__(256) void k_window_topk(const uint8_t* __restrict__
  * dist << 32 | ~pos.  The inputs live in host memory (the call's pinned mirror): the item record is one
  * wave-uniform read, then each lane reads its candidates' records. */
 __global__ __launch_bounds__(256) void k_triangulation(const TriItem* __restrict__ items,
-                                                       const TriTrain* __restrict__ trains, int nitems, TriParams tp,
+                                                       const TriTrain* __restrict__ trains, int nitems,
                                                        int* __restrict__ best_out) {
     const int it = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (it >= nitems) return;
     const TriItem q = items[it];
     const bool st1 = q.stereo != 0;
-    const float* F = tp.F;
-    // CheckDistEpipolarLine's float expressions with the contractions the reference's -O3 -march=native
-    // build applies (tools/ref_flags_probe.cpp fixes each form)
-    const float la = __builtin_fmaf(q.x, F[0], q.y * F[3]) + F[6];
-    const float lb = __builtin_fmaf(q.x, F[1], q.y * F[4]) + F[7];
-    const float lc = __builtin_fmaf(q.y, F[5], q.x * F[2]) + F[8];
+    // CheckDistEpipolarLine (the reference's contracted float forms, tools/ref_flags_probe.cpp): the line a, b, c
+    // comes staged with the query
+    const float la = q.la, lb = q.lb, lc = q.lc;
     const float den = __builtin_fmaf(la, la, lb * lb);
     unsigned long long bestKey = ~0ull;
     const int c0 = q.c0, c1 = q.c1;
     for (int pos = c0 + lane; pos < c1; pos += 64) {
         const TriTrain& tr = trains[pos];   // (no map point, stereo if asked: filtered on the host, :725-733)
         const uint4 ta = tr.desc[0], tb = tr.desc[1];
-        const float4 t = tr.info;   // x, y, octave, stereo
         const int dist = hamming256(q.desc[0], q.desc[1], ta, tb);
         if (dist > 50) continue;
-        const int oct = (int)t.z;
-        const bool st2 = t.w != 0.f;
-        if (!st1 && !st2) {
-            const float dex = tp.ex - t.x, dey = tp.ey - t.y;
-            if (__builtin_fmaf(dex, dex, dey * dey) < 100 * tp.scale2[oct]) continue;
-        }
+        const int fl = tr.flags;
+        if (!st1 && !(fl & 1) && (fl & 2)) continue;   // neither stereo and too close to the epipole (:743-748)
         if (den == 0) continue;
-        const float num = __builtin_fmaf(lb, t.y, la * t.x) + lc;
+        const float num = __builtin_fmaf(lb, tr.y, la * tr.x) + lc;
         const float dsqr = num * num / den;
-        if (!((double)dsqr < 3.84 * (double)tp.sigma2[oct])) continue;
+        if (!((double)dsqr < 3.84 * (double)tr.sigma2)) continue;
         const unsigned long long key = ((unsigned long long)dist << 32) | (unsigned)(0x7FFFFFFF - (pos - c0));
         bestKey = key < bestKey ? key : bestKey;
     }
@@ -251,11 +243,10 @@ hipError_t launch_window_topk(const uint8_t* d_q, const int* d_item_q, const flo
     return hipGetLastError();
 }
 
-hipError_t launch_triangulation(const TriItem* d_items, const TriTrain* d_trains, int nitems, const TriParams& tp,
-                                int* d_best, hipStream_t stream) {
+hipError_t launch_triangulation(const TriItem* d_items, const TriTrain* d_trains, int nitems, int* d_best,
+                                hipStream_t stream) {
     if (nitems <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_triangulation, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_items, d_trains, nitems, tp,
-                       d_best);
+    hipLaunchKernelGGL(k_triangulation, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_items, d_trains, nitems, d_best);
     return hipGetLastError();
 }
 

@@ -514,97 +514,108 @@ int orb_search_by_bow_kf_kf(orb_ctx* h, float nnratio, int check_ori, int n1, co
 
 /* SearchForTriangulation  ORBmatcher.cc:657-823: no cross-query dependence (vbMatched2 is never
  * set, :738), so every (idx1, node) item is decided on the GPU. */
-int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int n1, const uint8_t* desc1,
-                                 const orb_keypoint* kps1, const uint8_t* has_mp1, const float* uright1,
-                                 orb_featvec fv1, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
-                                 const uint8_t* has_mp2, const float* uright2, orb_featvec fv2, const float* F12,
-                                 float ex, float ey, const float* scale2, const float* sigma2_2, int nlevels2,
-                                 int* pairs_out, int cap, int* npairs) {
-    Ctx* c = reinterpret_cast<Ctx*>(h);
-    CTX_GUARD(c);
-    if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
-    if (!featvec_ok(fv1, n1) || !featvec_ok(fv2, n2))
-        return set_error("orb_search_for_triangulation: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
-    // The inputs, written once into the pinned mirror the kernel reads (the upload is the call's cost,
-    // DESIGN §4.8): per common node its candidates without a map point (and stereo ones only if asked,
-    // :725-733) as train records in the node's order (the reference keeps the last candidate reaching the
-    // minimum), then one item record per query of the node that has candidates (a query with none matches
-    // nothing).  Sizes are bounded by the FeatureVectors' lengths, so the mirror is sized before the walk.
-    std::vector<int>& item_q = c->tri_item_q;     // item -> idx1
-    std::vector<int>& train_of = c->tri_train_of; // train record -> idx2
-    const int cap_items = fv1.nnodes > 0 ? fv1.offsets[fv1.nnodes] : 0;
-    const int cap_trains = fv2.nnodes > 0 ? fv2.offsets[fv2.nnodes] : 0;
-    item_q.clear();
-    train_of.clear();
-    Stage st{c};
-    st.zc = 1;   // one kernel over small inputs: reading the pinned mirror beats the DMA (Stage::zc)
-    const size_t o_it = st.add((size_t)cap_items * sizeof(TriItem)),
-                 o_tr = st.add((size_t)cap_trains * sizeof(TriTrain)), o_b = st.add((size_t)cap_items * 4);
-    if (cap_items > 0 && cap_trains > 0) {
-        int r = st.alloc();
-        if (r != ORB_OK) return r;
-        TriItem* items = st.hi<TriItem>(o_it);
-        TriTrain* trains = st.hi<TriTrain>(o_tr);
-        for_common_nodes(fv1, fv2, [&](int a, int b) {
-            const int cb = (int)train_of.size();
-            for (int i = fv2.offsets[b]; i < fv2.offsets[b + 1]; i++) {
-                const int idx2 = fv2.indices[i];
-                if (has_mp2[idx2]) continue;
-                if (only_stereo && !(uright2[idx2] >= 0)) continue;
-                TriTrain& t = trains[train_of.size()];
-                std::memcpy(t.desc, desc2 + (size_t)idx2 * 32, 32);
-                t.info = make_float4(kps2[idx2].x, kps2[idx2].y, (float)kps2[idx2].octave, uright2[idx2] >= 0 ? 1.f : 0.f);
-                train_of.push_back(idx2);
-            }
-            const int ce = (int)train_of.size();
-            if (ce == cb) return;
-            for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
-                const int idx1 = fv1.indices[i];
-                if (has_mp1[idx1]) continue;                              // :694-696
-                if (only_stereo && !(uright1[idx1] >= 0)) continue;       // :698-702
-                TriItem& q = items[item_q.size()];
-                std::memcpy(q.desc, desc1 + (size_t)idx1 * 32, 32);
-                q.x = kps1[idx1].x;
-                q.y = kps1[idx1].y;
-                q.c0 = cb;
-                q.c1 = ce;
-                q.stereo = uright1[idx1] >= 0 ? 1 : 0;
-                item_q.push_back(idx1);
-            }
-        });
-    }
-    const int nitems = (int)item_q.size();
-    std::vector<int>& best = c->tri_best;
-    best.assign(nitems, -1);
-    if (nitems) {
-        TriParams tp;
-        std::memset(&tp, 0, sizeof tp);
-        std::memcpy(tp.F, F12, sizeof tp.F);
-        tp.ex = ex;
-        tp.ey = ey;
-        for (int l = 0; l < nlevels2; l++) {
-            tp.scale2[l] = scale2[l];
-            tp.sigma2[l] = sigma2_2[l];
+}  // extern "C"
+
+namespace orbgpu {
+namespace {
+// One keyframe pair's staging for k_triangulation, appended at the current ends of the item / train records:
+// per common node its candidates without a map point (and stereo ones only if asked, :725-733) as train records in
+// the node's order (the reference keeps the last candidate reaching the minimum), then one item record per query of
+// the node that has candidates (a query with none matches nothing).  The pair-dependent float work follows in
+// the reference build's forms (tri_geometry, below).
+struct TriSide {
+    int n;
+    const uint8_t* desc;
+    const orb_keypoint* kps;
+    const uint8_t* has_mp;
+    const float* uright;
+    orb_featvec fv;
+};
+void tri_stage_pair(const TriSide& a, const TriSide& b, int only_stereo, TriItem* items, TriTrain* trains,
+                    std::vector<int>& item_q, std::vector<int>& train_of) {
+    for_common_nodes(a.fv, b.fv, [&](int na, int nb) {
+        const int cb = (int)train_of.size();
+        for (int i = b.fv.offsets[nb]; i < b.fv.offsets[nb + 1]; i++) {
+            const int idx2 = b.fv.indices[i];
+            if (b.has_mp[idx2]) continue;
+            if (only_stereo && !(b.uright[idx2] >= 0)) continue;
+            TriTrain& t = trains[train_of.size()];
+            std::memcpy(t.desc, b.desc + (size_t)idx2 * 32, 32);
+            t.x = b.kps[idx2].x;
+            t.y = b.kps[idx2].y;
+            t.sigma2 = (float)b.kps[idx2].octave;   // (the octave until tri_geometry)
+            t.flags = b.uright[idx2] >= 0 ? 1 : 0;
+            train_of.push_back(idx2);
         }
-        tp.only_stereo = only_stereo;
-        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
-        hipError_t e = launch_triangulation(st.di<TriItem>(o_it), st.di<TriTrain>(o_tr), nitems, tp, st.h<int>(o_b),
-                                            c->stream);
-        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
-        if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
-        // the kernel writes its results straight into the pinned mirror (host-coherent memory): no D2H command
-        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
-            return set_error("download", e), ORB_ERR_HIP;
-        const int* hb = st.h<int>(o_b);
-        for (int i = 0; i < nitems; i++) best[i] = hb[i] >= 0 ? train_of[hb[i]] : -1;
+        const int ce = (int)train_of.size();
+        if (ce == cb) return;
+        for (int i = a.fv.offsets[na]; i < a.fv.offsets[na + 1]; i++) {
+            const int idx1 = a.fv.indices[i];
+            if (a.has_mp[idx1]) continue;                              // :694-696
+            if (only_stereo && !(a.uright[idx1] >= 0)) continue;       // :698-702
+            TriItem& q = items[item_q.size()];
+            std::memcpy(q.desc, a.desc + (size_t)idx1 * 32, 32);
+            q.la = a.kps[idx1].x;   // (the keypoint until tri_geometry)
+            q.lb = a.kps[idx1].y;
+            q.c0 = cb;
+            q.c1 = ce;
+            q.stereo = a.uright[idx1] >= 0 ? 1 : 0;
+            item_q.push_back(idx1);
+        }
+    });
+}
+
+// The pair's float work on its staged records: each item's epipolar line (:143-145, contracted as
+// tools/ref_flags_probe.cpp pins: a = fma(x, F00, y F10) + F20, b likewise, c = fma(y, F12, x F02) + F22), each
+// train's epipole test (:743-748, fma(dex, dex, dey dey) < 100 scale) and sigma^2 (:156).  Every fma is exact
+// whether it is an instruction or libm's fmaf, so the host picks the instruction when the CPU has it (a libm call
+// costs ~3.5 ns: ~4 us per C3 call).
+__attribute__((always_inline)) inline void tri_geometry_body(TriItem* items, int ib, int ie, TriTrain* trains, int tb,
+                                                              int te, const float* F, float ex, float ey,
+                                                              const float* scale2, const float* sigma2) {
+    for (int i = ib; i < ie; i++) {
+        TriItem& q = items[i];
+        const float x = q.la, y = q.lb;
+        q.la = __builtin_fmaf(x, F[0], y * F[3]) + F[6];
+        q.lb = __builtin_fmaf(x, F[1], y * F[4]) + F[7];
+        q.lc = __builtin_fmaf(y, F[5], x * F[2]) + F[8];
     }
+    for (int j = tb; j < te; j++) {
+        TriTrain& t = trains[j];
+        const int oct = (int)t.sigma2;
+        const float dex = ex - t.x, dey = ey - t.y;
+        if (__builtin_fmaf(dex, dex, dey * dey) < 100 * scale2[oct]) t.flags |= 2;
+        t.sigma2 = sigma2[oct];
+    }
+}
+#if !defined(__HIP_DEVICE_COMPILE__)   // (host code: the x86-64 FMA form and its dispatch)
+__attribute__((target("fma"))) void tri_geometry_fma(TriItem* items, int ib, int ie, TriTrain* trains, int tb, int te,
+                                                     const float* F, float ex, float ey, const float* scale2,
+                                                     const float* sigma2) {
+    tri_geometry_body(items, ib, ie, trains, tb, te, F, ex, ey, scale2, sigma2);
+}
+#endif
+void tri_geometry(TriItem* items, int ib, int ie, TriTrain* trains, int tb, int te, const float* F, float ex, float ey,
+                  const float* scale2, const float* sigma2) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    static const bool hw_fma = __builtin_cpu_supports("fma");
+    if (hw_fma) return tri_geometry_fma(items, ib, ie, trains, tb, te, F, ex, ey, scale2, sigma2);
+#endif
+    tri_geometry_body(items, ib, ie, trains, tb, te, F, ex, ey, scale2, sigma2);
+}
+
+// One pair's acceptance from the kernel's per-item best records [ib, ie): rotation check (:792-813) and the pair list
+// in ascending idx1 (:815-820).  Returns ORB_OK or ORB_ERR_CAPACITY (*npairs holds the full count either way).
+int tri_replay_pair(Ctx* c, int check_ori, int n1, const orb_keypoint* kps1, const orb_keypoint* kps2, int ib, int ie,
+                    const int* best, int* pairs_out, int cap, int* npairs) {
+    const std::vector<int>& item_q = c->tri_item_q;
     std::vector<int>& vMatches12 = c->tri_match;
     vMatches12.assign(n1, -1);
     static_assert(HISTO_LENGTH == 30, "Ctx::tri_hist");
     std::vector<int>* rotHist = c->tri_hist;
     for (int i = 0; i < HISTO_LENGTH; i++) rotHist[i].clear();
     int nmatches = 0;
-    for (int i = 0; i < nitems; i++) {
+    for (int i = ib; i < ie; i++) {
         if (best[i] < 0) continue;
         const int idx1 = item_q[i];
         vMatches12[idx1] = best[i];
@@ -630,8 +641,110 @@ int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int
         np++;
     }
     *npairs = np;
-    if (np > cap) return set_error("pairs_out too small", hipSuccess), ORB_ERR_CAPACITY;
-    return ORB_OK;
+    return np > cap ? ORB_ERR_CAPACITY : ORB_OK;
+}
+
+// The pairs' staging (items and trains of every pair in one pinned mirror), one k_triangulation launch over all of
+// them, one synchronisation, then each pair's replay.  A single call is the batch of one.
+int tri_run(Ctx* c, int check_ori, int only_stereo, const TriSide& a, int npairs, const orb_tri_pair* pairs) {
+    const int nnz1 = a.fv.nnodes > 0 ? a.fv.offsets[a.fv.nnodes] : 0;
+    size_t cap_items = 0, cap_trains = 0;
+    for (int p = 0; p < npairs; p++) {
+        cap_items += (size_t)nnz1;
+        cap_trains += pairs[p].fv2.nnodes > 0 ? (size_t)pairs[p].fv2.offsets[pairs[p].fv2.nnodes] : 0;
+    }
+    if (cap_items > (size_t)INT_MAX / 2 || cap_trains > (size_t)INT_MAX / 2)
+        return set_error("orb_search_for_triangulation: too many records", hipSuccess), ORB_ERR_ARG;
+    std::vector<int>& item_q = c->tri_item_q;     // item -> idx1
+    std::vector<int>& train_of = c->tri_train_of; // train record -> idx2
+    item_q.clear();
+    train_of.clear();
+    std::vector<int>& ranges = c->tri_ranges;     // pair p's items: [ranges[p], ranges[p + 1])
+    ranges.assign(npairs + 1, 0);
+    Stage st{c};
+    // the kernel reads the pinned mirror (zero copy) at every size: a DMA first measured slower for the single call
+    // and for ten pairs alike (profiles/r06/triangulation_batch.txt)
+    st.zc = 1;
+    const size_t o_it = st.add(cap_items * sizeof(TriItem)), o_tr = st.add(cap_trains * sizeof(TriTrain)),
+                 o_b = st.add(cap_items * 4);
+    if (cap_items > 0 && cap_trains > 0) {
+        const int r = st.alloc();
+        if (r != ORB_OK) return r;
+        TriItem* items = st.hi<TriItem>(o_it);
+        TriTrain* trains = st.hi<TriTrain>(o_tr);
+        for (int p = 0; p < npairs; p++) {
+            const orb_tri_pair& P = pairs[p];
+            const TriSide b{P.n2, P.desc2, P.kps2, P.has_mp2, P.uright2, P.fv2};
+            const int tb = (int)train_of.size();
+            tri_stage_pair(a, b, only_stereo, items, trains, item_q, train_of);
+            ranges[p + 1] = (int)item_q.size();
+            tri_geometry(items, ranges[p], ranges[p + 1], trains, tb, (int)train_of.size(), P.F12, P.ex, P.ey, P.scale2,
+                         P.sigma2_2);
+        }
+    }
+    const int nitems = (int)item_q.size();
+    std::vector<int>& best = c->tri_best;
+    best.assign(nitems, -1);
+    if (nitems) {
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 1, c->stream);
+        hipError_t e = launch_triangulation(st.di<TriItem>(o_it), st.di<TriTrain>(o_tr), nitems, st.h<int>(o_b), c->stream);
+        if (c->prof_on) Ctx::marker(c, ORB_K_HAMMING, 0, c->stream);
+        if (e != hipSuccess) return set_error("triangulation kernel", e), ORB_ERR_HIP;
+        // the kernel writes its results straight into the pinned mirror (host-coherent memory): no D2H command
+        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
+            return set_error("download", e), ORB_ERR_HIP;
+        const int* hb = st.h<int>(o_b);
+        for (int i = 0; i < nitems; i++) best[i] = hb[i] >= 0 ? train_of[hb[i]] : -1;
+    }
+    int rc = ORB_OK;
+    for (int p = 0; p < npairs; p++) {
+        const orb_tri_pair& P = pairs[p];
+        if (tri_replay_pair(c, check_ori, a.n, a.kps, P.kps2, ranges[p], ranges[p + 1], best.data(), P.pairs_out,
+                            P.cap, P.npairs) != ORB_OK)
+            rc = ORB_ERR_CAPACITY;
+    }
+    if (rc != ORB_OK) set_error("pairs_out too small", hipSuccess);
+    return rc;
+}
+
+bool tri_pair_ok(const orb_tri_pair& P) {
+    return P.n2 >= 0 && P.npairs && P.nlevels2 >= 1 && P.nlevels2 <= ORBGPU_MAX_LEVELS && P.F12 && P.scale2 &&
+           P.sigma2_2 && featvec_ok(P.fv2, P.n2) && (P.n2 == 0 || (P.desc2 && P.kps2 && P.has_mp2 && P.uright2));
+}
+}  // namespace
+}  // namespace orbgpu
+
+extern "C" {
+
+int orb_search_for_triangulation(orb_ctx* h, int check_ori, int only_stereo, int n1, const uint8_t* desc1,
+                                 const orb_keypoint* kps1, const uint8_t* has_mp1, const float* uright1,
+                                 orb_featvec fv1, int n2, const uint8_t* desc2, const orb_keypoint* kps2,
+                                 const uint8_t* has_mp2, const float* uright2, orb_featvec fv2, const float* F12,
+                                 float ex, float ey, const float* scale2, const float* sigma2_2, int nlevels2,
+                                 int* pairs_out, int cap, int* npairs) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || n2 < 0 || !npairs || nlevels2 < 1 || nlevels2 > ORBGPU_MAX_LEVELS) return ORB_ERR_ARG;
+    if (!featvec_ok(fv1, n1) || !featvec_ok(fv2, n2))
+        return set_error("orb_search_for_triangulation: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
+    const orb_tri_pair P{n2, desc2, kps2, has_mp2, uright2, fv2, F12, ex, ey, scale2, sigma2_2, nlevels2, pairs_out, cap,
+                         npairs};
+    return tri_run(c, check_ori, only_stereo, TriSide{n1, desc1, kps1, has_mp1, uright1, fv1}, 1, &P);
+}
+
+int orb_search_for_triangulation_batch(orb_ctx* h, int check_ori, int only_stereo, int n1, const uint8_t* desc1,
+                                       const orb_keypoint* kps1, const uint8_t* has_mp1, const float* uright1,
+                                       orb_featvec fv1, int npairs, const orb_tri_pair* pairs) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || npairs < 0 || (npairs > 0 && !pairs)) return ORB_ERR_ARG;
+    if (!featvec_ok(fv1, n1))
+        return set_error("orb_search_for_triangulation_batch: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
+    for (int p = 0; p < npairs; p++)
+        if (!tri_pair_ok(pairs[p]))
+            return set_error("orb_search_for_triangulation_batch: bad pair arguments", hipSuccess), ORB_ERR_ARG;
+    if (npairs == 0) return ORB_OK;
+    return tri_run(c, check_ori, only_stereo, TriSide{n1, desc1, kps1, has_mp1, uright1, fv1}, npairs, pairs);
 }
 
 }  // extern "C"

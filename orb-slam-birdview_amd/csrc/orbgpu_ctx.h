@@ -94,7 +94,7 @@ struct Ctx {
 
     // orb_search_for_triangulation's host lists, kept across calls (capacity reused: a call is ~30 us, and its
     // dozens of small allocations were a measurable part of it)
-    std::vector<int> tri_item_q, tri_train_of, tri_best, tri_match;
+    std::vector<int> tri_item_q, tri_train_of, tri_best, tri_match, tri_ranges;
     std::vector<int> tri_hist[30];
     // orb_hamming_top2_frames_device: the pair list on the device (re-uploaded only when it changes), the list it
     // holds, and two pinned staging slots used in turn

@@ -285,31 +285,30 @@ hipError_t launch_window_topk(const uint8_t* d_q, const int* d_item_q, const flo
                               const int* d_cell_off, const int* d_cell_idx, const WinGrid& wg, const int* d_thr,
                               int k, int* d_dist, int* d_idx, int* d_nvalid, hipStream_t stream);
 
-struct TriParams {
-    float F[9];
-    float ex, ey;
-    float scale2[ORBGPU_MAX_LEVELS];
-    float sigma2[ORBGPU_MAX_LEVELS];
-    int only_stereo;
-};
 // SearchForTriangulation's staged inputs, read by k_triangulation straight from the pinned mirror (over PCIe):
 // one record per query (item) holding everything its wave needs, and the candidate trains' records in
 // candidate order, so a wave's reads are two dependent round trips (its item record, then its candidates').
+// Everything that depends on the keyframe pair rather than on a (query, candidate) pair is evaluated on the host
+// while staging, with the reference build's float forms (tools/ref_flags_probe.cpp): the query's epipolar line
+// (CheckDistEpipolarLine's a, b, c, ORBmatcher.cc:143-145) and the candidate's epipole test (:743-748) and
+// sigma^2 (:156).  So one launch can serve several keyframe pairs (the batch call).
 struct TriItem {          // 64 B
     uint4 desc[2];
-    float x, y;
+    float la, lb, lc;     // a = x F00 + y F10 + F20, b = x F01 + y F11 + F21, c = x F02 + y F12 + F22 (contracted)
     int c0, c1;           // the item's candidates: train records [c0, c1)
     int stereo;           // mvuRight >= 0
-    int pad[3];
+    int pad[2];
 };
 struct TriTrain {         // 48 B
     uint4 desc[2];
-    float4 info;          // x, y, octave, stereo (1 / 0)
+    float x, y;           // KF2 keypoint
+    float sigma2;         // pKF2->mvLevelSigma2[octave]
+    int flags;            // bit 0: stereo (mvuRight >= 0); bit 1: inside the epipole radius (dex^2 + dey^2 < 100 scale)
 };
 static_assert(sizeof(TriItem) == 64 && sizeof(TriTrain) == 48, "k_triangulation's record layout");
 // One work item per query with candidates; returns per item the best train record (or -1).
-hipError_t launch_triangulation(const TriItem* d_items, const TriTrain* d_trains, int nitems, const TriParams& tp,
-                                int* d_best, hipStream_t stream);
+hipError_t launch_triangulation(const TriItem* d_items, const TriTrain* d_trains, int nitems, int* d_best,
+                                hipStream_t stream);
 
 // Frame::ComputeStereoMatches (stereo.hip).  One side of a rectified pair: its pyramid (level 0 in
 // `frames`, levels >= 1 in `pyr`) and extraction outputs, for pair p at frame frame0 + p*frame_step.

@@ -226,6 +226,52 @@ int ORBmatcher::SearchForTriangulation(const KeyFrameData& KF1, const KeyFrameDa
     return np;
 }
 
+int ORBmatcher::SearchForTriangulation(const KeyFrameData& KF1, const std::vector<TriangulationNeighbour>& neighbours,
+                                       std::vector<std::vector<std::pair<size_t, size_t> > >& vvMatchedPairs,
+                                       const bool bOnlyStereo) {
+    const int n1 = KF1.N(), np = (int)neighbours.size();
+    require(n1 == 0 || (KF1.keys && KF1.descriptors), "SearchForTriangulation: KF1 keys/descriptors");
+    Csr a(KF1.featVec);
+    std::vector<uint8_t> mp1 = flags_or(KF1.hasMapPoint, std::max(n1, 1), 0);
+    std::vector<float> ur1 = floats_or(KF1.uRight, std::max(n1, 1), -1.f);
+    struct Side {   // one neighbour's views, alive until the call returns
+        std::vector<uint8_t> mp;
+        std::vector<float> ur;
+        std::vector<int> pairs;
+        int n = 0;
+    };
+    std::vector<Side> side(np);
+    std::vector<Csr> csr;
+    csr.reserve(np);
+    std::vector<orb_tri_pair> P(np);
+    for (int p = 0; p < np; p++) {
+        require(neighbours[p].KF2 != nullptr, "SearchForTriangulation: neighbour KeyFrame");
+        const KeyFrameData& KF2 = *neighbours[p].KF2;
+        const int n2 = KF2.N();
+        require(n2 == 0 || (KF2.keys && KF2.descriptors), "SearchForTriangulation: KF2 keys/descriptors");
+        require(KF2.scaleFactors && KF2.levelSigma2 && KF2.nlevels > 0, "SearchForTriangulation: KF2 scale tables");
+        Side& sd = side[p];
+        sd.mp = flags_or(KF2.hasMapPoint, std::max(n2, 1), 0);
+        sd.ur = floats_or(KF2.uRight, std::max(n2, 1), -1.f);
+        sd.pairs.resize(2 * (size_t)std::max(n1, 1));
+        csr.emplace_back(KF2.featVec);
+        P[p] = orb_tri_pair{n2, desc_ptr(KF2), keys_ptr(KF2), sd.mp.data(), sd.ur.data(), csr.back().fv,
+                            neighbours[p].F12, neighbours[p].ex, neighbours[p].ey, KF2.scaleFactors, KF2.levelSigma2,
+                            KF2.nlevels, sd.pairs.data(), std::max(n1, 1), &sd.n};
+    }
+    check(orb_search_for_triangulation_batch(matcher_ctx(), mbCheckOrientation, bOnlyStereo, n1, desc_ptr(KF1),
+                                             keys_ptr(KF1), mp1.data(), ur1.data(), a.fv, np, P.data()),
+          "SearchForTriangulation(batch)");
+    vvMatchedPairs.assign(np, std::vector<std::pair<size_t, size_t> >());
+    int total = 0;
+    for (int p = 0; p < np; p++) {
+        for (int i = 0; i < side[p].n; i++)
+            vvMatchedPairs[p].push_back(std::make_pair((size_t)side[p].pairs[2 * i], (size_t)side[p].pairs[2 * i + 1]));
+        total += side[p].n;
+    }
+    return total;
+}
+
 int ORBmatcher::window_match(bool level0_only, const FeatureSet& F1, const FeatureSet& F2,
                              const std::vector<Point2f>* centres, int windowSize, std::vector<int>& vnMatches12) {
     const int n1 = F1.N(), n2 = F2.N();

@@ -102,6 +102,15 @@ public:
     // centre in KF2 (:662-668, computed by the caller from the poses).
     int SearchForTriangulation(const KeyFrameData& KF1, const KeyFrameData& KF2, const float F12[9], float ex, float ey,
                                std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo);
+    // KF1 against several KF2s in one call (LocalMapping.cc:247-278's neighbour loop; orb_search_for_triangulation_batch):
+    // vvMatchedPairs[p] == SearchForTriangulation(KF1, *neighbours[p].KF2, ...) for the same inputs.  Returns the total.
+    struct TriangulationNeighbour {
+        const KeyFrameData* KF2;
+        float F12[9];
+        float ex, ey;
+    };
+    int SearchForTriangulation(const KeyFrameData& KF1, const std::vector<TriangulationNeighbour>& neighbours,
+                               std::vector<std::vector<std::pair<size_t, size_t> > >& vvMatchedPairs, const bool bOnlyStereo);
 
     // ORBmatcher.cc:1667-1789 (window around vPrevMatched, level-0 only, updates vPrevMatched) and
     // :1790-1899 (window around each keypoint).  F1: keys (mvKeysBird), descriptors;

@@ -382,6 +382,37 @@ class ORBmatcher:
               "SearchForTriangulation")
         return pairs[:n.value]
 
+    def SearchForTriangulationBatch(self, desc1, kps1, has_mp1, uright1, featvec1, others, bOnlyStereo=False):
+        """orb_search_for_triangulation_batch: KF1 against several KF2s in one call (LocalMapping.cc:247-278's
+        loop).  others: a list of dicts with the single call's KF2 arguments (desc2, kps2, has_mp2, uright2,
+        featvec2, F12, ex, ey, scale_factors2, level_sigma2_2).  Returns one (n, 2) array per KF2, each equal to
+        SearchForTriangulation's for the same inputs."""
+        from ._lib import OrbTriPair
+        fa, ka = _featvec(featvec1)
+        a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(kps1, KP_DTYPE), np.asarray(has_mp1, np.uint8),
+                                                np.asarray(uright1, np.float32))]
+        keep, arr, outs, counts = [ka, a], (OrbTriPair * max(len(others), 1))(), [], []
+        for p, o in enumerate(others):
+            fb, kb = _featvec(o["featvec2"])
+            b = [np.ascontiguousarray(x) for x in (o["desc2"], np.asarray(o["kps2"], KP_DTYPE),
+                                                    np.asarray(o["has_mp2"], np.uint8), np.asarray(o["uright2"], np.float32),
+                                                    np.asarray(o["F12"], np.float32).reshape(9),
+                                                    np.asarray(o["scale_factors2"], np.float32),
+                                                    np.asarray(o["level_sigma2_2"], np.float32))]
+            cap = len(a[0]) + 1
+            out = np.zeros((cap, 2), np.int32)
+            n = ctypes.c_int()
+            keep += [kb, b, out, n]
+            outs.append(out)
+            counts.append(n)
+            arr[p] = OrbTriPair(len(b[0]), _p(b[0]), _p(b[1]), _p(b[2]), _p(b[3]), fb, _p(b[4]), float(o["ex"]),
+                                float(o["ey"]), _p(b[5]), _p(b[6]), len(b[5]), _p(out), cap, ctypes.pointer(n))
+        check(lib().orb_search_for_triangulation_batch(self._ctx.h, int(self.mbCheckOrientation), int(bOnlyStereo),
+                                                       len(a[0]), _p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]), fa,
+                                                       len(others), ctypes.cast(arr, ctypes.c_void_p)),
+              "SearchForTriangulationBatch")
+        return [out[:n.value] for out, n in zip(outs, counts)]
+
     def _window(self, level0_only, desc1, kps1, desc2, kps2, cand_off, cand_idx):
         a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(kps1, KP_DTYPE), desc2, np.asarray(kps2, KP_DTYPE),
                                                 np.asarray(cand_off, np.int32), np.asarray(cand_idx, np.int32))]

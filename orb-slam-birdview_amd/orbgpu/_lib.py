@@ -36,6 +36,12 @@ class OrbFeatVec(ctypes.Structure):
     _fields_ = [("nnodes", ci), ("node_ids", vp), ("offsets", vp), ("indices", vp)]
 
 
+class OrbTriPair(ctypes.Structure):   # orb_tri_pair
+    _fields_ = [("n2", ci), ("desc2", vp), ("kps2", vp), ("has_mp2", vp), ("uright2", vp), ("fv2", OrbFeatVec),
+                ("F12", vp), ("ex", cf), ("ey", cf), ("scale2", vp), ("sigma2_2", vp), ("nlevels2", ci),
+                ("pairs_out", vp), ("cap", ci), ("npairs", ctypes.POINTER(ci))]
+
+
 class OrbFrameGrid(ctypes.Structure):
     _fields_ = [("min_x", cf), ("min_y", cf), ("inv_w", cf), ("inv_h", cf), ("cell_off", vp), ("cell_idx", vp)]
 
@@ -78,6 +84,7 @@ SIGNATURES = {
                                      ctypes.POINTER(ci)]),
     "orb_search_for_triangulation": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, vp,
                                           OrbFeatVec, vp, cf, cf, vp, vp, ci, vp, ci, ctypes.POINTER(ci)]),
+    "orb_search_for_triangulation_batch": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, OrbFeatVec, ci, vp]),
     "orb_window_match": (ci, [vp, cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, ctypes.POINTER(ci)]),
     "orb_window_match_grid": (ci, [vp, cf, ci, ci, ci, vp, vp, vp, cf, ci, vp, vp, OrbFrameGrid, vp,
                                    ctypes.POINTER(ci)]),

@@ -352,6 +352,21 @@ int main(int argc, char** argv) {
                 for (int i = 0; ok && i < np; i++) ok = (int)pairs[i].first == op[2 * i] && (int)pairs[i].second == op[2 * i + 1];
                 report("SearchForTriangulation_stereo" + std::to_string(only_stereo), ok,
                        "n=" + std::to_string(np) + " oracle=" + std::to_string(onp));
+                // the batched form over two neighbours (the second with a near epipole): each list == the single call's
+                std::vector<ORBmatcher::TriangulationNeighbour> nb(2);
+                for (int p = 0; p < 2; p++) {
+                    nb[p].KF2 = &B;
+                    for (int i = 0; i < 9; i++) nb[p].F12[i] = F12[i];
+                    nb[p].ex = p ? 320.f : 5000.f;
+                    nb[p].ey = 300.f;
+                }
+                std::vector<std::vector<std::pair<size_t, size_t> > > vv;
+                const int tot = matcher.SearchForTriangulation(A, nb, vv, only_stereo != 0);
+                std::vector<std::pair<size_t, size_t> > near;
+                const int nn = matcher.SearchForTriangulation(A, B, F12, 320.f, 300.f, near, only_stereo != 0);
+                report("SearchForTriangulation_batch_stereo" + std::to_string(only_stereo),
+                       vv.size() == 2 && vv[0] == pairs && vv[1] == near && tot == np + nn,
+                       "total=" + std::to_string(tot));
             }
         }
 

@@ -271,6 +271,25 @@ int main(int argc, char** argv) {
             if (!stereo)
                 printf("TIME SearchForTriangulation %.1f\n",
                        time_us([&] { matcher.SearchForTriangulation(&KF1, &KF2, F12, vMatchedIndices, false); }, 20));
+            // the batched overload (LocalMapping's neighbour loop in one call): KF2 three times and KF1 against itself
+            // with the same F12, each entry equal to the single call's
+            {
+                std::vector<KeyFrame*> vpKF2 = {&KF2, &KF1, &KF2};
+                std::vector<cv::Mat> vF12 = {F12, F12, F12};
+                std::vector<std::vector<std::pair<size_t, size_t> > > vv;
+                const int tot = matcher.SearchForTriangulation(&KF1, vpKF2, vF12, vv, stereo != 0);
+                bool bok = vv.size() == 3;
+                int sum = 0;
+                for (int p = 0; bok && p < 3; p++) {
+                    std::vector<std::pair<size_t, size_t> > one;
+                    matcher.SearchForTriangulation(&KF1, vpKF2[p], F12, one, stereo != 0);
+                    bok = one == vv[p];
+                    sum += (int)vv[p].size();
+                }
+                bok = bok && sum == tot && vv[0] == vMatchedIndices;
+                snprintf(det, sizeof det, "total=%d", tot);
+                report(std::string("SearchForTriangulation_batch") + (stereo ? "_onlyStereo" : ""), bok, det);
+            }
         }
 
         // ---- SearchForInitialization: Tracking::MonocularInitialization (ORBmatcher(0.9,true), window 100,

@@ -381,6 +381,144 @@ def test_search_for_triangulation_nonfinite(orbgpu_mod, oracle_mod, frames, case
         assert len(op) > 0
 
 
+def _tri_batch_pairs(frames, oracle_mod, seed):
+    """Six KF2s for one KF1 (LocalMapping's neighbour loop): both frames as KF2, different F12 (epipolar lines
+    near y2 = y1, rotated), epipoles near, far and NaN, different map-point and stereo masks, and KF2 FeatureVectors
+    of different node granularity."""
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(seed)
+    t = oracle_mod.OracleExtractor(1000).tables()
+    base = np.array([[0, 0, 0], [0, 0, -1], [0, 1, 0]], np.float32)
+    out = []
+    for p in range(6):
+        k2, d2 = (kb, db) if p % 3 != 2 else (ka, da)
+        F = base + rng.normal(0, 1e-4 * (1 + p), (3, 3)).astype(np.float32)
+        ex, ey = [(320.0, 240.0), (1e5, 1e5), (float("nan"), 100.0), (50.0, 400.0), (320.0, 240.0), (1e5, -1e5)][p]
+        out.append(dict(desc2=d2, kps2=k2, has_mp2=(rng.random(len(d2)) < 0.2 + 0.1 * p).astype(np.uint8),
+                        uright2=np.where(rng.random(len(d2)) < 0.5, 10.0, -1.0).astype(np.float32),
+                        featvec2=_featvec(d2, [8, 6, 10, 8, 4, 8][p]), F12=F, ex=ex, ey=ey,
+                        scale_factors2=t["scale"], level_sigma2_2=t["sigma2"]))
+    return out
+
+
+@pytest.mark.parametrize("check_ori,only_stereo", [(False, False), (True, False), (False, True)])
+def test_search_for_triangulation_batch(orbgpu_mod, oracle_mod, frames, check_ori, only_stereo):
+    """orb_search_for_triangulation_batch: KF1 against six KF2s in one call gives, pair for pair, the single call's
+    result and the oracle's (ORBmatcher.cc:657-823 per pair)."""
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(31)
+    mp1 = (rng.random(len(da)) < 0.3).astype(np.uint8)
+    ur1 = np.where(rng.random(len(da)) < 0.5, 10.0, -1.0).astype(np.float32)
+    fva = _featvec(da, 8)
+    others = _tri_batch_pairs(frames, oracle_mod, 32)
+    m = orbgpu_mod.ORBmatcher(0.6, check_ori)
+    got = m.SearchForTriangulationBatch(da, ka, mp1, ur1, fva, others, only_stereo)
+    assert len(got) == len(others)
+    oa, _keep_a = _oracle_fv(oracle_mod, fva)
+    total = 0
+    for o, g in zip(others, got):
+        single = m.SearchForTriangulation(da, ka, mp1, ur1, fva, o["desc2"], o["kps2"], o["has_mp2"], o["uright2"],
+                                          o["featvec2"], o["F12"], o["ex"], o["ey"], o["scale_factors2"],
+                                          o["level_sigma2_2"], only_stereo)
+        ob, _keep_b = _oracle_fv(oracle_mod, o["featvec2"])
+        op = oracle_mod.search_for_triangulation(check_ori, only_stereo, da, ka, mp1, ur1, oa, o["desc2"], o["kps2"],
+                                                 o["has_mp2"], o["uright2"], ob, o["F12"], o["ex"], o["ey"],
+                                                 o["scale_factors2"], o["level_sigma2_2"])
+        assert np.array_equal(g, single) and np.array_equal(g, op)
+        total += len(op)
+    assert total > 0
+
+
+def test_search_for_triangulation_batch_local_mapping_order(orbgpu_mod, oracle_mod, frames):
+    """The documented use in LocalMapping::CreateNewMapPoints (LocalMapping.cc:247-278, 449): the reference calls
+    SearchForTriangulation per neighbour and gives KF1 features new map points between the calls.  With
+    check_ori = 0, the batch computed once plus dropping, pair by pair, the matches whose idx1 received a map point
+    from an earlier pair equals the sequential loop of single calls with the map-point mask updated as it goes
+    (here every other accepted match "triangulates")."""
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(33)
+    mp1 = (rng.random(len(da)) < 0.2).astype(np.uint8)
+    ur1 = np.full(len(da), -1.0, np.float32)
+    fva = _featvec(da, 8)
+    others = _tri_batch_pairs(frames, oracle_mod, 34)
+    m = orbgpu_mod.ORBmatcher(0.6, False)
+    # the reference order: single calls, the KF1 mask growing between them
+    seq, mask = [], mp1.copy()
+    for o in others:
+        r = m.SearchForTriangulation(da, ka, mask, ur1, fva, o["desc2"], o["kps2"], o["has_mp2"], o["uright2"],
+                                     o["featvec2"], o["F12"], o["ex"], o["ey"], o["scale_factors2"],
+                                     o["level_sigma2_2"])
+        seq.append(r)
+        mask[r[::2, 0]] = 1
+    # the batch, then the caller's filter
+    got = m.SearchForTriangulationBatch(da, ka, mp1, ur1, fva, others)
+    mask = mp1.copy()
+    n_dropped = 0
+    for r, g in zip(seq, got):
+        keep = mask[g[:, 0]] == 0
+        n_dropped += int((~keep).sum())
+        assert np.array_equal(g[keep], r)
+        mask[r[::2, 0]] = 1
+    assert sum(len(r) for r in seq) > 0 and n_dropped > 0
+
+
+def test_search_for_triangulation_batch_edges(orbgpu_mod, oracle_mod, frames):
+    """An empty pair list, a KF2 without features or without a common node, a malformed KF2 FeatureVector (the whole
+    call refused with ORB_ERR_ARG before anything runs or is written), and one pair's list overflowing (ORB_ERR_CAPACITY,
+    every pair's count and lists still filled)."""
+    import ctypes
+    from orbgpu import _lib
+    ka, da, kb, db = frames
+    L = _lib.lib()
+    m = orbgpu_mod.ORBmatcher(0.6, False)
+    n1 = len(da)
+    fva = _featvec(da, 8)
+    fa, _keep_a = orbgpu_mod._featvec(fva)
+    a = [np.ascontiguousarray(x) for x in (da, np.asarray(ka, orbgpu_mod.KP_DTYPE), np.zeros(n1, np.uint8),
+                                            np.full(n1, -1, np.float32))]
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    st = L.orb_search_for_triangulation_batch(m._ctx.h, 0, 0, n1, p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa, 0, None)
+    assert _lib.STATUS.get(st) == "ORB_OK"
+    others = _tri_batch_pairs(frames, oracle_mod, 35)[:3]
+    others[0] = dict(others[0], desc2=np.zeros((0, 32), np.uint8), kps2=np.zeros(0, orbgpu_mod.KP_DTYPE),
+                     has_mp2=np.zeros(0, np.uint8), uright2=np.zeros(0, np.float32), featvec2={})
+    others[1] = dict(others[1], featvec2={k + 1000: v for k, v in others[1]["featvec2"].items()})
+    got = m.SearchForTriangulationBatch(da, ka, a[2], a[3], fva, others)
+    assert len(got[0]) == 0 and len(got[1]) == 0 and len(got[2]) > 3
+    single = m.SearchForTriangulation(da, ka, a[2], a[3], fva, others[2]["desc2"], others[2]["kps2"],
+                                      others[2]["has_mp2"], others[2]["uright2"], others[2]["featvec2"],
+                                      others[2]["F12"], others[2]["ex"], others[2]["ey"],
+                                      others[2]["scale_factors2"], others[2]["level_sigma2_2"])
+    assert np.array_equal(got[2], single)
+    # one malformed KF2 CSR: refused, nothing written
+    o = others[2]
+    b = [np.ascontiguousarray(x) for x in (o["desc2"], np.asarray(o["kps2"], orbgpu_mod.KP_DTYPE), o["has_mp2"],
+                                            o["uright2"], np.asarray(o["F12"], np.float32).reshape(9),
+                                            np.asarray(o["scale_factors2"], np.float32),
+                                            np.asarray(o["level_sigma2_2"], np.float32))]
+    fb, _keep_b = orbgpu_mod._featvec(o["featvec2"])
+    ids, off, idx8 = np.array([0, 1], np.uint32), np.array([0, 5, 3], np.int32), np.arange(8, dtype=np.int32)
+    bad = orbgpu_mod.OrbFeatVec(2, ids.ctypes.data, off.ctypes.data, idx8.ctypes.data)
+    outs = [np.full((n1 + 1, 2), -7, np.int32) for _ in range(2)]
+    cnt = [ctypes.c_int(-5) for _ in range(2)]
+    arr = (_lib.OrbTriPair * 2)()
+    for i, fv in enumerate((fb, bad)):
+        arr[i] = _lib.OrbTriPair(len(b[0]), p(b[0]), p(b[1]), p(b[2]), p(b[3]), fv, p(b[4]), o["ex"], o["ey"], p(b[5]),
+                                 p(b[6]), len(b[5]), p(outs[i]), n1 + 1, ctypes.pointer(cnt[i]))
+    st = L.orb_search_for_triangulation_batch(m._ctx.h, 0, 0, n1, p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa, 2,
+                                              ctypes.cast(arr, ctypes.c_void_p))
+    assert _lib.STATUS.get(st) == "ORB_ERR_ARG"
+    assert all(c.value == -5 for c in cnt) and all((x == -7).all() for x in outs)
+    # the second pair's list too small: every count reported, the first pair complete, the second cut at cap
+    arr[1] = _lib.OrbTriPair(len(b[0]), p(b[0]), p(b[1]), p(b[2]), p(b[3]), fb, p(b[4]), o["ex"], o["ey"], p(b[5]),
+                             p(b[6]), len(b[5]), p(outs[1]), 2, ctypes.pointer(cnt[1]))
+    st = L.orb_search_for_triangulation_batch(m._ctx.h, 0, 0, n1, p(a[0]), p(a[1]), p(a[2]), p(a[3]), fa, 2,
+                                              ctypes.cast(arr, ctypes.c_void_p))
+    assert _lib.STATUS.get(st) == "ORB_ERR_CAPACITY"
+    assert cnt[0].value == len(single) and cnt[1].value == len(single)
+    assert np.array_equal(outs[0][:len(single)], single) and np.array_equal(outs[1][:2], single[:2])
+
+
 @pytest.mark.parametrize("level0_only,window", [(True, 100), (False, 15), (True, 40)])
 def test_window_match(orbgpu_mod, oracle_mod, frames, level0_only, window):
     ka, da, kb, db = frames

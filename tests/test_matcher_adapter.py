@@ -35,6 +35,11 @@ def test_adapter_defines_the_reference_signatures(adapter_bin):
         "ORB_SLAM2::ORBmatcher::SearchForTriangulation(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, cv::Mat, "
         "std::vector<std::pair<unsigned long, unsigned long>, std::allocator<std::pair<unsigned long, unsigned long> > >&,"
         " bool)",
+        "ORB_SLAM2::ORBmatcher::SearchForTriangulation(ORB_SLAM2::KeyFrame*, std::vector<ORB_SLAM2::KeyFrame*, "
+        "std::allocator<ORB_SLAM2::KeyFrame*> > const&, std::vector<cv::Mat, std::allocator<cv::Mat> > const&, "
+        "std::vector<std::vector<std::pair<unsigned long, unsigned long>, std::allocator<std::pair<unsigned long, "
+        "unsigned long> > >, std::allocator<std::vector<std::pair<unsigned long, unsigned long>, "
+        "std::allocator<std::pair<unsigned long, unsigned long> > > > >&, bool)",
         "ORB_SLAM2::ORBmatcher::SearchForInitialization(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, "
         "std::vector<cv::Point2f, std::allocator<cv::Point2f> >&, std::vector<int, std::allocator<int> >&, int)",
         "ORB_SLAM2::ORBmatcher::BirdviewMatch(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, std::vector<int, "

@@ -269,6 +269,17 @@ int main(int argc, char** argv) {
                                             scale.data(), sigma2.data(), pairs.data(), nA + 1);
         }, cpu_reps);
         emit("SearchForTriangulation", g, c, nm, onp, ok);
+        // LocalMapping's neighbour loop (LocalMapping.cc:247-278) as one batched call: KF1 against kNeigh KF2s (the
+        // second keyframe each time: the same work per pair), against kNeigh runs of the CPU loop
+        constexpr int kNeigh = 10;
+        std::vector<KeyFrame*> vpKF2(kNeigh, &KF[1]);
+        std::vector<cv::Mat> vF12(kNeigh, F12);
+        std::vector<std::vector<std::pair<size_t, size_t> > > vv;
+        const int tot = m.SearchForTriangulation(&KF[0], vpKF2, vF12, vv, false);
+        bool bok = (int)vv.size() == kNeigh && tot == kNeigh * onp;
+        for (int p = 0; bok && p < kNeigh; p++) bok = vv[p] == v;
+        const double gb = median_us([&] { m.SearchForTriangulation(&KF[0], vpKF2, vF12, vv, false); }, reps);
+        emit("SearchForTriangulation_x10", gb, kNeigh * c, tot, kNeigh * onp, bok && ok);
     }
     // ---- SearchForInitialization (window 100; vbPrevMatched = the first frame's keypoints)
     {
