@@ -400,8 +400,9 @@ def matcher_leg(img, w, h, nf, device):
         out = json.loads(r.stdout.strip().splitlines()[-1])
         out["note"] = ("median us per call, one call per frame / keyframe pair as Tracking.cc:1029-1032, "
                        "LoopClosing.cc:265, LocalMapping.cc:278, Tracking.cc:738-739, Frame.cc:562-569 and Frame.cc:141 make them "
-                       "(SearchForTriangulation_x10: LocalMapping.cc:247-278's neighbour loop over 10 keyframes as one batched "
-                       "call, against 10 runs of the CPU loop); "
+                       "(the _x10 entries: a caller's loop over 10 keyframes as one batched call against 10 runs of the CPU loop -- "
+                       "SearchByBoW_KF_F_x10 Tracking.cc:1931-1938, SearchByBoW_KF_KF_x10 LoopClosing.cc:252-265, "
+                       "SearchForTriangulation_x10 LocalMapping.cc:247-278); "
                        "GPU = adapter/ORBmatcher_gpu.cc (host inputs, upload + kernels + host replay), CPU = the "
                        "oracle's restatement of each body, single thread, same inputs; outputs compared equal")
         return out

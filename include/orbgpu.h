@@ -257,6 +257,30 @@ int orb_search_by_bow_kf_kf(orb_ctx* ctx, float nnratio, int check_ori,
                             orb_featvec fv1, int n2, const uint8_t* desc2, const float* angle2,
                             const uint8_t* mp2, orb_featvec fv2, int* match12, int* nmatches);
 
+/* The BoW searches over several keyframes in one call (one staging, one ranking launch, then each keyframe's
+ * replay in the reference's order): the loops of Tracking::Relocalization (Tracking.cc:1931-1938,
+ * SearchByBoW(pKF, mCurrentFrame, ...) per candidate keyframe) and LoopClosing::ComputeSim3 (LoopClosing.cc:252-265,
+ * SearchByBoW(mpCurrentKF, pKF, ...) per loop candidate), whose iterations are independent.  Entry p's outputs are
+ * exactly the single call's for the same inputs.
+ *   orb_search_by_bow_kf_f_batch:  KF = kfs[p] (n, desc, angle, mp = its map-point flags, fv) against one Frame;
+ *                                  match = match_f (n_f ints), *nmatches = the return value.
+ *   orb_search_by_bow_kf_kf_batch: KF1 against KF2 = kf2s[p] (mp = KF2's map-point flags); match = match12 (n1 ints).
+ * ORB_ERR_ARG for a malformed entry (nothing runs). */
+typedef struct orb_bow_kf {
+    int n;
+    const uint8_t* desc;
+    const float* angle;
+    const uint8_t* mp;
+    orb_featvec fv;
+    int* match;
+    int* nmatches;
+} orb_bow_kf;
+int orb_search_by_bow_kf_f_batch(orb_ctx* ctx, float nnratio, int check_ori, int n_f, const uint8_t* desc_f,
+                                 const float* angle_f, orb_featvec fv_f, int nkf, const orb_bow_kf* kfs);
+int orb_search_by_bow_kf_kf_batch(orb_ctx* ctx, float nnratio, int check_ori, int n1, const uint8_t* desc1,
+                                  const float* angle1, const uint8_t* mp1, orb_featvec fv1, int nkf,
+                                  const orb_bow_kf* kf2s);
+
 /* int ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12,
  *     vector<pair<size_t,size_t>>&, const bool bOnlyStereo)   ORBmatcher.cc:657-823
  * Keypoints are mvKeysUn; has_mp[i] <=> GetMapPoint(i) != NULL; uright = mvuRight; F12 row-major

@@ -14,9 +14,12 @@
  *   int ORBmatcher::BirdviewMatch(Frame&, Frame&, vector<int>&, vector<cv::Point2f>&, int)  :1667-1786
  *   int ORBmatcher::BirdviewMatch(const Frame&, const Frame&, vector<int>&, int)          :1788-1899
  *
- * plus one addition, SearchForTriangulation(KeyFrame*, const vector<KeyFrame*>&, const vector<cv::Mat>&,
- * vector<vector<pair<size_t,size_t>>>&, const bool): LocalMapping's neighbour loop in one call (its declaration
- * goes into include/ORBmatcher.h; INTEGRATION.md §3 shows the caller).
+ * plus three additions for the callers' loops over keyframes, one call each (their declarations go into
+ * include/ORBmatcher.h; INTEGRATION.md §3 shows the callers):
+ *   int SearchByBoW(const vector<KeyFrame*>&, Frame&, vector<vector<MapPoint*>>&, vector<int>&)   Tracking.cc:1931-1938
+ *   int SearchByBoW(KeyFrame*, const vector<KeyFrame*>&, vector<vector<MapPoint*>>&, vector<int>&) LoopClosing.cc:252-265
+ *   int SearchForTriangulation(KeyFrame*, const vector<KeyFrame*>&, const vector<cv::Mat>&,
+ *                              vector<vector<pair<size_t,size_t>>>&, const bool)                  LocalMapping.cc:247-278
  *
  * Everything else in ORBmatcher (the projection-gated searches, Fuse, SearchBySim3, DescriptorDistance,
  * CheckDistEpipolarLine, ComputeThreeMaxima) stays the reference's own CPU code.  Callers
@@ -205,6 +208,95 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
     for (int i1 = 0; i1 < n1; i1++)
         if (match[i1] >= 0) vpMatches12[i1] = vpMapPoints2[match[i1]];
     return nmatches;
+}
+
+// SearchByBoW(pKF, F) for every keyframe of vpKFs in one call (orb_search_by_bow_kf_f_batch): the relocalisation
+// candidates of Tracking::Relocalization (Tracking.cc:1931-1938), whose iterations are independent.
+// vvpMapPointMatches[i] / the returned vnMatches[i] are SearchByBoW(vpKFs[i], F, ...)'s outputs.
+int ORBmatcher::SearchByBoW(const std::vector<KeyFrame*>& vpKFs, Frame& F,
+                            std::vector<std::vector<MapPoint*> >& vvpMapPointMatches, std::vector<int>& vnMatches) {
+    const int nk = (int)vpKFs.size();
+    struct Side {
+        std::vector<MapPoint*> mps;
+        std::vector<uint8_t> mp, t;
+        std::vector<float> a;
+        FeatCsr f;
+        std::vector<int> match;
+        int n = 0;
+    };
+    std::vector<Side> side(nk);
+    std::vector<orb_bow_kf> K(nk);
+    Scratch& S = scratch();
+    const float* aF = angles_of(F.mvKeys, S.a2);
+    const FeatCsr& ff = S.f2.assign(F.mFeatVec);
+    for (int i = 0; i < nk; i++) {
+        KeyFrame* pKF = vpKFs[i];
+        Side& sd = side[i];
+        sd.mps = pKF->GetMapPointMatches();
+        sd.f.assign(pKF->mFeatVec);
+        sd.match.assign(F.N > 0 ? F.N : 1, -1);
+        K[i] = orb_bow_kf{pKF->N, desc_rows(pKF->mDescriptors, pKF->N, sd.t), angles_of(pKF->mvKeysUn, sd.a),
+                          good_points(sd.mps, sd.mp), sd.f.fv, sd.match.data(), &sd.n};
+    }
+    check(orb_search_by_bow_kf_f_batch(ctx(), mfNNratio, mbCheckOrientation, F.N, desc_rows(F.mDescriptors, F.N, S.t2),
+                                       aF, ff.fv, nk, K.data()),
+          "SearchByBoW(vector<KeyFrame*>, Frame&)");
+    vvpMapPointMatches.assign(nk, std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL)));
+    vnMatches.assign(nk, 0);
+    int total = 0;
+    for (int i = 0; i < nk; i++) {
+        for (int iF = 0; iF < F.N; iF++)
+            if (side[i].match[iF] >= 0) vvpMapPointMatches[i][iF] = side[i].mps[side[i].match[iF]];
+        vnMatches[i] = side[i].n;
+        total += side[i].n;
+    }
+    return total;
+}
+
+// SearchByBoW(pKF1, pKF2) for every pKF2 of vpKF2 in one call (orb_search_by_bow_kf_kf_batch): the loop candidates of
+// LoopClosing::ComputeSim3 (LoopClosing.cc:252-265).  vvpMatches12[i] / vnMatches[i] are SearchByBoW(pKF1,
+// vpKF2[i], ...)'s outputs.
+int ORBmatcher::SearchByBoW(KeyFrame* pKF1, const std::vector<KeyFrame*>& vpKF2,
+                            std::vector<std::vector<MapPoint*> >& vvpMatches12, std::vector<int>& vnMatches) {
+    const int nk = (int)vpKF2.size();
+    const std::vector<MapPoint*> vpMapPoints1 = pKF1->GetMapPointMatches();
+    const int n1 = (int)vpMapPoints1.size();
+    Scratch& S = scratch();
+    const uint8_t* mp1 = good_points(vpMapPoints1, S.mp1);
+    const float* a1 = angles_of(pKF1->mvKeysUn, S.a1);
+    const FeatCsr& f1 = S.f1.assign(pKF1->mFeatVec);
+    struct Side {
+        std::vector<MapPoint*> mps;
+        std::vector<uint8_t> mp, t;
+        std::vector<float> a;
+        FeatCsr f;
+        std::vector<int> match;
+        int n = 0;
+    };
+    std::vector<Side> side(nk);
+    std::vector<orb_bow_kf> K(nk);
+    for (int i = 0; i < nk; i++) {
+        KeyFrame* pKF2 = vpKF2[i];
+        Side& sd = side[i];
+        sd.mps = pKF2->GetMapPointMatches();
+        sd.f.assign(pKF2->mFeatVec);
+        sd.match.assign(n1 > 0 ? n1 : 1, -1);
+        K[i] = orb_bow_kf{(int)sd.mps.size(), desc_rows(pKF2->mDescriptors, (int)sd.mps.size(), sd.t),
+                          angles_of(pKF2->mvKeysUn, sd.a), good_points(sd.mps, sd.mp), sd.f.fv, sd.match.data(), &sd.n};
+    }
+    check(orb_search_by_bow_kf_kf_batch(ctx(), mfNNratio, mbCheckOrientation, n1,
+                                        desc_rows(pKF1->mDescriptors, n1, S.t1), a1, mp1, f1.fv, nk, K.data()),
+          "SearchByBoW(KeyFrame*, vector<KeyFrame*>)");
+    vvpMatches12.assign(nk, std::vector<MapPoint*>(n1, static_cast<MapPoint*>(NULL)));
+    vnMatches.assign(nk, 0);
+    int total = 0;
+    for (int i = 0; i < nk; i++) {
+        for (int i1 = 0; i1 < n1; i1++)
+            if (side[i].match[i1] >= 0) vvpMatches12[i][i1] = side[i].mps[side[i].match[i1]];
+        vnMatches[i] = side[i].n;
+        total += side[i].n;
+    }
+    return total;
 }
 
 int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,

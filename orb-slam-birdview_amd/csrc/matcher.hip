@@ -91,6 +91,10 @@ struct TopkSession {
     int nitems = 0, nt = 0;
     std::vector<int> item_q;         // query feature per item
     std::vector<int2> item_rng;      // [begin, end) into cand
+    // batch calls: the query row of each item (else qdesc + 32 item_q[i]) and the train set as consecutive parts
+    // (else tdesc): several keyframes' items / trains in one session
+    std::vector<const uint8_t*> item_src;
+    std::vector<std::pair<const uint8_t*, int> > tparts;
     const int* cand = nullptr;       // host candidate list
     int ncand = 0;
     Stage st{c};
@@ -124,8 +128,17 @@ struct TopkSession {
         const int r = st.alloc();
         if (r != ORB_OK) return r;
         uint8_t* hq = st.hi<uint8_t>(o_q);
-        for (int i = 0; i < nitems; i++) std::memcpy(hq + (size_t)i * 32, qdesc + (size_t)item_q[i] * 32, 32);
-        if (nt) std::memcpy(st.hi<uint8_t>(o_t), tdesc, (size_t)nt * 32);
+        for (int i = 0; i < nitems; i++)
+            std::memcpy(hq + (size_t)i * 32, item_src.empty() ? qdesc + (size_t)item_q[i] * 32 : item_src[i], 32);
+        if (tparts.empty()) {
+            if (nt) std::memcpy(st.hi<uint8_t>(o_t), tdesc, (size_t)nt * 32);
+        } else {
+            size_t o = 0;
+            for (const auto& tp : tparts) {
+                if (tp.second) std::memcpy(st.hi<uint8_t>(o_t) + o, tp.first, (size_t)tp.second * 32);
+                o += (size_t)tp.second * 32;
+            }
+        }
         std::memcpy(st.hi<int2>(o_rng), item_rng.data(), (size_t)nitems * 8);
         if (ncand) std::memcpy(st.hi<int>(o_cand), cand, (size_t)ncand * 4);
         dist = st.h<int>(o_dist);
@@ -180,9 +193,9 @@ struct TopkSession {
     }
     bool cen = false;
 
-    // Rank items [from, nitems) with train thresholds thr (NULL = admit all).
-    int run(int from, const int* thr) {
-        const int n = nitems - from;
+    // Rank items [from, to) (to < 0: nitems) with train thresholds thr (NULL = admit all).
+    int run(int from, const int* thr, int to = -1) {
+        const int n = (to < 0 ? nitems : to) - from;
         if (n <= 0) return ORB_OK;
         hipError_t e;
         if (thr) std::memcpy(st.hi<int>(o_thr), thr, (size_t)nt * 4);
@@ -229,6 +242,141 @@ struct TopkSession {
         return found == 2 || nvalid[i] <= K;
     }
 };
+
+// SearchByBoW(KeyFrame*, Frame&)'s acceptance (ORBmatcher.cc:175-283) over one keyframe's items [ib, ie), in the
+// reference's order: the first two admissible entries of each top-k list (a taken Frame feature is skipped), the
+// ratio test, the rotation histogram; a list the taken set exhausts is re-ranked on the GPU from that item on.
+// Trains are the Frame's features (indices 0..n_f).
+int bow_kf_f_replay(TopkSession& s, int ib, int ie, float nnratio, int check_ori, int n_f, const float* angle_kf,
+                    const float* angle_f, int* match_f, int* nmatches_out) {
+    std::vector<int> matches(n_f, -1);
+    std::vector<int> thr(n_f);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    auto admit = [&](int t, int) { return matches[t] < 0; };   // if(vpMapPointMatches[realIdxF]) continue;
+    for (int i = ib; i < ie; i++) {
+        int d1, i1, d2;
+        if (!s.best_two(i, admit, d1, i1, d2, 256)) {
+            for (int t = 0; t < n_f; t++) thr[t] = matches[t] >= 0 ? -1 : INT_MAX;
+            const int st = s.run(i, thr.data(), ie);
+            if (st != ORB_OK) return st;
+            s.best_two(i, admit, d1, i1, d2, 256);
+        }
+        if (d1 <= TH_LOW && static_cast<float>(d1) < nnratio * static_cast<float>(d2)) {   // :228-230
+            const int realIdxKF = s.item_q[i];
+            matches[i1] = realIdxKF;
+            if (check_ori) rotHist[rot_bin(angle_kf[realIdxKF], angle_f[i1])].push_back(i1);
+            nmatches++;
+        }
+    }
+    if (check_ori) cull_rotation(rotHist, matches, nmatches);
+    std::memcpy(match_f, matches.data(), (size_t)n_f * sizeof(int));
+    if (nmatches_out) *nmatches_out = nmatches;
+    return ORB_OK;
+}
+
+// SearchByBoW(KeyFrame*, KeyFrame*)'s acceptance (:559-653) over one KF2's items [ib, ie); its trains are the
+// session's train records [tb, tb + n2), thr the session-wide thresholds (this KF2's span rewritten on a re-rank).
+int bow_kf_kf_replay(TopkSession& s, int ib, int ie, int tb, std::vector<int>& thr, float nnratio, int check_ori,
+                     int n1, const float* angle1, int n2, const float* angle2, const uint8_t* mp2, int* match12,
+                     int* nmatches_out) {
+    std::vector<char> matched2(n2, 0);
+    std::vector<int> matches(n1, -1);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    auto admit = [&](int t, int) { return !matched2[t - tb]; };
+    for (int i = ib; i < ie; i++) {
+        int d1, i1, d2;
+        if (!s.best_two(i, admit, d1, i1, d2, 256)) {
+            for (int t = 0; t < n2; t++) thr[tb + t] = (matched2[t] || !mp2[t]) ? -1 : INT_MAX;
+            const int st = s.run(i, thr.data(), ie);
+            if (st != ORB_OK) return st;
+            s.best_two(i, admit, d1, i1, d2, 256);
+        }
+        if (d1 < TH_LOW && static_cast<float>(d1) < nnratio * static_cast<float>(d2)) {   // :598-600
+            const int idx1 = s.item_q[i], j2 = i1 - tb;
+            matches[idx1] = j2;
+            matched2[j2] = 1;
+            if (check_ori) rotHist[rot_bin(angle1[idx1], angle2[j2])].push_back(idx1);
+            nmatches++;
+        }
+    }
+    if (check_ori) cull_rotation(rotHist, matches, nmatches);
+    std::memcpy(match12, matches.data(), (size_t)n1 * sizeof(int));
+    if (nmatches_out) *nmatches_out = nmatches;
+    return ORB_OK;
+}
+
+bool bow_kf_ok(const orb_bow_kf& k) {
+    return k.n >= 0 && k.match && featvec_ok(k.fv, k.n) && (k.n == 0 || (k.desc && k.angle && k.mp));
+}
+
+// SearchByBoW(KeyFrame*, Frame&) for nkf keyframes against one Frame: every keyframe's items in one session (the
+// Frame's features are the shared trains and its FeatureVector the shared candidate list), one ranking launch, then
+// each keyframe's replay.  The single call is the batch of one.
+int bow_kf_f_run(Ctx* c, float nnratio, int check_ori, int n_f, const uint8_t* desc_f, const float* angle_f,
+                 orb_featvec fv_f, int nkf, const orb_bow_kf* kfs) {
+    TopkSession s{c};
+    s.cand = fv_f.indices;
+    s.ncand = fv_f.nnodes ? fv_f.offsets[fv_f.nnodes] : 0;
+    std::vector<int> first(nkf + 1, 0);
+    for (int p = 0; p < nkf; p++) {
+        const orb_bow_kf& K = kfs[p];
+        for_common_nodes(K.fv, fv_f, [&](int a, int b) {
+            for (int iKF = K.fv.offsets[a]; iKF < K.fv.offsets[a + 1]; iKF++) {
+                const int realIdxKF = K.fv.indices[iKF];
+                if (!K.mp[realIdxKF]) continue;   // !pMP || pMP->isBad()  (:204-208)
+                s.item_q.push_back(realIdxKF);
+                s.item_src.push_back(K.desc + (size_t)realIdxKF * 32);
+                s.item_rng.push_back(make_int2(fv_f.offsets[b], fv_f.offsets[b + 1]));
+            }
+        });
+        first[p + 1] = (int)s.item_q.size();
+    }
+    int st = s.setup(nullptr, desc_f, n_f);
+    if (st == ORB_OK) st = s.run(0, nullptr);
+    if (st != ORB_OK) return st;
+    for (int p = 0; p < nkf && st == ORB_OK; p++)
+        st = bow_kf_f_replay(s, first[p], first[p + 1], nnratio, check_ori, n_f, kfs[p].angle, angle_f, kfs[p].match,
+                             kfs[p].nmatches);
+    return st;
+}
+
+// SearchByBoW(KeyFrame*, KeyFrame*) for one KF1 against nkf KF2s: the KF2s' features concatenated as the trains
+// (KF2 p at [tb_p, tb_p + n2_p)), their FeatureVector indices concatenated (offset by tb_p) as the candidates.
+int bow_kf_kf_run(Ctx* c, float nnratio, int check_ori, int n1, const uint8_t* desc1, const float* angle1,
+                  const uint8_t* mp1, orb_featvec fv1, int nkf, const orb_bow_kf* kf2s) {
+    TopkSession s{c};
+    std::vector<int> first(nkf + 1, 0), tb(nkf + 1, 0), cand;
+    std::vector<int> thr;
+    for (int p = 0; p < nkf; p++) {
+        const orb_bow_kf& K = kf2s[p];
+        const int cb = (int)cand.size();
+        const int nnz = K.fv.nnodes ? K.fv.offsets[K.fv.nnodes] : 0;
+        for (int i = 0; i < nnz; i++) cand.push_back(tb[p] + K.fv.indices[i]);
+        for_common_nodes(fv1, K.fv, [&](int a, int b) {
+            for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
+                const int idx1 = fv1.indices[i];
+                if (!mp1[idx1]) continue;   // :567-571
+                s.item_q.push_back(idx1);
+                s.item_rng.push_back(make_int2(cb + K.fv.offsets[b], cb + K.fv.offsets[b + 1]));
+            }
+        });
+        first[p + 1] = (int)s.item_q.size();
+        tb[p + 1] = tb[p] + K.n;
+        s.tparts.push_back(std::make_pair(K.desc, K.n));
+        for (int t = 0; t < K.n; t++) thr.push_back(K.mp[t] ? INT_MAX : -1);   // !pMP2 || isBad (:584-588)
+    }
+    s.cand = cand.data();
+    s.ncand = (int)cand.size();
+    int st = s.setup(desc1, nullptr, tb[nkf]);
+    if (st == ORB_OK) st = s.run(0, thr.data());
+    if (st != ORB_OK) return st;
+    for (int p = 0; p < nkf && st == ORB_OK; p++)
+        st = bow_kf_kf_replay(s, first[p], first[p + 1], tb[p], thr, nnratio, check_ori, n1, angle1, kf2s[p].n,
+                              kf2s[p].angle, kf2s[p].mp, kf2s[p].match, kf2s[p].nmatches);
+    return st;
+}
 
 }  // namespace
 }  // namespace orbgpu
@@ -421,43 +569,21 @@ int orb_search_by_bow_kf_f(orb_ctx* h, float nnratio, int check_ori, int n_kf, c
     if (n_kf < 0 || n_f < 0 || !match_f) return ORB_ERR_ARG;
     if (!featvec_ok(fv_kf, n_kf) || !featvec_ok(fv_f, n_f))
         return set_error("orb_search_by_bow_kf_f: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
-    TopkSession s{c};
-    s.cand = fv_f.indices;
-    s.ncand = fv_f.nnodes ? fv_f.offsets[fv_f.nnodes] : 0;
-    for_common_nodes(fv_kf, fv_f, [&](int a, int b) {
-        for (int iKF = fv_kf.offsets[a]; iKF < fv_kf.offsets[a + 1]; iKF++) {
-            const int realIdxKF = fv_kf.indices[iKF];
-            if (!mp_kf[realIdxKF]) continue;   // !pMP || pMP->isBad()  (:204-208)
-            s.item_q.push_back(realIdxKF);
-            s.item_rng.push_back(make_int2(fv_f.offsets[b], fv_f.offsets[b + 1]));
-        }
-    });
-    int st = s.setup(desc_kf, desc_f, n_f);
-    if (st == ORB_OK) st = s.run(0, nullptr);
-    if (st != ORB_OK) return st;
-    std::vector<int> matches(n_f, -1);
-    std::vector<int> thr(n_f);
-    std::vector<int> rotHist[HISTO_LENGTH];
-    int nmatches = 0;
-    auto admit = [&](int t, int) { return matches[t] < 0; };   // if(vpMapPointMatches[realIdxF]) continue;
-    for (int i = 0; i < s.nitems; i++) {
-        int d1, i1, d2;
-        if (!s.best_two(i, admit, d1, i1, d2, 256)) {
-            for (int t = 0; t < n_f; t++) thr[t] = matches[t] >= 0 ? -1 : INT_MAX;
-            if ((st = s.run(i, thr.data())) != ORB_OK) return st;
-            s.best_two(i, admit, d1, i1, d2, 256);
-        }
-        if (d1 <= TH_LOW && static_cast<float>(d1) < nnratio * static_cast<float>(d2)) {   // :228-230
-            const int realIdxKF = s.item_q[i];
-            matches[i1] = realIdxKF;
-            if (check_ori) rotHist[rot_bin(angle_kf[realIdxKF], angle_f[i1])].push_back(i1);
-            nmatches++;
-        }
-    }
-    if (check_ori) cull_rotation(rotHist, matches, nmatches);
-    std::memcpy(match_f, matches.data(), (size_t)n_f * sizeof(int));
-    if (nmatches_out) *nmatches_out = nmatches;
-    return ORB_OK;
+    const orb_bow_kf K{n_kf, desc_kf, angle_kf, mp_kf, fv_kf, match_f, nmatches_out};
+    return bow_kf_f_run(c, nnratio, check_ori, n_f, desc_f, angle_f, fv_f, 1, &K);
+}
+
+int orb_search_by_bow_kf_f_batch(orb_ctx* h, float nnratio, int check_ori, int n_f, const uint8_t* desc_f,
+                                 const float* angle_f, orb_featvec fv_f, int nkf, const orb_bow_kf* kfs) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n_f < 0 || nkf < 0 || (nkf > 0 && !kfs) || (n_f > 0 && !(desc_f && angle_f))) return ORB_ERR_ARG;
+    if (!featvec_ok(fv_f, n_f))
+        return set_error("orb_search_by_bow_kf_f_batch: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
+    for (int p = 0; p < nkf; p++)
+        if (!bow_kf_ok(kfs[p]))
+            return set_error("orb_search_by_bow_kf_f_batch: bad keyframe arguments", hipSuccess), ORB_ERR_ARG;
+    return nkf ? bow_kf_f_run(c, nnratio, check_ori, n_f, desc_f, angle_f, fv_f, nkf, kfs) : ORB_OK;
 }
 
 /* SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)  ORBmatcher.cc:522-655 */
@@ -470,46 +596,27 @@ int orb_search_by_bow_kf_kf(orb_ctx* h, float nnratio, int check_ori, int n1, co
     if (n1 < 0 || n2 < 0 || !match12) return ORB_ERR_ARG;
     if (!featvec_ok(fv1, n1) || !featvec_ok(fv2, n2))
         return set_error("orb_search_by_bow_kf_kf: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
-    TopkSession s{c};
-    s.cand = fv2.indices;
-    s.ncand = fv2.nnodes ? fv2.offsets[fv2.nnodes] : 0;
-    for_common_nodes(fv1, fv2, [&](int a, int b) {
-        for (int i = fv1.offsets[a]; i < fv1.offsets[a + 1]; i++) {
-            const int idx1 = fv1.indices[i];
-            if (!mp1[idx1]) continue;   // :567-571
-            s.item_q.push_back(idx1);
-            s.item_rng.push_back(make_int2(fv2.offsets[b], fv2.offsets[b + 1]));
-        }
-    });
-    std::vector<int> thr(n2);
-    std::vector<char> matched2(n2, 0);
-    for (int t = 0; t < n2; t++) thr[t] = mp2[t] ? INT_MAX : -1;   // !pMP2 || isBad (:584-588)
-    int st = s.setup(desc1, desc2, n2);
-    if (st == ORB_OK) st = s.run(0, thr.data());
-    if (st != ORB_OK) return st;
-    std::vector<int> matches(n1, -1);
-    std::vector<int> rotHist[HISTO_LENGTH];
-    int nmatches = 0;
-    auto admit = [&](int t, int) { return !matched2[t]; };
-    for (int i = 0; i < s.nitems; i++) {
-        int d1, i1, d2;
-        if (!s.best_two(i, admit, d1, i1, d2, 256)) {
-            for (int t = 0; t < n2; t++) thr[t] = (matched2[t] || !mp2[t]) ? -1 : INT_MAX;
-            if ((st = s.run(i, thr.data())) != ORB_OK) return st;
-            s.best_two(i, admit, d1, i1, d2, 256);
-        }
-        if (d1 < TH_LOW && static_cast<float>(d1) < nnratio * static_cast<float>(d2)) {   // :598-600
-            const int idx1 = s.item_q[i];
-            matches[idx1] = i1;
-            matched2[i1] = 1;
-            if (check_ori) rotHist[rot_bin(angle1[idx1], angle2[i1])].push_back(idx1);
-            nmatches++;
-        }
+    const orb_bow_kf K{n2, desc2, angle2, mp2, fv2, match12, nmatches_out};
+    return bow_kf_kf_run(c, nnratio, check_ori, n1, desc1, angle1, mp1, fv1, 1, &K);
+}
+
+int orb_search_by_bow_kf_kf_batch(orb_ctx* h, float nnratio, int check_ori, int n1, const uint8_t* desc1,
+                                  const float* angle1, const uint8_t* mp1, orb_featvec fv1, int nkf,
+                                  const orb_bow_kf* kf2s) {
+    Ctx* c = reinterpret_cast<Ctx*>(h);
+    CTX_GUARD(c);
+    if (n1 < 0 || nkf < 0 || (nkf > 0 && !kf2s) || (n1 > 0 && !(desc1 && angle1 && mp1))) return ORB_ERR_ARG;
+    if (!featvec_ok(fv1, n1))
+        return set_error("orb_search_by_bow_kf_kf_batch: malformed FeatureVector CSR", hipSuccess), ORB_ERR_ARG;
+    long long ntot = 0;
+    for (int p = 0; p < nkf; p++) {
+        if (!bow_kf_ok(kf2s[p]))
+            return set_error("orb_search_by_bow_kf_kf_batch: bad keyframe arguments", hipSuccess), ORB_ERR_ARG;
+        ntot += kf2s[p].n;
     }
-    if (check_ori) cull_rotation(rotHist, matches, nmatches);
-    std::memcpy(match12, matches.data(), (size_t)n1 * sizeof(int));
-    if (nmatches_out) *nmatches_out = nmatches;
-    return ORB_OK;
+    if (ntot > INT_MAX / 64)
+        return set_error("orb_search_by_bow_kf_kf_batch: too many features", hipSuccess), ORB_ERR_ARG;
+    return nkf ? bow_kf_kf_run(c, nnratio, check_ori, n1, desc1, angle1, mp1, fv1, nkf, kf2s) : ORB_OK;
 }
 
 /* SearchForTriangulation  ORBmatcher.cc:657-823: no cross-query dependence (vbMatched2 is never

@@ -361,6 +361,47 @@ class ORBmatcher:
                                             _p(a[5]), fb, _p(out), ctypes.byref(nm)), "SearchByBoW(KF,KF)")
         return nm.value, out
 
+    def _bow_entries(self, kfs, nout):
+        """(ctypes array of orb_bow_kf, outputs, counts, keepalive) for dicts {desc, angle, mp, featvec}."""
+        from ._lib import OrbBowKf
+        arr, outs, counts, keep = (OrbBowKf * max(len(kfs), 1))(), [], [], []
+        for p, k in enumerate(kfs):
+            f, kf = _featvec(k["featvec"])
+            a = [np.ascontiguousarray(x) for x in (k["desc"], np.asarray(k["angle"], np.float32),
+                                                    np.asarray(k["mp"], np.uint8))]
+            out = np.full(max(nout, 1), -1, np.int32)
+            n = ctypes.c_int()
+            keep += [kf, a, out, n]
+            outs.append(out[:nout])
+            counts.append(n)
+            arr[p] = OrbBowKf(len(a[0]), _p(a[0]), _p(a[1]), _p(a[2]), f, _p(out), ctypes.pointer(n))
+        return arr, outs, counts, keep
+
+    def SearchByBoW_KF_F_batch(self, kfs, desc_f, angle_f, featvec_f):
+        """orb_search_by_bow_kf_f_batch: SearchByBoW(pKF, F) for every keyframe of kfs (dicts with desc, angle, mp,
+        featvec) in one call (Tracking::Relocalization's candidate loop, Tracking.cc:1931-1938).  Returns a list of
+        (nmatches, match_f), each equal to SearchByBoW_KF_F's."""
+        fb, kb = _featvec(featvec_f)
+        d = np.ascontiguousarray(desc_f)
+        ang = np.ascontiguousarray(angle_f, np.float32)
+        arr, outs, counts, keep = self._bow_entries(kfs, len(d))
+        check(lib().orb_search_by_bow_kf_f_batch(self._ctx.h, self.mfNNratio, int(self.mbCheckOrientation), len(d),
+                                                 _p(d), _p(ang), fb, len(kfs), ctypes.cast(arr, ctypes.c_void_p)),
+              "SearchByBoW(KF,F) batch")
+        return [(n.value, o) for n, o in zip(counts, outs)]
+
+    def SearchByBoW_KF_KF_batch(self, desc1, angle1, mp1, featvec1, kf2s):
+        """orb_search_by_bow_kf_kf_batch: SearchByBoW(KF1, pKF2) for every KF2 of kf2s (dicts with desc, angle, mp,
+        featvec) in one call (LoopClosing::ComputeSim3's candidate loop, LoopClosing.cc:252-265).  Returns a list
+        of (nmatches, match12), each equal to SearchByBoW_KF_KF's."""
+        fa, ka = _featvec(featvec1)
+        a = [np.ascontiguousarray(x) for x in (desc1, np.asarray(angle1, np.float32), np.asarray(mp1, np.uint8))]
+        arr, outs, counts, keep = self._bow_entries(kf2s, len(a[0]))
+        check(lib().orb_search_by_bow_kf_kf_batch(self._ctx.h, self.mfNNratio, int(self.mbCheckOrientation),
+                                                  len(a[0]), _p(a[0]), _p(a[1]), _p(a[2]), fa, len(kf2s),
+                                                  ctypes.cast(arr, ctypes.c_void_p)), "SearchByBoW(KF,KF) batch")
+        return [(n.value, o) for n, o in zip(counts, outs)]
+
     def SearchForTriangulation(self, desc1, kps1, has_mp1, uright1, featvec1, desc2, kps2, has_mp2, uright2,
                                featvec2, F12, ex, ey, scale_factors2, level_sigma2_2, bOnlyStereo=False):
         """SearchForTriangulation (ORBmatcher.cc:657-823). Returns an (n, 2) array of (idx1, idx2)."""

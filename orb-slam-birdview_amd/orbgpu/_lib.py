@@ -42,6 +42,11 @@ class OrbTriPair(ctypes.Structure):   # orb_tri_pair
                 ("pairs_out", vp), ("cap", ci), ("npairs", ctypes.POINTER(ci))]
 
 
+class OrbBowKf(ctypes.Structure):   # orb_bow_kf
+    _fields_ = [("n", ci), ("desc", vp), ("angle", vp), ("mp", vp), ("fv", OrbFeatVec), ("match", vp),
+                ("nmatches", ctypes.POINTER(ci))]
+
+
 class OrbFrameGrid(ctypes.Structure):
     _fields_ = [("min_x", cf), ("min_y", cf), ("inv_w", cf), ("inv_h", cf), ("cell_off", vp), ("cell_idx", vp)]
 
@@ -84,6 +89,8 @@ SIGNATURES = {
                                      ctypes.POINTER(ci)]),
     "orb_search_for_triangulation": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, OrbFeatVec, ci, vp, vp, vp, vp,
                                           OrbFeatVec, vp, cf, cf, vp, vp, ci, vp, ci, ctypes.POINTER(ci)]),
+    "orb_search_by_bow_kf_f_batch": (ci, [vp, cf, ci, ci, vp, vp, OrbFeatVec, ci, vp]),
+    "orb_search_by_bow_kf_kf_batch": (ci, [vp, cf, ci, ci, vp, vp, vp, OrbFeatVec, ci, vp]),
     "orb_search_for_triangulation_batch": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, OrbFeatVec, ci, vp]),
     "orb_window_match": (ci, [vp, cf, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, ctypes.POINTER(ci)]),
     "orb_window_match_grid": (ci, [vp, cf, ci, ci, ci, vp, vp, vp, cf, ci, vp, vp, OrbFrameGrid, vp,

@@ -27,7 +27,11 @@ public:
                                 std::vector<int>& vnMatches12, int windowSize = 10);
     int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
                                std::vector<pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo);
-    // the one declaration a maintainer adds to include/ORBmatcher.h for the batched form
+    // the declarations a maintainer adds to include/ORBmatcher.h for the batched forms
+    int SearchByBoW(const std::vector<KeyFrame*>& vpKFs, Frame& F, std::vector<std::vector<MapPoint*> >& vvpMapPointMatches,
+                    std::vector<int>& vnMatches);
+    int SearchByBoW(KeyFrame* pKF1, const std::vector<KeyFrame*>& vpKF2, std::vector<std::vector<MapPoint*> >& vvpMatches12,
+                    std::vector<int>& vnMatches);
     int SearchForTriangulation(KeyFrame* pKF1, const std::vector<KeyFrame*>& vpKF2, const std::vector<cv::Mat>& vF12,
                                std::vector<std::vector<pair<size_t, size_t> > >& vvMatchedPairs, const bool bOnlyStereo);
     int BirdviewMatch(Frame& F1, Frame& F2, vector<int>& vnMatches12, vector<cv::Point2f>& vPrevMatched,

@@ -197,6 +197,19 @@ int main(int argc, char** argv) {
             if (ratio == 0.7f)
                 printf("TIME SearchByBoW_KF_F %.1f\n",
                        time_us([&] { matcher.SearchByBoW(&KF1, F, vpMapPointMatches); }, 20));
+            // the batched overload (Tracking::Relocalization's candidates): KF1, KF2, KF1, each == the single call
+            std::vector<KeyFrame*> vpKFs = {&KF1, &KF2, &KF1};
+            std::vector<std::vector<MapPoint*> > vv;
+            std::vector<int> vn;
+            const int tot = matcher.SearchByBoW(vpKFs, F, vv, vn);
+            bool bok = vv.size() == 3 && vn.size() == 3 && vv[0] == vpMapPointMatches && vn[0] == nm;
+            int sum = 0;
+            for (int i = 0; bok && i < 3; i++) {
+                std::vector<MapPoint*> one;
+                bok = matcher.SearchByBoW(vpKFs[i], F, one) == vn[i] && one == vv[i];
+                sum += vn[i];
+            }
+            report("SearchByBoW_KF_F_batch_ratio" + std::to_string(ratio).substr(0, 4), bok && sum == tot, "");
         }
 
         // ---- SearchByBoW(KeyFrame*, KeyFrame*): LoopClosing::ComputeSim3 (ORBmatcher(0.75,true), LoopClosing.cc:265)
@@ -218,6 +231,19 @@ int main(int argc, char** argv) {
             snprintf(det, sizeof det, "nmatches=%d oracle=%d", nm, onm);
             report("SearchByBoW_KF_KF", ok && nm > 50, det);
             printf("TIME SearchByBoW_KF_KF %.1f\n", time_us([&] { matcher.SearchByBoW(&KF1, &KF2, vpMatches12); }, 20));
+            // the batched overload (LoopClosing::ComputeSim3's candidates): KF2, KF1, KF2, each == the single call
+            std::vector<KeyFrame*> vpKF2 = {&KF2, &KF1, &KF2};
+            std::vector<std::vector<MapPoint*> > vv;
+            std::vector<int> vn;
+            const int tot = matcher.SearchByBoW(&KF1, vpKF2, vv, vn);
+            bool bok = vv.size() == 3 && vn.size() == 3 && vv[0] == vpMatches12 && vn[0] == nm;
+            int sum = 0;
+            for (int i = 0; bok && i < 3; i++) {
+                std::vector<MapPoint*> one;
+                bok = matcher.SearchByBoW(&KF1, vpKF2[i], one) == vn[i] && one == vv[i];
+                sum += vn[i];
+            }
+            report("SearchByBoW_KF_KF_batch", bok && sum == tot, "");
         }
 
         // ---- SearchForTriangulation: LocalMapping::CreateNewMapPoints (ORBmatcher(0.6,false),

@@ -150,6 +150,97 @@ def test_search_by_bow_kf_kf(orbgpu_mod, oracle_mod, frames, ratio, check_ori):
     assert n == on and np.array_equal(m, om)
 
 
+@pytest.mark.parametrize("ratio,check_ori", [(0.75, True), (0.7, False)])
+def test_search_by_bow_batches(orbgpu_mod, oracle_mod, frames, ratio, check_ori):
+    """The BoW searches over several keyframes in one call (Tracking.cc:1931-1938's relocalisation candidates against
+    one Frame; LoopClosing.cc:252-265's loop candidates against one KF1): each entry equals the single call and the
+    oracle.  Keyframes: both frames with different map-point masks and FeatureVector granularities, one without
+    features, one without a common node."""
+    ka, da, kb, db = frames
+    rng = np.random.default_rng(41)
+    kfs = []
+    for p, (d, k, nodes) in enumerate([(da, ka, 16), (db, kb, 8), (da, ka, 24), (db, kb, 16)]):
+        kfs.append(dict(desc=d, angle=k["angle"], mp=(rng.random(len(d)) < 0.6 + 0.1 * p).astype(np.uint8),
+                        featvec=_featvec(d, nodes)))
+    kfs.append(dict(desc=np.zeros((0, 32), np.uint8), angle=np.zeros(0, np.float32), mp=np.zeros(0, np.uint8),
+                    featvec={}))
+    kfs.append(dict(kfs[1], featvec={k + 5000: v for k, v in kfs[1]["featvec"].items()}))
+    m = orbgpu_mod.ORBmatcher(ratio, check_ori)
+    # (KF, F): every keyframe against the Frame db
+    fvf = _featvec(db, 16)
+    ob_f, _kf = _oracle_fv(oracle_mod, fvf)
+    got = m.SearchByBoW_KF_F_batch(kfs, db, kb["angle"], fvf)
+    for k, (n, mt) in zip(kfs, got):
+        sn, sm = m.SearchByBoW_KF_F(k["desc"], k["angle"], k["mp"], k["featvec"], db, kb["angle"], fvf)
+        oa, _ka = _oracle_fv(oracle_mod, k["featvec"])
+        on, om = oracle_mod.search_by_bow_kf_f(ratio, check_ori, k["desc"], k["angle"], k["mp"], oa, db, kb["angle"],
+                                               ob_f)
+        assert n == sn == on and np.array_equal(mt, sm) and np.array_equal(mt, om)
+    assert got[0][0] > 50 and got[4][0] == 0 and got[5][0] == 0
+    # (KF, KF): KF1 = da against every keyframe
+    mp1 = (rng.random(len(da)) < 0.85).astype(np.uint8)
+    fv1 = _featvec(da, 16)
+    o1, _k1 = _oracle_fv(oracle_mod, fv1)
+    got = m.SearchByBoW_KF_KF_batch(da, ka["angle"], mp1, fv1, kfs)
+    for k, (n, mt) in zip(kfs, got):
+        sn, sm = m.SearchByBoW_KF_KF(da, ka["angle"], mp1, fv1, k["desc"], k["angle"], k["mp"], k["featvec"])
+        ob, _kb = _oracle_fv(oracle_mod, k["featvec"])
+        on, om = oracle_mod.search_by_bow_kf_kf(ratio, check_ori, da, ka["angle"], mp1, o1, k["desc"], k["angle"],
+                                                k["mp"], ob)
+        assert n == sn == on and np.array_equal(mt, sm) and np.array_equal(mt, om)
+    assert got[1][0] > 50 and got[4][0] == 0 and got[5][0] == 0
+
+
+def test_search_by_bow_batches_rerank_and_errors(orbgpu_mod, oracle_mod):
+    """The re-rank path inside a batch (identical queries against trains at distances 0..39 exhaust the 8-entry lists,
+    so items are re-ranked on the GPU with the taken set: only the keyframe's own items, between other keyframes'),
+    an empty batch, and a malformed entry refused before anything runs."""
+    import ctypes
+    from orbgpu import _lib
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 256, 32, dtype=np.uint8)
+    bits = np.unpackbits(base)
+    trains = []
+    for d in range(40):
+        b = bits.copy()
+        b[:d] ^= 1
+        trains.append(np.packbits(b))
+    t = np.array(trains, np.uint8)
+    q = np.repeat(base[None], 40, 0)
+    ang = np.zeros(40, np.float32)
+    fv = {0: list(range(40))}
+    oq, _kq = _oracle_fv(oracle_mod, fv)
+    m = orbgpu_mod.ORBmatcher(0.99, False)
+    mps = [np.ones(40, np.uint8), (np.arange(40) % 3 != 0).astype(np.uint8), np.ones(40, np.uint8)]
+    kfs = [dict(desc=q, angle=ang, mp=mps[0], featvec=fv), dict(desc=q, angle=ang, mp=mps[1], featvec=fv),
+           dict(desc=t, angle=ang, mp=mps[2], featvec=fv)]
+    got = m.SearchByBoW_KF_F_batch(kfs, t, ang, fv)
+    for k, (n, mt) in zip(kfs, got):
+        on, om = oracle_mod.search_by_bow_kf_f(0.99, False, k["desc"], ang, k["mp"], oq, t, ang, oq)
+        assert n == on and np.array_equal(mt, om)
+    assert got[0][0] > 30
+    got = m.SearchByBoW_KF_KF_batch(q, ang, np.ones(40, np.uint8), fv, kfs[::-1])
+    for k, (n, mt) in zip(kfs[::-1], got):
+        on, om = oracle_mod.search_by_bow_kf_kf(0.99, False, q, ang, np.ones(40, np.uint8), oq, k["desc"], ang,
+                                                k["mp"], oq)
+        assert n == on and np.array_equal(mt, om)
+    L = _lib.lib()
+    f, _kf = orbgpu_mod._featvec(fv)
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    assert _lib.STATUS.get(L.orb_search_by_bow_kf_f_batch(m._ctx.h, 0.7, 1, 40, p(t), p(ang), f, 0, None)) == "ORB_OK"
+    ids, off, idx = np.array([0, 1], np.uint32), np.array([0, 30, 20], np.int32), np.arange(40, dtype=np.int32)
+    bad = orbgpu_mod.OrbFeatVec(2, ids.ctypes.data, off.ctypes.data, idx.ctypes.data)
+    out = np.full(40, -7, np.int32)
+    n = ctypes.c_int(-5)
+    arr = (_lib.OrbBowKf * 1)()
+    arr[0] = _lib.OrbBowKf(40, p(q), p(ang), p(mps[0]), bad, p(out), ctypes.pointer(n))
+    for st in (L.orb_search_by_bow_kf_f_batch(m._ctx.h, 0.7, 1, 40, p(t), p(ang), f, 1, ctypes.cast(arr, ctypes.c_void_p)),
+               L.orb_search_by_bow_kf_kf_batch(m._ctx.h, 0.7, 1, 40, p(q), p(ang), p(mps[0]), f, 1,
+                                               ctypes.cast(arr, ctypes.c_void_p))):
+        assert _lib.STATUS.get(st) == "ORB_ERR_ARG"
+    assert n.value == -5 and (out == -7).all()
+
+
 def test_exhaustion_rerank_path(orbgpu_mod, oracle_mod):
     # identical queries against trains at distances 0..39: each query takes the next train, so the
     # 8-entry GPU lists run out and the remaining queries are re-ranked on the GPU.

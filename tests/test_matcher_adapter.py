@@ -40,6 +40,14 @@ def test_adapter_defines_the_reference_signatures(adapter_bin):
         "std::vector<std::vector<std::pair<unsigned long, unsigned long>, std::allocator<std::pair<unsigned long, "
         "unsigned long> > >, std::allocator<std::vector<std::pair<unsigned long, unsigned long>, "
         "std::allocator<std::pair<unsigned long, unsigned long> > > > >&, bool)",
+        "ORB_SLAM2::ORBmatcher::SearchByBoW(std::vector<ORB_SLAM2::KeyFrame*, std::allocator<ORB_SLAM2::KeyFrame*> > "
+        "const&, ORB_SLAM2::Frame&, std::vector<std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >, "
+        "std::allocator<std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> > > >&, "
+        "std::vector<int, std::allocator<int> >&)",
+        "ORB_SLAM2::ORBmatcher::SearchByBoW(ORB_SLAM2::KeyFrame*, std::vector<ORB_SLAM2::KeyFrame*, "
+        "std::allocator<ORB_SLAM2::KeyFrame*> > const&, std::vector<std::vector<ORB_SLAM2::MapPoint*, "
+        "std::allocator<ORB_SLAM2::MapPoint*> >, std::allocator<std::vector<ORB_SLAM2::MapPoint*, "
+        "std::allocator<ORB_SLAM2::MapPoint*> > > >&, std::vector<int, std::allocator<int> >&)",
         "ORB_SLAM2::ORBmatcher::SearchForInitialization(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, "
         "std::vector<cv::Point2f, std::allocator<cv::Point2f> >&, std::vector<int, std::allocator<int> >&, int)",
         "ORB_SLAM2::ORBmatcher::BirdviewMatch(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, std::vector<int, "

@@ -206,6 +206,16 @@ int main(int argc, char** argv) {
                                       aB.data(), fvB.fv, om.data());
         }, cpu_reps);
         emit("SearchByBoW_KF_F", g, c, nm, onm, ok);
+        // Tracking::Relocalization's candidate loop (Tracking.cc:1931-1938) as one batched call: 10 keyframes (the
+        // same one: the same work per entry) against 10 runs of the CPU loop
+        std::vector<KeyFrame*> vk(10, &KF[0]);
+        std::vector<std::vector<MapPoint*> > vv;
+        std::vector<int> vn;
+        const int tot = m.SearchByBoW(vk, F[1], vv, vn);
+        bool bok = tot == 10 * onm && (int)vv.size() == 10;
+        for (int p = 0; bok && p < 10; p++) bok = vv[p] == v;
+        const double gb = median_us([&] { m.SearchByBoW(vk, F[1], vv, vn); }, reps);
+        emit("SearchByBoW_KF_F_x10", gb, 10 * c, tot, 10 * onm, bok && ok);
     }
     // ---- SearchByBoW(KF, KF)
     {
@@ -223,6 +233,15 @@ int main(int argc, char** argv) {
                                        fe[1].desc.data, aB.data(), mpB.data(), fvB.fv, om.data());
         }, cpu_reps);
         emit("SearchByBoW_KF_KF", g, c, nm, onm, ok);
+        // LoopClosing::ComputeSim3's candidate loop (LoopClosing.cc:252-265) as one batched call: 10 candidates
+        std::vector<KeyFrame*> vk(10, &KF[1]);
+        std::vector<std::vector<MapPoint*> > vv;
+        std::vector<int> vn;
+        const int tot = m.SearchByBoW(&KF[0], vk, vv, vn);
+        bool bok = tot == 10 * onm && (int)vv.size() == 10;
+        for (int p = 0; bok && p < 10; p++) bok = vv[p] == v;
+        const double gb = median_us([&] { m.SearchByBoW(&KF[0], vk, vv, vn); }, reps);
+        emit("SearchByBoW_KF_KF_x10", gb, 10 * c, tot, 10 * onm, bok && ok);
     }
     // ---- SearchForTriangulation (R = I, F12 = K^-T [t12]x K^-1, LocalMapping::ComputeF12's form)
     {
