@@ -356,8 +356,10 @@ int Ctx::ensure_flow(int nframes) {
     std::vector<FlowTask> tasks;
     FlowPlan pl;
     const int blocks = std::min(num_cu, flow_blocks > 0 ? flow_blocks : kFlowDefaultBlocks * nframes);
-    // (ORBGPU_FLOW_CHAIN=0: per-level resize tasks instead of chain tasks)
-    const bool use_chain = chain.nseg > 0 && !(std::getenv("ORBGPU_FLOW_CHAIN") && std::getenv("ORBGPU_FLOW_CHAIN")[0] == '0');
+    // per-level resize tasks; ORBGPU_FLOW_CHAIN=1: chain-job pyramid tasks (each tile's region chain from the segment
+    // base, as k_pyramid_chain), measured slower at one frame, both forms in tests/test_gpu_flow.py
+    const char* fc = std::getenv("ORBGPU_FLOW_CHAIN");
+    const bool use_chain = chain.nseg > 0 && fc && fc[0] == '1';
     if (!build_flow(geom, nframes, blocks, use_chain ? &chain : nullptr, &chain_jobs_host, tasks, pl)) return ORB_OK;
     flow_chain_plan = use_chain ? chain : ChainPlan{};
     hipError_t e;

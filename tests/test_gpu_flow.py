@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True)
 def _flow_on(monkeypatch):
     monkeypatch.setenv("ORBGPU_FLOW", "1")   # (read at orb_create)
+    monkeypatch.delenv("ORBGPU_FLOW_CHAIN", raising=False)
 
 
 def _check(e, o, frames, B, levels=True):
@@ -45,6 +46,23 @@ def test_flow_bit_exact(orbgpu_mod, oracle_mod, w, h, nf, B):
         for _ in range(2):
             e.launch()
             e.sync()
+        _check(e, o, frames, B)
+    e.close()
+
+
+@pytest.mark.parametrize("w,h,nf,B", [(1280, 720, 4000, 1), (1280, 720, 2000, 2), (640, 480, 1000, 1)])
+def test_flow_chain_pyramid_tasks(orbgpu_mod, oracle_mod, monkeypatch, w, h, nf, B):
+    """ORBGPU_FLOW_CHAIN=1: the pyramid as chain-job tasks (every tile's region chain recomputed from the segment base,
+    k_pyramid_chain's arithmetic) instead of per-level resize tasks; the same bytes."""
+    from orbgpu.synth import bench_frames
+    monkeypatch.setenv("ORBGPU_FLOW_CHAIN", "1")
+    e = orbgpu_mod.BatchExtractor(nf, w, h, B)
+    o = oracle_mod.OracleExtractor(nf)
+    for rnd in range(2):
+        frames = bench_frames(w, h, B, first=11 + 5 * rnd)
+        e.upload(frames)
+        e.launch()
+        e.sync()
         _check(e, o, frames, B)
     e.close()
 
