@@ -129,6 +129,11 @@ struct FeatCsr {
         ids.clear();
         off.clear();
         idx.clear();
+        size_t nnz = 0;
+        for (DBoW2::FeatureVector::const_iterator it = f.begin(); it != f.end(); ++it) nnz += it->second.size();
+        ids.reserve(f.size());
+        off.reserve(f.size() + 1);
+        idx.reserve(nnz + 1);
         off.push_back(0);
         for (DBoW2::FeatureVector::const_iterator it = f.begin(); it != f.end(); ++it) {
             ids.push_back(it->first);
@@ -315,8 +320,11 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
     std::vector<uint8_t>&mp1 = S.mp1, &mp2 = S.mp2;   // GetMapPoint(idx) != NULL (:699, :722)
     mp1.assign(n1 > 0 ? n1 : 1, 0);
     mp2.assign(n2 > 0 ? n2 : 1, 0);
-    for (int i = 0; i < n1; i++) mp1[i] = pKF1->GetMapPoint(i) != NULL;
-    for (int i = 0; i < n2; i++) mp2[i] = pKF2->GetMapPoint(i) != NULL;
+    {   // GetMapPoint(idx) != NULL (:699, :722), from one snapshot (one lock instead of one per feature)
+        const std::vector<MapPoint*> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
+        for (int i = 0; i < n1; i++) mp1[i] = v1[i] != NULL;
+        for (int i = 0; i < n2; i++) mp2[i] = v2[i] != NULL;
+    }
     float F[9];
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) F[3 * r + c] = F12.at<float>(r, c);   // CheckDistEpipolarLine (:143-147)
@@ -356,7 +364,10 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, const std::vector<KeyFram
     Scratch& S = scratch();
     std::vector<uint8_t>& mp1 = S.mp1;
     mp1.assign(n1 > 0 ? n1 : 1, 0);
-    for (int i = 0; i < n1; i++) mp1[i] = pKF1->GetMapPoint(i) != NULL;
+    {
+        const std::vector<MapPoint*> v1 = pKF1->GetMapPointMatches();   // (one lock, not one per feature)
+        for (int i = 0; i < n1; i++) mp1[i] = v1[i] != NULL;
+    }
     std::vector<float>& ur1 = S.ur1;
     ur1.assign(pKF1->mvuRight.begin(), pKF1->mvuRight.end());
     ur1.resize(n1 > 0 ? n1 : 1, -1.f);
@@ -381,7 +392,10 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, const std::vector<KeyFram
         const float ey = pKF2->fy * C2.at<float>(1) * invz + pKF2->cy;
         const int n2 = pKF2->N;
         sd.mp.assign(n2 > 0 ? n2 : 1, 0);
-        for (int i = 0; i < n2; i++) sd.mp[i] = pKF2->GetMapPoint(i) != NULL;
+        {
+            const std::vector<MapPoint*> v2 = pKF2->GetMapPointMatches();
+            for (int i = 0; i < n2; i++) sd.mp[i] = v2[i] != NULL;
+        }
         sd.ur.assign(pKF2->mvuRight.begin(), pKF2->mvuRight.end());
         sd.ur.resize(n2 > 0 ? n2 : 1, -1.f);
         sd.f.assign(pKF2->mFeatVec);
