@@ -3,7 +3,7 @@ by the GPU extractor (its parity is fuzz_parity.py's) at a random size / feature
 a random function of the descriptor, random node counts), random map-point and stereo masks, random ratio /
 orientation check; the GPU calls -- SearchByBoW (KF,F) and (KF,KF), SearchForTriangulation, and their batched forms
 over 1-6 keyframes -- against the oracle's restatements of ORBmatcher.cc:159-288, 522-655, 657-823.
-usage: python3 tools/fuzz_matcher.py <n> [seed0]"""
+usage: python3 tools/fuzz_matcher.py <n> [seed0]; tests/test_gpu_fuzz.py runs a few seeded cases through matcher_case()."""
 import sys
 
 import numpy as np
@@ -29,27 +29,24 @@ def ofv(fv):
     return oracle.make_featvec(ids, [fv[i] for i in ids])
 
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-seed0 = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-ok = fail = refused = 0
-for s in range(seed0, seed0 + n):
+def matcher_case(s):
+    """Case s: returns (status, info, bad) with status "equal", "mismatch" or "refused" (a frame geometry both the
+    oracle and the GPU refuse) and bad the list of calls that differed from the oracle."""
     rng = np.random.default_rng(5000 + s)
     w, h = int(rng.integers(320, 1281)), int(rng.integers(240, 721))
     nf = int(rng.choice([500, 1000, 2000]))
     img = synth_frame(w, h, s)
     shift = (int(rng.integers(-4, 5)), int(rng.integers(-4, 5)))
     ex_ = oracle.OracleExtractor(nf)
-    g = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7)  # frames are inputs here; extraction parity is fuzz_parity.py's
+    ext = orbgpu.ORBextractor(nf, 1.2, 8, 20, 7)  # frames are inputs here; extraction parity is fuzz_parity.py's
     if ex_.run(img) < 0:  # a geometry the reference cannot run (a level's cell grid degenerates): both refuse
         try:
-            g(img)
-            print("MISMATCH seed", s, (w, h, nf), "oracle refuses, GPU extracts")
-            fail += 1
+            ext(img)
         except orbgpu.OrbError:
-            refused += 1
-        continue
-    ka, da = g(img)
-    kb, db = g(np.ascontiguousarray(np.roll(img, shift, axis=(0, 1))))
+            return "refused", (w, h, nf), []
+        return "mismatch", (w, h, nf), [("oracle refuses, GPU extracts",)]
+    ka, da = ext(img)
+    kb, db = ext(np.ascontiguousarray(np.roll(img, shift, axis=(0, 1))))
     ratio = float(rng.choice([0.6, 0.7, 0.75, 0.9]))
     ori = bool(rng.random() < 0.6)
     m = orbgpu.ORBmatcher(ratio, ori)
@@ -72,7 +69,7 @@ for s in range(seed0, seed0 + n):
             sn, sm = m.SearchByBoW_KF_F(kf["desc"], kf["angle"], kf["mp"], kf["featvec"], db, kb["angle"], fvf)
             if sn != on or not np.array_equal(sm, om):
                 bad.append(("bow_kf_f_single",))
-    # SearchByBoW (KF, KF) batch
+    # SearchByBoW (KF, KF) batch, and the single call on the first keyframe
     mp1 = (rng.random(len(da)) < rng.random()).astype(np.uint8)
     fv1 = featvec(da, rng)
     o1, keep1 = ofv(fv1)
@@ -82,7 +79,12 @@ for s in range(seed0, seed0 + n):
         on, om = oracle.search_by_bow_kf_kf(ratio, ori, da, ka["angle"], mp1, o1, kf["desc"], kf["angle"], kf["mp"], ob)
         if gn != on or not np.array_equal(gm, om):
             bad.append(("bow_kf_kf", i))
-    # SearchForTriangulation batch (random F near a horizontal epipolar geometry, random epipoles)
+        if i == 0:
+            sn, sm = m.SearchByBoW_KF_KF(da, ka["angle"], mp1, fv1, kf["desc"], kf["angle"], kf["mp"], kf["featvec"])
+            if sn != on or not np.array_equal(sm, om):
+                bad.append(("bow_kf_kf_single",))
+    # SearchForTriangulation batch (random F near a horizontal epipolar geometry, random epipoles), and the single
+    # call on the first neighbour
     t = ex_.tables()
     ur1 = np.where(rng.random(len(da)) < 0.3, 10.0, -1.0).astype(np.float32)
     others = []
@@ -97,18 +99,38 @@ for s in range(seed0, seed0 + n):
                            level_sigma2_2=t["sigma2"]))
     stereo = bool(rng.random() < 0.2)
     got = m.SearchForTriangulationBatch(da, ka, mp1, ur1, fv1, others, stereo)
-    for i, (o, g) in enumerate(zip(others, got)):
+    for i, (o, gp) in enumerate(zip(others, got)):
         ob, keep_b = ofv(o["featvec2"])
         op = oracle.search_for_triangulation(ori, stereo, da, ka, mp1, ur1, o1, o["desc2"], o["kps2"], o["has_mp2"],
                                              o["uright2"], ob, o["F12"], o["ex"], o["ey"], t["scale"], t["sigma2"])
-        if not np.array_equal(g, op):
+        if not np.array_equal(gp, op):
             bad.append(("triangulation", i))
-    if bad:
-        fail += 1
-        print("MISMATCH seed", s, (w, h, nf, ratio, ori), bad)
-    else:
-        ok += 1
-    if (s - seed0) % 10 == 9:
-        print(f"progress {s - seed0 + 1}/{n} equal={ok} mismatched={fail} refused={refused}", flush=True)
-print(f"SUMMARY iterations={n} equal={ok} mismatched={fail} refused={refused}", flush=True)
-sys.exit(1 if fail else 0)
+        if i == 0:
+            sp = m.SearchForTriangulation(da, ka, mp1, ur1, fv1, o["desc2"], o["kps2"], o["has_mp2"], o["uright2"],
+                                          o["featvec2"], o["F12"], o["ex"], o["ey"], t["scale"], t["sigma2"], stereo)
+            if not np.array_equal(sp, op):
+                bad.append(("triangulation_single",))
+    return ("mismatch" if bad else "equal"), (w, h, nf, ratio, ori), bad
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    seed0 = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    ok = fail = refused = 0
+    for s in range(seed0, seed0 + n):
+        st, info, bad = matcher_case(s)
+        if st == "equal":
+            ok += 1
+        elif st == "refused":
+            refused += 1
+        else:
+            fail += 1
+            print("MISMATCH seed", s, info, bad)
+        if (s - seed0) % 10 == 9:
+            print(f"progress {s - seed0 + 1}/{n} equal={ok} mismatched={fail} refused={refused}", flush=True)
+    print(f"SUMMARY iterations={n} equal={ok} mismatched={fail} refused={refused}", flush=True)
+    return 1 if fail else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
