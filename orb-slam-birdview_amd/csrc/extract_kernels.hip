@@ -149,14 +149,17 @@ constexpr int kCpSc1 = 16;
 // One 128 x TH output tile (bx, by) of level `level` for frame f, by the 256 threads tid = 0..255 of a block (or
 // of a quarter of k_extract_flow's 1024-thread block: every thread of the block reaches its one barrier; an
 // inactive quarter stages nothing and stores nothing).
-template <int kRsTileH, bool GENERIC, int CP>
+// KP: 16-byte source chunks each thread stages (0: the tile height's worst case; the batch launch picks the
+// level's own bound, LevelGeom::rs_chunks, so a 1.2-scale level issues two loads per thread instead of five
+// clamped duplicates).
+template <int kRsTileH, bool GENERIC, int CP, int KP = 0>
 __device__ __forceinline__ void resize_tile(const Geom* __restrict__ g, const ResizeCoef* __restrict__ coef, int level,
                                             const uint8_t* __restrict__ frames, long long framePitch, int rowStride,
                                             uint8_t* __restrict__ pyr, int f, int bx, int by, int tid, uint8_t* s_src,
                                             int4* s_cx, int4* s_cy, bool active) {
     constexpr int kRows = rs_rows(kRsTileH);
     constexpr int kQ = kRsPitch / 16;                                  // 16-byte chunks per LDS row
-    constexpr int kPer = (kRows * kQ + 255) / 256;                     // chunks per thread (upper bound)
+    constexpr int kPer = KP > 0 ? KP : (kRows * kQ + 255) / 256;       // chunks per thread (upper bound)
     const int dw = g->L[level].w, dh = g->L[level].h;
     const int x0 = bx * kRsTileW, y0 = by * kRsTileH;
     const LevelPtr src = level_ptr(g, level - 1, frames, framePitch, rowStride, pyr, f);
@@ -310,7 +313,7 @@ __device__ __forceinline__ void resize_tile(const Geom* __restrict__ g, const Re
     }
 }
 
-template <int kRsTileH, bool GENERIC>
+template <int kRsTileH, bool GENERIC, int KP>
 __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g,
                                                       const ResizeCoef* __restrict__ coef, int level,
                                                       const uint8_t* __restrict__ frames, long long framePitch,
@@ -320,8 +323,8 @@ __global__ __launch_bounds__(256) void k_resize_tiled(const Geom* __restrict__ g
     extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
     __shared__ int4 s_cx[kRsTileW];
     __shared__ int4 s_cy[kRsTileH];
-    resize_tile<kRsTileH, GENERIC, 0>(g, coef, level, frames, framePitch, rowStride, pyr, blockIdx.z, blockIdx.x,
-                                      blockIdx.y, threadIdx.x, s_src, s_cx, s_cy, true);
+    resize_tile<kRsTileH, GENERIC, 0, KP>(g, coef, level, frames, framePitch, rowStride, pyr, blockIdx.z, blockIdx.x,
+                                          blockIdx.y, threadIdx.x, s_src, s_cx, s_cy, true);
 }
 
 /* Few-launch pyramid for small batches (the host path's single frame, C5's per-GPU frame): the levels
@@ -2949,8 +2952,14 @@ hipError_t launch_extract(const Geom& g, const ExtractBuffers& b, const uint8_t*
             const int th = (t & 2) ? 32 : 16;
             const dim3 grid(cdiv(g.L[l].w, kRsTileW), cdiv(g.L[l].h, th), nframes);
             const size_t lds = (size_t)g.L[l].rs_span_rows * kRsPitch;
-            auto kern = th == 32 ? (gen ? k_resize_tiled<32, true> : k_resize_tiled<32, false>)
-                                 : (gen ? k_resize_tiled<16, true> : k_resize_tiled<16, false>);
+            // staging loads per thread: the level's own bound where two or three cover it, else the worst case
+            const int kp = g.L[l].rs_chunks <= 512 ? 2 : g.L[l].rs_chunks <= 768 ? 3 : 0;
+            auto kern = th == 32 ? (gen ? (kp == 2 ? k_resize_tiled<32, true, 2> : kp == 3 ? k_resize_tiled<32, true, 3>
+                                                                                          : k_resize_tiled<32, true, 0>)
+                                        : (kp == 2 ? k_resize_tiled<32, false, 2> : kp == 3 ? k_resize_tiled<32, false, 3>
+                                                                                           : k_resize_tiled<32, false, 0>))
+                                 : (gen ? (kp == 2 ? k_resize_tiled<16, true, 2> : k_resize_tiled<16, true, 0>)
+                                        : (kp == 2 ? k_resize_tiled<16, false, 2> : k_resize_tiled<16, false, 0>));
             hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, b.d_geom, cf, l, d_frames, frame_pitch, row_stride,
                                b.d_pyr);
         } else {

@@ -155,6 +155,21 @@ int build_geometry(Ctx* c, int W, int H, Geom& g, std::vector<ResizeCoef>& coefs
             }
             // the LDS source tile is sized to the tile height the launch uses (32 rows when they fit)
             L.rs_span_rows = (L.rs_tiled & 2) ? span_rows[1] : span_rows[0];
+            // and the staging loop to the tile with the most 16-byte source chunks (the aligned-source path)
+            L.rs_chunks = 0;
+            if (L.rs_tiled & 3) {
+                const int th = (L.rs_tiled & 2) ? 32 : 16;
+                int nq_max = 0, nr_max = 0;
+                for (int x0 = 0; x0 < L.w; x0 += kRsTileW) {
+                    const int x1 = std::min(x0 + kRsTileW, L.w) - 1;
+                    nq_max = std::max(nq_max, ((cx[x1].s1 - (cx[x0].s0 & ~15)) >> 4) + 1);
+                }
+                for (int y0 = 0; y0 < L.h; y0 += th) {
+                    const int y1 = std::min(y0 + th, L.h) - 1;
+                    nr_max = std::max(nr_max, cy[y1].s1 - cy[y0].s0 + 1);
+                }
+                L.rs_chunks = nq_max * nr_max;
+            }
         }
         L.maxBX = L.w - kEdgeThreshold + 3;
         L.maxBY = L.h - kEdgeThreshold + 3;

@@ -49,6 +49,8 @@ struct LevelGeom {
     float scale;         // mvScaleFactor
     float patch_size;    // (int)(PATCH_SIZE*scale) (:837)
     int rs_span_rows;    // k_resize_tiled: the largest source span (rows) of a tile: its LDS tile height
+    int rs_chunks;       // k_resize_tiled: the most 16-byte source chunks of a tile (rows x chunks per row), so
+                         // the launch issues ceil(rs_chunks / 256) loads per thread, not the worst case's
 };
 
 struct Geom {
