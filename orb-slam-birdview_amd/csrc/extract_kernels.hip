@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void k_resize(const Geom* __restrict__ g, cons
 // h < 2^19 keep both operands within 24 bits); unshifted for the generic form
 template <bool GENERIC>
 __device__ __forceinline__ int4 rs_row_entry(const ResizeCoef& c, int sy0) {
-    return make_int4((c.s0 - sy0) * kRsPitch, (c.s1 - sy0) * kRsPitch, GENERIC ? c.c0 : c.c0 << 12,
+    return make_int4(__mul24(c.s0 - sy0, kRsPitch), __mul24(c.s1 - sy0, kRsPitch), GENERIC ? c.c0 : c.c0 << 12,
                      GENERIC ? c.c1 : c.c1 << 12);
 }
 // one output pixel's vertical pass from the two rows' horizontal sums (weights from rs_row_entry)
@@ -149,6 +149,10 @@ constexpr int kCpSc1 = 16;
 // One 128 x TH output tile (bx, by) of level `level` for frame f, by the 256 threads tid = 0..255 of a block (or
 // of a quarter of k_extract_flow's 1024-thread block: every thread of the block reaches its one barrier; an
 // inactive quarter stages nothing and stores nothing).
+// (65536 + n - 1) / n for n = 0..17 (n = 0 unused): the staging loop's i / nq as a multiply; a table lookup with a
+// block-uniform index is one scalar load, where the division is a VALU sequence with two quarter-rate multiplies
+__constant__ unsigned kRsMagic[18] = {0,    65536, 32768, 21846, 16384, 13108, 10923, 9363, 8192,
+                                      7282, 6554,  5958,  5462,  5042,  4682,  4370,  4096, 3856};
 // KP: 16-byte source chunks each thread stages (0: the tile height's worst case; the batch launch picks the
 // level's own bound, LevelGeom::rs_chunks, so a 1.2-scale level issues two loads per thread instead of five
 // clamped duplicates).
@@ -177,7 +181,7 @@ __device__ __forceinline__ void resize_tile(const Geom* __restrict__ g, const Re
     int4 cxv = make_int4(0, 0, 0, 0), cyv = make_int4(0, 0, 0, 0);
     if (vec16) {
         const int nq = ((sx1 - sx0) >> 4) + 1;
-        const unsigned magic = (65536u + nq - 1) / nq;                  // i / nq for i < 4096, nq <= 17
+        const unsigned magic = kRsMagic[nq];                            // i / nq for i < 4096, nq <= 17
         const int total = nr * nq;
         // a buffer descriptor over the span (SGPRs): 32-bit row offsets (r * stride < 2^24 * 100 fits), no
         // 64-bit address arithmetic per chunk
